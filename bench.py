@@ -1,0 +1,134 @@
+"""bench.py -- full RMT time step (soft disc in the lid-driven cavity, configs 2/4
+physics) on MI355X: cell-updates/s at N=4096 (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--no-cpu-baseline]
+
+A step is one loop body of benchmarks/soft_disc_in_lid_driven.py:206-235 (timestep,
+reference-map advection, narrow-band extrapolation, level-set rebuild, RK4 momentum,
+Rhie-Chow + DCT-I projection, centroid/J diagnostics) on synthetic state of that shape
+(the driver's own initial condition: disc (0.6, 0.5, 0.2), fluid at rest, lid U=1).
+
+Multi-GPU: the fused step is not domain-decomposed yet, so N > 1 runs N independent
+replicas of the full N=4096 problem, one per rank ("replicas only");
+`value` counts the cells all ranks updated, timed by the max over ranks.
+"""
+import argparse
+import json
+import os
+import platform
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# algorithmic fp64 plane traffic of the stress + 4-stage RK4 pass
+# (reads u, v, p, X1, X2; writes u*, v*) = 7 planes x 8 B per cell for one RK4 pass.
+RK4_ALG_BYTES_PER_CELL = 7 * 8
+STEP_ALG_BYTES_PER_CELL = 208  # the whole step
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def cpu_baseline(n, steps):
+    """The oracle (C restatement of the reference's Numba kernels + the same NumPy/SciPy
+    calls) timed on this host: faithful threading (OpenMP only in the kernels that Numba
+    runs parallel=True)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    cores = min(16, os.cpu_count() or 1)
+    O.set_threads(cores)
+    sim = O.SoftDisc(n, "lid")
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sim.step()
+    dt = time.perf_counter() - t0
+    return {"value": n * n * steps / dt, "unit": "cell-updates/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{steps} full steps of the N={n} soft-disc loop body (oracle, "
+                      f"OpenMP only where the reference uses Numba parallel=True), "
+                      f"{dt:.1f} s on {platform.processor() or platform.machine()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    ws, rank, local = _dist()
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import sys
+    sys.path.insert(0, ROOT)
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+
+    N = args.n
+    sim = soft_disc_in_lid_driven(N)
+    sim.step(args.warmup)
+    torch.cuda.synchronize()
+    sim.set_profiling(True)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sim.step(args.steps)
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ph = sim.phase_times()
+    d = sim.diagnostics()
+    assert np.all(np.isfinite(d["cx"])) and np.all(np.isfinite(d["umax"])), "non-finite state"
+
+    if rank == 0:
+        cells = N * N * args.steps * ws
+        value = cells / elapsed
+        rk_ms, rk_launches = ph["rk4_stage_kernels"]
+        per_launch_s = rk_ms / 1e3 / rk_launches
+        # achieved: algorithmic bytes of one RK4 pass (4 launches) spread over its launches
+        alg_per_launch = RK4_ALG_BYTES_PER_CELL * N * N / 4
+        achieved = alg_per_launch / per_launch_s / 1e9
+        out = {
+            "metric": "cell-updates/s (full RMT step) at N=4096; achieved HBM GB/s vs peak",
+            "value": value, "unit": "cell-updates/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic (driver initial condition: disc at rest, lid U=1)",
+            "config": {"workload": f"soft_disc_in_lid_driven N={N} semilagrangian "
+                                   "(configs 2/4 loop body)", "grid": N,
+                       "parallelism": "replicas" if ws > 1 else "single-gpu"},
+            "roofline": {"bound": "hbm", "kernel": "k_mom_stage (RK4 stage, 4 launches/step)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+            "step_roofline": {"alg_bytes_per_cell": STEP_ALG_BYTES_PER_CELL,
+                              "achieved_GBs": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9,
+                              "frac": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9 / HBM_PEAK_GBS},
+            "phase_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ph.items()},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(N, args.cpu_steps)
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

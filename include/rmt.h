@@ -1,0 +1,204 @@
+/*
+ * rmt.h -- C ABI of librmt, the MI355X-native 2D Reference Map Technique (RMT) time step.
+ *
+ * This is the drop-in boundary for pyRMT's per-step hot path.  The
+ * reference has no native library: its operator surface is the set of module-level
+ * Python functions re-exported by pyRMT/__init__.py:1-57, called by the benchmark loop
+ * bodies (e.g. benchmarks/soft_disc_in_lid_driven.py:206-235).  Each entry point below
+ * replaces one of those functions (cited per entry); pyrmt_amd/functions.py binds them
+ * with ctypes under the reference names and signatures.
+ *
+ * Conventions
+ *   - Fields are float64, C-contiguous, shape (ny, nx), element [j*nx + i] (j <-> y).
+ *   - Every array argument is a DEVICE pointer (hipMalloc / torch.cuda memory) on the
+ *     context's device.  Calls are stream-ordered on the context stream and return once
+ *     enqueued, except where a host result is returned (documented per call).
+ *   - The caller allocates and frees every I/O buffer.  The context owns scratch space,
+ *     FFT plans and the step state of an rmt_sim.
+ *   - Errors: every call returns an rmt_status; rmt_last_error() describes the last
+ *     failure on the calling thread.  The Python shim maps RMT_ENONFINITE to
+ *     FloatingPointError and RMT_EINVAL to ValueError, like the reference
+ *     (functions.py:524-526, :539-542).
+ *   - Velocity BCs and level-set shapes cross as enums + parameters instead of the
+ *     reference's Python callables (functions.py:946-947, :1366-1367).
+ *   - Not re-entrant per context.
+ */
+#ifndef RMT_H
+#define RMT_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    RMT_OK = 0,
+    RMT_EINVAL = 1,      /* bad argument (unknown scheme / bc / shape, bad size)   */
+    RMT_ENONFINITE = 2,  /* non-finite velocity fed to advection                  */
+    RMT_EDEVICE = 3,     /* HIP / rocFFT failure                                   */
+    RMT_ENOTSUP = 4,     /* valid in the reference but outside this build's path   */
+    RMT_ENOMEM = 5
+} rmt_status;
+
+/* Velocity boundary conditions (benchmarks/common.py:27-50). */
+typedef enum {
+    RMT_BC_NONE = 0,          /* identity                                            */
+    RMT_BC_NOSLIP_LID = 1,    /* no_slip_lid_bc: walls 0, top row u = lid, corners 0  */
+    RMT_BC_FREESLIP_BOX = 2   /* free_slip_box_bc: normal 0, tangential copied        */
+} rmt_bc_kind;
+
+/* Reference-map advection schemes (functions.py:501-542). */
+typedef enum {
+    RMT_SCHEME_SEMILAGRANGIAN = 0,  /* advect_semilagrangian_rk4 (bilinear)            */
+    RMT_SCHEME_WENO5 = 1            /* advect_weno5_rk3                               */
+} rmt_scheme;
+
+typedef struct rmt_ctx rmt_ctx;
+
+const char *rmt_last_error(void);
+int rmt_version(void);
+
+/* Context: one device, one stream, one grid shape.  stream may be NULL (null stream)
+ * or a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
+int rmt_ctx_create(int ny, int nx, int device, void *stream, rmt_ctx **out);
+int rmt_ctx_set_stream(rmt_ctx *ctx, void *stream);
+int rmt_ctx_destroy(rmt_ctx *ctx);
+int rmt_ctx_sync(rmt_ctx *ctx);
+
+/* ---- finite-difference helpers (pyRMT/utils.py) ----------------------------------- */
+/* utils.py:4-14 grad_central_x_2nd / utils.py:16-25 grad_central_y_2nd */
+int rmt_grad_x_2nd(rmt_ctx *ctx, const double *f, double h, double *out);
+int rmt_grad_y_2nd(rmt_ctx *ctx, const double *f, double h, double *out);
+/* utils.py:61-114 diff_upwind_3rd (axis 1 = x, 0 = y) */
+int rmt_diff_upwind_3rd(rmt_ctx *ctx, const double *f, const double *vel, double h, int axis,
+                        double *out);
+
+/* ---- interpolation / reference-map transport (interpolators.py, functions.py) ------ */
+/* interpolators.py:4-61 bilinear_interpolate: u is (ny, nx) of the ctx grid, nq queries. */
+int rmt_bilinear_interpolate(rmt_ctx *ctx, const double *u, const double *xq, const double *yq,
+                             long nq, double dx, double dy, double *out);
+/* functions.py:194-227 advect_semilagrangian_rk4 */
+int rmt_advect_sl_rk4(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                      const double *X, const double *Y, double dt, double dx, double dy,
+                      double *out);
+/* functions.py:321-393 _weno5_rhs and functions.py:396-415 advect_weno5_rk3 */
+int rmt_weno5_rhs(rmt_ctx *ctx, const double *q, const double *a, const double *b, double dx,
+                  double dy, const double *phi, double w_cut, double *rhs);
+int rmt_advect_weno5_rk3(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                         double dx, double dy, double dt, const double *phi, double w_cut,
+                         double *out);
+/* functions.py:524-526 guard: sets *finite (host) to 1 if every a, b is finite.  Blocks. */
+int rmt_all_finite2(rmt_ctx *ctx, const double *a, const double *b, int *finite);
+
+/* functions.py:48-163 extrapolate_reference_map: exact raster-order (Gauss-Seidel)
+ * semantics of the reference; outputs may alias the inputs. */
+int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, const double *X2,
+                                  const double *phi, double dx, double dy, int max_layers,
+                                  double *X1_out, double *X2_out);
+
+/* functions.py:1366-1367 with benchmarks/common.py:55-57: phi = |xi - (x0,y0)| - R */
+int rmt_rebuild_phi_disc(rmt_ctx *ctx, const double *X1, const double *X2, double x0, double y0,
+                         double R, double *phi);
+
+/* ---- stress / momentum (functions.py:545-944) -------------------------------------- */
+/* functions.py:545-658 solid_cauchy_stress */
+int rmt_solid_cauchy_stress(rmt_ctx *ctx, const double *X1, const double *X2, double dx,
+                            double dy, double mu_s, double kappa, const double *phi,
+                            double w_cut, double detg_clamp, int isochoric, double *sxx,
+                            double *sxy, double *syy, double *J);
+/* functions.py:660-671 smoothed_heaviside; n elements */
+int rmt_smoothed_heaviside(rmt_ctx *ctx, const double *x, long n, double w_t, double *H);
+/* benchmarks/common.py:27-50, in place */
+int rmt_apply_velocity_bc(rmt_ctx *ctx, int bc_kind, double lid, double *u, double *v);
+
+typedef struct {
+    int bc_kind;        /* rmt_bc_kind */
+    double lid;         /* lid speed for RMT_BC_NOSLIP_LID */
+    double mu_s, kappa, eta_s, rho_s, rho_f, mu_f, w_t;
+    double dx, dy, dt;
+    int stress_band;    /* functions.py:673-674 stress_band */
+    double detg_clamp;
+} rmt_momentum_params;
+
+/* functions.py:673-762 momentum_step_rk4 (gamma = 0: surface tension is outside the
+ * path).  Outputs u*, v* and the elastic sxx, sxy, syy, J it precomputes. */
+int rmt_momentum_step_rk4(rmt_ctx *ctx, const rmt_momentum_params *prm, const double *u,
+                          const double *v, const double *p, const double *X1, const double *X2,
+                          const double *phi, double *u_new, double *v_new, double *sxx,
+                          double *sxy, double *syy, double *J);
+
+/* ---- projection (functions.py:1005-1364) ------------------------------------------- */
+/* functions.py:1016-1071 _compute_divergence_rc, constant density: d_f = dt / mean(rho) */
+int rmt_divergence_rc(rmt_ctx *ctx, const double *a, const double *b, const double *p,
+                      double d_f, double dx, double dy, double *divU);
+/* functions.py:1005-1014 _compute_divergence */
+int rmt_divergence_central(rmt_ctx *ctx, const double *a, const double *b, double dx,
+                           double dy, double *divU);
+/* functions.py:1073-1089 _compute_pressure_gradient */
+int rmt_pressure_gradient(rmt_ctx *ctx, const double *p, double dx, double dy, double *gx,
+                          double *gy);
+/* functions.py:1107-1119 _solve_poisson_dct: idctn(dctn(rhs,1)/eig,1) - mean, with eig
+ * the DCT-I symbol of functions.py:1091-1104 for this grid (dx, dy). */
+int rmt_solve_poisson_dct(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p);
+/* functions.py:1255-1364 pressure_projection_amg, Neumann branch, constant density rho
+ * (the variable-density CG branch returns RMT_ENOTSUP).  p_prev may be NULL. */
+int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_star,
+                            double dx, double dy, double dt, double rho, int bc_kind,
+                            double lid, const double *p_prev, double *a, double *b, double *p);
+
+/* functions.py:165-192 compute_timestep; host result, blocks. */
+int rmt_compute_timestep(rmt_ctx *ctx, const double *a, const double *b, double dx, double dy,
+                         double CFL, double dt_min_cap, double mu_s, double rho_s, double gamma,
+                         double rho_f, double mu_f, double eta_s, double kappa, double *dt);
+
+/* ---- fused, device-resident time step (the loop body of the benchmark drivers) ----- */
+typedef enum {
+    RMT_SHAPE_NONE = 0,   /* pure fluid (lid_driven_cavity.py): phi = 1, no solid       */
+    RMT_SHAPE_DISC = 1    /* one disc: phi = |xi - (x0,y0)| - R                         */
+} rmt_shape_kind;
+
+typedef struct {
+    int ny, nx;
+    double dx, dy;
+    const double *xs, *ys;   /* HOST node coordinates, length nx and ny (create_grid) */
+    int scheme;              /* rmt_scheme                                            */
+    int bc_kind;             /* rmt_bc_kind                                           */
+    double lid;
+    int shape;               /* rmt_shape_kind                                        */
+    double x0, y0, R;
+    double mu_s, kappa, rho_s, eta_s, mu_f, rho_f, w_t;
+    int layers;              /* extrapolation layers                                  */
+    double cfl, dt_cap;      /* compute_timestep CFL and dt_min_cap                   */
+    int stress_band;
+    double detg_clamp;
+    int energies;            /* per-step KE / SE / dissipation (disc_in_taylor_green) */
+} rmt_sim_params;
+
+typedef struct rmt_sim rmt_sim;
+
+/* Per-step diagnostics, one record per completed step (soft_disc_in_lid_driven.py:233
+ * traj tuple, disc_in_taylor_green.py:243 hist tuple). */
+typedef struct {
+    double t, dt, cx, cy, minJ, maxJ, umax;
+    double ke, se, diss, integ, ry;
+} rmt_diag;
+
+int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out);
+int rmt_sim_destroy(rmt_sim *sim);
+/* field ids: 0 u (a), 1 v (b), 2 p, 3 X1, 4 X2, 5 phi (last rebuilt), 6 J */
+int rmt_sim_field(rmt_sim *sim, int field, double **dev_ptr);
+/* Enqueue nsteps loop bodies.  dt comes from compute_timestep on device and is clipped to
+ * t_end - t as the drivers do; steps after t >= t_end are no-ops.  No host sync. */
+int rmt_sim_step(rmt_sim *sim, int nsteps, double t_end);
+/* Phase timers (HIP events on the context stream, accumulated over steps while on):
+ * ms[0] dt reduction, [1] advection, [2] extrapolation, [3] momentum (prep + 4 stages +
+ * BC), [4] projection, [5] diagnostics, [6] the four RK4 stage kernels alone,
+ * [7] the extrapolation sweep kernel alone; calls[k] = number of timed intervals. */
+int rmt_sim_set_profiling(rmt_sim *sim, int on);
+int rmt_sim_phase_times(rmt_sim *sim, double *ms8, long *calls8);
+/* Copy the diagnostics of all completed steps since creation (blocks). */
+int rmt_sim_diagnostics(rmt_sim *sim, rmt_diag *out, int max_records, int *n_records);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RMT_H */

@@ -1,0 +1,120 @@
+"""ctypes binding of librmt.so (include/rmt.h).  The product path has no CPU fallback:
+if the HIP library is missing or no GPU is visible, calls fail loudly."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librmt.so")
+
+RMT_OK, RMT_EINVAL, RMT_ENONFINITE, RMT_EDEVICE, RMT_ENOTSUP, RMT_ENOMEM = range(6)
+
+
+class RMTError(RuntimeError):
+    pass
+
+
+class rmt_momentum_params(ctypes.Structure):
+    _fields_ = [("bc_kind", ctypes.c_int), ("lid", ctypes.c_double),
+                ("mu_s", ctypes.c_double), ("kappa", ctypes.c_double),
+                ("eta_s", ctypes.c_double), ("rho_s", ctypes.c_double),
+                ("rho_f", ctypes.c_double), ("mu_f", ctypes.c_double), ("w_t", ctypes.c_double),
+                ("dx", ctypes.c_double), ("dy", ctypes.c_double), ("dt", ctypes.c_double),
+                ("stress_band", ctypes.c_int), ("detg_clamp", ctypes.c_double)]
+
+
+class rmt_sim_params(ctypes.Structure):
+    _fields_ = [("ny", ctypes.c_int), ("nx", ctypes.c_int),
+                ("dx", ctypes.c_double), ("dy", ctypes.c_double),
+                ("xs", ctypes.c_void_p), ("ys", ctypes.c_void_p),
+                ("scheme", ctypes.c_int), ("bc_kind", ctypes.c_int), ("lid", ctypes.c_double),
+                ("shape", ctypes.c_int), ("x0", ctypes.c_double), ("y0", ctypes.c_double),
+                ("R", ctypes.c_double),
+                ("mu_s", ctypes.c_double), ("kappa", ctypes.c_double), ("rho_s", ctypes.c_double),
+                ("eta_s", ctypes.c_double), ("mu_f", ctypes.c_double), ("rho_f", ctypes.c_double),
+                ("w_t", ctypes.c_double), ("layers", ctypes.c_int),
+                ("cfl", ctypes.c_double), ("dt_cap", ctypes.c_double),
+                ("stress_band", ctypes.c_int), ("detg_clamp", ctypes.c_double),
+                ("energies", ctypes.c_int)]
+
+
+class rmt_diag(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in
+                ("t", "dt", "cx", "cy", "minJ", "maxJ", "umax", "ke", "se", "diss", "integ", "ry")]
+
+
+_P, _D, _I, _L = ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_long
+SIGNATURES = {
+    "rmt_last_error": (ctypes.c_char_p, []),
+    "rmt_version": (_I, []),
+    "rmt_ctx_create": (_I, [_I, _I, _I, _P, ctypes.POINTER(_P)]),
+    "rmt_ctx_set_stream": (_I, [_P, _P]),
+    "rmt_ctx_destroy": (_I, [_P]),
+    "rmt_ctx_sync": (_I, [_P]),
+    "rmt_grad_x_2nd": (_I, [_P, _P, _D, _P]),
+    "rmt_grad_y_2nd": (_I, [_P, _P, _D, _P]),
+    "rmt_diff_upwind_3rd": (_I, [_P, _P, _P, _D, _I, _P]),
+    "rmt_bilinear_interpolate": (_I, [_P, _P, _P, _P, _L, _D, _D, _P]),
+    "rmt_advect_sl_rk4": (_I, [_P, _P, _P, _P, _P, _P, _D, _D, _D, _P]),
+    "rmt_weno5_rhs": (_I, [_P, _P, _P, _P, _D, _D, _P, _D, _P]),
+    "rmt_advect_weno5_rk3": (_I, [_P, _P, _P, _P, _D, _D, _D, _P, _D, _P]),
+    "rmt_all_finite2": (_I, [_P, _P, _P, ctypes.POINTER(_I)]),
+    "rmt_extrapolate_reference_map": (_I, [_P, _P, _P, _P, _D, _D, _I, _P, _P]),
+    "rmt_rebuild_phi_disc": (_I, [_P, _P, _P, _D, _D, _D, _P]),
+    "rmt_solid_cauchy_stress": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _D, _D, _I, _P, _P, _P, _P]),
+    "rmt_smoothed_heaviside": (_I, [_P, _P, _L, _D, _P]),
+    "rmt_apply_velocity_bc": (_I, [_P, _I, _D, _P, _P]),
+    "rmt_momentum_step_rk4": (_I, [_P, ctypes.POINTER(rmt_momentum_params), _P, _P, _P, _P, _P,
+                                   _P, _P, _P, _P, _P, _P, _P]),
+    "rmt_divergence_rc": (_I, [_P, _P, _P, _P, _D, _D, _D, _P]),
+    "rmt_divergence_central": (_I, [_P, _P, _P, _D, _D, _P]),
+    "rmt_pressure_gradient": (_I, [_P, _P, _D, _D, _P, _P]),
+    "rmt_solve_poisson_dct": (_I, [_P, _P, _D, _D, _P]),
+    "rmt_pressure_projection": (_I, [_P, _P, _P, _D, _D, _D, _D, _I, _D, _P, _P, _P, _P]),
+    "rmt_compute_timestep": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D,
+                                  ctypes.POINTER(_D)]),
+    "rmt_sim_create": (_I, [_P, ctypes.POINTER(rmt_sim_params), ctypes.POINTER(_P)]),
+    "rmt_sim_destroy": (_I, [_P]),
+    "rmt_sim_field": (_I, [_P, _I, ctypes.POINTER(_P)]),
+    "rmt_sim_step": (_I, [_P, _I, _D]),
+    "rmt_sim_diagnostics": (_I, [_P, ctypes.POINTER(rmt_diag), _I, ctypes.POINTER(_I)]),
+    "rmt_sim_set_profiling": (_I, [_P, _I]),
+    "rmt_sim_phase_times": (_I, [_P, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load librmt.so (once).  Raises if the HIP library was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"librmt.so not found at {LIB_PATH}: build it first "
+                "(python -c 'import __graft_entry__ as g; g.build()')")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+_DEBUG_SYNC = bool(os.environ.get("RMT_DEBUG_SYNC"))
+
+
+def check(status, what=""):
+    if status == RMT_OK:
+        if _DEBUG_SYNC:      # debugging aid: surface asynchronous faults at the call
+            import torch
+            torch.cuda.synchronize()
+        return
+    msg = (lib().rmt_last_error() or b"").decode(errors="replace")
+    if status == RMT_ENONFINITE:
+        raise FloatingPointError(msg or what)
+    if status == RMT_EINVAL:
+        raise ValueError(msg or what)
+    if status == RMT_ENOTSUP:
+        raise NotImplementedError(msg or what)
+    raise RMTError(f"{what}: {msg} (status {status})")

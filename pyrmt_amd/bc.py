@@ -1,0 +1,111 @@
+"""Velocity BCs and level-set shapes as descriptors (they cross the C ABI as enums).
+
+The reference passes Python callables: ``velocity_bc(u, v) -> (u, v)``
+(functions.py:946-947; benchmarks/common.py:27-50) and ``phi_init_func(X1, X2)``
+(functions.py:1366-1367; benchmarks/common.py:55-57).  The drop-in functions accept
+either a descriptor below or such a callable; a callable is identified by probing it
+on small deterministic arrays and must reproduce one of the known BCs / a disc exactly,
+otherwise NotImplementedError is raised (no silent host path).
+"""
+import numpy as np
+
+NONE, NOSLIP_LID, FREESLIP_BOX = 0, 1, 2
+
+
+class VelocityBC:
+    kind = NONE
+    lid = 0.0
+
+    def __call__(self, u, v):
+        """Host restatement for setup code (never on the device path)."""
+        u = np.array(u, dtype=np.float64, copy=True)
+        v = np.array(v, dtype=np.float64, copy=True)
+        if self.kind == NOSLIP_LID:
+            for a in (u, v):
+                a[:, 0] = 0.0; a[:, -1] = 0.0; a[0, :] = 0.0; a[-1, :] = 0.0
+            u[-1, 1:-1] = self.lid
+        elif self.kind == FREESLIP_BOX:
+            u[:, 0] = 0.0; u[:, -1] = 0.0
+            v[:, 0] = v[:, 1]; v[:, -1] = v[:, -2]
+            v[0, :] = 0.0; v[-1, :] = 0.0
+            u[0, :] = u[1, :]; u[-1, :] = u[-2, :]
+        return u, v
+
+
+class NoSlipLid(VelocityBC):
+    """benchmarks/common.py:27-37 no_slip_lid_bc(u, v, lid_speed)."""
+    kind = NOSLIP_LID
+
+    def __init__(self, lid_speed=1.0):
+        self.lid = float(lid_speed)
+
+
+class FreeSlipBox(VelocityBC):
+    """benchmarks/common.py:40-50 free_slip_box_bc(u, v)."""
+    kind = FREESLIP_BOX
+
+
+class Identity(VelocityBC):
+    kind = NONE
+
+
+def resolve_bc(bc):
+    """Map a descriptor or a reference-style callable to (kind, lid)."""
+    if isinstance(bc, VelocityBC):
+        return bc.kind, bc.lid
+    if not callable(bc):
+        raise ValueError(f"velocity_bc must be a BC descriptor or callable, got {bc!r}")
+    rng = np.random.default_rng(12345)
+    u = rng.standard_normal((7, 9)) + 3.0
+    v = rng.standard_normal((7, 9)) - 3.0
+    ru, rv = bc(u.copy(), v.copy())
+    ru = np.asarray(ru); rv = np.asarray(rv)
+    lid = float(ru[-1, 4])
+    for cand in (NoSlipLid(lid), FreeSlipBox(), Identity()):
+        cu, cv = cand(u, v)
+        if np.array_equal(cu, ru) and np.array_equal(cv, rv):
+            return cand.kind, cand.lid
+    raise NotImplementedError(
+        "velocity_bc callable does not match no_slip_lid_bc / free_slip_box_bc; "
+        "pass a pyrmt_amd.bc descriptor")
+
+
+class Disc:
+    """benchmarks/common.py:55-57 initialize_disc: phi = |xi - (x0, y0)| - R."""
+
+    def __init__(self, x0, y0, R):
+        self.x0, self.y0, self.R = float(x0), float(y0), float(R)
+
+    def __call__(self, X1, X2):
+        return np.sqrt((X1 - self.x0) ** 2 + (X2 - self.y0) ** 2) - self.R
+
+
+def resolve_shape(phi_init_func):
+    """Map a Disc or a disc-SDF callable (e.g. the drivers' lambda) to a Disc."""
+    if isinstance(phi_init_func, Disc):
+        return phi_init_func
+    if not callable(phi_init_func):
+        raise ValueError("phi_init_func must be callable")
+    # fit (x0, y0, R) from the values at three points, then verify on a grid bitwise
+    f = lambda x, y: float(np.asarray(phi_init_func(np.array([[x]]), np.array([[y]])))[0, 0])
+    p0, px, py = f(0.0, 0.0), f(1.0, 0.0), f(0.0, 1.0)
+    # |(x,y)-c| - R; solve with squared distances: d0 = p0 + R, etc.  Try R from a 4th point.
+    pm = f(-1.0, 0.0)
+    # (p(1,0)+R)^2 - (p(-1,0)+R)^2 = -4 x0 ; use candidate R over a scan-free closed form:
+    # from d(1,0)^2 + d(-1,0)^2 = 2 d(0,0)^2 + 2  ->  quadratic in R
+    a = 2.0 - 2.0
+    b = 2 * (px + pm) - 4 * p0
+    c = px ** 2 + pm ** 2 - 2 * p0 ** 2 - 2.0
+    if abs(b) < 1e-300:
+        raise NotImplementedError("phi_init_func is not a disc signed distance")
+    R = -c / b if a == 0.0 else None
+    x0 = -((px + R) ** 2 - (pm + R) ** 2) / 4.0
+    y0 = ((p0 + R) ** 2 - (py + R) ** 2 + 1.0) / 2.0
+    disc = Disc(x0, y0, R)
+    g = np.linspace(-0.3, 1.3, 13)
+    X, Y = np.meshgrid(g, g)
+    ref = np.asarray(phi_init_func(X, Y))
+    for cand in (disc, Disc(round(x0, 12), round(y0, 12), round(R, 12))):
+        if np.array_equal(cand(X, Y), ref):
+            return cand
+    raise NotImplementedError("phi_init_func is not a disc signed distance; pass pyrmt_amd.bc.Disc")

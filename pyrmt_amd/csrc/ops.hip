@@ -1,0 +1,512 @@
+// ops.hip -- context, reductions and the per-operator kernels of librmt.
+// Each kernel restates one reference operator per cell (cited); launch shapes are
+// 1D over cells with 256-thread workgroups (memory-bound elementwise / small-stencil
+// work: reads coalesce along i, neighbours come from L2).
+#include "rmt_internal.hpp"
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace rmt {
+static thread_local std::string g_err;
+void set_error(const std::string &m) { g_err = m; }
+
+int ensure_scratch(rmt_ctx *ctx, size_t bytes) {
+    if (ctx->scratch_bytes >= bytes) return RMT_OK;
+    if (ctx->scratch) RMT_HIP(hipFree(ctx->scratch));
+    ctx->scratch = nullptr; ctx->scratch_bytes = 0;
+    RMT_HIP(hipMalloc(&ctx->scratch, bytes));
+    ctx->scratch_bytes = bytes;
+    return RMT_OK;
+}
+int ensure_bytes(rmt_ctx *ctx, size_t bytes) {
+    if (ctx->bytes_len >= bytes) return RMT_OK;
+    if (ctx->bytes) RMT_HIP(hipFree(ctx->bytes));
+    ctx->bytes = nullptr; ctx->bytes_len = 0;
+    RMT_HIP(hipMalloc(&ctx->bytes, bytes));
+    ctx->bytes_len = bytes;
+    return RMT_OK;
+}
+
+// ------------------------------------------------------------------ reductions ----
+// Deterministic two-pass reductions: RED_BLOCKS fixed workgroups each fold a strided
+// slice in a fixed order, then one workgroup folds the partials in a fixed tree.
+
+template <int OP>  // 0 sum, 1 max, 2 max(a*a+b*b)
+__global__ void __launch_bounds__(RED_T) k_reduce_p1(const double *__restrict__ a,
+                                                     const double *__restrict__ b, long n,
+                                                     double *__restrict__ part) {
+    __shared__ double s[RED_T];
+    double acc = OP == 0 ? 0.0 : -INFINITY;
+    for (long k = blockIdx.x * (long)RED_T + threadIdx.x; k < n; k += (long)RED_BLOCKS * RED_T) {
+        double x = OP == 2 ? a[k] * a[k] + b[k] * b[k] : a[k];
+        if (OP == 0) acc += x;
+        else acc = fmax(acc, x);   // NaN inputs are not on the path (guarded upstream)
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = RED_T / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            s[threadIdx.x] = OP == 0 ? s[threadIdx.x] + s[threadIdx.x + w]
+                                     : fmax(s[threadIdx.x], s[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+
+template <int OP>
+__global__ void __launch_bounds__(RED_T) k_reduce_p2(const double *__restrict__ part, double *out,
+                                                     double scale) {
+    __shared__ double s[RED_T];
+    double acc = OP == 0 ? 0.0 : -INFINITY;
+    for (int k = threadIdx.x; k < RED_BLOCKS; k += RED_T)
+        acc = OP == 0 ? acc + part[k] : fmax(acc, part[k]);
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = RED_T / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            s[threadIdx.x] = OP == 0 ? s[threadIdx.x] + s[threadIdx.x + w]
+                                     : fmax(s[threadIdx.x], s[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = OP == 0 ? s[0] * scale : s[0];
+}
+
+static int reduce_impl(rmt_ctx *ctx, int op, const double *a, const double *b, long n,
+                       double *out, double scale) {
+    if (op == 0) {
+        k_reduce_p1<0><<<RED_BLOCKS, RED_T, 0, ctx->stream>>>(a, b, n, ctx->red);
+        k_reduce_p2<0><<<1, RED_T, 0, ctx->stream>>>(ctx->red, out, scale);
+    } else if (op == 1) {
+        k_reduce_p1<1><<<RED_BLOCKS, RED_T, 0, ctx->stream>>>(a, b, n, ctx->red);
+        k_reduce_p2<1><<<1, RED_T, 0, ctx->stream>>>(ctx->red, out, scale);
+    } else {
+        k_reduce_p1<2><<<RED_BLOCKS, RED_T, 0, ctx->stream>>>(a, b, n, ctx->red);
+        k_reduce_p2<1><<<1, RED_T, 0, ctx->stream>>>(ctx->red, out, scale);
+    }
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int reduce_sum(rmt_ctx *ctx, const double *x, long n, double *o) { return reduce_impl(ctx, 0, x, x, n, o, 1.0); }
+int reduce_max(rmt_ctx *ctx, const double *x, long n, double *o) { return reduce_impl(ctx, 1, x, x, n, o, 1.0); }
+int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double *o) {
+    return reduce_impl(ctx, 2, a, b, n, o, 1.0);
+}
+int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *o) {
+    return reduce_impl(ctx, 0, x, x, n, o, 1.0 / (double)n);
+}
+int read_scalar(rmt_ctx *ctx, const double *dev, double *host) {
+    RMT_HIP(hipMemcpyAsync(host, dev, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    return RMT_OK;
+}
+
+// ------------------------------------------------------------------ FD helpers ----
+__global__ void k_grad_x(const double *__restrict__ f, int ny, int nx, double h2,
+                         double *__restrict__ out) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int i = (int)(c % nx);
+    out[c] = grad2(f + c, 1, i, nx, h2);
+}
+__global__ void k_grad_y(const double *__restrict__ f, int ny, int nx, double h2,
+                         double *__restrict__ out) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    out[c] = grad2(f + c, nx, j, ny, h2);
+}
+__global__ void k_upwind(const double *__restrict__ f, const double *__restrict__ vel, int ny,
+                         int nx, double h, int axis, double *__restrict__ out) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    out[c] = axis == 1 ? upwind3(f + c, 1, i, nx, vel[c], h) : upwind3(f + c, nx, j, ny, vel[c], h);
+}
+
+// ---------------------------------------------------------- interpolation / SL ----
+__global__ void k_bilinear(const double *__restrict__ u, const double *__restrict__ xq,
+                           const double *__restrict__ yq, long nq, double dx, double dy, int nx,
+                           int ny, double *__restrict__ out) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < nq) out[k] = bilinear(u, xq[k], yq[k], dx, dy, nx, ny);
+}
+__global__ void k_sl_rk4(const double *__restrict__ q, const double *__restrict__ a,
+                         const double *__restrict__ b, const double *__restrict__ X,
+                         const double *__restrict__ Y, int ny, int nx, double dt, double dx,
+                         double dy, double *__restrict__ out) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    double xb, yb;
+    sl_backtrace(a, b, X[c], Y[c], dt, dx, dy, nx, ny, xb, yb);
+    out[c] = bilinear(q, xb, yb, dx, dy, nx, ny);
+}
+__global__ void k_all_finite2(const double *__restrict__ a, const double *__restrict__ b, long n,
+                              int *bad) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    bool ok = true;
+    for (; k < n; k += (long)gridDim.x * blockDim.x) ok &= isfinite(a[k]) && isfinite(b[k]);
+    if (!ok) atomicOr(bad, 1);
+}
+__global__ void k_phi_disc(const double *__restrict__ X1, const double *__restrict__ X2, long n,
+                           double x0, double y0, double R, double *__restrict__ phi) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < n) phi[k] = disc_phi(X1[k], X2[k], x0, y0, R);
+}
+
+// ------------------------------------------------------------------------ WENO5 ----
+__global__ void k_weno5_rhs(const double *__restrict__ q, const double *__restrict__ a,
+                            const double *__restrict__ b, int ny, int nx, double dx, double dy,
+                            const double *__restrict__ phi, double w_cut,
+                            double *__restrict__ rhs) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    double r = 0.0;
+    if (j >= 2 && j < ny - 2 && i >= 2 && i < nx - 2 && !(phi[c] > w_cut)) {
+        double u = a[c], v = b[c];
+        double dqdx = weno5_diff(q + c, 1, i, nx, u) / dx;
+        double dqdy = weno5_diff(q + c, nx, j, ny, v) / dy;
+        r = -(u * dqdx + v * dqdy);
+    }
+    rhs[c] = r;
+}
+// SSP-RK3 stage combinations (functions.py:407-413); stage 0: q + dt r,
+// stage 1: 0.75 q + 0.25 (q1 + dt r), stage 2: (1/3) q + (2/3) (q2 + dt r).
+__global__ void k_ssprk3_combine(const double *__restrict__ q, const double *__restrict__ qs,
+                                 const double *__restrict__ r, long n, double dt, int stage,
+                                 double *__restrict__ out) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    if (stage == 0) out[k] = q[k] + dt * r[k];
+    else if (stage == 1) out[k] = 0.75 * q[k] + 0.25 * (qs[k] + dt * r[k]);
+    else out[k] = (1.0 / 3.0) * q[k] + (2.0 / 3.0) * (qs[k] + dt * r[k]);
+}
+
+// ------------------------------------------------------------------ solid stress ----
+__global__ void k_solid_stress(const double *__restrict__ X1, const double *__restrict__ X2,
+                               const double *__restrict__ phi, int ny, int nx, double dx,
+                               double dy, double mu_s, double kappa, double w_cut, double clamp,
+                               int iso, double *__restrict__ sxx, double *__restrict__ sxy,
+                               double *__restrict__ syy, double *__restrict__ J) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    Stress s{0.0, 0.0, 0.0, 1.0};
+    if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1)
+        solid_stress_cell(X1, X2, phi, c, nx, dx, dy, mu_s, kappa, w_cut, clamp, iso != 0, s);
+    sxx[c] = s.sxx; sxy[c] = s.sxy; syy[c] = s.syy; J[c] = s.J;
+}
+__global__ void k_heaviside(const double *__restrict__ x, long n, double w_t,
+                            double *__restrict__ H) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < n) H[k] = heaviside(x[k], w_t);
+}
+
+// ----------------------------------------------------------------------- BCs ----
+__global__ void k_apply_bc(int kind, double lid, double *u, double *v, int ny, int nx) {
+    // one thread per boundary cell; reads only interior (never-written) neighbours
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    if (!(i == 0 || i == nx - 1 || j == 0 || j == ny - 1)) return;
+    auto ru = [&](int jj, int ii) { return u[(long)jj * nx + ii]; };
+    auto rv = [&](int jj, int ii) { return v[(long)jj * nx + ii]; };
+    double uu, vv;
+    bc_value(kind, lid, j, i, ny, nx, ru, rv, uu, vv);   // edge cells read interior cells only
+    u[c] = uu; v[c] = vv;
+}
+
+// -------------------------------------------------------------------- projection ----
+__global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
+                                const double *__restrict__ p, int ny, int nx, double d_f,
+                                double dx, double dy, double *__restrict__ divU) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) { divU[c] = 0.0; return; }
+    const double h2x = 2.0 * dx, h2y = 2.0 * dy;
+    double gxl = grad2(p + c - 1, 1, i - 1, nx, h2x), gxc = grad2(p + c, 1, i, nx, h2x),
+           gxr = grad2(p + c + 1, 1, i + 1, nx, h2x);
+    double gyd = grad2(p + c - nx, nx, j - 1, ny, h2y), gyc = grad2(p + c, nx, j, ny, h2y),
+           gyu = grad2(p + c + nx, nx, j + 1, ny, h2y);
+    double ue = 0.5 * (a[c] + a[c + 1]) - d_f * ((p[c + 1] - p[c]) / dx - 0.5 * (gxc + gxr));
+    double uw = 0.5 * (a[c - 1] + a[c]) - d_f * ((p[c] - p[c - 1]) / dx - 0.5 * (gxl + gxc));
+    double vn = 0.5 * (b[c] + b[c + nx]) - d_f * ((p[c + nx] - p[c]) / dy - 0.5 * (gyc + gyu));
+    double vs = 0.5 * (b[c - nx] + b[c]) - d_f * ((p[c] - p[c - nx]) / dy - 0.5 * (gyd + gyc));
+    divU[c] = (ue - uw) / dx + (vn - vs) / dy;
+}
+__global__ void k_divergence_central(const double *__restrict__ a, const double *__restrict__ b,
+                                     int ny, int nx, double dx, double dy,
+                                     double *__restrict__ divU) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    divU[c] = (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1)
+                  ? 0.0
+                  : (a[c + 1] - a[c - 1]) / (2 * dx) + (b[c + nx] - b[c - nx]) / (2 * dy);
+}
+// functions.py:1073-1089 at one cell.
+__device__ __forceinline__ void pgrad_cell(const double *__restrict__ p, long c, int j, int i,
+                                           int ny, int nx, double dx, double dy, double &gx,
+                                           double &gy) {
+    const double *row = p + (c - i), *col = p + i;
+    gx = 0.0; gy = 0.0;
+    if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1) {
+        gx = (p[c + 1] - p[c - 1]) / (2 * dx);
+        gy = (p[c + nx] - p[c - nx]) / (2 * dy);
+    }
+    if (i == 0) gx = (-3.0 * row[0] + 4.0 * row[1] - row[2]) / (2.0 * dx);
+    if (i == nx - 1) gx = (3.0 * row[nx - 1] - 4.0 * row[nx - 2] + row[nx - 3]) / (2.0 * dx);
+    if (j == 0) gy = (-3.0 * col[0] + 4.0 * col[nx] - col[2L * nx]) / (2.0 * dy);
+    if (j == ny - 1)
+        gy = (3.0 * col[(long)(ny - 1) * nx] - 4.0 * col[(long)(ny - 2) * nx] +
+              col[(long)(ny - 3) * nx]) / (2.0 * dy);
+}
+__global__ void k_pressure_gradient(const double *__restrict__ p, int ny, int nx, double dx,
+                                    double dy, double *__restrict__ gx, double *__restrict__ gy) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    double x, y;
+    pgrad_cell(p, c, (int)(c / nx), (int)(c % nx), ny, nx, dx, dy, x, y);
+    gx[c] = x; gy[c] = y;
+}
+// functions.py:1330-1362 after the solve: a = a* - (dt/rho) dpc/dx, BC, p = p_prev + pc,
+// with pc = p_raw - mean(p_raw) (mean on device).  Writes p before its own mean removal.
+__global__ void k_project_correct(const double *__restrict__ a_s, const double *__restrict__ b_s,
+                                  const double *__restrict__ pc, const double *__restrict__ p_prev,
+                                  int ny, int nx, double dx, double dy, double dt_rho, int bc,
+                                  double lid, double *__restrict__ a, double *__restrict__ b,
+                                  double *__restrict__ p) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    auto ru = [&](int jj, int ii) {
+        long cc = (long)jj * nx + ii; double gx, gy;
+        pgrad_cell(pc, cc, jj, ii, ny, nx, dx, dy, gx, gy);
+        return a_s[cc] - dt_rho * gx;
+    };
+    auto rv = [&](int jj, int ii) {
+        long cc = (long)jj * nx + ii; double gx, gy;
+        pgrad_cell(pc, cc, jj, ii, ny, nx, dx, dy, gx, gy);
+        return b_s[cc] - dt_rho * gy;
+    };
+    double uu, vv;
+    bc_value(bc, lid, j, i, ny, nx, ru, rv, uu, vv);
+    a[c] = uu; b[c] = vv;
+    p[c] = p_prev ? p_prev[c] + pc[c] : pc[c];
+}
+__global__ void k_sub_scalar(double *__restrict__ x, long n, const double *__restrict__ s) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < n) x[k] = x[k] - *s;
+}
+__global__ void k_scale_copy(const double *__restrict__ x, long n, double s,
+                             double *__restrict__ y) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < n) y[k] = s * x[k];
+}
+__global__ void k_div_scalar(const double *__restrict__ x, long n, double s,
+                             double *__restrict__ y) {
+    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < n) y[k] = x[k] / s;
+}
+}  // namespace rmt
+
+using namespace rmt;
+
+// ======================================================================== C ABI ====
+extern "C" {
+
+const char *rmt_last_error(void) { return g_err.c_str(); }
+int rmt_version(void) { return 1; }
+
+int rmt_ctx_create(int ny, int nx, int device, void *stream, rmt_ctx **out) {
+    RMT_CHECK(out && ny >= 5 && nx >= 5, RMT_EINVAL, "rmt_ctx_create: need ny, nx >= 5");
+    RMT_HIP(hipSetDevice(device));
+    rmt_ctx *c = new rmt_ctx;
+    c->ny = ny; c->nx = nx; c->device = device; c->stream = (hipStream_t)stream;
+    RMT_HIP(hipMalloc(&c->red, (RED_BLOCKS + 64) * sizeof(double)));
+    *out = c;
+    return RMT_OK;
+}
+int rmt_ctx_set_stream(rmt_ctx *ctx, void *stream) {
+    RMT_CHECK(ctx, RMT_EINVAL, "null ctx");
+    ctx->stream = (hipStream_t)stream;
+    return RMT_OK;
+}
+int rmt_ctx_sync(rmt_ctx *ctx) {
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    return RMT_OK;
+}
+int rmt_ctx_destroy(rmt_ctx *ctx) {
+    if (!ctx) return RMT_OK;
+    hipSetDevice(ctx->device);
+    if (ctx->scratch) hipFree(ctx->scratch);
+    if (ctx->red) hipFree(ctx->red);
+    if (ctx->bytes) hipFree(ctx->bytes);
+    if (ctx->dct) dct_destroy(ctx->dct);
+    delete ctx;
+    return RMT_OK;
+}
+
+#define N_CELLS ((long)ctx->ny * ctx->nx)
+#define LAUNCH1D(n) grid1d((n), 256), 256, 0, ctx->stream
+
+int rmt_grad_x_2nd(rmt_ctx *ctx, const double *f, double h, double *out) {
+    k_grad_x<<<LAUNCH1D(N_CELLS)>>>(f, ctx->ny, ctx->nx, 2 * h, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_grad_y_2nd(rmt_ctx *ctx, const double *f, double h, double *out) {
+    k_grad_y<<<LAUNCH1D(N_CELLS)>>>(f, ctx->ny, ctx->nx, 2 * h, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_diff_upwind_3rd(rmt_ctx *ctx, const double *f, const double *vel, double h, int axis,
+                        double *out) {
+    RMT_CHECK(axis == 0 || axis == 1, RMT_EINVAL, "diff_upwind_3rd: axis must be 0 or 1");
+    k_upwind<<<LAUNCH1D(N_CELLS)>>>(f, vel, ctx->ny, ctx->nx, h, axis, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_bilinear_interpolate(rmt_ctx *ctx, const double *u, const double *xq, const double *yq,
+                             long nq, double dx, double dy, double *out) {
+    if (nq <= 0) return RMT_OK;
+    k_bilinear<<<LAUNCH1D(nq)>>>(u, xq, yq, nq, dx, dy, ctx->nx, ctx->ny, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_advect_sl_rk4(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                      const double *X, const double *Y, double dt, double dx, double dy,
+                      double *out) {
+    k_sl_rk4<<<LAUNCH1D(N_CELLS)>>>(q, a, b, X, Y, ctx->ny, ctx->nx, dt, dx, dy, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_all_finite2(rmt_ctx *ctx, const double *a, const double *b, int *finite) {
+    RMT_TRY(ensure_bytes(ctx, 64));
+    int *bad = (int *)ctx->bytes;
+    RMT_HIP(hipMemsetAsync(bad, 0, sizeof(int), ctx->stream));
+    k_all_finite2<<<1024, 256, 0, ctx->stream>>>(a, b, N_CELLS, bad);
+    int h = 0;
+    RMT_HIP(hipMemcpyAsync(&h, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    *finite = !h;
+    return RMT_OK;
+}
+int rmt_rebuild_phi_disc(rmt_ctx *ctx, const double *X1, const double *X2, double x0, double y0,
+                         double R, double *phi) {
+    k_phi_disc<<<LAUNCH1D(N_CELLS)>>>(X1, X2, N_CELLS, x0, y0, R, phi);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_weno5_rhs(rmt_ctx *ctx, const double *q, const double *a, const double *b, double dx,
+                  double dy, const double *phi, double w_cut, double *rhs) {
+    k_weno5_rhs<<<LAUNCH1D(N_CELLS)>>>(q, a, b, ctx->ny, ctx->nx, dx, dy, phi, w_cut, rhs);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_advect_weno5_rk3(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                         double dx, double dy, double dt, const double *phi, double w_cut,
+                         double *out) {
+    long n = N_CELLS;
+    RMT_TRY(ensure_scratch(ctx, 3 * n * sizeof(double)));
+    double *r = ctx->scratch, *q1 = r + n, *q2 = q1 + n;
+    RMT_TRY(rmt_weno5_rhs(ctx, q, a, b, dx, dy, phi, w_cut, r));
+    k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q, r, n, dt, 0, q1);
+    RMT_TRY(rmt_weno5_rhs(ctx, q1, a, b, dx, dy, phi, w_cut, r));
+    k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q1, r, n, dt, 1, q2);
+    RMT_TRY(rmt_weno5_rhs(ctx, q2, a, b, dx, dy, phi, w_cut, r));
+    k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q2, r, n, dt, 2, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_solid_cauchy_stress(rmt_ctx *ctx, const double *X1, const double *X2, double dx,
+                            double dy, double mu_s, double kappa, const double *phi,
+                            double w_cut, double detg_clamp, int isochoric, double *sxx,
+                            double *sxy, double *syy, double *J) {
+    k_solid_stress<<<LAUNCH1D(N_CELLS)>>>(X1, X2, phi, ctx->ny, ctx->nx, dx, dy, mu_s, kappa,
+                                          w_cut, detg_clamp, isochoric, sxx, sxy, syy, J);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_smoothed_heaviside(rmt_ctx *ctx, const double *x, long n, double w_t, double *H) {
+    if (n <= 0) return RMT_OK;
+    k_heaviside<<<LAUNCH1D(n)>>>(x, n, w_t, H);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_apply_velocity_bc(rmt_ctx *ctx, int bc_kind, double lid, double *u, double *v) {
+    RMT_CHECK(bc_kind >= 0 && bc_kind <= 2, RMT_EINVAL, "unknown velocity bc kind");
+    k_apply_bc<<<LAUNCH1D(N_CELLS)>>>(bc_kind, lid, u, v, ctx->ny, ctx->nx);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_divergence_rc(rmt_ctx *ctx, const double *a, const double *b, const double *p,
+                      double d_f, double dx, double dy, double *divU) {
+    k_divergence_rc<<<LAUNCH1D(N_CELLS)>>>(a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_divergence_central(rmt_ctx *ctx, const double *a, const double *b, double dx,
+                           double dy, double *divU) {
+    k_divergence_central<<<LAUNCH1D(N_CELLS)>>>(a, b, ctx->ny, ctx->nx, dx, dy, divU);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_pressure_gradient(rmt_ctx *ctx, const double *p, double dx, double dy, double *gx,
+                          double *gy) {
+    k_pressure_gradient<<<LAUNCH1D(N_CELLS)>>>(p, ctx->ny, ctx->nx, dx, dy, gx, gy);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_solve_poisson_dct(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p) {
+    return dct_solve(ctx, rhs, dx, dy, p);
+}
+int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_star,
+                            double dx, double dy, double dt, double rho, int bc_kind,
+                            double lid, const double *p_prev, double *a, double *b, double *p) {
+    RMT_CHECK(bc_kind >= 0 && bc_kind <= 2, RMT_EINVAL, "unknown velocity bc kind");
+    long n = N_CELLS;
+    RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
+    double *rhs = ctx->scratch, *pc = rhs + n;
+    // functions.py:1292-1295 + :1331: rhs = rho * divU / dt, d_f = dt / mean(rho)
+    if (p_prev) RMT_TRY(rmt_divergence_rc(ctx, a_star, b_star, p_prev, dt / rho, dx, dy, rhs));
+    else RMT_TRY(rmt_divergence_central(ctx, a_star, b_star, dx, dy, rhs));
+    k_scale_copy<<<LAUNCH1D(n)>>>(rhs, n, rho, rhs);
+    k_div_scalar<<<LAUNCH1D(n)>>>(rhs, n, dt, rhs);
+    RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc));
+    k_project_correct<<<LAUNCH1D(n)>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy,
+                                       dt / rho, bc_kind, lid, a, b, p);
+    RMT_LAUNCHED();
+    double *mean = ctx->red + RED_BLOCKS;
+    RMT_TRY(reduce_mean(ctx, p, n, mean));
+    k_sub_scalar<<<LAUNCH1D(n)>>>(p, n, mean);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_compute_timestep(rmt_ctx *ctx, const double *a, const double *b, double dx, double dy,
+                         double CFL, double dt_min_cap, double mu_s, double rho_s, double gamma,
+                         double rho_f, double mu_f, double eta_s, double kappa, double *dt) {
+    (void)dy;
+    RMT_TRY(reduce_maxsq2(ctx, a, b, N_CELLS, ctx->red + RED_BLOCKS));
+    double m2;
+    RMT_TRY(read_scalar(ctx, ctx->red + RED_BLOCKS, &m2));
+    // functions.py:165-192 on the host (scalars); max(sqrt(.)) == sqrt(max(.))
+    double cs = std::sqrt((kappa + mu_s * 4.0 / 3.0) / (rho_s + 1e-12));
+    double d = CFL * dx / (cs + 1e-14);
+    d = std::fmin(d, CFL * dx / (std::sqrt(m2) + 1e-6));
+    if (gamma > 1e-12) {
+        double ra = 0.5 * (rho_s + rho_f);
+        d = std::fmin(d, std::sqrt((ra * std::pow(dx, 3.0)) / (2 * M_PI * gamma)) * 0.5);
+    } else {
+        d = std::fmin(d, 1.0);
+    }
+    double mu_max = std::fmax(mu_f, eta_s), rho_min = std::fmin(rho_s, rho_f);
+    d = std::fmin(d, (mu_max > 1e-12 && rho_min > 1e-12) ? CFL * rho_min * std::pow(dx, 2.0) / (4.0 * mu_max)
+                                                         : 1.0);
+    *dt = std::fmin(d, dt_min_cap);
+    return RMT_OK;
+}
+}  // extern "C"

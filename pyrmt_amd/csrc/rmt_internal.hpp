@@ -1,0 +1,290 @@
+// rmt_internal.hpp -- shared state and per-cell device arithmetic of librmt.
+//
+// Every __device__ formula below keeps the reference's floating-point operation order
+// (Python evaluates left to right; `c * x * y` is `(c*x)*y`) and is compiled with
+// -ffp-contract=off, so kernels built from them reproduce the CPU reference bit for bit
+// wherever no transcendental function or FFT is involved.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rocfft/rocfft.h>
+#include <cmath>
+#include <cstdint>
+#include <string>
+#include "../../include/rmt.h"
+
+namespace rmt {
+
+// ---------------------------------------------------------------- error plumbing --
+void set_error(const std::string &msg);
+#define RMT_HIP(call)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            ::rmt::set_error(std::string(#call) + ": " + hipGetErrorString(e_));        \
+            return RMT_EDEVICE;                                                         \
+        }                                                                               \
+    } while (0)
+// after a launch: report the failing host line (file:line names the kernel launched above)
+#define RMT_LAUNCHED()                                                                  \
+    do {                                                                                \
+        hipError_t e_ = hipGetLastError();                                              \
+        if (e_ != hipSuccess) {                                                         \
+            ::rmt::set_error(std::string(__FILE__) + ":" + std::to_string(__LINE__) +   \
+                             " launch: " + hipGetErrorString(e_));                      \
+            return RMT_EDEVICE;                                                         \
+        }                                                                               \
+    } while (0)
+#define RMT_CHECK(cond, code, msg)                                                      \
+    do {                                                                                \
+        if (!(cond)) { ::rmt::set_error(msg); return (code); }                          \
+    } while (0)
+#define RMT_TRY(expr)                                                                   \
+    do { int s_ = (expr); if (s_ != RMT_OK) return s_; } while (0)
+
+struct DctPlan;  // poisson.hip
+
+}  // namespace rmt
+
+struct rmt_ctx {
+    int ny = 0, nx = 0, device = 0;
+    hipStream_t stream = nullptr;
+    // scratch (grown on demand, owned)
+    double *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    double *red = nullptr;      // reduction partials (host-visible results copied out)
+    unsigned char *bytes = nullptr;
+    size_t bytes_len = 0;
+    rmt::DctPlan *dct = nullptr;
+    // optional kernel timers (rmt_sim profiling): [0,1] around the four RK4 stage kernels,
+    // [2,3] around the extrapolation sweep kernel
+    bool prof = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+namespace rmt {
+
+int ensure_scratch(rmt_ctx *ctx, size_t bytes);    // >= bytes of double scratch
+int ensure_bytes(rmt_ctx *ctx, size_t bytes);      // >= bytes of byte scratch
+inline unsigned grid1d(long n, int block) { return (unsigned)((n + block - 1) / block); }
+
+// ------------------------------------------------------------- device arithmetic --
+// utils.py:4-25: second-order gradient along a line of length n (stride s) at index k;
+// f points at element k itself (works on global rows/columns and on LDS tiles).
+__device__ __forceinline__ double grad2(const double *f, long s, int k, int n, double h2) {
+    if (k == 0) return (-3 * f[0] + 4 * f[s] - f[2 * s]) / h2;
+    if (k == n - 1) return (3 * f[0] - 4 * f[-s] + f[-2 * s]) / h2;
+    return (f[s] - f[-s]) / h2;
+}
+
+// utils.py:61-114 diff_upwind_3rd along a line; f points at element k.
+__device__ __forceinline__ double upwind3(const double *f, long s, int k, int n, double vel,
+                                          double h) {
+    if (k >= 2 && k < n - 2) {
+        if (vel > 0) return (2 * f[s] + 3 * f[0] - 6 * f[-s] + f[-2 * s]) / (6 * h);
+        return (-f[2 * s] + 6 * f[s] - 3 * f[0] - 2 * f[-s]) / (6 * h);
+    }
+    if (vel > 0 && k > 0) return (f[0] - f[-s]) / h;
+    if (vel <= 0 && k < n - 1) return (f[s] - f[0]) / h;
+    if (k > 0) return (f[0] - f[-s]) / h;
+    if (k < n - 1) return (f[s] - f[0]) / h;
+    return 0.0;
+}
+
+// interpolators.py:4-61 bilinear_interpolate at one query point.
+__device__ __forceinline__ double bilinear(const double *__restrict__ u, double xq, double yq,
+                                           double dx, double dy, int nx, int ny) {
+    double x = xq / dx, y = yq / dy;
+    if (!(isfinite(x) && isfinite(y))) return __builtin_nan("");
+    if (x < 0.0) x = 0.0; else if (x > nx - 1.0) x = nx - 1.0;
+    if (y < 0.0) y = 0.0; else if (y > ny - 1.0) y = ny - 1.0;
+    int ix = (int)floor(x), iy = (int)floor(y);
+    if (ix >= nx - 1) ix = nx - 2;
+    if (iy >= ny - 1) iy = ny - 2;
+    double fx = x - ix, fy = y - iy;
+    const double *r0 = u + (long)iy * nx, *r1 = r0 + nx;
+    return (1 - fx) * (1 - fy) * r0[ix] + fx * (1 - fy) * r0[ix + 1] +
+           (1 - fx) * fy * r1[ix] + fx * fy * r1[ix + 1];
+}
+
+// functions.py:194-227: RK4 backtrace of one point; returns the foot (xb, yb).
+__device__ __forceinline__ void sl_backtrace(const double *__restrict__ a,
+                                             const double *__restrict__ b, double x, double y,
+                                             double dt, double dx, double dy, int nx, int ny,
+                                             double &xb, double &yb) {
+    const double hdt = 0.5 * dt, dt6 = dt / 6.0;
+    double k1x = bilinear(a, x, y, dx, dy, nx, ny), k1y = bilinear(b, x, y, dx, dy, nx, ny);
+    double x2 = x - hdt * k1x, y2 = y - hdt * k1y;
+    double k2x = bilinear(a, x2, y2, dx, dy, nx, ny), k2y = bilinear(b, x2, y2, dx, dy, nx, ny);
+    double x3 = x - hdt * k2x, y3 = y - hdt * k2y;
+    double k3x = bilinear(a, x3, y3, dx, dy, nx, ny), k3y = bilinear(b, x3, y3, dx, dy, nx, ny);
+    double x4 = x - dt * k3x, y4 = y - dt * k3y;
+    double k4x = bilinear(a, x4, y4, dx, dy, nx, ny), k4y = bilinear(b, x4, y4, dx, dy, nx, ny);
+    xb = x - dt6 * (k1x + 2 * k2x + 2 * k3x + k4x);
+    yb = y - dt6 * (k1y + 2 * k2y + 2 * k3y + k4y);
+}
+
+// benchmarks/common.py:55-57 disc signed distance, numpy order: sqrt(dx*dx + dy*dy) - R.
+__device__ __forceinline__ double disc_phi(double X1, double X2, double x0, double y0,
+                                           double R) {
+    double a = X1 - x0, b = X2 - y0;
+    return sqrt(a * a + b * b) - R;
+}
+
+// functions.py:660-671 smoothed_heaviside.
+__device__ __forceinline__ double heaviside(double v, double w_t) {
+    const double inv_wt = 1.0 / w_t, inv_pi = 1.0 / M_PI;
+    double h = 0.5 * (1.0 + v * inv_wt + inv_pi * sin(M_PI * v * inv_wt));
+    if (v > w_t) h = 1.0;
+    if (v < -w_t) h = 0.0;
+    return h;
+}
+
+// functions.py:545-658 solid_cauchy_stress at interior cell c (neighbour offsets 1, nx).
+struct Stress { double sxx, sxy, syy, J; };
+__device__ __forceinline__ bool solid_stress_cell(const double *__restrict__ X1,
+                                                  const double *__restrict__ X2,
+                                                  const double *__restrict__ phi, long c,
+                                                  long nx, double dx, double dy, double mu_s,
+                                                  double kappa, double w_cut, double clamp,
+                                                  bool iso, Stress &out) {
+    out = {0.0, 0.0, 0.0, 1.0};
+    double pc = phi[c];
+    bool in_band = w_cut > 0.0 ? (pc < w_cut) : (pc <= 0.0);
+    if (!in_band) return false;
+    const double inv_2dx = 1.0 / (2.0 * dx), inv_2dy = 1.0 / (2.0 * dy);
+    long l = c - 1, r = c + 1, d = c - nx, u = c + nx;
+    double g11, g21, g12, g22;
+    if (w_cut > 0.0) {
+        g11 = (X1[r] - X1[l]) * inv_2dx; g21 = (X2[r] - X2[l]) * inv_2dx;
+        g12 = (X1[u] - X1[d]) * inv_2dy; g22 = (X2[u] - X2[d]) * inv_2dy;
+    } else {
+        bool lf = phi[l] > 0.0, rf = phi[r] > 0.0;
+        if (lf && !rf) { g11 = (X1[r] - X1[c]) / dx; g21 = (X2[r] - X2[c]) / dx; }
+        else if (rf && !lf) { g11 = (X1[c] - X1[l]) / dx; g21 = (X2[c] - X2[l]) / dx; }
+        else { g11 = (X1[r] - X1[l]) * inv_2dx; g21 = (X2[r] - X2[l]) * inv_2dx; }
+        bool bf = phi[d] > 0.0, tf = phi[u] > 0.0;
+        if (bf && !tf) { g12 = (X1[u] - X1[c]) / dy; g22 = (X2[u] - X2[c]) / dy; }
+        else if (tf && !bf) { g12 = (X1[c] - X1[d]) / dy; g22 = (X2[c] - X2[d]) / dy; }
+        else { g12 = (X1[u] - X1[d]) * inv_2dy; g22 = (X2[u] - X2[d]) * inv_2dy; }
+    }
+    double detG = g11 * g22 - g12 * g21;
+    if (fabs(detG) < 1e-10) return false;
+    if (clamp > 0.0) {
+        double lo = 1.0 / clamp;
+        if (detG < lo) detG = lo; else if (detG > clamp) detG = clamp;
+    }
+    double f11 = g22 / detG, f12 = -g12 / detG, f21 = -g21 / detG, f22 = g11 / detG;
+    double b11 = f11 * f11 + f12 * f12, b12 = f11 * f21 + f12 * f22, b22 = f21 * f21 + f22 * f22;
+    double jv = 1.0 / detG;
+    double vol = kappa * (jv - 1.0);
+    if (iso) {
+        double trh = 0.5 * (b11 + b22), jm2 = 1.0 / (jv * jv);
+        out = {mu_s * jm2 * (b11 - trh) + vol, mu_s * jm2 * b12, mu_s * jm2 * (b22 - trh) + vol, jv};
+    } else {
+        out = {mu_s * b11 + vol, mu_s * b12, mu_s * b22 + vol, jv};
+    }
+    return true;
+}
+
+// functions.py:256-318 WENO5 reconstructions (Jiang-Shu, eps 1e-6; x**2 as x*x like Numba).
+__device__ __forceinline__ double weno5_combine(double r0, double r1, double r2, double s0,
+                                                double t0, double s1, double t1, double s2,
+                                                double t2) {
+    const double eps = 1.0e-6;
+    double b0 = (13.0 / 12.0) * (s0 * s0) + (1.0 / 4.0) * (t0 * t0);
+    double b1 = (13.0 / 12.0) * (s1 * s1) + (1.0 / 4.0) * (t1 * t1);
+    double b2 = (13.0 / 12.0) * (s2 * s2) + (1.0 / 4.0) * (t2 * t2);
+    double e0 = eps + b0, e1 = eps + b1, e2 = eps + b2;
+    double a0 = 0.1 / (e0 * e0), a1 = 0.6 / (e1 * e1), a2 = 0.3 / (e2 * e2);
+    double as = a0 + a1 + a2;
+    return (a0 / as) * r0 + (a1 / as) * r1 + (a2 / as) * r2;
+}
+__device__ __forceinline__ double weno5_left(double vm2, double vm1, double v0, double vp1,
+                                             double vp2) {
+    return weno5_combine((2.0 * vm2 - 7.0 * vm1 + 11.0 * v0) / 6.0,
+                         (-vm1 + 5.0 * v0 + 2.0 * vp1) / 6.0,
+                         (2.0 * v0 + 5.0 * vp1 - vp2) / 6.0,
+                         vm2 - 2.0 * vm1 + v0, vm2 - 4.0 * vm1 + 3.0 * v0,
+                         vm1 - 2.0 * v0 + vp1, vm1 - vp1,
+                         v0 - 2.0 * vp1 + vp2, 3.0 * v0 - 4.0 * vp1 + vp2);
+}
+__device__ __forceinline__ double weno5_right(double vm1, double v0, double vp1, double vp2,
+                                              double vp3) {
+    return weno5_combine((2.0 * vp3 - 7.0 * vp2 + 11.0 * vp1) / 6.0,
+                         (-vp2 + 5.0 * vp1 + 2.0 * v0) / 6.0,
+                         (2.0 * vp1 + 5.0 * v0 - vm1) / 6.0,
+                         vp3 - 2.0 * vp2 + vp1, 3.0 * vp1 - 4.0 * vp2 + vp3,
+                         vp2 - 2.0 * vp1 + v0, vp2 - v0,
+                         vp1 - 2.0 * v0 + vm1, vp1 - 4.0 * v0 + 3.0 * vm1);
+}
+// functions.py:347-389: (q_{k+1/2} - q_{k-1/2}) along a line with domain-edge fallbacks;
+// f points at element k.
+__device__ __forceinline__ double weno5_diff(const double *f, long s, int k, int n, double vel) {
+#define F_(o) f[(long)(o) * s]
+    double qp, qm;
+    if (vel >= 0.0) {
+        qp = weno5_left(F_(-2), F_(-1), F_(0), F_(1), F_(2));
+        qm = k >= 3 ? weno5_left(F_(-3), F_(-2), F_(-1), F_(0), F_(1))
+                    : weno5_left(F_(-2), F_(-1), F_(0), F_(1), F_(2));
+    } else {
+        qp = k + 3 < n ? weno5_right(F_(-1), F_(0), F_(1), F_(2), F_(3))
+                       : weno5_left(F_(-2), F_(-1), F_(0), F_(1), F_(2));
+        qm = weno5_right(F_(-1), F_(0), F_(1), F_(2), k + 3 < n ? F_(3) : F_(n - 1 - k));
+    }
+#undef F_
+    return qp - qm;
+}
+
+// benchmarks/common.py:27-50: BC'd value of a stage velocity component at (j, i), given
+// the raw (pre-BC) component values through `raw(j, i)`.
+template <class RawU, class RawV>
+__device__ __forceinline__ void bc_value(int kind, double lid, int j, int i, int ny, int nx,
+                                         RawU rawu, RawV rawv, double &u, double &v) {
+    if (kind == RMT_BC_NOSLIP_LID) {
+        bool edge = (i == 0 || i == nx - 1 || j == 0 || j == ny - 1);
+        if (!edge) { u = rawu(j, i); v = rawv(j, i); return; }
+        v = 0.0;
+        u = (j == ny - 1 && i != 0 && i != nx - 1) ? lid : 0.0;
+    } else if (kind == RMT_BC_FREESLIP_BOX) {
+        if (i == 0 || i == nx - 1) u = 0.0;
+        else if (j == 0) u = rawu(1, i);
+        else if (j == ny - 1) u = rawu(ny - 2, i);
+        else u = rawu(j, i);
+        if (j == 0 || j == ny - 1) v = 0.0;
+        else if (i == 0) v = rawv(j, 1);
+        else if (i == nx - 1) v = rawv(j, nx - 2);
+        else v = rawv(j, i);
+    } else {
+        u = rawu(j, i); v = rawv(j, i);
+    }
+}
+
+// ------------------------------------------------------------------- reductions --
+constexpr int RED_BLOCKS = 1024, RED_T = 256;   // ctx->red holds RED_BLOCKS + 64 doubles
+int reduce_sum(rmt_ctx *ctx, const double *x, long n, double *dev_out);     // device scalar
+int reduce_max(rmt_ctx *ctx, const double *x, long n, double *dev_out);
+int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double *dev_out);
+int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *dev_out);
+int read_scalar(rmt_ctx *ctx, const double *dev, double *host);
+
+// --------------------------------------------------------------------- momentum --
+struct MomWork {                 // 8 planes + solid byte plane + flag
+    double *H, *rho, *k1u, *k1v, *k2u, *k2v, *accu, *accv;
+    unsigned char *solid;
+    int *any_solid;
+};
+int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
+                 const double *p, const double *X1, const double *X2, const double *phi,
+                 double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
+                 const MomWork &W);
+
+// ---------------------------------------------------------------------- poisson --
+int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
+              const double *dev_mean_sub = nullptr);
+void dct_destroy(DctPlan *);
+
+// ------------------------------------------------------------------ extrapolate --
+int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
+                double dy, int max_layers, double *X1o, double *X2o, const int *dev_skip = nullptr);
+
+}  // namespace rmt

@@ -1,0 +1,414 @@
+// sim.hip -- the RMT loop body of the reference drivers as one device-resident step.
+//
+// benchmarks/soft_disc_in_lid_driven.py:206-235 (configs 2/4), disc_in_taylor_green.py
+// :206-242 (config 3) and lid_driven_cavity.py:58-80 (config 1):
+//   dt = compute_timestep(u);  clip to t_end
+//   phi = rebuild(X1, X2); mask = phi <= 0
+//   X1, X2 = advect(X1, X2) * mask;  extrapolate(X1, X2, phi)
+//   phi = rebuild(X1, X2)
+//   u*, v* = momentum_step_rk4(...);  u, v, p = pressure_projection(u*, v*, p)
+//   diagnostics: centroid of phi <= 0, J min/max (+ KE, SE, dissipation)
+// State (u, v, p, X1, X2) stays in HBM; one host sync per step reads dt.
+#include "rmt_internal.hpp"
+#include <vector>
+
+namespace rmt {
+
+
+constexpr int DIAG_VALS = 10, DIAG_BLOCKS = 512, DIAG_T = 256;
+
+}  // namespace rmt
+
+struct rmt_sim {
+    rmt_ctx *ctx = nullptr;
+    rmt_sim_params P{};
+    double *xs = nullptr, *ys = nullptr;
+    // fields
+    double *u = nullptr, *v = nullptr, *p = nullptr, *X1 = nullptr, *X2 = nullptr;
+    double *phi = nullptr, *phi_pre = nullptr, *J = nullptr;
+    double *X1n = nullptr, *X2n = nullptr, *us = nullptr, *vs = nullptr;
+    double *sxx = nullptr, *sxy = nullptr, *syy = nullptr;
+    double *mw = nullptr;            // momentum workspace (8 planes)
+    unsigned char *mbytes = nullptr; // solid mask + flag
+    double *dscr = nullptr;          // diag partials + scalars
+    int *flag = nullptr;             // non-finite flag
+    double dt_const = 0, t = 0, integ = 0;
+    std::vector<rmt_diag> diag;
+    void *block = nullptr;
+    bool prof = false;
+    hipEvent_t pev[7] = {};
+    double ms[8] = {};
+    long calls[8] = {};
+};
+
+namespace rmt {
+
+// SL advection of (X1, X2) with the pre-advection level set and mask (one pass).
+__global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict__ X2,
+                         const double *__restrict__ a, const double *__restrict__ b,
+                         const double *__restrict__ xs, const double *__restrict__ ys, int ny,
+                         int nx, double dt, double dx, double dy, int shape, double x0, double y0,
+                         double R, double *__restrict__ X1n, double *__restrict__ X2n,
+                         double *__restrict__ phi_pre, int *bad) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    bool fin = isfinite(a[c]) && isfinite(b[c]);
+    if (__any(!fin) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+    double ph = disc_phi(X1[c], X2[c], x0, y0, R);
+    phi_pre[c] = ph;
+    double m = ph <= 0 ? 1.0 : 0.0;
+    double xb, yb;
+    sl_backtrace(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, xb, yb);
+    X1n[c] = bilinear(X1, xb, yb, dx, dy, nx, ny) * m;
+    X2n[c] = bilinear(X2, xb, yb, dx, dy, nx, ny) * m;
+}
+
+__global__ void k_sim_phi_mask(const double *__restrict__ X1, const double *__restrict__ X2,
+                               const double *__restrict__ a, const double *__restrict__ b,
+                               long n, double x0, double y0, double R,
+                               double *__restrict__ phi_pre, int *bad) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    bool fin = isfinite(a[c]) && isfinite(b[c]);
+    if (__any(!fin) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+    phi_pre[c] = disc_phi(X1[c], X2[c], x0, y0, R);
+}
+
+__global__ void k_mask_mul(double *__restrict__ X1, double *__restrict__ X2,
+                           const double *__restrict__ phi, long n) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    double m = phi[c] <= 0 ? 1.0 : 0.0;
+    X1[c] = X1[c] * m;
+    X2[c] = X2[c] * m;
+}
+
+// phi = rebuild(X1n, X2n) (functions.py:1366) fused with the copy of the extrapolated
+// map back into the state planes (keeps rmt_sim_field pointers stable).
+__global__ void k_phi_rebuild(const double *__restrict__ X1n, const double *__restrict__ X2n,
+                              long n, int shape, double x0, double y0, double R,
+                              double *__restrict__ phi, double *__restrict__ X1,
+                              double *__restrict__ X2) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    if (shape == RMT_SHAPE_DISC) {
+        double a = X1n[c], b = X2n[c];
+        X1[c] = a; X2[c] = b;
+        phi[c] = disc_phi(a, b, x0, y0, R);
+    } else {
+        phi[c] = 1.0;
+    }
+}
+
+// dt on device-ready scalars: returned to the host (one sync per step).
+__global__ void k_dt(const double *m2, double dt_const, double cfl, double dx, double *out) {
+    *out = fmin(dt_const, cfl * dx / (sqrt(*m2) + 1e-6));
+}
+
+// output.py:41-134 strain-energy density at one cell (4-cell edge-padded central grads).
+__device__ __forceinline__ double se_density(const double *__restrict__ X1,
+                                             const double *__restrict__ X2, long c, int j, int i,
+                                             int ny, int nx, double dx, double dy, double mu_s,
+                                             double kappa) {
+    long cl = i > 0 ? c - 1 : c, cr = i < nx - 1 ? c + 1 : c;
+    long cd = j > 0 ? c - nx : c, cu = j < ny - 1 ? c + nx : c;
+    double G11 = (X1[cr] - X1[cl]) / (2 * dx), G12 = (X1[cu] - X1[cd]) / (2 * dy);
+    double G21 = (X2[cr] - X2[cl]) / (2 * dx), G22 = (X2[cu] - X2[cd]) / (2 * dy);
+    double detG = G11 * G22 - G12 * G21;
+    if (!(fabs(detG) > 1e-10)) return 0.0;
+    double F11 = G22 / detG, F12 = -G12 / detG, F21 = -G21 / detG, F22 = G11 / detG;
+    double I1 = (F11 * F11 + F21 * F21) + (F12 * F12 + F22 * F22);
+    double Jv = 1.0 / detG, jm = Jv - 1.0;
+    return 0.5 * mu_s * (I1 - 2.0) + 0.5 * kappa * (jm * jm);
+}
+
+struct DiagArgs {
+    const double *phi, *J, *xs, *ys, *u, *v, *X1, *X2;
+    int ny, nx, energies;
+    double dx, dy, w_t, rho_s, rho_f, mu_f, eta_s, mu_s, kappa;
+};
+// partial [sx, sy, cnt, Jmin, Jmax, ke, se, diss, ymin, ymax] per block
+__global__ void __launch_bounds__(DIAG_T) k_diag_p1(DiagArgs A, double *__restrict__ part) {
+    __shared__ double s[DIAG_VALS][DIAG_T];
+    double v[DIAG_VALS] = {0, 0, 0, INFINITY, -INFINITY, 0, 0, 0, INFINITY, -INFINITY};
+    const long n = (long)A.ny * A.nx;
+    for (long c = blockIdx.x * (long)DIAG_T + threadIdx.x; c < n; c += (long)DIAG_BLOCKS * DIAG_T) {
+        int j = (int)(c / A.nx), i = (int)(c % A.nx);
+        double ph = A.phi[c];
+        bool solid = ph <= 0.0;
+        if (solid) {
+            v[0] += A.xs[i]; v[1] += A.ys[j]; v[2] += 1.0;
+            v[8] = fmin(v[8], A.ys[j]); v[9] = fmax(v[9], A.ys[j]);
+        }
+        double Jc = A.J[c];
+        v[3] = fmin(v[3], Jc); v[4] = fmax(v[4], Jc);
+        if (A.energies) {
+            double H = heaviside(ph, A.w_t);
+            double rho = (1 - H) * A.rho_s + H * A.rho_f;
+            double uc = A.u[c], vc = A.v[c];
+            v[5] += 0.5 * rho * (uc * uc + vc * vc);
+            if (solid) v[6] += se_density(A.X1, A.X2, c, j, i, A.ny, A.nx, A.dx, A.dy, A.mu_s, A.kappa);
+            const double h2x = 2 * A.dx, h2y = 2 * A.dy;
+            double dudx = grad2(A.u + c, 1, i, A.nx, h2x), dvdy = grad2(A.v + c, A.nx, j, A.ny, h2y);
+            double dxy = 0.5 * (grad2(A.u + c, A.nx, j, A.ny, h2y) + grad2(A.v + c, 1, i, A.nx, h2x));
+            double mu = H * A.mu_f + (1 - H) * A.eta_s;
+            v[7] += 2.0 * mu * (dudx * dudx + dvdy * dvdy + 2.0 * (dxy * dxy));
+        }
+    }
+    for (int k = 0; k < DIAG_VALS; ++k) s[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = DIAG_T / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < DIAG_VALS; ++k) {
+                double x = s[k][threadIdx.x], y = s[k][threadIdx.x + w];
+                s[k][threadIdx.x] = (k == 3 || k == 8) ? fmin(x, y) : (k == 4 || k == 9) ? fmax(x, y) : x + y;
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < DIAG_VALS) part[blockIdx.x * DIAG_VALS + threadIdx.x] = s[threadIdx.x][0];
+}
+__global__ void __launch_bounds__(DIAG_T) k_diag_p2(const double *__restrict__ part,
+                                                    double *__restrict__ out) {
+    __shared__ double s[DIAG_VALS][DIAG_T];
+    double v[DIAG_VALS] = {0, 0, 0, INFINITY, -INFINITY, 0, 0, 0, INFINITY, -INFINITY};
+    for (int b = threadIdx.x; b < DIAG_BLOCKS; b += DIAG_T)
+        for (int k = 0; k < DIAG_VALS; ++k) {
+            double y = part[b * DIAG_VALS + k];
+            v[k] = (k == 3 || k == 8) ? fmin(v[k], y) : (k == 4 || k == 9) ? fmax(v[k], y) : v[k] + y;
+        }
+    for (int k = 0; k < DIAG_VALS; ++k) s[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = DIAG_T / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < DIAG_VALS; ++k) {
+                double x = s[k][threadIdx.x], y = s[k][threadIdx.x + w];
+                s[k][threadIdx.x] = (k == 3 || k == 8) ? fmin(x, y) : (k == 4 || k == 9) ? fmax(x, y) : x + y;
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < DIAG_VALS) out[threadIdx.x] = s[threadIdx.x][0];
+}
+
+}  // namespace rmt
+
+using namespace rmt;
+
+extern "C" {
+
+int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
+    RMT_CHECK(ctx && prm && out, RMT_EINVAL, "null argument");
+    RMT_CHECK(prm->ny == ctx->ny && prm->nx == ctx->nx, RMT_EINVAL, "sim grid != ctx grid");
+    RMT_CHECK(prm->scheme == RMT_SCHEME_SEMILAGRANGIAN || prm->scheme == RMT_SCHEME_WENO5,
+              RMT_EINVAL, "unknown advection scheme");
+    RMT_CHECK(prm->bc_kind >= 0 && prm->bc_kind <= 2, RMT_EINVAL, "unknown bc kind");
+    RMT_CHECK(prm->shape == RMT_SHAPE_NONE || prm->shape == RMT_SHAPE_DISC, RMT_EINVAL,
+              "unknown shape");
+    RMT_CHECK(prm->shape == RMT_SHAPE_NONE || prm->rho_s == prm->rho_f, RMT_ENOTSUP,
+              "rho_s != rho_f needs the variable-density CG projection (not on this path)");
+    rmt_sim *S = new rmt_sim;
+    S->ctx = ctx;
+    S->P = *prm;
+    S->P.xs = S->P.ys = nullptr;
+    const int ny = prm->ny, nx = prm->nx;
+    const size_t n = (size_t)ny * nx;
+    const int nplanes = 16 + 8;
+    size_t bytes = (nplanes * n + nx + ny + DIAG_BLOCKS * DIAG_VALS + 64) * sizeof(double) + n + 256;
+    RMT_HIP(hipMalloc(&S->block, bytes));
+    RMT_HIP(hipMemsetAsync(S->block, 0, bytes, ctx->stream));
+    double *q = (double *)S->block;
+    double **planes[] = {&S->u, &S->v, &S->p, &S->X1, &S->X2, &S->phi, &S->phi_pre, &S->J,
+                         &S->X1n, &S->X2n, &S->us, &S->vs, &S->sxx, &S->sxy, &S->syy};
+    for (auto pp : planes) { *pp = q; q += n; }
+    q += n;  // spare
+    S->mw = q; q += 8 * n;
+    S->xs = q; q += nx;
+    S->ys = q; q += ny;
+    S->dscr = q; q += DIAG_BLOCKS * DIAG_VALS + 64;
+    S->mbytes = (unsigned char *)q;
+    S->flag = (int *)(S->mbytes + n + 64);
+    RMT_HIP(hipMemcpyAsync(S->xs, prm->xs, nx * 8, hipMemcpyHostToDevice, ctx->stream));
+    RMT_HIP(hipMemcpyAsync(S->ys, prm->ys, ny * 8, hipMemcpyHostToDevice, ctx->stream));
+    // constant part of functions.py:165-192 (everything but the advective limit); the
+    // reference's h**2 on a numpy float64 scalar is libm pow.
+    const double dx = prm->dx, CFL = prm->cfl;
+    double cs = std::sqrt((prm->kappa + prm->mu_s * 4.0 / 3.0) / (prm->rho_s + 1e-12));
+    double d = std::fmin(CFL * dx / (cs + 1e-14), 1.0);
+    double mu_max = std::fmax(prm->mu_f, prm->eta_s), rho_min = std::fmin(prm->rho_s, prm->rho_f);
+    if (mu_max > 1e-12 && rho_min > 1e-12)
+        d = std::fmin(d, CFL * rho_min * std::pow(dx, 2.0) / (4.0 * mu_max));
+    S->dt_const = std::fmin(d, prm->dt_cap);
+    // size the shared scratch once (WENO5: 3 planes, projection: 2) and the extrapolation's
+    // byte workspace, so nothing is reallocated while kernels are queued
+    RMT_TRY(ensure_scratch(ctx, 3 * n * sizeof(double)));
+    {
+        size_t nb = (n + 2047) / 2048, kb = (n + 255) / 256 * 256;
+        RMT_TRY(ensure_bytes(ctx, kb + sizeof(int) * (2 * nb + 2 * n + 16)));
+    }
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    *out = S;
+    return RMT_OK;
+}
+
+int rmt_sim_destroy(rmt_sim *S) {
+    if (!S) return RMT_OK;
+    hipFree(S->block);
+    for (auto e : S->pev) if (e) hipEventDestroy(e);
+    S->ctx->prof = false;
+    delete S;
+    return RMT_OK;
+}
+
+int rmt_sim_field(rmt_sim *S, int field, double **ptr) {
+    RMT_CHECK(S && ptr, RMT_EINVAL, "null argument");
+    double *f[] = {S->u, S->v, S->p, S->X1, S->X2, S->phi, S->J};
+    RMT_CHECK(field >= 0 && field < 7, RMT_EINVAL, "unknown field id");
+    *ptr = f[field];
+    return RMT_OK;
+}
+
+int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
+    RMT_CHECK(S, RMT_EINVAL, "null sim");
+    rmt_ctx *ctx = S->ctx;
+    const rmt_sim_params &P = S->P;
+    const int ny = P.ny, nx = P.nx;
+    const long n = (long)ny * nx;
+    const unsigned g = grid1d(n, 256);
+    hipStream_t st = ctx->stream;
+    double *sc = S->dscr + DIAG_BLOCKS * DIAG_VALS;   // [0] maxsq, [1] dt, [2..11] diag
+    for (int it = 0; it < nsteps; ++it) {
+        if (!(S->t < t_end)) break;
+        if (S->prof) RMT_HIP(hipEventRecord(S->pev[0], st));
+        // 1. dt (compute_timestep + the drivers' clip to t_end)
+        RMT_TRY(reduce_maxsq2(ctx, S->u, S->v, n, sc));
+        k_dt<<<1, 1, 0, st>>>(sc, S->dt_const, P.cfl, P.dx, sc + 1);
+        double hv[2];
+        RMT_HIP(hipMemcpyAsync(hv, sc, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+        RMT_HIP(hipStreamSynchronize(st));
+        double dt = hv[1];
+        if (S->t + dt > t_end) dt = t_end - S->t;
+        const bool solid = P.shape != RMT_SHAPE_NONE;
+        if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
+        if (solid) {
+            // 2. advect the reference map with the pre-advection level set and mask
+            RMT_HIP(hipMemsetAsync(S->flag, 0, sizeof(int), st));
+            if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
+                k_sim_sl<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt,
+                                            P.dx, P.dy, P.shape, P.x0, P.y0, P.R, S->X1n, S->X2n,
+                                            S->phi_pre, S->flag);
+            } else {
+                k_sim_phi_mask<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, n, P.x0, P.y0, P.R,
+                                                  S->phi_pre, S->flag);
+                RMT_TRY(rmt_advect_weno5_rk3(ctx, S->X1, S->u, S->v, P.dx, P.dy, dt, S->phi_pre,
+                                             0.0, S->X1n));
+                RMT_TRY(rmt_advect_weno5_rk3(ctx, S->X2, S->u, S->v, P.dx, P.dy, dt, S->phi_pre,
+                                             0.0, S->X2n));
+                k_mask_mul<<<g, 256, 0, st>>>(S->X1n, S->X2n, S->phi_pre, n);
+            }
+            RMT_LAUNCHED();
+            int bad = 0;
+            RMT_HIP(hipMemcpyAsync(&bad, S->flag, sizeof(int), hipMemcpyDeviceToHost, st));
+            if (S->prof) RMT_HIP(hipEventRecord(S->pev[2], st));
+            // 3. narrow-band extrapolation (exact raster-order semantics), in place
+            RMT_TRY(extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers, S->X1n,
+                                S->X2n, nullptr));
+            if (S->prof) RMT_HIP(hipEventRecord(S->pev[3], st));
+            RMT_HIP(hipStreamSynchronize(st));
+            RMT_CHECK(!bad, RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
+                                            "simulation diverged)");
+        }
+        if (S->prof && !solid) {
+            RMT_HIP(hipEventRecord(S->pev[2], st));
+            RMT_HIP(hipEventRecord(S->pev[3], st));
+        }
+        // 4. phi from the advected + extrapolated map
+        k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R, S->phi,
+                                          S->X1, S->X2);
+        // 5. momentum (RK4)
+        rmt_momentum_params M{};
+        M.bc_kind = P.bc_kind; M.lid = P.lid; M.mu_s = P.mu_s; M.kappa = P.kappa;
+        M.eta_s = P.eta_s; M.rho_s = P.rho_s; M.rho_f = P.rho_f; M.mu_f = P.mu_f; M.w_t = P.w_t;
+        M.dx = P.dx; M.dy = P.dy; M.dt = dt; M.stress_band = P.stress_band;
+        M.detg_clamp = P.detg_clamp;
+        double *w = S->mw;
+        MomWork W{w, w + n, w + 2 * n, w + 3 * n, w + 4 * n, w + 5 * n, w + 6 * n, w + 7 * n,
+                  S->mbytes, S->flag + 1};
+        RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
+                             S->sxx, S->sxy, S->syy, S->J, W));
+        if (S->prof) RMT_HIP(hipEventRecord(S->pev[4], st));
+        // 6. projection (constant density rho_f; Neumann DCT-I)
+        RMT_TRY(rmt_pressure_projection(ctx, S->us, S->vs, P.dx, P.dy, dt, P.rho_f, P.bc_kind,
+                                        P.lid, S->p, S->u, S->v, S->p));
+        if (S->prof) RMT_HIP(hipEventRecord(S->pev[5], st));
+        // 7. diagnostics
+        DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
+                   P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa};
+        k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, S->dscr);
+        k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, sc + 2);
+        RMT_LAUNCHED();
+        double dv[DIAG_VALS];
+        RMT_HIP(hipMemcpyAsync(dv, sc + 2, sizeof(dv), hipMemcpyDeviceToHost, st));
+        if (S->prof) RMT_HIP(hipEventRecord(S->pev[6], st));
+        RMT_HIP(hipStreamSynchronize(st));
+        if (S->prof) {
+            float f;
+            for (int k = 0; k < 6; ++k) {
+                RMT_HIP(hipEventElapsedTime(&f, S->pev[k], S->pev[k + 1]));
+                S->ms[k] += f; S->calls[k] += 1;
+            }
+            RMT_HIP(hipEventElapsedTime(&f, ctx->ev[0], ctx->ev[1]));
+            S->ms[6] += f; S->calls[6] += 4;
+            if (solid) {
+                RMT_HIP(hipEventElapsedTime(&f, ctx->ev[2], ctx->ev[3]));
+                S->ms[7] += f; S->calls[7] += 1;
+            }
+        }
+        S->t += dt;
+        rmt_diag r{};
+        r.t = S->t; r.dt = dt;
+        r.cx = dv[2] > 0 ? dv[0] / dv[2] : NAN;
+        r.cy = dv[2] > 0 ? dv[1] / dv[2] : NAN;
+        r.minJ = dv[3]; r.maxJ = dv[4]; r.umax = std::sqrt(hv[0]);
+        if (P.energies) {
+            r.ke = dv[5] * P.dx * P.dy;
+            r.se = dv[6] * P.dx * P.dy;
+            r.diss = dv[7] * P.dx * P.dy;
+            S->integ += r.diss * dt;
+            r.integ = S->integ;
+            r.ry = dv[2] > 0 ? 0.5 * (dv[9] - dv[8]) : NAN;
+        }
+        S->diag.push_back(r);
+    }
+    return RMT_OK;
+}
+
+int rmt_sim_set_profiling(rmt_sim *S, int on) {
+    RMT_CHECK(S, RMT_EINVAL, "null sim");
+    if (on && !S->pev[0]) {
+        for (auto &e : S->pev) RMT_HIP(hipEventCreate(&e));
+        for (auto &e : S->ctx->ev) RMT_HIP(hipEventCreate(&e));
+    }
+    S->prof = on != 0;
+    S->ctx->prof = on != 0;
+    for (int k = 0; k < 8; ++k) { S->ms[k] = 0; S->calls[k] = 0; }
+    return RMT_OK;
+}
+
+int rmt_sim_phase_times(rmt_sim *S, double *ms8, long *calls8) {
+    RMT_CHECK(S && ms8, RMT_EINVAL, "null argument");
+    for (int k = 0; k < 8; ++k) {
+        ms8[k] = S->ms[k];
+        if (calls8) calls8[k] = S->calls[k];
+    }
+    return RMT_OK;
+}
+
+int rmt_sim_diagnostics(rmt_sim *S, rmt_diag *out, int max_records, int *n_records) {
+    RMT_CHECK(S && n_records, RMT_EINVAL, "null argument");
+    int m = (int)std::min<size_t>(S->diag.size(), (size_t)std::max(0, max_records));
+    for (int k = 0; k < m; ++k) out[k] = S->diag[S->diag.size() - m + k];
+    *n_records = (int)S->diag.size();
+    return RMT_OK;
+}
+
+}  // extern "C"

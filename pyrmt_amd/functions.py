@@ -1,0 +1,368 @@
+"""Drop-in operator surface of pyRMT (pyRMT/__init__.py:1-57) on MI355X.
+
+Same names, argument meaning, return values and error behaviour as the reference's
+module-level functions; every array operation runs in librmt's HIP kernels on the
+current CUDA(=HIP) device.  Arrays may be numpy (copied to / from the device per call,
+like a drop-in) or torch CUDA float64 tensors (no copies; results come back as tensors).
+
+Device memory and streams come from torch (plumbing only); the kernels are librmt's.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from .bc import resolve_bc, resolve_shape, Disc
+
+_ctxs = {}
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("pyrmt_amd needs a visible MI355X (torch.cuda.is_available() is False)")
+    return torch
+
+
+class _Ctx:
+    def __init__(self, ny, nx, device):
+        self.ny, self.nx, self.device = ny, nx, device
+        h = ctypes.c_void_p()
+        L.check(L.lib().rmt_ctx_create(ny, nx, device, None, ctypes.byref(h)), "rmt_ctx_create")
+        self.h = h
+
+    def bind(self):
+        torch = _torch()
+        L.check(L.lib().rmt_ctx_set_stream(self.h, torch.cuda.current_stream().cuda_stream))
+        return self.h
+
+
+def ctx_for(ny, nx):
+    torch = _torch()
+    dev = torch.cuda.current_device()
+    key = (int(ny), int(nx), dev)
+    if key not in _ctxs:
+        _ctxs[key] = _Ctx(int(ny), int(nx), dev)
+    return _ctxs[key]
+
+
+class _IO:
+    """Moves inputs to the device and results back to the caller's array type."""
+
+    def __init__(self, *arrays):
+        torch = _torch()
+        self.torch = torch
+        self.host = any(not isinstance(a, torch.Tensor) for a in arrays if a is not None)
+
+    def dev(self, a):
+        torch = self.torch
+        if a is None:
+            return None
+        if isinstance(a, torch.Tensor):
+            t = a
+            if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous():
+                t = t.to(device="cuda", dtype=torch.float64).contiguous()
+            return t
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+
+    def empty(self, shape):
+        return self.torch.empty(tuple(shape), dtype=self.torch.float64, device="cuda")
+
+    def out(self, t):
+        return t.cpu().numpy() if self.host else t
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+# ── grid / setup (host-side, as the reference) ───────────────────────────────────
+def create_grid(Nx, Ny, Lx, Ly):
+    """functions.py:25-31 (np.linspace node grid; setup, host)."""
+    x = np.linspace(0, Lx, Nx)
+    y = np.linspace(0, Ly, Ny)
+    X, Y = np.meshgrid(x, y)
+    return X, Y, x[1] - x[0], y[1] - y[0]
+
+
+def apply_phi_BCs(phi):
+    """functions.py:33-46 (init only, in place on the host array)."""
+    phi[0:3, :] = phi[-6:-3, :]
+    phi[-3:, :] = phi[3:6, :]
+    phi[:, 0:3] = phi[:, -6:-3]
+    phi[:, -3:] = phi[:, 3:6]
+    return phi
+
+
+def _precompute_poisson_eigenvalues(Nx, Ny, dx, dy):
+    """functions.py:1091-1104 (setup, host).  The device solver recomputes the same
+    separable symbol; `eigenvalues` is accepted by the solvers for API parity."""
+    lx = -2.0 * (1.0 - np.cos(np.pi * np.arange(Nx) / (Nx - 1))) / dx ** 2
+    ly = -2.0 * (1.0 - np.cos(np.pi * np.arange(Ny) / (Ny - 1))) / dy ** 2
+    eig = lx[np.newaxis, :] + ly[:, np.newaxis]
+    eig[0, 0] = 1.0
+    return eig
+
+
+def _grid_of_eigenvalues(eig):
+    """Recover (dx, dy) of a _precompute_poisson_eigenvalues table and check it."""
+    eig = np.asarray(eig)
+    Ny, Nx = eig.shape
+    dx = np.sqrt(-2.0 * (1.0 - np.cos(np.pi / (Nx - 1))) / eig[0, 1])
+    dy = np.sqrt(-2.0 * (1.0 - np.cos(np.pi / (Ny - 1))) / eig[1, 0])
+    ref = _precompute_poisson_eigenvalues(Nx, Ny, dx, dy)
+    if not np.allclose(ref, eig, rtol=1e-12, atol=0):
+        raise NotImplementedError("eigenvalues are not the DCT-I Neumann symbol of a uniform grid")
+    return float(dx), float(dy)
+
+
+# ── FD helpers / interpolation (utils.py, interpolators.py) ──────────────────────
+def grad_central_x_2nd(f, dx):
+    io = _IO(f); f = io.dev(f); out = io.empty(f.shape)
+    c = ctx_for(*f.shape)
+    L.check(L.lib().rmt_grad_x_2nd(c.bind(), _p(f), dx, _p(out)), "grad_central_x_2nd")
+    return io.out(out)
+
+
+def grad_central_y_2nd(f, dy):
+    io = _IO(f); f = io.dev(f); out = io.empty(f.shape)
+    c = ctx_for(*f.shape)
+    L.check(L.lib().rmt_grad_y_2nd(c.bind(), _p(f), dy, _p(out)), "grad_central_y_2nd")
+    return io.out(out)
+
+
+def diff_upwind_3rd(f, u, h, axis):
+    io = _IO(f, u); f = io.dev(f); u = io.dev(u); out = io.empty(f.shape)
+    c = ctx_for(*f.shape)
+    L.check(L.lib().rmt_diff_upwind_3rd(c.bind(), _p(f), _p(u), h, int(axis), _p(out)),
+            "diff_upwind_3rd")
+    return io.out(out)
+
+
+def bilinear_interpolate(u, xq, yq, dx, dy, Nx, Ny):
+    io = _IO(u, xq, yq); u = io.dev(u); xq = io.dev(xq); yq = io.dev(yq)
+    if u.shape != (Ny, Nx):
+        raise ValueError("bilinear_interpolate: u must have shape (Ny, Nx)")
+    out = io.empty(xq.shape)
+    c = ctx_for(Ny, Nx)
+    L.check(L.lib().rmt_bilinear_interpolate(c.bind(), _p(u), _p(xq), _p(yq), xq.numel(), dx, dy,
+                                             _p(out)), "bilinear_interpolate")
+    return io.out(out)
+
+
+# ── reference-map transport (functions.py:48-542) ─────────────────────────────────
+def extrapolate_reference_map(X1, X2, phi, dx, dy, max_layers):
+    io = _IO(X1, X2, phi); X1 = io.dev(X1); X2 = io.dev(X2); phi = io.dev(phi)
+    o1 = io.empty(X1.shape); o2 = io.empty(X1.shape)
+    c = ctx_for(*X1.shape)
+    L.check(L.lib().rmt_extrapolate_reference_map(c.bind(), _p(X1), _p(X2), _p(phi), dx, dy,
+                                                  int(max_layers), _p(o1), _p(o2)),
+            "extrapolate_reference_map")
+    return io.out(o1), io.out(o2)
+
+
+def advect_semilagrangian_rk4(q, a, b, X, Y, dt, dx, dy):
+    io = _IO(q, a, b, X, Y); q, a, b, X, Y = map(io.dev, (q, a, b, X, Y))
+    out = io.empty(q.shape)
+    c = ctx_for(*q.shape)
+    L.check(L.lib().rmt_advect_sl_rk4(c.bind(), _p(q), _p(a), _p(b), _p(X), _p(Y), dt, dx, dy,
+                                      _p(out)), "advect_semilagrangian_rk4")
+    return io.out(out)
+
+
+def _weno5_rhs(q, a, b, dx, dy, phi, w_cut):
+    io = _IO(q, a, b, phi); q, a, b, phi = map(io.dev, (q, a, b, phi))
+    out = io.empty(q.shape)
+    c = ctx_for(*q.shape)
+    L.check(L.lib().rmt_weno5_rhs(c.bind(), _p(q), _p(a), _p(b), dx, dy, _p(phi), w_cut, _p(out)),
+            "_weno5_rhs")
+    return io.out(out)
+
+
+def advect_weno5_rk3(q, a, b, dx, dy, dt, phi, w_cut=0.0):
+    io = _IO(q, a, b, phi); q, a, b, phi = map(io.dev, (q, a, b, phi))
+    out = io.empty(q.shape)
+    c = ctx_for(*q.shape)
+    L.check(L.lib().rmt_advect_weno5_rk3(c.bind(), _p(q), _p(a), _p(b), dx, dy, dt, _p(phi), w_cut,
+                                         _p(out)), "advect_weno5_rk3")
+    return io.out(out)
+
+
+def advect_reference_map(q, a, b, X, Y, dt, dx, dy, phi, scheme='semilagrangian', w_cut=0.0):
+    """functions.py:501-542: raises FloatingPointError on non-finite velocity, ValueError
+    on an unknown scheme; 'semilagrangian_cubic', 'central2', 'conservative' are the
+    next tier and raise NotImplementedError."""
+    io = _IO(q, a, b, X, Y, phi)
+    ad, bd = io.dev(a), io.dev(b)
+    c = ctx_for(*ad.shape)
+    fin = ctypes.c_int(0)
+    L.check(L.lib().rmt_all_finite2(c.bind(), _p(ad), _p(bd), ctypes.byref(fin)))
+    if not fin.value:
+        raise FloatingPointError("advect_reference_map: non-finite velocity (the simulation diverged)")
+    if scheme == 'semilagrangian':
+        return advect_semilagrangian_rk4(q, a, b, X, Y, dt, dx, dy)
+    if scheme == 'weno5':
+        return advect_weno5_rk3(q, a, b, dx, dy, dt, phi, w_cut)
+    if scheme in ('semilagrangian_cubic', 'central2', 'conservative'):
+        raise NotImplementedError(f"advection scheme {scheme!r} is outside this build's path")
+    raise ValueError("Unknown advection scheme %r (expected 'semilagrangian', "
+                     "'central2', 'weno5' or 'conservative')" % (scheme,))
+
+
+def rebuild_phi_from_reference_map(X1, X2, phi_init_func):
+    """functions.py:1366-1367 for a disc level set (the drivers' lambda or bc.Disc)."""
+    d = resolve_shape(phi_init_func)
+    io = _IO(X1, X2); X1 = io.dev(X1); X2 = io.dev(X2); out = io.empty(X1.shape)
+    c = ctx_for(*X1.shape)
+    L.check(L.lib().rmt_rebuild_phi_disc(c.bind(), _p(X1), _p(X2), d.x0, d.y0, d.R, _p(out)),
+            "rebuild_phi_from_reference_map")
+    return io.out(out)
+
+
+def reinitialize_level_set(phi, dx, dy, method='none', num_iters=20, dt_reinit_factor=0.2,
+                           apply_phi_BCs_func=None):
+    """functions.py:1436-1456: 'none' is the identity used on the hot path."""
+    if method == 'none':
+        return phi
+    if method in ('pde', 'fmm'):
+        raise NotImplementedError(f"reinit method {method!r} is outside this build's path")
+    raise ValueError("Unknown reinit method %r (expected 'none', 'pde' or 'fmm')" % (method,))
+
+
+# ── stress / momentum (functions.py:545-944) ──────────────────────────────────────
+def solid_cauchy_stress(X1, X2, dx, dy, mu_s, kappa, phi, w_cut=0.0, detg_clamp=0.0,
+                        isochoric=False):
+    io = _IO(X1, X2, phi); X1, X2, phi = map(io.dev, (X1, X2, phi))
+    outs = [io.empty(X1.shape) for _ in range(4)]
+    c = ctx_for(*X1.shape)
+    L.check(L.lib().rmt_solid_cauchy_stress(c.bind(), _p(X1), _p(X2), dx, dy, mu_s, kappa, _p(phi),
+                                            w_cut, detg_clamp, int(bool(isochoric)),
+                                            *map(_p, outs)), "solid_cauchy_stress")
+    return tuple(io.out(o) for o in outs)
+
+
+def smoothed_heaviside(x, w_t):
+    io = _IO(x); xd = io.dev(x); out = io.empty(xd.shape)
+    c = ctx_for(*(xd.shape if xd.dim() == 2 else (1, xd.numel())))
+    L.check(L.lib().rmt_smoothed_heaviside(c.bind(), _p(xd), xd.numel(), w_t, _p(out)),
+            "smoothed_heaviside")
+    return io.out(out)
+
+
+def apply_velocity_BCs(bc, u, v):
+    """functions.py:946-947: applies the BC to copies."""
+    kind, lid = resolve_bc(bc)
+    io = _IO(u, v); ud = io.dev(u).clone(); vd = io.dev(v).clone()
+    c = ctx_for(*ud.shape)
+    L.check(L.lib().rmt_apply_velocity_bc(c.bind(), kind, lid, _p(ud), _p(vd)), "apply_velocity_BCs")
+    return io.out(ud), io.out(vd)
+
+
+def momentum_step_rk4(u, v, p, X1, X2, velocity_bc, mu_s, kappa, eta_s, dx, dy, dt, rho_s, rho_f,
+                      phi, mu_f, w_t, gamma=0.0, stress_band=False, detg_clamp=3.0):
+    """functions.py:673-762.  Returns (u_new, v_new, sxx, sxy, syy, J)."""
+    if gamma > 1e-12:
+        raise NotImplementedError("surface tension (gamma > 0) is outside this build's path")
+    kind, lid = resolve_bc(velocity_bc)
+    io = _IO(u, v, p, X1, X2, phi)
+    u, v, p, X1, X2, phi = map(io.dev, (u, v, p, X1, X2, phi))
+    outs = [io.empty(u.shape) for _ in range(6)]
+    prm = L.rmt_momentum_params(kind, lid, mu_s, kappa, eta_s, rho_s, rho_f, mu_f, w_t, dx, dy, dt,
+                                int(bool(stress_band)), detg_clamp)
+    c = ctx_for(*u.shape)
+    L.check(L.lib().rmt_momentum_step_rk4(c.bind(), ctypes.byref(prm), _p(u), _p(v), _p(p), _p(X1),
+                                          _p(X2), _p(phi), *map(_p, outs)), "momentum_step_rk4")
+    return tuple(io.out(o) for o in outs)
+
+
+# ── projection (functions.py:1005-1364) ──────────────────────────────────────────
+def _rho_scalar(rho):
+    """The constant-density branch (functions.py:1298): rho scalar, or an array whose
+    ptp <= 1e-10 and that is exactly constant (as (1-H) rho_s + H rho_f is for
+    rho_s == rho_f == 1).  Variable density -> NotImplementedError."""
+    if np.isscalar(rho) or (hasattr(rho, "ndim") and rho.ndim == 0):
+        return float(rho)
+    r = rho.detach().cpu().numpy() if hasattr(rho, "detach") else np.asarray(rho)
+    if np.ptp(r) > 1e-10:
+        raise NotImplementedError("variable-density projection (CG) is outside this build's path")
+    r0 = float(r.flat[0])
+    if not np.all(r == r0):
+        raise NotImplementedError("rho must be exactly constant on the device path")
+    return r0
+
+
+def _compute_divergence_rc(a_star, b_star, p_prev, dt, rho, dx, dy):
+    r = _rho_scalar(rho)
+    io = _IO(a_star, b_star, p_prev); a, b, p = map(io.dev, (a_star, b_star, p_prev))
+    out = io.empty(a.shape)
+    c = ctx_for(*a.shape)
+    L.check(L.lib().rmt_divergence_rc(c.bind(), _p(a), _p(b), _p(p), dt / r, dx, dy, _p(out)),
+            "_compute_divergence_rc")
+    return io.out(out)
+
+
+def _compute_divergence(a_star, b_star, dx, dy):
+    io = _IO(a_star, b_star); a, b = io.dev(a_star), io.dev(b_star)
+    out = io.empty(a.shape)
+    c = ctx_for(*a.shape)
+    L.check(L.lib().rmt_divergence_central(c.bind(), _p(a), _p(b), dx, dy, _p(out)),
+            "_compute_divergence")
+    return io.out(out)
+
+
+def _compute_pressure_gradient(p, dx, dy):
+    io = _IO(p); pd = io.dev(p); gx = io.empty(pd.shape); gy = io.empty(pd.shape)
+    c = ctx_for(*pd.shape)
+    L.check(L.lib().rmt_pressure_gradient(c.bind(), _p(pd), dx, dy, _p(gx), _p(gy)),
+            "_compute_pressure_gradient")
+    return io.out(gx), io.out(gy)
+
+
+def _solve_poisson_dct(rhs_2d, eigenvalues):
+    dx, dy = _grid_of_eigenvalues(eigenvalues)
+    io = _IO(rhs_2d); r = io.dev(rhs_2d); out = io.empty(r.shape)
+    c = ctx_for(*r.shape)
+    L.check(L.lib().rmt_solve_poisson_dct(c.bind(), _p(r), dx, dy, _p(out)), "_solve_poisson_dct")
+    return io.out(out)
+
+
+def pressure_projection_amg(a_star, b_star, dx, dy, dt, rho, velocity_bc, A=None, ml=None,
+                            p_prev=None, eigenvalues=None, bc_type='neumann'):
+    """functions.py:1255-1364, Neumann branch with the DCT direct solve and constant
+    density.  Returns (a, b, p, A, ml) like the reference."""
+    if bc_type != 'neumann':
+        raise NotImplementedError("bc_type %r is outside this build's path" % (bc_type,))
+    if eigenvalues is None:
+        raise NotImplementedError("the AMG fallback (eigenvalues=None) is outside this build's path")
+    _grid_of_eigenvalues(eigenvalues)
+    kind, lid = resolve_bc(velocity_bc)
+    r = _rho_scalar(rho)
+    io = _IO(a_star, b_star, p_prev)
+    a_s, b_s, pp = map(io.dev, (a_star, b_star, p_prev))
+    a = io.empty(a_s.shape); b = io.empty(a_s.shape); p = io.empty(a_s.shape)
+    c = ctx_for(*a_s.shape)
+    L.check(L.lib().rmt_pressure_projection(c.bind(), _p(a_s), _p(b_s), dx, dy, dt, r, kind, lid,
+                                            _p(pp), _p(a), _p(b), _p(p)), "pressure_projection_amg")
+    return io.out(a), io.out(b), io.out(p), A, ml
+
+
+def compute_timestep(a, b, dx, dy, CFL, dt_min_cap, mu_s, rho_s, gamma, rho_f, mu_f=0.0,
+                     eta_s=0.0, kappa=0.0):
+    """functions.py:165-192 (max |u| reduced on the device)."""
+    io = _IO(a, b); ad, bd = io.dev(a), io.dev(b)
+    c = ctx_for(*ad.shape)
+    out = ctypes.c_double()
+    L.check(L.lib().rmt_compute_timestep(c.bind(), _p(ad), _p(bd), dx, dy, CFL, dt_min_cap, mu_s,
+                                         rho_s, gamma, rho_f, mu_f, eta_s, kappa,
+                                         ctypes.byref(out)), "compute_timestep")
+    return out.value
+
+
+# Deprecated aliases (functions.py:1462-1466)
+velocity_RK4 = momentum_step_rk4
+heaviside_smooth_alt = smoothed_heaviside
+compute_solid_stress = solid_cauchy_stress
+extrapolate_transverse_layers_2field = extrapolate_reference_map
+advect_semi_lagrangian_rk4 = advect_semilagrangian_rk4
+__all__ = [k for k in dir() if not k.startswith("__")]
+_ = Disc
