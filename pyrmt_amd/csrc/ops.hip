@@ -206,15 +206,14 @@ __global__ void k_heaviside(const double *__restrict__ x, long n, double w_t,
 
 // ----------------------------------------------------------------------- BCs ----
 __global__ void k_apply_bc(int kind, double lid, double *u, double *v, int ny, int nx) {
-    // one thread per boundary cell; reads only interior (never-written) neighbours
+    // in place: boundary cells only read interior (never written) source cells
     long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (c >= (long)ny * nx) return;
     int j = (int)(c / nx), i = (int)(c % nx);
     if (!(i == 0 || i == nx - 1 || j == 0 || j == ny - 1)) return;
-    auto ru = [&](int jj, int ii) { return u[(long)jj * nx + ii]; };
-    auto rv = [&](int jj, int ii) { return v[(long)jj * nx + ii]; };
-    double uu, vv;
-    bc_value(kind, lid, j, i, ny, nx, ru, rv, uu, vv);   // edge cells read interior cells only
+    BCSrc s = bc_source(kind, lid, j, i, ny, nx);
+    double uu = s.u_const ? s.u_val : u[s.u_src];
+    double vv = s.v_const ? s.v_val : v[s.v_src];
     u[c] = uu; v[c] = vv;
 }
 
@@ -274,6 +273,16 @@ __global__ void k_pressure_gradient(const double *__restrict__ p, int ny, int nx
 }
 // functions.py:1330-1362 after the solve: a = a* - (dt/rho) dpc/dx, BC, p = p_prev + pc,
 // with pc = p_raw - mean(p_raw) (mean on device).  Writes p before its own mean removal.
+// functions.py:1350-1358 after the solve: a = a* - (dt/rho) dpc/dx, BC, p = p_prev + pc.
+// Writes p before its mean removal.
+__device__ __forceinline__ double corrected(const double *__restrict__ s,
+                                            const double *__restrict__ pc, long c, int ny, int nx,
+                                            double dx, double dy, double dt_rho, int comp) {
+    int j = (int)(c / nx), i = (int)(c % nx);
+    double gx, gy;
+    pgrad_cell(pc, c, j, i, ny, nx, dx, dy, gx, gy);
+    return s[c] - dt_rho * (comp == 0 ? gx : gy);
+}
 __global__ void k_project_correct(const double *__restrict__ a_s, const double *__restrict__ b_s,
                                   const double *__restrict__ pc, const double *__restrict__ p_prev,
                                   int ny, int nx, double dx, double dy, double dt_rho, int bc,
@@ -282,19 +291,9 @@ __global__ void k_project_correct(const double *__restrict__ a_s, const double *
     long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (c >= (long)ny * nx) return;
     int j = (int)(c / nx), i = (int)(c % nx);
-    auto ru = [&](int jj, int ii) {
-        long cc = (long)jj * nx + ii; double gx, gy;
-        pgrad_cell(pc, cc, jj, ii, ny, nx, dx, dy, gx, gy);
-        return a_s[cc] - dt_rho * gx;
-    };
-    auto rv = [&](int jj, int ii) {
-        long cc = (long)jj * nx + ii; double gx, gy;
-        pgrad_cell(pc, cc, jj, ii, ny, nx, dx, dy, gx, gy);
-        return b_s[cc] - dt_rho * gy;
-    };
-    double uu, vv;
-    bc_value(bc, lid, j, i, ny, nx, ru, rv, uu, vv);
-    a[c] = uu; b[c] = vv;
+    BCSrc s = bc_source(bc, lid, j, i, ny, nx);
+    a[c] = s.u_const ? s.u_val : corrected(a_s, pc, s.u_src, ny, nx, dx, dy, dt_rho, 0);
+    b[c] = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, dx, dy, dt_rho, 1);
     p[c] = p_prev ? p_prev[c] + pc[c] : pc[c];
 }
 __global__ void k_sub_scalar(double *__restrict__ x, long n, const double *__restrict__ s) {

@@ -235,28 +235,31 @@ __device__ __forceinline__ double weno5_diff(const double *f, long s, int k, int
     return qp - qm;
 }
 
-// benchmarks/common.py:27-50: BC'd value of a stage velocity component at (j, i), given
-// the raw (pre-BC) component values through `raw(j, i)`.
-template <class RawU, class RawV>
-__device__ __forceinline__ void bc_value(int kind, double lid, int j, int i, int ny, int nx,
-                                         RawU rawu, RawV rawv, double &u, double &v) {
+// benchmarks/common.py:27-50 as data: for boundary kind `kind`, the BC'd value of each
+// velocity component at (j, i) is either a constant or the raw (pre-BC) value of one
+// source cell.  Callers read the raw value themselves (no device lambdas).
+struct BCSrc {
+    bool u_const, v_const;
+    double u_val, v_val;
+    long u_src, v_src;
+};
+__device__ __forceinline__ BCSrc bc_source(int kind, double lid, int j, int i, int ny, int nx) {
+    const long c = (long)j * nx + i;
+    BCSrc s{false, false, 0.0, 0.0, c, c};
     if (kind == RMT_BC_NOSLIP_LID) {
-        bool edge = (i == 0 || i == nx - 1 || j == 0 || j == ny - 1);
-        if (!edge) { u = rawu(j, i); v = rawv(j, i); return; }
-        v = 0.0;
-        u = (j == ny - 1 && i != 0 && i != nx - 1) ? lid : 0.0;
+        if (i == 0 || i == nx - 1 || j == 0 || j == ny - 1) {
+            s.u_const = s.v_const = true;
+            s.u_val = (j == ny - 1 && i != 0 && i != nx - 1) ? lid : 0.0;
+        }
     } else if (kind == RMT_BC_FREESLIP_BOX) {
-        if (i == 0 || i == nx - 1) u = 0.0;
-        else if (j == 0) u = rawu(1, i);
-        else if (j == ny - 1) u = rawu(ny - 2, i);
-        else u = rawu(j, i);
-        if (j == 0 || j == ny - 1) v = 0.0;
-        else if (i == 0) v = rawv(j, 1);
-        else if (i == nx - 1) v = rawv(j, nx - 2);
-        else v = rawv(j, i);
-    } else {
-        u = rawu(j, i); v = rawv(j, i);
+        if (i == 0 || i == nx - 1) s.u_const = true;
+        else if (j == 0) s.u_src = c + nx;
+        else if (j == ny - 1) s.u_src = c - nx;
+        if (j == 0 || j == ny - 1) s.v_const = true;
+        else if (i == 0) s.v_src = c + 1;
+        else if (i == nx - 1) s.v_src = c - 1;
     }
+    return s;
 }
 
 // ------------------------------------------------------------------- reductions --
@@ -268,11 +271,16 @@ int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *dev_out);
 int read_scalar(rmt_ctx *ctx, const double *dev, double *host);
 
 // --------------------------------------------------------------------- momentum --
-struct MomWork {                 // 8 planes + solid byte plane + flag
-    double *H, *rho, *k1u, *k1v, *k2u, *k2v, *accu, *accv;
+constexpr int MOM_WORK_PLANES = 13;
+struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + flag
+    double *H, *rho, *k1u, *k1v, *k2u, *k2v, *accu, *accv, *us, *vs, *gxx, *gxy, *gyy;
     unsigned char *solid;
     int *any_solid;
 };
+inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
+    return MomWork{w,         w + n,     w + 2 * n, w + 3 * n,  w + 4 * n,  w + 5 * n, w + 6 * n,
+                   w + 7 * n, w + 8 * n, w + 9 * n, w + 10 * n, w + 11 * n, w + 12 * n, solid, flag};
+}
 int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                  const double *p, const double *X1, const double *X2, const double *phi,
                  double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,

@@ -212,7 +212,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     S->P.xs = S->P.ys = nullptr;
     const int ny = prm->ny, nx = prm->nx;
     const size_t n = (size_t)ny * nx;
-    const int nplanes = 16 + 8;
+    const int nplanes = 16 + MOM_WORK_PLANES;
     size_t bytes = (nplanes * n + nx + ny + DIAG_BLOCKS * DIAG_VALS + 64) * sizeof(double) + n + 256;
     RMT_HIP(hipMalloc(&S->block, bytes));
     RMT_HIP(hipMemsetAsync(S->block, 0, bytes, ctx->stream));
@@ -221,7 +221,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
                          &S->X1n, &S->X2n, &S->us, &S->vs, &S->sxx, &S->sxy, &S->syy};
     for (auto pp : planes) { *pp = q; q += n; }
     q += n;  // spare
-    S->mw = q; q += 8 * n;
+    S->mw = q; q += MOM_WORK_PLANES * n;
     S->xs = q; q += nx;
     S->ys = q; q += ny;
     S->dscr = q; q += DIAG_BLOCKS * DIAG_VALS + 64;
@@ -331,8 +331,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         M.dx = P.dx; M.dy = P.dy; M.dt = dt; M.stress_band = P.stress_band;
         M.detg_clamp = P.detg_clamp;
         double *w = S->mw;
-        MomWork W{w, w + n, w + 2 * n, w + 3 * n, w + 4 * n, w + 5 * n, w + 6 * n, w + 7 * n,
-                  S->mbytes, S->flag + 1};
+        MomWork W = mom_work(w, n, S->mbytes, S->flag + 1);
         RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
                              S->sxx, S->sxy, S->syy, S->J, W));
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[4], st));

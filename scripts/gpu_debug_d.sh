@@ -10,7 +10,7 @@ for f in ops momentum extrap poisson sim; do
 done
 cd ../..
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared gpurun_out/chk/*.o -L/opt/rocm/lib -lrocfft -o gpurun_out/chk/librmt_checked.so || exit 1
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 tools/mom_check.cpp gpurun_out/chk/librmt_checked.so -Wl,-rpath,$PWD/gpurun_out/chk -o gpurun_out/chk/mom_check || exit 1
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -Wno-unused-value -c tools/mom_check.cpp -o gpurun_out/chk/mom_check.o && /opt/rocm/bin/hipcc --offload-arch=gfx950 gpurun_out/chk/mom_check.o -L$PWD/gpurun_out/chk -lrmt_checked -Wl,-rpath,$PWD/gpurun_out/chk -o gpurun_out/chk/mom_check || exit 1
 AMD_SERIALIZE_KERNEL=3 timeout -k 10 120 gpurun_out/chk/mom_check 129 > gpurun_out/mom_check.log 2>&1
 rc=$?
 echo "mom_check exit $rc" >> gpurun_out/mom_check.log
