@@ -292,7 +292,9 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
 void dct_destroy(DctPlan *);
 
 // ------------------------------------------------------------------ extrapolate --
+// dev_status (optional, device): receives {cells fitted, aborted} after the sweep
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
-                double dy, int max_layers, double *X1o, double *X2o, const int *dev_skip = nullptr);
+                double dy, int max_layers, double *X1o, double *X2o, int *dev_status = nullptr);
+size_t extrap_workspace(int ny, int nx);   // bytes of ctx->bytes the extrapolation uses
 
 }  // namespace rmt

@@ -241,10 +241,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     // size the shared scratch once (WENO5: 3 planes, projection: 2) and the extrapolation's
     // byte workspace, so nothing is reallocated while kernels are queued
     RMT_TRY(ensure_scratch(ctx, 3 * n * sizeof(double)));
-    {
-        size_t nb = (n + 2047) / 2048, kb = (n + 255) / 256 * 256;
-        RMT_TRY(ensure_bytes(ctx, kb + sizeof(int) * (2 * nb + 2 * n + 16)));
-    }
+    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx)));
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
     return RMT_OK;
@@ -306,16 +303,17 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 k_mask_mul<<<g, 256, 0, st>>>(S->X1n, S->X2n, S->phi_pre, n);
             }
             RMT_LAUNCHED();
-            int bad = 0;
-            RMT_HIP(hipMemcpyAsync(&bad, S->flag, sizeof(int), hipMemcpyDeviceToHost, st));
             if (S->prof) RMT_HIP(hipEventRecord(S->pev[2], st));
             // 3. narrow-band extrapolation (exact raster-order semantics), in place
             RMT_TRY(extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers, S->X1n,
-                                S->X2n, nullptr));
+                                S->X2n, S->flag + 2));
             if (S->prof) RMT_HIP(hipEventRecord(S->pev[3], st));
+            int fl[4] = {0, 0, 0, 0};   // non-finite, (momentum), fitted, sweep aborted
+            RMT_HIP(hipMemcpyAsync(fl, S->flag, sizeof(fl), hipMemcpyDeviceToHost, st));
             RMT_HIP(hipStreamSynchronize(st));
-            RMT_CHECK(!bad, RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
-                                            "simulation diverged)");
+            RMT_CHECK(!fl[0], RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
+                                              "simulation diverged)");
+            RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
         }
         if (S->prof && !solid) {
             RMT_HIP(hipEventRecord(S->pev[2], st));
