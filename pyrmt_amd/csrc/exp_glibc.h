@@ -156,7 +156,8 @@ static const unsigned long long kExpTab[256] = {
     0x3c5305c14160cc89ull, 0x3feff3c22b8f71f1ull,
 };
 
-RMT_HD inline double exp_glibc(double x) {
+// tab: kExpTab or a copy of it (e.g. in LDS)
+RMT_HD inline double exp_glibc_tab(double x, const unsigned long long *tab) {
     const double InvLn2N = 0x1.71547652b82fep0 * 128, NegLn2hiN = -0x1.62e42fefa0000p-8,
                  NegLn2loN = -0x1.cf79abc9e3b3ap-47, Shift = 0x1.8p52;
     const double C2 = 0x1.ffffffffffdbdp-2, C3 = 0x1.555555555543cp-3,
@@ -169,10 +170,10 @@ RMT_HD inline double exp_glibc(double x) {
     kd -= Shift;
     double r = __builtin_fma(kd, NegLn2loN, __builtin_fma(kd, NegLn2hiN, x));
     uint64_t idx = 2 * (ki % 128), top = ki << 45;
-    uint64_t tb = kExpTab[idx];
+    uint64_t tb = tab[idx];
     double tail;
     std::memcpy(&tail, &tb, 8);
-    uint64_t sbits = kExpTab[idx + 1] + top;
+    uint64_t sbits = tab[idx + 1] + top;
     double r2 = r * r;
     double tmp = __builtin_fma(r2 * r2, __builtin_fma(r, C5, C4),
                                __builtin_fma(r2, __builtin_fma(r, C3, C2), tail + r));
@@ -180,5 +181,7 @@ RMT_HD inline double exp_glibc(double x) {
     std::memcpy(&scale, &sbits, 8);
     return __builtin_fma(scale, tmp, scale);
 }
+
+RMT_HD inline double exp_glibc(double x) { return exp_glibc_tab(x, kExpTab); }
 
 }  // namespace rmt

@@ -6,29 +6,31 @@
 // and a parallel fixed-point iteration needs as many sweeps as the dependency depth (DESIGN.md
 // §5).  librmt executes the same dependency DAG, just not in one thread:
 //
-//   1. k_ex_bits / k_ex_dilate (chip-wide, bit planes): known = (phi < 0) as 64-cell words;
-//      candidates = interior unknown cells within Chebyshev distance max_layers of a known cell
-//      (the only cells that can ever become known), their layer byte set to "unknown".
+//   1. k_ex_bits / k_ex_dilate (chip-wide, bit planes of 64-cell words): kbits = (phi < 0);
+//      cbits = candidates = interior unknown cells within Chebyshev distance max_layers of a
+//      known cell (the only cells that can ever become known); K[L] = "known after layer L",
+//      initialised to kbits for every L and OR-ed by each fit of layer L into K[L..ML-1].
 //   2. k_ex_sweep (one workgroup of EXW waves): work item = (layer L, row j), taken from an LDS
 //      ticket counter in order of j + 5L.  A target (L, j, i) reads the 9x9 window around it, so
 //      at its fit the serial state is exactly reproduced when
 //        - rows j-4..j+4 of layer L-1 are complete (the window and the 3x3 target test see the
-//          state at the start of layer L), and
+//          state at the start of layer L: K[L-1] is final there), and
 //        - rows j-1..j-4 of layer L have finished every target at column <= i+4 (the targets
 //          before it in raster order that lie in its window); its own row runs in order.
 //      Nothing later in raster order can be inside the window yet: row j+r of layer L waits for
 //      row j to pass its columns, and layer L+1 waits for layer L.  Every wait is on a lower
 //      ticket, so the lowest active ticket always proceeds.  Rows publish progress ("all my
-//      targets left of column c are done") in an LDS ring; a layer byte per candidate cell
-//      (0..: fitted in layer byte-1, 255: unknown) says whether a cell is known for layer L
-//      (byte <= L) or at a fit inside layer L (byte <= L+1).
-//   Each fit: lanes own window cells (geometry and glibc-exact weights computed before the
-//   wait), 12 lanes fold the 12 sums of functions.py:128-145 in loop order, every lane runs
-//   the 3x3 solve on the broadcast sums, lane 0 writes.
+//      targets left of column c are done, and their stores have reached L2") in an LDS ring.
+//   Each fit: lanes own window cells.  Before the wait a lane computes its geometry and
+//   glibc-exact weight and loads everything already final (static cells, rows below, its own
+//   row, and cells of rows above left of that row's progress), so after the wait only the cells
+//   that became final during it are loaded (one round trip, usually none).  Then 12 lanes fold
+//   the 12 sums of functions.py:128-145 in loop order, every lane runs the 3x3 solve on the
+//   broadcast sums, lane 0 writes.
 //
-// Visibility: bytes written inside the sweep (layer bytes, fitted X values) are stored with
-// plain stores drained by s_waitcnt vmcnt(0) before the LDS progress word is released, and
-// read with sc1 (L2) loads after the acquire; bytes fixed before the launch use plain loads.
+// Visibility: bytes written inside the sweep (fitted X values, K words) are stored with plain
+// stores / L2 atomics drained by s_waitcnt vmcnt(0) before the LDS progress word is released,
+// and read only with sc1 (L2) loads; bytes fixed before the launch use plain loads.
 #include "rmt_internal.hpp"
 #include "exp_glibc.h"
 
@@ -36,15 +38,17 @@ namespace rmt {
 
 typedef unsigned long long u64;
 
-constexpr int EXW = 16;                       // waves of the sweep workgroup
+constexpr int EXW = 8;                        // waves of the sweep workgroup (2 per SIMD)
 constexpr int EX_RING = 1024;                 // progress ring entries (tickets)
 constexpr int EX_WIN = 81;                    // 9x9 window
 constexpr unsigned EX_DONE = 0x7fffffffu;     // progress of a completed row
 constexpr long EX_SPIN_LIMIT = 1L << 25;      // ~1-2 s of polling, then abort (bug guard)
 
-// known bit plane: word (j, w) bit b <=> phi[j, 64w+b] < 0; row flags / row range reset
+// known bit plane: word (j, w) bit b <=> phi[j, 64w+b] < 0, copied into K[0..ML-1]; row flags
+// and the band's row range reset
 __global__ void __launch_bounds__(256) k_ex_bits(const double *__restrict__ phi, int ny, int nx,
-                                                 int W, u64 *__restrict__ kbits,
+                                                 int W, int ML, u64 *__restrict__ kbits,
+                                                 u64 *__restrict__ K,
                                                  unsigned char *__restrict__ rowcand,
                                                  int *__restrict__ jrange,
                                                  const double *__restrict__ X1,
@@ -57,7 +61,11 @@ __global__ void __launch_bounds__(256) k_ex_bits(const double *__restrict__ phi,
     const bool k = in && phi[c] < 0;
     if (in && copy) { X1o[c] = X1[c]; X2o[c] = X2[c]; }
     const u64 m = __ballot(k);
-    if ((threadIdx.x & 63) == 0 && (i >> 6) < W) kbits[(long)j * W + (i >> 6)] = m;
+    if ((threadIdx.x & 63) == 0 && (i >> 6) < W) {
+        const long wd = (long)j * W + (i >> 6), plane = (long)ny * W;
+        kbits[wd] = m;
+        for (int L = 0; L < ML; ++L) K[L * plane + wd] = m;
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         rowcand[j] = 0;
         if (j == 0) { jrange[0] = 0x7fffffff; jrange[1] = -1; }
@@ -67,7 +75,6 @@ __global__ void __launch_bounds__(256) k_ex_bits(const double *__restrict__ phi,
 // candidate bit plane: Chebyshev dilation of known by L, minus known, interior cells only
 __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits, int ny, int nx,
                                                    int W, int L, u64 *__restrict__ cbits,
-                                                   unsigned char *__restrict__ lay,
                                                    unsigned char *__restrict__ rowcand,
                                                    int *__restrict__ jrange) {
     const long t = blockIdx.x * 256L + threadIdx.x;
@@ -97,11 +104,10 @@ __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits
         rowcand[j] = 1;
         atomicMin(&jrange[0], j);
         atomicMax(&jrange[1], j);
-        for (u64 m = cw; m; m &= m - 1) lay[(long)j * nx + i0 + __builtin_ctzll(m)] = 255;
     }
 }
 
-__device__ __forceinline__ unsigned char ld_sc1_u8(const unsigned char *p) {
+__device__ __forceinline__ u64 ld_sc1_u64(const u64 *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ double ld_sc1_f64(const double *p) {
@@ -119,8 +125,8 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 
 struct ExSweep {
     double *X1e, *X2e;
-    unsigned char *lay;
     const u64 *kbits, *cbits;
+    u64 *K;                      // ML planes of ny*W words
     const unsigned char *rowcand;
     const int *jrange;
     int ny, nx, W, ML;
@@ -162,103 +168,153 @@ __device__ __forceinline__ void ex_publish(const ExState &S, int T, unsigned pro
                        __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// known_flag as the 3x3 target test sees it at the start of layer L (functions.py:81-90)
-__device__ __forceinline__ bool ex_known_at_start(const ExSweep &A, int jj, int ii, int L) {
-    const long wd = (long)jj * A.W + (ii >> 6);
-    const u64 bit = 1ull << (ii & 63);
-    if (A.kbits[wd] & bit) return true;
-    if (!(A.cbits[wd] & bit)) return false;
-    return ld_sc1_u8(A.lay + (long)jj * A.nx + ii) <= L;
-}
-
-// one window cell: geometry, weight and (static) value before the wait
-struct ExCell {
-    long cc;
-    double xi, yi, w, b1, b2;
-    bool geo;      // inside the grid and within the stencil radius
-    bool kstat;    // known before the launch (solid)
-    bool cand;     // may become known during the sweep
+// A wave's view of the rows around its row j: lane l holds word (wb - 1 + l) of each plane
+// (0 outside the grid), so a fit's window masks are read with readlane, not loaded.
+struct ExRow {
+    u64 ks[9];   // kbits, rows j-4..j+4
+    u64 ca[4];   // cbits, rows j-4..j-1 (may become known while this row runs)
+    u64 kn[5];   // known: row j = K[L] (start of layer + this row's own fits), rows j+1..j+4 =
+                 // K[L-1] (no layer-L fit of those rows lies inside a window of row j yet)
 };
 
-__device__ __forceinline__ ExCell ex_cell(const ExSweep &A, int q, int j, int i, double x0,
-                                          double y0, double r2) {
-    ExCell e{};
-    const int jj = j - 4 + q / 9, ii = i - 4 + q % 9;
-    const bool in = q < EX_WIN && jj >= 0 && jj < A.ny && ii >= 0 && ii < A.nx;
-    e.geo = false; e.kstat = false; e.cand = false;
-    e.cc = in ? (long)jj * A.nx + ii : 0;
-    e.xi = A.dx * ii; e.yi = A.dy * jj;
-    e.w = 0.0; e.b1 = 0.0; e.b2 = 0.0;
-    if (in) {
-        const double ax = e.xi - x0, ay = e.yi - y0;
-        const double d2 = ax * ax + ay * ay;
-        e.geo = d2 <= r2;
-        if (e.geo) {
-            const long wd = (long)jj * A.W + (ii >> 6);
-            const u64 bit = 1ull << (ii & 63);
-            e.kstat = (A.kbits[wd] & bit) != 0;
-            e.cand = !e.kstat && (A.cbits[wd] & bit) != 0;
-            if (e.kstat || e.cand) e.w = exp_glibc(-d2 / r2);   // libm exp, bit for bit
-            if (e.kstat) { e.b1 = A.X1e[e.cc]; e.b2 = A.X2e[e.cc]; }
-        }
-    }
-    return e;
+// columns cb..cb+8 of a row held one word per lane; la = lane of word cb >> 6, sh = cb & 63
+__device__ __forceinline__ unsigned ex_slice(u64 reg, int la, int sh) {
+    const u64 lo = readlane64(reg, la), hi = readlane64(reg, la + 1);
+    const u64 v = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    return (unsigned)(v & 0x1ff);
 }
 
-// after the wait: is the cell known now, and its value (functions.py:105-119)
-__device__ __forceinline__ bool ex_cell_live(const ExSweep &A, ExCell &e, int L) {
-    if (!e.geo) return false;
-    if (e.kstat) return true;
-    if (!e.cand) return false;
-    if (ld_sc1_u8(A.lay + e.cc) > L + 1) return false;
-    e.b1 = ld_sc1_f64(A.X1e + e.cc);
-    e.b2 = ld_sc1_f64(A.X2e + e.cc);
-    return true;
+// 81-bit window mask (bit q = 9 * row + col) as lo (q < 64) / hi (q >= 64)
+__device__ __forceinline__ void ex_put(u64 &lo, u64 &hi, int r, unsigned m) {
+    const int b = 9 * r;
+    if (b + 9 <= 64) lo |= (u64)m << b;
+    else if (b < 64) { lo |= (u64)m << b; hi |= (u64)m >> (64 - b); }
+    else hi |= (u64)m << (b - 64);
 }
 
-__device__ __forceinline__ void ex_terms(double *t, int q, const ExCell &e, bool inc) {
-    // t is the wave's [12][EX_WIN] buffer; excluded cells contribute +0.0 (exact: the sums
-    // start at +0.0 and never become -0.0)
-    double v[12];
-    if (inc) {
-        const double wa0 = e.w * 1.0, wa1 = e.w * e.xi, wa2 = e.w * e.yi;
-        v[0] = wa0 * e.b1; v[1] = wa1 * e.b1; v[2] = wa2 * e.b1;
-        v[3] = wa0 * e.b2; v[4] = wa1 * e.b2; v[5] = wa2 * e.b2;
-        v[6] = wa0 * 1.0; v[7] = wa0 * e.xi; v[8] = wa0 * e.yi;
-        v[9] = wa1 * e.xi; v[10] = wa1 * e.yi; v[11] = wa2 * e.yi;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) v[k] = 0.0;
+constexpr int EXS = 82;   // term buffer row stride (16-B aligned rows)
+
+// diagnostic build (RMT_EX_PROFILE=1): per-phase shader-clock totals, see extrapolate()
+constexpr int EX_NPROF = 8;
+#define EX_STAMP(k)                                                     \
+    if constexpr (PROF) {                                               \
+        const long long t_ = __builtin_amdgcn_s_memtime();              \
+        prof[k] += t_ - t_last; t_last = t_;                            \
     }
-#pragma unroll
-    for (int k = 0; k < 12; ++k) t[k * EX_WIN + q] = v[k];
-}
 
 // fit target (j, i) of layer L; returns true if the cell became known
-__device__ bool ex_fit(const ExSweep &A, const ExState &S, double *tbuf, int T, int L, int j,
-                       int i, double r2, int lane, bool &ok) {
+template <bool PROF>
+__device__ bool ex_fit(const ExSweep &A, const ExState &S, double *tbuf, const u64 *tab, int L,
+                       int j, int i, double r2, int lane, int wb, ExRow &R, bool &ok,
+                       long long *prof, long long &t_last) {
     const double x0 = A.dx * i, y0 = A.dy * j;
-    ExCell c0 = ex_cell(A, lane, j, i, x0, y0, r2);
-    ExCell c1 = ex_cell(A, lane + 64, j, i, x0, y0, r2);
-    // wait for rows j-1..j-4 of this layer to pass column i+4
+    const int cb = i - 4, la = (cb >> 6) - wb + 1, sh = cb & 63;
+    // static / start-of-layer window masks from the row registers
+    u64 KSl = 0, KSh = 0, CAl = 0, CAh = 0, KBl = 0, KBh = 0;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) ex_put(KSl, KSh, r, ex_slice(R.ks[r], la, sh));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ex_put(CAl, CAh, r, ex_slice(R.ca[r], la, sh));
+#pragma unroll
+    for (int r = 0; r < 5; ++r) ex_put(KBl, KBh, r + 4, ex_slice(R.kn[r], la, sh));
+    // this lane's cells q = lane and q = lane + 64
+    double xi[2], yi[2], w[2], b1[2], b2[2];
+    bool maybe[2], kst[2], above[2], below[2];
+    long cc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = cb + q % 9;
+        const bool in = q < EX_WIN && jj >= 0 && jj < A.ny && ii >= 0 && ii < A.nx;
+        cc[h] = in ? (long)jj * A.nx + ii : 0;
+        xi[h] = A.dx * ii; yi[h] = A.dy * jj;
+        const u64 ksm = h ? KSh : KSl, cam = h ? CAh : CAl, kbm = h ? KBh : KBl;
+        kst[h] = (ksm >> lane) & 1;
+        above[h] = !kst[h] && ((cam >> lane) & 1);
+        below[h] = (kbm >> lane) & 1;
+        double d2 = 0.0;
+        bool geo = false;
+        if (in) {
+            const double ax = xi[h] - x0, ay = yi[h] - y0;
+            d2 = ax * ax + ay * ay;
+            geo = d2 <= r2;
+        }
+        maybe[h] = geo && (kst[h] || above[h] || below[h]);
+        w[h] = maybe[h] ? exp_glibc_tab(-d2 / r2, tab) : 0.0;   // libm exp, bit for bit
+        b1[h] = 0.0; b2[h] = 0.0;
+    }
+    EX_STAMP(1);
+    // rows j-1..j-4 of this layer must have passed column i+4
     const unsigned need = (unsigned)(i + 5);
     long spins = 0;
     for (int r = 1; r <= 4; ++r)
         while (ex_progress(S, L, j - r) < need)
             if (!ex_spin(S, spins)) { ok = false; return false; }
-    const bool inc0 = ex_cell_live(A, c0, L), inc1 = ex_cell_live(A, c1, L);
-    ex_terms(tbuf, lane, c0, inc0);
-    if (lane < EX_WIN - 64) ex_terms(tbuf, lane + 64, c1, inc1);
-    const int count = __popcll(__ballot(inc0)) + __popcll(__ballot(inc1 && lane < EX_WIN - 64));
+    EX_STAMP(2);
+    // one round trip: K[L] words of rows j-4..j-1 (lanes 0..7) and every value that may be known
+    u64 kw = 0;
+    {
+        const int r = lane >> 1, jj = j - 4 + r, wd = (cb >> 6) + (lane & 1);
+        if (lane < 8 && jj >= 0 && wd >= 0 && wd < A.W)
+            kw = ld_sc1_u64(A.K + ((long)L * A.ny + jj) * A.W + wd);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+        if (maybe[h]) {
+            if (kst[h]) { b1[h] = A.X1e[cc[h]]; b2[h] = A.X2e[cc[h]]; }
+            else { b1[h] = ld_sc1_f64(A.X1e + cc[h]); b2[h] = ld_sc1_f64(A.X2e + cc[h]); }
+        }
+    u64 KAl = 0, KAh = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const u64 lo = readlane64(kw, 2 * r), hi = readlane64(kw, 2 * r + 1);
+        const u64 v = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+        ex_put(KAl, KAh, r, (unsigned)(v & 0x1ff));
+    }
+    bool inc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const bool ka = ((h ? KAh : KAl) >> lane) & 1;
+        inc[h] = maybe[h] && (kst[h] || below[h] || (above[h] && ka));
+    }
+    inc[1] = inc[1] && lane < EX_WIN - 64;
+    if constexpr (PROF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    EX_STAMP(3);
+    // terms of functions.py:128-145; excluded cells contribute +0.0 (exact: the sums start at
+    // +0.0 and never become -0.0)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h == 1 && lane >= EX_WIN - 64) break;
+        const int q = lane + 64 * h;
+        double v[12];
+        const double wa0 = w[h] * 1.0, wa1 = w[h] * xi[h], wa2 = w[h] * yi[h];
+        v[0] = wa0 * b1[h]; v[1] = wa1 * b1[h]; v[2] = wa2 * b1[h];
+        v[3] = wa0 * b2[h]; v[4] = wa1 * b2[h]; v[5] = wa2 * b2[h];
+        v[6] = wa0 * 1.0; v[7] = wa0 * xi[h]; v[8] = wa0 * yi[h];
+        v[9] = wa1 * xi[h]; v[10] = wa1 * yi[h]; v[11] = wa2 * yi[h];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) tbuf[k * EXS + q] = inc[h] ? v[k] : 0.0;
+    }
+    const int count = __popcll(__ballot(inc[0])) + __popcll(__ballot(inc[1]));
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     double acc = 0.0;
     if (lane < 12) {
-        const double *t = tbuf + lane * EX_WIN;
+        // functions.py:128-145 loop order; 41 LDS reads issued ahead of the dependent adds
+        const double2 *t2 = (const double2 *)(tbuf + lane * EXS);
+        double2 t[40];
 #pragma unroll
-        for (int q = 0; q < EX_WIN; ++q) acc += t[q];   // functions.py:128-145 loop order
+        for (int q2 = 0; q2 < 40; ++q2) t[q2] = t2[q2];
+        const double last = tbuf[lane * EXS + 80];
+#pragma unroll
+        for (int q2 = 0; q2 < 40; ++q2) {
+            acc += t[q2].x;
+            acc += t[q2].y;
+        }
+        acc += last;
     }
     __builtin_amdgcn_wave_barrier();
+    if constexpr (PROF) asm volatile("" : "+v"(acc));
+    EX_STAMP(4);
     if (count < 3) return false;
     const double B10 = readlane_f64(acc, 0), B11 = readlane_f64(acc, 1), B12 = readlane_f64(acc, 2);
     const double B20 = readlane_f64(acc, 3), B21 = readlane_f64(acc, 4), B22 = readlane_f64(acc, 5);
@@ -287,34 +343,48 @@ __device__ bool ex_fit(const ExSweep &A, const ExState &S, double *tbuf, int T, 
                           b[0] * (M[3] * M[7] - M[4] * M[6])) * inv_det;
         o[s] = x + y * x0 + z * y0;
     }
+    const u64 bit = 1ull << (i & 63);
     if (lane == 0) {
-        const long c = (long)j * A.nx + i;
-        A.X1e[c] = o[0];
-        A.X2e[c] = o[1];
-        A.lay[c] = (unsigned char)(L + 1);
+        const long c0 = (long)j * A.nx + i, wd = (long)j * A.W + (i >> 6), plane = (long)A.ny * A.W;
+        A.X1e[c0] = o[0];
+        A.X2e[c0] = o[1];
+        for (int Lp = L; Lp < A.ML; ++Lp)
+            __hip_atomic_fetch_or(A.K + Lp * plane + wd, bit, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (lane == (i >> 6) - wb + 1) R.kn[0] |= bit;   // the next targets of this row see it
+    if constexpr (PROF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    EX_STAMP(5);
     return true;
 }
 
-__global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A) {
+template <bool PROF>
+__global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A, long long *gprof) {
     __shared__ u64 ring[EX_RING];
-    __shared__ double term[EXW][12 * EX_WIN];
+    __shared__ __attribute__((aligned(16))) double term[EXW][12 * EXS];
+    __shared__ u64 tab[256];
     __shared__ int s_ticket, s_abort;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int s = threadIdx.x; s < EX_RING; s += blockDim.x)
         ring[s] = ((u64)(unsigned)(s - EX_RING) << 32) | EX_DONE;   // virtual done tickets
+    for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
     if (threadIdx.x == 0) { s_ticket = 0; s_abort = 0; }
     __syncthreads();
     ExState S{ring, &s_abort, A.jrange[0], A.jrange[1], A.ML};
     if (S.jhi < S.jlo) return;   // no candidates at all
-    const int ML = A.ML;
+    const int ML = A.ML, W = A.W, ny = A.ny;
     const int ntick = (S.jhi - S.jlo + 1 + 5 * (ML - 1)) * ML;
     double r = 4 * sqrt(A.dx * A.dx + A.dy * A.dy);
     const double r2 = r * r;
+    const long plane = (long)ny * W;
     double *tbuf = term[wv];
     int filled = 0;
     bool ok = true;
+    long long prof[EX_NPROF] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long t_last = 0;
+    if constexpr (PROF) t_last = __builtin_amdgcn_s_memtime();
     for (;;) {
+        EX_STAMP(0);
         int T = 0;
         if (lane == 0) T = atomicAdd(&s_ticket, 1);
         T = __builtin_amdgcn_readfirstlane(T);
@@ -334,6 +404,7 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A) {
         const bool active = j >= S.jlo && j <= S.jhi && A.rowcand[j];
         if (!active) { ex_publish(S, T, EX_DONE); continue; }
         ex_publish(S, T, 0);
+        if constexpr (PROF) prof[7] += 1;
         // rows j-4..j+4 of the previous layer complete
         if (L > 0) {
             for (int rr = -4; rr <= 4 && ok; ++rr)
@@ -341,26 +412,49 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A) {
                     if (!ex_spin(S, spins)) { ok = false; break; }
             if (!ok) break;
         }
-        // targets of row j, in column order (functions.py:81-90 then :95-96)
-        for (int wb = 0; wb < A.W && ok; wb += 64) {
-            const int w = wb + lane;
-            const u64 cw = w < A.W ? A.cbits[(long)j * A.W + w] : 0;
-            u64 tw = 0;
-            for (u64 m = cw; m; m &= m - 1) {
-                const int b = __builtin_ctzll(m), i = 64 * w + b;
-                if (ld_sc1_u8(A.lay + (long)j * A.nx + i) <= L) continue;   // known already
-                bool nb = false;
-                for (int dj = -1; dj <= 1 && !nb; ++dj)
-                    for (int di = -1; di <= 1 && !nb; ++di)
-                        nb = ex_known_at_start(A, j + dj, i + di, L);
-                if (nb) tw |= 1ull << b;
+        EX_STAMP(6);
+        const u64 *Kp = L > 0 ? A.K + (long)(L - 1) * plane : A.kbits, *KL = A.K + (long)L * plane;
+        // chunks of 62 words: lanes hold words wb-1 .. wb+62, targets lie in wb .. wb+61
+        for (int wb = 0; wb < W && ok; wb += 62) {
+            const int wl = wb - 1 + lane;
+            const bool wok = wl >= 0 && wl < W;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own earlier K updates landed
+            ExRow R;
+#pragma unroll
+            for (int r = 0; r < 9; ++r) {
+                const int jj = j - 4 + r;
+                R.ks[r] = wok && jj >= 0 && jj < ny ? A.kbits[(long)jj * W + wl] : 0;
             }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jj = j - 4 + r;
+                R.ca[r] = wok && jj >= 0 ? A.cbits[(long)jj * W + wl] : 0;
+            }
+            R.kn[0] = wok ? ld_sc1_u64(KL + (long)j * W + wl) : 0;
+#pragma unroll
+            for (int r = 1; r < 5; ++r) {
+                const int jj = j + r;
+                R.kn[r] = wok && jj < ny ? ld_sc1_u64(Kp + (long)jj * W + wl) : 0;
+            }
+            // targets (functions.py:81-90): candidates unknown at the start of layer L with a
+            // known 3x3 neighbour at the start of layer L
+            const u64 km1 = wok ? ld_sc1_u64(Kp + (long)(j - 1) * W + wl) : 0;
+            const u64 k0 = wok ? ld_sc1_u64(Kp + (long)j * W + wl) : 0;
+            const u64 cw = wok ? A.cbits[(long)j * W + wl] : 0;
+            const u64 m = km1 | k0 | R.kn[1];
+            const u64 a = (u64)__shfl((long long)m, (lane + 63) & 63);
+            const u64 e = (u64)__shfl((long long)m, (lane + 1) & 63);
+            u64 tw = 0;
+            if (lane >= 1 && lane <= 62 && wok)
+                tw = cw & ~k0 & (m | (m << 1) | (m >> 1) | (a >> 63) | (e << 63));
             for (u64 lanes = __ballot(tw != 0); lanes && ok; lanes &= lanes - 1) {
                 const int src = __builtin_ctzll(lanes);
                 for (u64 t = readlane64(tw, src); t && ok; t &= t - 1) {
-                    const int i = 64 * (wb + src) + __builtin_ctzll(t);
+                    const int i = 64 * (wb - 1 + src) + __builtin_ctzll(t);
                     ex_publish(S, T, (unsigned)i);   // every target left of i is done
-                    if (ex_fit(A, S, tbuf, T, L, j, i, r2, lane, ok)) ++filled;
+                    EX_STAMP(0);
+                    if (ex_fit<PROF>(A, S, tbuf, tab, L, j, i, r2, lane, wb, R, ok, prof, t_last))
+                        ++filled;
                 }
             }
         }
@@ -370,12 +464,14 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A) {
     if (lane == 0) {
         atomicAdd(&A.status[0], filled);
         if (!ok) atomicExch(&A.status[1], 1);
+        if constexpr (PROF)
+            for (int k = 0; k < EX_NPROF; ++k) atomicAdd((unsigned long long *)&gprof[k], prof[k]);
     }
 }
 
-size_t extrap_workspace(int ny, int nx) {
-    const size_t n = (size_t)ny * nx, W = (nx + 63) / 64;
-    return 2 * (size_t)ny * W * 8 + (n + 255) / 256 * 256 + ((size_t)ny + 255) / 256 * 256 + 64;
+size_t extrap_workspace(int ny, int nx, int max_layers) {
+    const size_t W = (nx + 63) / 64, plane = (size_t)ny * W * 8;
+    return (2 + (size_t)std::max(max_layers, 1)) * plane + ((size_t)ny + 255) / 256 * 256 + 64;
 }
 
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
@@ -388,23 +484,49 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
         if (X2o != X2) RMT_HIP(hipMemcpyAsync(X2o, X2, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
         return RMT_OK;
     }
-    RMT_CHECK(ny >= 3 && nx >= 3 && ny < (1 << 20), RMT_EINVAL, "extrapolation grid size");
-    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx)));
-    // byte workspace: kbits | cbits | layer bytes | row flags | jrange[2], status[4]
-    u64 *kbits = (u64 *)ctx->bytes, *cbits = kbits + (size_t)ny * W;
-    unsigned char *lay = (unsigned char *)(cbits + (size_t)ny * W);
-    unsigned char *rowcand = lay + (n + 255) / 256 * 256;
+    RMT_CHECK(ny >= 3 && nx >= 3 && ny < (1 << 20) && nx < (1 << 30), RMT_EINVAL,
+              "extrapolation grid size");
+    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, max_layers)));
+    // byte workspace: kbits | cbits | K[0..ML-1] | row flags | jrange[2], status[4]
+    const size_t plane = (size_t)ny * W;
+    u64 *kbits = (u64 *)ctx->bytes, *cbits = kbits + plane, *K = cbits + plane;
+    unsigned char *rowcand = (unsigned char *)(K + plane * max_layers);
     int *jrange = (int *)(rowcand + ((size_t)ny + 255) / 256 * 256), *status = jrange + 2;
     const int copy = (X1o != X1) || (X2o != X2);
-    k_ex_bits<<<dim3((nx + 255) / 256, ny), 256, 0, ctx->stream>>>(phi, ny, nx, W, kbits, rowcand,
-                                                                   jrange, X1, X2, X1o, X2o, copy);
+    k_ex_bits<<<dim3((nx + 255) / 256, ny), 256, 0, ctx->stream>>>(
+        phi, ny, nx, W, max_layers, kbits, K, rowcand, jrange, X1, X2, X1o, X2o, copy);
     k_ex_dilate<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(kbits, ny, nx, W, max_layers,
-                                                                    cbits, lay, rowcand, jrange);
+                                                                    cbits, rowcand, jrange);
     RMT_HIP(hipMemsetAsync(status, 0, 4 * sizeof(int), ctx->stream));
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
-    ExSweep A{X1o, X2o, lay, kbits, cbits, rowcand, jrange, ny, nx, W, max_layers, dx, dy, status};
-    k_ex_sweep<<<1, EXW * 64, 0, ctx->stream>>>(A);
-    RMT_LAUNCHED();
+    ExSweep A{X1o, X2o, kbits, cbits, K, rowcand, jrange, ny, nx, W, max_layers, dx, dy, status};
+    static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
+    if (!prof) {
+        k_ex_sweep<false><<<1, EXW * 64, 0, ctx->stream>>>(A, nullptr);
+        RMT_LAUNCHED();
+    } else {
+        // diagnostic: phase totals summed over waves, in shader clocks (s_memtime)
+        long long *gp = nullptr, hp[EX_NPROF];
+        int hs[2];
+        RMT_HIP(hipMalloc(&gp, sizeof(hp)));
+        RMT_HIP(hipMemsetAsync(gp, 0, sizeof(hp), ctx->stream));
+        hipEvent_t e0, e1;
+        RMT_HIP(hipEventCreate(&e0)); RMT_HIP(hipEventCreate(&e1));
+        RMT_HIP(hipEventRecord(e0, ctx->stream));
+        k_ex_sweep<true><<<1, EXW * 64, 0, ctx->stream>>>(A, gp);
+        RMT_LAUNCHED();
+        RMT_HIP(hipEventRecord(e1, ctx->stream));
+        RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, ctx->stream));
+        RMT_HIP(hipMemcpyAsync(hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
+        RMT_HIP(hipStreamSynchronize(ctx->stream));
+        float ms = 0;
+        RMT_HIP(hipEventElapsedTime(&ms, e0, e1));
+        fprintf(stderr, "[ex-prof] %.3f ms fitted=%d rows=%lld | ticket+targets %.3g rowwait %.3g "
+                "window %.3g wait %.3g load %.3g sum %.3g solve+store %.3g (Mclk, all waves)\n",
+                ms, hs[0], hp[7], hp[0] / 1e6, hp[6] / 1e6, hp[1] / 1e6, hp[2] / 1e6,
+                hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6);
+        hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
+    }
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
     if (dev_status)
         RMT_HIP(hipMemcpyAsync(dev_status, status, 2 * sizeof(int), hipMemcpyDeviceToDevice,

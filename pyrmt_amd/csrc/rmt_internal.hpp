@@ -295,6 +295,6 @@ void dct_destroy(DctPlan *);
 // dev_status (optional, device): receives {cells fitted, aborted} after the sweep
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
                 double dy, int max_layers, double *X1o, double *X2o, int *dev_status = nullptr);
-size_t extrap_workspace(int ny, int nx);   // bytes of ctx->bytes the extrapolation uses
+size_t extrap_workspace(int ny, int nx, int max_layers);   // bytes of ctx->bytes it uses
 
 }  // namespace rmt

@@ -241,7 +241,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     // size the shared scratch once (WENO5: 3 planes, projection: 2) and the extrapolation's
     // byte workspace, so nothing is reallocated while kernels are queued
     RMT_TRY(ensure_scratch(ctx, 3 * n * sizeof(double)));
-    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx)));
+    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, prm->layers)));
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
     return RMT_OK;
