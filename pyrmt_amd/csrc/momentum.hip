@@ -117,6 +117,171 @@ __global__ void k_stage_rhs(const double *__restrict__ us, const double *__restr
     }
 }
 
+// Fused stage: the three passes above in one LDS-tiled kernel (same arithmetic, same operand
+// order).  Tile MS_TX x MS_TY output cells; the BC'd stage velocity is staged on the tile plus
+// a 3-cell halo and the blended stress on the tile plus a 2-cell halo, which holds every
+// point the one-sided edge stencils of grad2 / upwind3 reach.  Tiles are dealt so that the
+// blocks of one XCD take a contiguous band of tile rows (shared halos stay in that XCD's L2).
+constexpr int MS_TX = 64, MS_TY = 16, MS_T = 512;
+constexpr int MS_UX = MS_TX + 6, MS_UY = MS_TY + 6;
+constexpr int MS_GX = MS_TX + 4, MS_GY = MS_TY + 4;
+constexpr int MS_NU = (MS_UX * MS_UY + MS_T - 1) / MS_T;   // per-thread items, phase 1
+constexpr int MS_NG = (MS_GX * MS_GY + MS_T - 1) / MS_T;   // phase 2
+constexpr int MS_NO = (MS_TX * MS_TY + MS_T - 1) / MS_T;   // phase 3
+
+__device__ __forceinline__ int xcd_tile(int b, int nb) {
+    const int per = nb / 8;
+    return b < 8 * per ? (b % 8) * per + b / 8 : b;
+}
+
+__global__ void __launch_bounds__(MS_T) k_mom_stage(
+    const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
+    const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
+    const double *__restrict__ sxx, const double *__restrict__ sxy,
+    const double *__restrict__ syy, const double *__restrict__ H,
+    const unsigned char *__restrict__ solid, int visc, double mu_f, double eta_s, double rho_s,
+    double rho_f, const double *__restrict__ p, double dt6, double dx, double dy, int ny, int nx,
+    int tiles_x, int ntiles, double *__restrict__ ku, double *__restrict__ kv,
+    double *__restrict__ accu, double *__restrict__ accv, double *__restrict__ outu,
+    double *__restrict__ outv) {
+    __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
+    __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
+    const int tile = xcd_tile(blockIdx.x, ntiles);
+    const int i0 = (tile % tiles_x) * MS_TX, j0 = (tile / tiles_x) * MS_TY;
+    const double h2x = 2 * dx, h2y = 2 * dy;
+    // 1. stage velocity (functions.py:714), BC applied; all loads issued before the LDS stores
+    {
+        double a[MS_NU], b[MS_NU], ka[MS_NU], kb[MS_NU];
+        bool ok[MS_NU], uc[MS_NU], vc[MS_NU];
+        double uval[MS_NU];
+#pragma unroll
+        for (int it = 0; it < MS_NU; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q % MS_UX;
+            const int j = j0 - 3 + ry, i = i0 - 3 + rx;
+            ok[it] = q < MS_UX * MS_UY && j >= 0 && j < ny && i >= 0 && i < nx;
+            const BCSrc s = bc_source(bc, lid, ok[it] ? j : 1, ok[it] ? i : 1, ny, nx);
+            uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
+            const long cu = ok[it] ? s.u_src : 0, cv = ok[it] ? s.v_src : 0;
+            a[it] = u[cu]; b[it] = v[cv];
+            ka[it] = stage ? kpu[cu] : 0.0; kb[it] = stage ? kpv[cv] : 0.0;
+        }
+#pragma unroll
+        for (int it = 0; it < MS_NU; ++it) {
+            const int q = threadIdx.x + it * MS_T;
+            if (q >= MS_UX * MS_UY) break;
+            const double ru = stage == 0 ? a[it] : a[it] + coef * ka[it];
+            const double rv = stage == 0 ? b[it] : b[it] + coef * kb[it];
+            (&su[0][0])[q] = !ok[it] ? 0.0 : uc[it] ? uval[it] : ru;
+            (&sv[0][0])[q] = !ok[it] ? 0.0 : vc[it] ? 0.0 : rv;
+        }
+    }
+    __syncthreads();
+    // 2. blended stress (functions.py:717-735, 906-921)
+    {
+        double ex[MS_NG], ey[MS_NG], exy[MS_NG], hh[MS_NG];
+        bool sol[MS_NG], ok[MS_NG];
+#pragma unroll
+        for (int it = 0; it < MS_NG; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
+            const int j = j0 - 2 + ry, i = i0 - 2 + rx;
+            ok[it] = q < MS_GX * MS_GY && j >= 0 && j < ny && i >= 0 && i < nx;
+            const long c = ok[it] ? (long)j * nx + i : 0;
+            ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh[it] = H[c];
+            sol[it] = solid[c] != 0;
+        }
+#pragma unroll
+        for (int it = 0; it < MS_NG; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
+            if (q >= MS_GX * MS_GY) break;
+            const int j = j0 - 2 + ry, i = i0 - 2 + rx;
+            double oxx = 0.0, oxy = 0.0, oyy = 0.0;
+            if (ok[it]) {
+                const double *pu = &su[ry + 1][rx + 1], *pv = &sv[ry + 1][rx + 1];
+                const double dudx = grad2(pu, 1, i, nx, h2x), dvdy = grad2(pv, MS_UX, j, ny, h2y);
+                const double dudy = grad2(pu, MS_UX, j, ny, h2y), dvdx = grad2(pv, 1, i, nx, h2x);
+                double e1 = ex[it], e2 = ey[it], e3 = exy[it];
+                if (visc && sol[it]) {
+                    e1 = e1 + eta_s * dudx;
+                    e2 = e2 + eta_s * dvdy;
+                    e3 = e3 + eta_s * 0.5 * (dudy + dvdx);
+                }
+                const double h = hh[it], omh = 1 - h;
+                oxx = h * (2 * mu_f * dudx) + omh * e1;
+                oyy = h * (2 * mu_f * dvdy) + omh * e2;
+                oxy = h * (mu_f * (dudy + dvdx)) + omh * e3;
+            }
+            (&gx[0][0])[q] = oxx; (&gm[0][0])[q] = oxy; (&gy[0][0])[q] = oyy;
+        }
+    }
+    __syncthreads();
+    // 3. RHS and RK4 accumulation (functions.py:923-944, 743-758)
+    {
+        double pc[MS_NO], pxm[MS_NO], pxp[MS_NO], pym[MS_NO], pyp[MS_NO], hh[MS_NO];
+        double x0[MS_NO], x1[MS_NO], y0[MS_NO], y1[MS_NO];
+        bool ok[MS_NO];
+#pragma unroll
+        for (int it = 0; it < MS_NO; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+            const int j = j0 + ry, i = i0 + rx;
+            ok[it] = q < MS_TX * MS_TY && j < ny && i < nx;
+            const long c = ok[it] ? (long)j * nx + i : 0;
+            // grad2(p) operands (functions.py:941): centred inside, one-sided at the edges
+            // (inside: c+1 / c-1; i == 0: c+1; i == nx-1: c-1 as the "+s" operand; the "-s"
+            // operand only inside) -- every index stays in the grid
+            const bool ex = i == 0 || i == nx - 1, ey = j == 0 || j == ny - 1;
+            const long sx = i == nx - 1 ? -1 : 1, sy = j == ny - 1 ? -(long)nx : (long)nx;
+            pc[it] = p[c];
+            pxp[it] = ok[it] ? p[c + sx] : 0.0; pxm[it] = ok[it] && !ex ? p[c - 1] : 0.0;
+            pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !ey ? p[c - nx] : 0.0;
+            hh[it] = H[c];
+            // accumulation operands
+            x0[it] = stage == 1 ? kpu[c] : (stage >= 2 ? accu[c] : 0.0);
+            y0[it] = stage == 1 ? kpv[c] : (stage >= 2 ? accv[c] : 0.0);
+            x1[it] = stage == 3 ? u[c] : 0.0;
+            y1[it] = stage == 3 ? v[c] : 0.0;
+        }
+#pragma unroll
+        for (int it = 0; it < MS_NO; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+            const int j = j0 + ry, i = i0 + rx;
+            if (!ok[it]) continue;
+            const long c = (long)j * nx + i;
+            const double divx = grad2(&gx[ry + 2][rx + 2], 1, i, nx, h2x) +
+                                grad2(&gm[ry + 2][rx + 2], MS_GX, j, ny, h2y);
+            const double divy = grad2(&gm[ry + 2][rx + 2], 1, i, nx, h2x) +
+                                grad2(&gy[ry + 2][rx + 2], MS_GX, j, ny, h2y);
+            const double *pu = &su[ry + 3][rx + 3], *pv = &sv[ry + 3][rx + 3];
+            const double uc = *pu, vc = *pv;
+            const double uadv = -uc * upwind3(pu, 1, i, nx, uc, dx) - vc * upwind3(pu, MS_UX, j, ny, vc, dy);
+            const double vadv = -uc * upwind3(pv, 1, i, nx, uc, dx) - vc * upwind3(pv, MS_UX, j, ny, vc, dy);
+            // grad2 of p with the operands loaded above (same expressions as grad2)
+            double dpx, dpy;
+            if (i == 0) dpx = (-3 * pc[it] + 4 * pxp[it] - p[c + 2]) / h2x;
+            else if (i == nx - 1) dpx = (3 * pc[it] - 4 * pxp[it] + p[c - 2]) / h2x;
+            else dpx = (pxp[it] - pxm[it]) / h2x;
+            if (j == 0) dpy = (-3 * pc[it] + 4 * pyp[it] - p[c + 2L * nx]) / h2y;
+            else if (j == ny - 1) dpy = (3 * pc[it] - 4 * pyp[it] + p[c - 2L * nx]) / h2y;
+            else dpy = (pyp[it] - pym[it]) / h2y;
+            const double h = hh[it];
+            const double den = ((1 - h) * rho_s + h * rho_f) + 1e-12;
+            const double k1 = uadv + (divx + 0.0 - dpx) / den;
+            const double k2 = vadv + (divy + 0.0 - dpy) / den;
+            if (stage == 0) {
+                ku[c] = k1; kv[c] = k2;
+            } else if (stage == 1) {
+                accu[c] = x0[it] + 2 * k1; accv[c] = y0[it] + 2 * k2;
+                ku[c] = k1; kv[c] = k2;
+            } else if (stage == 2) {
+                accu[c] = x0[it] + 2 * k1; accv[c] = y0[it] + 2 * k2;
+                ku[c] = k1; kv[c] = k2;
+            } else {
+                outu[c] = x1[it] + dt6 * (x0[it] + k1);
+                outv[c] = y1[it] + dt6 * (y0[it] + k2);
+            }
+        }
+    }
+}
+
 // Final BC (functions.py:760) on the boundary cells only: 2(nx + ny) threads.
 __global__ void k_bc_edges(int kind, double lid, double *u, double *v, int ny, int nx) {
     int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -151,7 +316,17 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     const double coef[4] = {0.0, 0.5 * P->dt, 0.5 * P->dt, P->dt}, dt6 = P->dt / 6.0;
     double *kbu[2] = {W.k1u, W.k2u}, *kbv[2] = {W.k1v, W.k2v};
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-    for (int s = 0; s < 4; ++s) {
+    static const bool unfused = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED"));
+    const int tiles_x = (nx + MS_TX - 1) / MS_TX, ntiles = tiles_x * ((ny + MS_TY - 1) / MS_TY);
+    for (int s = 0; s < 4 && !unfused; ++s) {
+        const double *kpu = s ? kbu[(s - 1) & 1] : u, *kpv = s ? kbv[(s - 1) & 1] : v;
+        k_mom_stage<<<ntiles, MS_T, 0, ctx->stream>>>(
+            u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid, visc,
+            P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx, tiles_x, ntiles,
+            kbu[s & 1], kbv[s & 1], W.accu, W.accv, u_new, v_new);
+        RMT_LAUNCHED();
+    }
+    for (int s = 0; s < 4 && unfused; ++s) {
         // stage 0 reads only u, v; kp* still point at valid planes
         const double *kpu = s ? kbu[(s - 1) & 1] : u, *kpv = s ? kbv[(s - 1) & 1] : v;
         k_stage_vel<<<g, 256, 0, ctx->stream>>>(u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid,
