@@ -26,6 +26,12 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # (reads u, v, p, X1, X2; writes u*, v*) = 7 planes x 8 B per cell for one RK4 pass.
 RK4_ALG_BYTES_PER_CELL = 7 * 8
 STEP_ALG_BYTES_PER_CELL = 208  # the whole step
+# HBM bytes per k_mom_stage launch at N=4096 from the PMC passes (FETCH_SIZE + WRITE_SIZE,
+# calibrated; profiles/r01/), None where not measured for this N
+TRAFFIC_PER_LAUNCH = 2134390187   # 15.9 planes: 12.9 read + 3.0 written (profiles/r01/hbm_traffic_n4096.md)
+# longest dependency chain of the bench-state extrapolation at N=4096 in fits, scheduled
+# row by row on 8 waves (tools/extrap_depth.py)
+CHAIN_DEPTH_4096 = 4493
 
 
 def _dist():
@@ -103,9 +109,11 @@ def main():
         value = cells / elapsed
         rk_ms, rk_launches = ph["rk4_stage_kernels"]
         per_launch_s = rk_ms / 1e3 / rk_launches
-        # achieved: algorithmic bytes of one RK4 pass (4 launches) spread over its launches
+        # achieved: SURVEY 8(d)'s algorithmic bytes of the stress + RK4 pass (7 planes per cell
+        # for the 4 stage launches) spread over the launches, / the HIP-event launch time
         alg_per_launch = RK4_ALG_BYTES_PER_CELL * N * N / 4
         achieved = alg_per_launch / per_launch_s / 1e9
+        ex_ms, ex_calls = ph["extrap_sweep_kernel"]
         out = {
             "metric": "cell-updates/s (full RMT step) at N=4096; achieved HBM GB/s vs peak",
             "value": value, "unit": "cell-updates/s", "n_gpus": ws, "steps": args.steps,
@@ -115,9 +123,17 @@ def main():
             "config": {"workload": f"soft_disc_in_lid_driven N={N} semilagrangian "
                                    "(configs 2/4 loop body)", "grid": N,
                        "parallelism": "replicas" if ws > 1 else "single-gpu"},
-            "roofline": {"bound": "hbm", "kernel": "k_mom_stage (RK4 stage, 4 launches/step)",
+            # the dominant HBM-bound kernel: the fused RK4 stage (4 launches per step)
+            "roofline": {"bound": "hbm", "kernel": "k_mom_stage (fused RK4 stage, 4 launches/step)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": TRAFFIC_PER_LAUNCH if N == 4096 else None,
+                         "launch_ms": per_launch_s * 1e3,
+                         "alg_bytes_per_launch": alg_per_launch},
+            # the dominant kernel by time is not HBM-bound: the exact raster-order extrapolation
+            # chain runs on one workgroup, bounded by its dependency depth
+            "latency_bound": {"kernel": "k_ex_sweep (exact serial-order extrapolation chain)",
+                              "ms_per_step": ex_ms / max(1, ex_calls),
+                              "critical_path_fits": CHAIN_DEPTH_4096 if N == 4096 else None},
             "step_roofline": {"alg_bytes_per_cell": STEP_ALG_BYTES_PER_CELL,
                               "achieved_GBs": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9,
                               "frac": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9 / HBM_PEAK_GBS},
