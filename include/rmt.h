@@ -94,6 +94,12 @@ int rmt_all_finite2(rmt_ctx *ctx, const double *a, const double *b, int *finite)
 int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, const double *X2,
                                   const double *phi, double dx, double dy, int max_layers,
                                   double *X1_out, double *X2_out);
+/* librmt diagnostics for the extrapolation (no reference counterpart).  mode 0 (default):
+ * geometry-first chain path, row-ticket sweep when its capacity limits are exceeded;
+ * 1: sweep only; 2: chain path's pre-passes, then the sweep forced.  rmt_extrap_last_path
+ * (blocks) reports what the last call on ctx ran: 0 chain, 1 sweep. */
+int rmt_extrap_set_mode(int mode);
+int rmt_extrap_last_path(rmt_ctx *ctx, int *path);
 
 /* functions.py:1366-1367 with benchmarks/common.py:55-57: phi = |xi - (x0,y0)| - R */
 int rmt_rebuild_phi_disc(rmt_ctx *ctx, const double *X1, const double *X2, double x0, double y0,

@@ -59,6 +59,8 @@ SIGNATURES = {
     "rmt_advect_weno5_rk3": (_I, [_P, _P, _P, _P, _D, _D, _D, _P, _D, _P]),
     "rmt_all_finite2": (_I, [_P, _P, _P, ctypes.POINTER(_I)]),
     "rmt_extrapolate_reference_map": (_I, [_P, _P, _P, _P, _D, _D, _I, _P, _P]),
+    "rmt_extrap_set_mode": (_I, [_I]),
+    "rmt_extrap_last_path": (_I, [_P, ctypes.POINTER(_I)]),
     "rmt_rebuild_phi_disc": (_I, [_P, _P, _P, _D, _D, _D, _P]),
     "rmt_solid_cauchy_stress": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _D, _D, _I, _P, _P, _P, _P]),
     "rmt_smoothed_heaviside": (_I, [_P, _P, _L, _D, _P]),

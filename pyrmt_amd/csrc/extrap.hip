@@ -31,12 +31,10 @@
 // Visibility: bytes written inside the sweep (fitted X values, K words) are stored with plain
 // stores / L2 atomics drained by s_waitcnt vmcnt(0) before the LDS progress word is released,
 // and read only with sc1 (L2) loads; bytes fixed before the launch use plain loads.
-#include "rmt_internal.hpp"
+#include "extrap.hpp"
 #include "exp_glibc.h"
 
 namespace rmt {
-
-typedef unsigned long long u64;
 
 constexpr int EXW = 8;                        // waves of the sweep workgroup (2 per SIMD)
 constexpr int EX_RING = 1024;                 // progress ring entries (tickets)
@@ -76,7 +74,9 @@ __global__ void __launch_bounds__(256) k_ex_bits(const double *__restrict__ phi,
 __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits, int ny, int nx,
                                                    int W, int L, u64 *__restrict__ cbits,
                                                    unsigned char *__restrict__ rowcand,
-                                                   int *__restrict__ jrange) {
+                                                   int *__restrict__ jrange,
+                                                   const int *__restrict__ ctl) {
+    if (ctl && !ctl[EXC_FALLBACK]) return;   // the chain path handled this call
     const long t = blockIdx.x * 256L + threadIdx.x;
     if (t >= (long)ny * W) return;
     const int j = (int)(t / W), w = (int)(t % W);
@@ -132,6 +132,7 @@ struct ExSweep {
     int ny, nx, W, ML;
     double dx, dy;
     int *status;   // [0] fitted cells, [1] abort
+    const int *ctl;   // chain-path control words (null: no chain path this call)
 };
 
 struct ExState {
@@ -364,6 +365,7 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A, long long *gpr
     __shared__ __attribute__((aligned(16))) double term[EXW][12 * EXS];
     __shared__ u64 tab[256];
     __shared__ int s_ticket, s_abort;
+    if (A.ctl && !A.ctl[EXC_FALLBACK]) return;   // the chain path handled this call
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int s = threadIdx.x; s < EX_RING; s += blockDim.x)
         ring[s] = ((u64)(unsigned)(s - EX_RING) << 32) | EX_DONE;   // virtual done tickets
@@ -469,9 +471,50 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A, long long *gpr
     }
 }
 
+static int g_ex_mode = 0;   // rmt_extrap_set_mode
+
+// byte workspace: both paths' bit planes, the chain path's tables and its record arena
+ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes) {
+    const int ML = std::max(max_layers, 1), W = (nx + 63) / 64;
+    const long plane = (long)ny * W;
+    const long interior = (long)std::max(ny - 2, 0) * std::max(nx - 2, 0);
+    const long maxt = std::max(64L, std::min((long)ML * interior, 4L * ML * (nx + ny) + 4096));
+    char *p = (char *)base;
+    size_t o = 0;
+    auto take = [&](size_t n) { char *q = p ? p + o : nullptr; o += (n + 255) & ~(size_t)255; return q; };
+    ExWs w{};
+    w.kbits = (u64 *)take(plane * 8);
+    w.cbits = (u64 *)take(plane * 8);
+    w.Kold = (u64 *)take(plane * 8 * ML);
+    w.rowcand = (unsigned char *)take(ny);
+    w.jrange = (int *)take(64);
+    w.status = w.jrange + 2;
+    w.T = (u64 *)take(plane * 8 * ML);
+    w.ACC = (u64 *)take(plane * 8 * ML);
+    w.KN = (u64 *)take(plane * 8 * ML);
+    w.rowcnt = (int *)take((size_t)ML * ny * 4);
+    w.rowoff = (int *)take((size_t)ML * (ny + 1) * 4);
+    w.wordoff = (int *)take(plane * 4 * ML);
+    w.cbase = (int *)take((size_t)ML * ny * 4);
+    w.tcell = (long long *)take(maxt * 8);
+    w.recoff = (long long *)take(maxt * 8);
+    w.rec_by_chain = (long long *)take(maxt * 8);
+    w.chain_of = (int *)take(maxt * 4);
+    w.dmark = (int *)take(maxt * 4);
+    w.rej = (int *)take((size_t)ML * EX_MAXREJ * 4);
+    w.ctl = (int *)take(EXC_WORDS * 4);
+    w.arena_bytes = maxt * 2560LL;   // ~2 KB per record on average at the bench sizes
+    w.arena = take(w.arena_bytes);
+    w.maxt = maxt;
+    w.plane = plane;
+    if (bytes) *bytes = o;
+    return w;
+}
+
 size_t extrap_workspace(int ny, int nx, int max_layers) {
-    const size_t W = (nx + 63) / 64, plane = (size_t)ny * W * 8;
-    return (2 + (size_t)std::max(max_layers, 1)) * plane + ((size_t)ny + 255) / 256 * 256 + 64;
+    size_t b = 0;
+    extrap_layout(nullptr, ny, nx, max_layers, &b);
+    return b;
 }
 
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
@@ -482,24 +525,37 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
     if (max_layers <= 0) {
         if (X1o != X1) RMT_HIP(hipMemcpyAsync(X1o, X1, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
         if (X2o != X2) RMT_HIP(hipMemcpyAsync(X2o, X2, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        if (dev_status) RMT_HIP(hipMemsetAsync(dev_status, 0, 2 * sizeof(int), ctx->stream));
         return RMT_OK;
     }
     RMT_CHECK(ny >= 3 && nx >= 3 && ny < (1 << 20) && nx < (1 << 30), RMT_EINVAL,
               "extrapolation grid size");
     RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, max_layers)));
-    // byte workspace: kbits | cbits | K[0..ML-1] | row flags | jrange[2], status[4]
-    const size_t plane = (size_t)ny * W;
-    u64 *kbits = (u64 *)ctx->bytes, *cbits = kbits + plane, *K = cbits + plane;
-    unsigned char *rowcand = (unsigned char *)(K + plane * max_layers);
-    int *jrange = (int *)(rowcand + ((size_t)ny + 255) / 256 * 256), *status = jrange + 2;
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
+    const int force = g_ex_mode;
+    const bool chain = force != 1 && extrap_chain_supported(ny, nx, max_layers);
+    ctx->ex_layers = max_layers;
+    ctx->ex_chain = chain;
     const int copy = (X1o != X1) || (X2o != X2);
     k_ex_bits<<<dim3((nx + 255) / 256, ny), 256, 0, ctx->stream>>>(
-        phi, ny, nx, W, max_layers, kbits, K, rowcand, jrange, X1, X2, X1o, X2o, copy);
-    k_ex_dilate<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(kbits, ny, nx, W, max_layers,
-                                                                    cbits, rowcand, jrange);
-    RMT_HIP(hipMemsetAsync(status, 0, 4 * sizeof(int), ctx->stream));
-    if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
-    ExSweep A{X1o, X2o, kbits, cbits, K, rowcand, jrange, ny, nx, W, max_layers, dx, dy, status};
+        phi, ny, nx, W, max_layers, ws.kbits, ws.Kold, ws.rowcand, ws.jrange, X1, X2, X1o, X2o,
+        copy);
+    RMT_HIP(hipMemsetAsync(ws.status, 0, 4 * sizeof(int), ctx->stream));
+    if (chain) {
+        RMT_HIP(hipMemsetAsync(ws.ctl, 0, EXC_WORDS * sizeof(int), ctx->stream));
+        if (force == 2) {   // diagnostic: exercise the fallback sweep behind the chain path
+            const int one = 1;
+            RMT_HIP(hipMemcpyAsync(ws.ctl + EXC_FALLBACK, &one, sizeof(int),
+                                   hipMemcpyHostToDevice, ctx->stream));
+        }
+        RMT_TRY(extrap_chain_launch(ctx, ws, X1o, X2o, dx, dy, max_layers));
+    }
+    const int *ctl = chain ? ws.ctl : nullptr;
+    k_ex_dilate<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(
+        ws.kbits, ny, nx, W, max_layers, ws.cbits, ws.rowcand, ws.jrange, ctl);
+    if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
+    ExSweep A{X1o, X2o, ws.kbits, ws.cbits, ws.Kold, ws.rowcand, ws.jrange, ny, nx, W,
+              max_layers, dx, dy, ws.status, ctl};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
     if (!prof) {
         k_ex_sweep<false><<<1, EXW * 64, 0, ctx->stream>>>(A, nullptr);
@@ -517,7 +573,7 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, ctx->stream));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, ctx->stream));
-        RMT_HIP(hipMemcpyAsync(hs, status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
+        RMT_HIP(hipMemcpyAsync(hs, ws.status, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
         RMT_HIP(hipStreamSynchronize(ctx->stream));
         float ms = 0;
         RMT_HIP(hipEventElapsedTime(&ms, e0, e1));
@@ -527,9 +583,9 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6);
         hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
     }
-    if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
+    if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
     if (dev_status)
-        RMT_HIP(hipMemcpyAsync(dev_status, status, 2 * sizeof(int), hipMemcpyDeviceToDevice,
+        RMT_HIP(hipMemcpyAsync(dev_status, ws.status, 2 * sizeof(int), hipMemcpyDeviceToDevice,
                                ctx->stream));
     return RMT_OK;
 }
@@ -541,4 +597,24 @@ extern "C" int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, con
                                              int max_layers, double *X1_out, double *X2_out) {
     RMT_CHECK(ctx, RMT_EINVAL, "null ctx");
     return rmt::extrapolate(ctx, X1, X2, phi, dx, dy, max_layers, X1_out, X2_out, nullptr);
+}
+
+extern "C" int rmt_extrap_set_mode(int mode) {
+    RMT_CHECK(mode >= 0 && mode <= 2, RMT_EINVAL, "extrapolation mode must be 0, 1 or 2");
+    rmt::g_ex_mode = mode;
+    return RMT_OK;
+}
+
+extern "C" int rmt_extrap_last_path(rmt_ctx *ctx, int *path) {
+    RMT_CHECK(ctx && path, RMT_EINVAL, "null argument");
+    RMT_CHECK(ctx->bytes, RMT_EINVAL, "no extrapolation has run on this context");
+    const rmt::ExWs ws = rmt::extrap_layout(ctx->bytes, ctx->ny, ctx->nx, ctx->ex_layers, nullptr);
+    int fb = 1;
+    if (ctx->ex_chain) {
+        RMT_HIP(hipMemcpyAsync(&fb, ws.ctl + rmt::EXC_FALLBACK, sizeof(int),
+                               hipMemcpyDeviceToHost, ctx->stream));
+        RMT_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    *path = fb ? 1 : 0;
+    return RMT_OK;
 }

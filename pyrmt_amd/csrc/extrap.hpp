@@ -1,0 +1,48 @@
+// extrap.hpp -- shared layout of the extrapolation workspace (extrap.hip: band detection and
+// the row-ticket sweep used as the general fallback; extrap_chain.hip: the geometry-first
+// chain path used whenever its capacity limits hold).
+#pragma once
+#include "rmt_internal.hpp"
+
+namespace rmt {
+
+typedef unsigned long long u64;
+
+constexpr int EX_MAXL = 8;          // layers the chain path handles (more -> fallback sweep)
+constexpr int CH_R = 4096;          // chain value ring (slots, chain order); deps < CH_R/2 back
+constexpr int CH_W = 8;             // chain workgroup waves
+constexpr int CH_HDR = 24;          // record header, doubles
+constexpr int CH_TVS = 88;          // padded fold terms per sum (81 rounded up to 8)
+constexpr int CH_MAXREC = 8 * (CH_HDR + 6 * CH_TVS) + 8 * 81;   // 5064 B
+constexpr int EX_MAXREJ = 4096;     // rejected fits per layer the fix-up handles
+constexpr int EX_DCAP = 8192;       // fix-up dirty-list capacity
+
+// ctl words (int): fallback flag, abort flag, accepted count, and 64-bit arena cursor
+enum { EXC_FALLBACK = 0, EXC_ABORT = 1, EXC_FILLED = 2, EXC_ARENA = 4, EXC_REJ = 8,
+       EXC_BASE = 8 + EX_MAXL, EXC_WORDS = 8 + 2 * EX_MAXL + 8 };
+
+struct ExWs {
+    // band detection (both paths) and the fallback sweep
+    u64 *kbits, *cbits, *Kold;     // Kold: ML planes
+    unsigned char *rowcand;
+    int *jrange, *status;          // status[0] filled, [1] abort (fallback sweep)
+    // chain path
+    u64 *T, *ACC, *KN;             // ML planes each: targets, accepted, known after layer
+    int *rowcnt, *rowoff, *wordoff, *cbase;   // ML*ny, ML*(ny+1), ML*ny*W, ML*ny
+    long long *tcell, *recoff, *rec_by_chain; // MAXT each
+    int *chain_of, *dmark;                    // MAXT each
+    int *rej;                                 // ML * EX_MAXREJ
+    int *ctl;                                 // EXC_WORDS
+    char *arena;
+    long long arena_bytes;
+    long maxt;
+    long plane;                               // ny * W
+};
+
+ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes);
+// chain path: queue the kernels; they check ctl[EXC_FALLBACK] themselves
+int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
+                        double dx, double dy, int ML);
+bool extrap_chain_supported(int ny, int nx, int ML);
+
+}  // namespace rmt

@@ -1,0 +1,689 @@
+// extrap_chain.hip -- functions.py:48-163 extrapolate_reference_map, geometry first.
+//
+// The reference fits the targets of a layer in raster order and marks each one known at once,
+// so a fit sees every earlier accepted fit of its layer (Gauss-Seidel).  Everything a fit
+// computes EXCEPT its right-hand sides is value-independent: which window cells are known
+// (acceptance: count >= 3 and det > 1e-10 depends on the known set only), the weights
+// w = exp(-d^2/r^2), the normal matrix Aw, its det and Cramer cofactors.  Only the sums
+// Bw = sum w*a*X over the window (functions.py:128-133) read values that earlier fits produce.
+// So the exact serial result is computed in three stages:
+//
+//   1. per layer, chip-wide: targets (k_tg_rows/scan/emit: bit planes, raster-order ids),
+//      then one wave per target (k_ex_geom) computes the fit assuming every earlier target of
+//      its layer was accepted, and emits a RECORD: Cramer constants, the partial sums of the
+//      static (phi < 0) terms before the first value an earlier fit produces, and for every
+//      later included cell either its 6 products w*a*X (static) or its 3 coefficients w*a
+//      plus the id of the fit that produces X (dynamic).  Speculation is exact unless a target
+//      is rejected: k_ex_fix then re-fits, Jacobi-style, every later target whose window holds
+//      a rejected one until acceptance is a fixed point -- the DAG's unique fixed point is the
+//      serial answer (acceptance only flows forward in raster order).
+//   2. chain order (k_ex_order/chainidx/relink): fits are numbered in order of (j + 5L, L, i),
+//      a topological order of the true dependency DAG (a layer-L fit reads layer L rows j-4..j
+//      and layer L-1 rows j-4..j+4), and record sources are rewritten to chain indices.
+//   3. k_ex_chain, one workgroup: waves take chain indices round-robin; a fit waits for its
+//      dynamic sources in an LDS value ring (tag == chain index), forms their products, folds
+//      the 6 ordered sums over its record terms (lanes 0-5) and runs the 3x3 solve of
+//      utils.py:134-166 with the precomputed cofactors -- the same operations, in the same
+//      order, as the reference, on the same values.
+//
+// Capacity limits (ids, record arena, fix-up lists, ring distance) set ctl[EXC_FALLBACK]
+// on the device; extrap.hip then runs the row-ticket sweep instead.
+#include "extrap.hpp"
+#include "exp_glibc.h"
+
+namespace rmt {
+
+constexpr int EXS = 82;   // term-buffer row stride of the geometry fold (16-B aligned rows)
+
+__device__ __forceinline__ u64 ld_l2(const u64 *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ u64 rl64(u64 v, int l) {
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)v, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), l);
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ double rlf(double v, int l) {
+    return __longlong_as_double((long long)rl64((u64)__double_as_longlong(v), l));
+}
+// raster rank -> id of the layer-Ls target at word o, bit mask `bit`
+__device__ __forceinline__ int ex_id(const ExWs &ws, int ny, int Ls, int jj, long o, u64 bit) {
+    return ws.ctl[EXC_BASE + Ls] + ws.rowoff[(long)Ls * (ny + 1) + jj] +
+           ws.wordoff[(long)Ls * ws.plane + o] + __popcll(ws.T[(long)Ls * ws.plane + o] & (bit - 1));
+}
+
+// ------------------------------------------------------------------ 1. targets -----
+// functions.py:79-90: targets of layer L = interior cells unknown at the start of L with a
+// known 3x3 neighbour.  Known at the start of L: kbits (L = 0) or KN[L-1] = KN[L-2] | ACC[L-1],
+// materialised here row by row.  One wave per row, lanes over 64-cell words; ACC[L] starts as
+// T[L] (speculation), wordoff = exclusive popcount within the row, rowcnt = row total.
+__global__ void __launch_bounds__(256) k_tg_rows(ExWs ws, int ny, int nx, int W, int L) {
+    const int lane = threadIdx.x & 63, j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= ny) return;
+    const long plane = ws.plane;
+    const u64 *Kpp = L >= 2 ? ws.KN + (long)(L - 2) * plane : ws.kbits;
+    const u64 *Ap = L >= 1 ? ws.ACC + (long)(L - 1) * plane : nullptr;
+    auto K = [&](int jj, int w) -> u64 {
+        if (jj < 0 || jj >= ny || w < 0 || w >= W) return 0;
+        const long o = (long)jj * W + w;
+        return Ap ? (Kpp[o] | Ap[o]) : Kpp[o];
+    };
+    int run = 0;
+    for (int w0 = 0; w0 < W; w0 += 64) {
+        const int w = w0 + lane;
+        u64 t = 0;
+        if (w < W) {
+            u64 d = 0;
+            for (int r = -1; r <= 1; ++r) {
+                const u64 a = K(j + r, w - 1), b = K(j + r, w), c = K(j + r, w + 1);
+                d |= b | (b << 1) | (a >> 63) | (b >> 1) | (c << 63);
+            }
+            const u64 k0 = K(j, w);
+            const long o = (long)j * W + w;
+            if (L >= 1) ws.KN[(long)(L - 1) * plane + o] = k0;
+            const int i0 = 64 * w, lo = max(1, i0) - i0, hi = min(nx - 2, i0 + 63) - i0;
+            u64 cols = hi >= lo ? (~0ull >> (63 - hi)) & (~0ull << lo) : 0;
+            if (j < 1 || j > ny - 2) cols = 0;
+            t = d & ~k0 & cols;
+            ws.T[(long)L * plane + o] = t;
+            ws.ACC[(long)L * plane + o] = t;
+        }
+        const int c = __popcll(t), inc = wave_incl_scan(c, lane);
+        if (w < W) ws.wordoff[(long)L * plane + (long)j * W + w] = run + inc - c;
+        run += __shfl(inc, 63);
+    }
+    if (lane == 0) ws.rowcnt[(long)L * ny + j] = run;
+}
+
+// exclusive scan of the row counts -> rowoff[L][j]; ids of layer L are base[L] + raster rank
+__global__ void __launch_bounds__(1024) k_tg_scan(ExWs ws, int ny, int L) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x, per = (ny + 1023) / 1024;
+    const int j0 = min(ny, t * per), j1 = min(ny, j0 + per);
+    const int *rc = ws.rowcnt + (long)L * ny;
+    int s = 0;
+    for (int j = j0; j < j1; ++j) s += rc[j];
+    part[t] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = part[t] - s;
+    int *ro = ws.rowoff + (long)L * (ny + 1);
+    for (int j = j0; j < j1; ++j) { ro[j] = run; run += rc[j]; }
+    if (t == 1023) {
+        const int total = part[1023], b = ws.ctl[EXC_BASE + L];
+        ro[ny] = total;
+        ws.ctl[EXC_BASE + L + 1] = b + total;
+        if ((long)b + total > ws.maxt) ws.ctl[EXC_FALLBACK] = 1;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tg_emit(ExWs ws, int ny, int nx, int W, int L) {
+    const int lane = threadIdx.x & 63, j = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (j >= ny || ws.ctl[EXC_FALLBACK]) return;
+    const int base = ws.ctl[EXC_BASE + L] + ws.rowoff[(long)L * (ny + 1) + j];
+    for (int w = lane; w < W; w += 64) {
+        const long o = (long)L * ws.plane + (long)j * W + w;
+        u64 t = ws.T[o];
+        int id = base + ws.wordoff[o];
+        for (; t; t &= t - 1, ++id) {
+            ws.tcell[id] = (long)j * nx + 64 * w + __builtin_ctzll(t);
+            ws.dmark[id] = -1;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 1. geometry ----
+struct ExGeoArgs {
+    ExWs ws;
+    const double *X1, *X2;   // static values (phi < 0 cells are never written)
+    int ny, nx, W, L;
+    double dx, dy, r2;
+};
+
+// One wave fits target `id` of layer A.L.  Same-layer acceptance of earlier targets is read
+// from T (FIX = false: speculation) or from ACC through L2 (FIX = true: k_ex_fix, where ACC
+// changes inside the launch).  Emits the record if accepted; returns acceptance (uniform).
+template <bool FIX>
+__device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, int lane) {
+    const ExWs &ws = A.ws;
+    const int L = A.L, W = A.W, nx = A.nx, ny = A.ny;
+    const long plane = ws.plane, c = ws.tcell[id];
+    const int j = (int)(c / nx), i = (int)(c % nx);
+    const u64 *Kst = L == 0 ? ws.kbits : ws.KN + (long)(L - 1) * plane;
+    const u64 *SL = (FIX ? ws.ACC : ws.T) + (long)L * plane;
+    const double x0 = A.dx * i, y0 = A.dy * j;
+    bool inc[2], st[2];
+    double w[2], xi[2], yi[2], b1[2], b2[2];
+    int src[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
+        inc[h] = false; st[h] = false;
+        w[h] = 0.0; b1[h] = 0.0; b2[h] = 0.0; src[h] = -1;
+        xi[h] = A.dx * ii; yi[h] = A.dy * jj;
+        if (q < 81 && jj >= 0 && jj < ny && ii >= 0 && ii < nx) {
+            const double ax = xi[h] - x0, ay = yi[h] - y0, d2 = ax * ax + ay * ay;
+            if (d2 <= A.r2) {
+                const long o = (long)jj * W + (ii >> 6);
+                const u64 bit = 1ull << (ii & 63);
+                const bool ks = (Kst[o] & bit) != 0;
+                bool sl = false;
+                if (!ks && (jj < j || (jj == j && ii < i)))
+                    sl = ((FIX ? ld_l2(SL + o) : SL[o]) & bit) != 0;
+                inc[h] = ks || sl;
+                if (inc[h]) {
+                    w[h] = exp_glibc_tab(-d2 / A.r2, tab);   // libm exp, bit for bit
+                    st[h] = (ws.kbits[o] & bit) != 0;
+                    if (st[h]) {
+                        const long cc = (long)jj * nx + ii;
+                        b1[h] = A.X1[cc]; b2[h] = A.X2[cc];
+                    } else {
+                        int Ls = L;
+                        if (!sl)
+                            for (Ls = 0; Ls < L; ++Ls)
+                                if (ws.ACC[(long)Ls * plane + o] & bit) break;
+                        src[h] = ex_id(ws, ny, Ls, jj, o, bit);
+                    }
+                }
+            }
+        }
+    }
+    // first dynamic window position (the static prefix before it is pre-summed)
+    const u64 dl = __ballot(inc[0] && !st[0]), dh = __ballot(inc[1] && !st[1] && lane < 17);
+    const int qf = dl ? __builtin_ctzll(dl) : (dh ? 64 + __builtin_ctzll(dh) : 81);
+    // terms of functions.py:128-145: rows 0-5 Aw (every included cell), rows 6-11 the
+    // Bw prefix (static cells before qf); excluded cells contribute +0.0 (exact)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = lane + 64 * h;
+        if (q >= 81) break;
+        const double wa0 = w[h] * 1.0, wa1 = w[h] * xi[h], wa2 = w[h] * yi[h];
+        const bool pre = st[h] && q < qf;
+        tb[0 * EXS + q] = inc[h] ? wa0 * 1.0 : 0.0;
+        tb[1 * EXS + q] = inc[h] ? wa0 * xi[h] : 0.0;
+        tb[2 * EXS + q] = inc[h] ? wa0 * yi[h] : 0.0;
+        tb[3 * EXS + q] = inc[h] ? wa1 * xi[h] : 0.0;
+        tb[4 * EXS + q] = inc[h] ? wa1 * yi[h] : 0.0;
+        tb[5 * EXS + q] = inc[h] ? wa2 * yi[h] : 0.0;
+        tb[6 * EXS + q] = pre ? wa0 * b1[h] : 0.0;
+        tb[7 * EXS + q] = pre ? wa1 * b1[h] : 0.0;
+        tb[8 * EXS + q] = pre ? wa2 * b1[h] : 0.0;
+        tb[9 * EXS + q] = pre ? wa0 * b2[h] : 0.0;
+        tb[10 * EXS + q] = pre ? wa1 * b2[h] : 0.0;
+        tb[11 * EXS + q] = pre ? wa2 * b2[h] : 0.0;
+    }
+    const u64 il = __ballot(inc[0]), ih = __ballot(inc[1] && lane < 17);
+    const int count = __popcll(il) + __popcll(ih);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    double acc = 0.0;
+    if (lane < 12) {
+        const double2 *t2 = (const double2 *)(tb + lane * EXS);
+        double2 t[40];
+#pragma unroll
+        for (int q2 = 0; q2 < 40; ++q2) t[q2] = t2[q2];
+        const double last = tb[lane * EXS + 80];
+#pragma unroll
+        for (int q2 = 0; q2 < 40; ++q2) { acc += t[q2].x; acc += t[q2].y; }
+        acc += last;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const double A00 = rlf(acc, 0), A01 = rlf(acc, 1), A02 = rlf(acc, 2);
+    const double A11 = rlf(acc, 3), A12 = rlf(acc, 4), A22 = rlf(acc, 5);
+    const double M[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
+    const double det = (M[0] * (M[4] * M[8] - M[5] * M[7])
+                      - M[1] * (M[3] * M[8] - M[5] * M[6])
+                      + M[2] * (M[3] * M[7] - M[4] * M[6]));
+    const bool accept = count >= 3 && fabs(det) > 1e-10;
+    if (!accept) {
+        if (lane == 0) ws.recoff[id] = -1;
+        return false;
+    }
+    // record: compact the included cells from qf on (static: 6 products; dynamic: 3 coefs)
+    const u64 lt = (1ull << lane) - 1;
+    const u64 tl = il & ~((qf >= 64) ? ~0ull : ((1ull << qf) - 1));
+    const u64 th = ih & ~((qf >= 64) ? ((1ull << (qf - 64)) - 1) : 0ull);
+    const int n = __popcll(tl) + __popcll(th), npad = (n + 7) & ~7;
+    const int nd = __popcll(dl) + __popcll(dh);
+    const long long bytes = ((8LL * (CH_HDR + 6 * npad) + 8LL * nd) + 63) & ~63LL;
+    unsigned long long off = 0;
+    if (lane == 0) {
+        off = atomicAdd((unsigned long long *)(ws.ctl + EXC_ARENA), (unsigned long long)bytes);
+        if ((long long)(off + bytes) > ws.arena_bytes) ws.ctl[EXC_FALLBACK] = 1;
+    }
+    off = rl64(off, 0);
+    if ((long long)(off + bytes) > ws.arena_bytes) {
+        if (lane == 0) ws.recoff[id] = -1;
+        return true;   // (fallback sweep recomputes everything)
+    }
+    double *rec = (double *)(ws.arena + off);
+    double *tv = rec + CH_HDR;
+    int2 *dyn = (int2 *)(tv + 6 * npad);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const bool term = h ? ((th >> lane) & 1) && lane < 17 : (tl >> lane) & 1;
+        if (!term) continue;
+        const int k = h ? __popcll(tl) + __popcll(th & lt) : __popcll(tl & lt);
+        const double wa0 = w[h] * 1.0, wa1 = w[h] * xi[h], wa2 = w[h] * yi[h];
+        if (st[h]) {
+            tv[0 * npad + k] = wa0 * b1[h]; tv[1 * npad + k] = wa1 * b1[h];
+            tv[2 * npad + k] = wa2 * b1[h]; tv[3 * npad + k] = wa0 * b2[h];
+            tv[4 * npad + k] = wa1 * b2[h]; tv[5 * npad + k] = wa2 * b2[h];
+        } else {
+            tv[0 * npad + k] = wa0; tv[1 * npad + k] = wa1; tv[2 * npad + k] = wa2;
+            tv[3 * npad + k] = wa0; tv[4 * npad + k] = wa1; tv[5 * npad + k] = wa2;
+            const int dk = h ? __popcll(dl) + __popcll(dh & lt) : __popcll(dl & lt);
+            dyn[dk] = make_int2(k, src[h]);
+        }
+    }
+    if (lane < 6 * (npad - n)) tv[(lane / (npad - n)) * npad + n + lane % (npad - n)] = 0.0;
+    if (lane == 0) {
+        rec[0] = __longlong_as_double((long long)c);
+        rec[1] = __longlong_as_double(((long long)nd << 32) | (unsigned)npad);
+        rec[2] = x0; rec[3] = y0;
+        for (int k = 0; k < 9; ++k) rec[4 + k] = M[k];
+        rec[13] = M[4] * M[8] - M[5] * M[7];
+        rec[14] = M[3] * M[8] - M[5] * M[6];
+        rec[15] = M[3] * M[7] - M[4] * M[6];
+        rec[16] = 1.0 / det;
+        rec[23] = 0.0;
+    }
+    if (lane >= 6 && lane < 12) rec[17 + lane - 6] = acc;   // P[0..5]
+    if (lane == 0) ws.recoff[id] = ((long long)(bytes >> 6) << 32) | (long long)(off >> 6);
+    return true;
+}
+
+__global__ void __launch_bounds__(256) k_ex_geom(ExGeoArgs A) {
+    __shared__ u64 tab[256];
+    __shared__ __attribute__((aligned(16))) double tb[4][12 * EXS];
+    for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
+    __syncthreads();
+    const ExWs &ws = A.ws;
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b0 = ws.ctl[EXC_BASE + A.L], b1 = ws.ctl[EXC_BASE + A.L + 1];
+    for (int id = b0 + blockIdx.x * 4 + wv; id < b1; id += gridDim.x * 4) {
+        if (ex_geom<false>(A, id, tb[wv], tab, lane) || lane != 0) continue;
+        const long c = ws.tcell[id];
+        const int j = (int)(c / A.nx), i = (int)(c % A.nx);
+        atomicAnd(ws.ACC + (long)A.L * ws.plane + (long)j * A.W + (i >> 6), ~(1ull << (i & 63)));
+        const int r = atomicAdd(ws.ctl + EXC_REJ + A.L, 1);
+        if (r < EX_MAXREJ) ws.rej[A.L * EX_MAXREJ + r] = id;
+        else ws.ctl[EXC_FALLBACK] = 1;
+    }
+}
+
+// ------------------------------------------------------------------ 1. fix-up ------
+constexpr int FIXW = 8;
+
+// append the later same-layer targets whose window holds target `id` (dedup by dmark)
+__device__ void ex_add_dependents(const ExGeoArgs &A, int id, int *dlist, int *dn) {
+    const ExWs &ws = A.ws;
+    const long c = ws.tcell[id];
+    const int j = (int)(c / A.nx), i = (int)(c % A.nx);
+    const u64 *T = ws.T + (long)A.L * ws.plane;
+    for (int jj = j; jj <= min(A.ny - 1, j + 4); ++jj)
+        for (int ii = max(0, i - 4); ii <= min(A.nx - 1, i + 4); ++ii) {
+            if (jj == j && ii <= i) continue;
+            const long o = (long)jj * A.W + (ii >> 6);
+            const u64 bit = 1ull << (ii & 63);
+            if (!(T[o] & bit)) continue;
+            const int d = ex_id(ws, A.ny, A.L, jj, o, bit);
+            if (atomicExch(ws.dmark + d, 1) == 1) continue;
+            const int p = atomicAdd(dn, 1);
+            if (p < EX_DCAP) dlist[p] = d;
+        }
+}
+
+// Jacobi re-fits of the targets downstream of rejections until acceptance is a fixed point.
+__global__ void __launch_bounds__(FIXW * 64) k_ex_fix(ExGeoArgs A) {
+    __shared__ u64 tab[256];
+    __shared__ __attribute__((aligned(16))) double tb[FIXW][12 * EXS];
+    __shared__ int dlist[EX_DCAP];
+    __shared__ unsigned char dres[EX_DCAP];
+    __shared__ int dn, nflip;
+    const ExWs &ws = A.ws;
+    const int nrej = ws.ctl[EXC_REJ + A.L];
+    if (nrej == 0 || ws.ctl[EXC_FALLBACK]) return;
+    for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
+    if (threadIdx.x == 0) dn = 0;
+    __syncthreads();
+    for (int r = threadIdx.x; r < min(nrej, EX_MAXREJ); r += blockDim.x)
+        ex_add_dependents(A, ws.rej[A.L * EX_MAXREJ + r], dlist, &dn);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u64 *ACC = ws.ACC + (long)A.L * ws.plane;
+    for (int iter = 0;; ++iter) {
+        __syncthreads();
+        const int m = dn;
+        if (m > EX_DCAP || iter > (1 << 20)) {
+            if (threadIdx.x == 0) ws.ctl[EXC_FALLBACK] = 1;
+            return;
+        }
+        for (int e = wv; e < m; e += FIXW) {
+            const bool a = ex_geom<true>(A, dlist[e], tb[wv], tab, lane);
+            if (lane == 0) dres[e] = a;
+        }
+        if (threadIdx.x == 0) nflip = 0;
+        __syncthreads();
+        for (int e = threadIdx.x; e < m; e += blockDim.x) {
+            const long c = ws.tcell[dlist[e]];
+            const int j = (int)(c / A.nx), i = (int)(c % A.nx);
+            const long o = (long)j * A.W + (i >> 6);
+            const u64 bit = 1ull << (i & 63);
+            const bool cur = (ld_l2(ACC + o) & bit) != 0;
+            if (cur != (bool)(dres[e] & 1)) {
+                atomicXor((u64 *)ACC + o, bit);
+                dres[e] |= 2;
+                atomicAdd(&nflip, 1);
+            }
+        }
+        __threadfence();
+        __syncthreads();
+        if (nflip == 0) break;
+        for (int e = threadIdx.x; e < m; e += blockDim.x)
+            if (dres[e] & 2) ex_add_dependents(A, dlist[e], dlist, &dn);
+        __threadfence();
+    }
+}
+
+// ------------------------------------------------------------------ 2. chain order -
+// chain order (k = j + 5L, L, i): exclusive scan of the row counts over (k, L) slots
+__global__ void __launch_bounds__(1024) k_ex_order(ExWs ws, int ny, int ML) {
+    __shared__ int part[1024];
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int t = threadIdx.x, nslot = (ny + 5 * (ML - 1)) * ML, per = (nslot + 1023) / 1024;
+    const int s0 = min(nslot, t * per), s1 = min(nslot, s0 + per);
+    auto cnt = [&](int s) {
+        const int L = s % ML, j = s / ML - 5 * L;
+        return j >= 0 && j < ny ? ws.rowcnt[(long)L * ny + j] : 0;
+    };
+    int sum = 0;
+    for (int s = s0; s < s1; ++s) sum += cnt(s);
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = part[t] - sum;
+    for (int s = s0; s < s1; ++s) {
+        const int L = s % ML, j = s / ML - 5 * L;
+        if (j >= 0 && j < ny) ws.cbase[(long)L * ny + j] = run;
+        run += cnt(s);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, int ML,
+                                                     int *status) {
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int id = blockIdx.x * 256 + threadIdx.x, total = ws.ctl[EXC_BASE + ML];
+    bool acc = false;
+    if (id < total) {
+        int L = ML - 1;
+        while (L > 0 && id < ws.ctl[EXC_BASE + L]) --L;
+        const int j = (int)(ws.tcell[id] / nx);
+        const int x = ws.cbase[(long)L * ny + j] +
+                      (id - ws.ctl[EXC_BASE + L] - ws.rowoff[(long)L * (ny + 1) + j]);
+        ws.chain_of[id] = x;
+        const long long r = ws.recoff[id];
+        ws.rec_by_chain[x] = r;
+        acc = r >= 0;
+    }
+    const u64 b = __ballot(acc);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(status, __popcll(b));
+}
+
+// record sources: fit ids -> chain indices; the ring needs every source < CH_R/2 back
+__global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int id = blockIdx.x * 256 + threadIdx.x;
+    if (id >= ws.ctl[EXC_BASE + ML]) return;
+    const long long r = ws.recoff[id];
+    if (r < 0) return;
+    double *rec = (double *)(ws.arena + ((r & 0xffffffffLL) << 6));
+    const long long meta = __double_as_longlong(rec[1]);
+    const int npad = (int)(meta & 0xffffffff), nd = (int)(meta >> 32);
+    int2 *dyn = (int2 *)(rec + CH_HDR + 6 * npad);
+    const int x = ws.chain_of[id];
+    for (int d = 0; d < nd; ++d) {
+        const int xs = ws.chain_of[dyn[d].y];
+        dyn[d].y = xs;
+        if (xs >= x) { ws.ctl[EXC_ABORT] = 1; atomicExch(ws.status + 1, 1); }   // a bug
+        else if (x - xs >= CH_R / 2) ws.ctl[EXC_FALLBACK] = 1;
+    }
+}
+
+// ------------------------------------------------------------------ 3. the chain ---
+constexpr int CH_BUFD = CH_MAXREC / 8 + 8;          // doubles per wave record buffer
+constexpr long CH_SPIN_LIMIT = 1L << 25;
+
+struct ChainArgs {
+    ExWs ws;
+    double *X1e, *X2e;
+    int ML;
+    int *status;
+};
+
+struct Rec5 { double2 v0, v1, v2, v3, v4; };   // one record, 16 B per lane per KB
+
+// this wave's LDS record buffer <- the prefetched registers
+__device__ __forceinline__ void ch_stage(double *B, long long r, int lane, Rec5 d) {
+    if (r < 0) return;
+    const int n16 = (int)((r >> 32) << 2);
+    double2 *B2 = (double2 *)B;
+    if (lane < n16) B2[lane] = d.v0;
+    if (64 + lane < n16) B2[64 + lane] = d.v1;
+    if (128 + lane < n16) B2[128 + lane] = d.v2;
+    if (192 + lane < n16) B2[192 + lane] = d.v3;
+    if (256 + lane < n16) B2[256 + lane] = d.v4;
+}
+
+__device__ __forceinline__ void ch_load(const char *arena, long long r, int lane, Rec5 &v) {
+    // rejected fits (r < 0) load piece 0 of the arena (never used); lanes past the record
+    // re-read its last piece (same line), so every lane issues the same 5 loads
+    const double2 *p = (const double2 *)(arena + (r < 0 ? 0 : (r & 0xffffffffLL) << 6));
+    const int last = r < 0 ? 0 : (int)((r >> 32) << 2) - 1;
+    v.v0 = p[min(lane, last)];
+    v.v1 = p[min(64 + lane, last)];
+    v.v2 = p[min(128 + lane, last)];
+    v.v3 = p[min(192 + lane, last)];
+    v.v4 = p[min(256 + lane, last)];
+}
+
+// one fit of the chain (chain index x, record r0 whose bytes are in d0); false on a timeout
+__device__ __forceinline__ bool ch_fit(double *X1e, double *X2e, int x, long long r0,
+                                       int lane, int wv, double *B,
+                                       double2 *val, int *tag, int *cur, int &wm) {
+    bool ok = true;
+    __hip_atomic_store(&cur[wv], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (r0 >= 0) {
+        // ring reuse: every fit < x - CH_R/2 is done (their readers are all < x)
+        long spins = 0;
+        while (x - CH_R / 2 >= wm) {
+            int m = 0x7fffffff;
+            for (int k = 0; k < CH_W; ++k)
+                m = min(m, __hip_atomic_load(&cur[k], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WORKGROUP));
+            wm = m;
+            if (x - CH_R / 2 >= wm) {
+                if (++spins > CH_SPIN_LIMIT) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (!ok) return false;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const long long meta = __double_as_longlong(B[1]);
+        const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
+        const int nd = __builtin_amdgcn_readfirstlane((int)(meta >> 32));
+        double *tv = B + CH_HDR;
+        // dynamic sources: wait for their values, then form the products in place
+        if (nd > 0) {
+            const int2 *dyn = (const int2 *)(tv + 6 * npad);
+            for (int d0i = 0; d0i < nd; d0i += 64) {
+                const int d = d0i + lane;
+                int2 e = make_int2(0, -1);
+                if (d < nd) e = dyn[d];
+                const int slot = e.y & (CH_R - 1);
+                bool ready = d >= nd;
+                long sp = 0;
+                while (true) {
+                    if (!ready)
+                        ready = __hip_atomic_load(&tag[slot], __ATOMIC_ACQUIRE,
+                                                  __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
+                    if (__ballot(!ready) == 0) break;
+                    if (++sp > CH_SPIN_LIMIT) { ok = false; break; }
+                    __builtin_amdgcn_s_sleep(0);
+                }
+                if (!ok) return false;
+                if (d < nd) {
+                    const double2 v = val[slot];
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) {
+                        double *p = tv + s * npad + e.x;
+                        *p = *p * (s < 3 ? v.x : v.y);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        // the 6 ordered sums of functions.py:128-133 (lanes 0-5), from the static prefix
+        double acc = 0.0;
+        if (lane < 6) {
+            acc = B[17 + lane];
+            const double2 *row = (const double2 *)(tv + lane * npad);
+            const int nq = npad >> 2;   // 4-term quads
+            double2 a0, a1, b0, b1;
+            if (nq > 0) { a0 = row[0]; a1 = row[1]; }
+            for (int qd = 0; qd < nq; qd += 2) {
+                if (qd + 1 < nq) { b0 = row[2 * qd + 2]; b1 = row[2 * qd + 3]; }
+                acc += a0.x; acc += a0.y; acc += a1.x; acc += a1.y;
+                if (qd + 1 < nq) {
+                    if (qd + 2 < nq) { a0 = row[2 * qd + 4]; a1 = row[2 * qd + 5]; }
+                    acc += b0.x; acc += b0.y; acc += b1.x; acc += b1.y;
+                }
+            }
+        }
+        // utils.py:134-166 on lanes 0 (X1) and 3 (X2) with the precomputed cofactors
+        const double bb1 = __shfl(acc, lane + 1), bb2 = __shfl(acc, lane + 2);
+        if (lane == 0 || lane == 3) {
+            const double b[3] = {acc, bb1, bb2};
+            const double *M = B + 4;
+            const double C0 = B[13], C1 = B[14], C2 = B[15], inv_det = B[16];
+            const double xs = (b[0] * C0 - M[1] * (b[1] * M[8] - M[5] * b[2]) +
+                               M[2] * (b[1] * M[7] - M[4] * b[2])) * inv_det;
+            const double ys = (M[0] * (b[1] * M[8] - M[5] * b[2]) - b[0] * C1 +
+                               M[2] * (M[3] * b[2] - b[1] * M[6])) * inv_det;
+            const double zs = (M[0] * (M[4] * b[2] - b[1] * M[7]) -
+                               M[1] * (M[3] * b[2] - b[1] * M[6]) + b[0] * C2) * inv_det;
+            const double o = xs + ys * B[2] + zs * B[3];
+            const int slot = x & (CH_R - 1);
+            ((double *)&val[slot])[lane == 0 ? 0 : 1] = o;
+            const long c0 = __double_as_longlong(B[0]);
+            (lane == 0 ? X1e : X2e)[c0] = o;
+        }
+        if (lane == 0)
+            __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return ok;
+}
+
+__global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C) {
+    __shared__ double2 val[CH_R];
+    __shared__ int tag[CH_R];
+    __shared__ __attribute__((aligned(16))) double buf[CH_W][CH_BUFD];
+    __shared__ int cur[CH_W];
+    __shared__ int s_abort;
+    const int *ctl = C.ws.ctl;
+    const long long *rbc = C.ws.rec_by_chain;
+    const char *arena = C.ws.arena;
+    double *X1e = C.X1e, *X2e = C.X2e;
+    for (int s = threadIdx.x; s < CH_R; s += blockDim.x) tag[s] = -1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x < CH_W) cur[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_abort = 0;
+    __syncthreads();
+    if (ctl[EXC_FALLBACK] || ctl[EXC_ABORT]) return;
+    const int total = ctl[EXC_BASE + C.ML];
+    double *B = buf[wv];
+    // record pipeline: offsets two ahead, data one ahead
+    long long r0 = wv < total ? rbc[wv] : -1;
+    long long r1 = wv + CH_W < total ? rbc[wv + CH_W] : -1;
+    Rec5 d0, d1;
+    ch_load(arena, r0, lane, d0);
+    int wm = 0;
+    bool ok = true;
+    for (int x = wv; x < total; x += 2 * CH_W) {
+        // two fits per trip so the prefetched bytes never move between registers
+        const long long r2 = x + 2 * CH_W < total ? rbc[x + 2 * CH_W] : -1;
+        ch_stage(B, r0, lane, d0);
+        ch_load(arena, r1, lane, d1);
+        if (!ch_fit(X1e, X2e, x, r0, lane, wv, B, val, tag, cur, wm)) { ok = false; break; }
+        const int x1 = x + CH_W;
+        if (x1 >= total) break;
+        const long long r3 = x1 + 2 * CH_W < total ? rbc[x1 + 2 * CH_W] : -1;
+        ch_stage(B, r1, lane, d1);
+        ch_load(arena, r2, lane, d0);
+        if (!ch_fit(X1e, X2e, x1, r1, lane, wv, B, val, tag, cur, wm)) { ok = false; break; }
+        r0 = r2; r1 = r3;
+    }
+    __hip_atomic_store(&cur[wv], 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!ok && lane == 0) {
+        C.ws.ctl[EXC_ABORT] = 1;
+        atomicExch(&C.status[1], 1);
+    }
+}
+
+// ------------------------------------------------------------------ host side ------
+bool extrap_chain_supported(int ny, int nx, int ML) {
+    return ML >= 1 && ML <= EX_MAXL && ny >= 3 && nx >= 3;
+}
+
+int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
+                        double dx, double dy, int ML) {
+    const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
+    hipStream_t st = ctx->stream;
+    const unsigned rows = grid1d(ny, 4);
+    double r = 4 * std::sqrt(dx * dx + dy * dy);
+    ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r};
+    const unsigned gblocks = (unsigned)std::min<long>(1024, std::max<long>(1, ws.maxt / 4));
+    for (int L = 0; L < ML; ++L) {
+        A.L = L;
+        k_tg_rows<<<rows, 256, 0, st>>>(ws, ny, nx, W, L);
+        k_tg_scan<<<1, 1024, 0, st>>>(ws, ny, L);
+        k_tg_emit<<<rows, 256, 0, st>>>(ws, ny, nx, W, L);
+        k_ex_geom<<<gblocks, 256, 0, st>>>(A);
+        k_ex_fix<<<1, FIXW * 64, 0, st>>>(A);
+        RMT_LAUNCHED();
+    }
+    k_ex_order<<<1, 1024, 0, st>>>(ws, ny, ML);
+    const unsigned idb = grid1d(ws.maxt, 256);
+    k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
+    k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
+    if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
+    ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status};
+    k_ex_chain<<<1, CH_W * 64, 0, st>>>(C);
+    RMT_LAUNCHED();
+    if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], st));
+    return RMT_OK;
+}
+
+}  // namespace rmt

@@ -58,6 +58,8 @@ struct rmt_ctx {
     // optional kernel timers (rmt_sim profiling): [0,1] around the four RK4 stage kernels,
     // [2,3] around the extrapolation sweep kernel
     bool prof = false;
+    int ex_layers = 0;          // last extrapolation call (rmt_extrap_last_path)
+    bool ex_chain = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 

@@ -161,6 +161,21 @@ def extrapolate_reference_map(X1, X2, phi, dx, dy, max_layers):
     return io.out(o1), io.out(o2)
 
 
+def extrapolation_mode(mode):
+    """librmt diagnostic: 0 chain path (default, sweep on capacity fallback), 1 sweep only,
+    2 chain pre-passes then the sweep forced."""
+    L.check(L.lib().rmt_extrap_set_mode(int(mode)), "rmt_extrap_set_mode")
+
+
+def extrapolation_last_path(ny, nx):
+    """librmt diagnostic: 0 if the last extrapolation on this grid ran the chain path,
+    1 if it ran the row-ticket sweep."""
+    p = ctypes.c_int(-1)
+    L.check(L.lib().rmt_extrap_last_path(ctx_for(ny, nx).bind(), ctypes.byref(p)),
+            "rmt_extrap_last_path")
+    return p.value
+
+
 def advect_semilagrangian_rk4(q, a, b, X, Y, dt, dx, dy):
     io = _IO(q, a, b, X, Y); q, a, b, X, Y = map(io.dev, (q, a, b, X, Y))
     out = io.empty(q.shape)

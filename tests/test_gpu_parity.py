@@ -123,15 +123,40 @@ def _extrap_case(name):
     return X1 * solid, X2 * solid, phi, 1.0 / (nx - 1), 1.0 / (ny - 1), layers
 
 
+# cases the chain path must take itself (the others exceed its ring distance and fall back)
+_CHAIN_CASES = {"disc1024", "discs3", "rect_l1", "rect_l6", "corner", "empty", "full", "disc4096"}
+
+
 @pytest.mark.parametrize("name", ["disc1024", "slab", "discs3", "rect_l1", "rect_l6", "wide",
                                   "corner", "empty", "full", "disc4096"])
-def test_extrapolation_vs_oracle(gpu, oracle, name):
-    """The multi-wave sweep reproduces the serial raster-order chain bit for bit, at the bench
-    size (4096^2) too."""
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_extrapolation_vs_oracle(gpu, oracle, name, mode):
+    """Both extrapolation paths reproduce the serial raster-order chain bit for bit, at the
+    bench size (4096^2) too: mode 0 = geometry-first chain (extrap_chain.hip), 1 = row-ticket
+    sweep alone, 2 = the chain's pre-passes followed by a forced sweep fallback."""
     X1, X2, phi, dx, dy, layers = _extrap_case(name)
-    r1, r2 = oracle.extrapolate_reference_map(X1, X2, phi, dx, dy, layers)
-    g1, g2 = gpu.extrapolate_reference_map(X1, X2, phi, dx, dy, layers)
+    r1, r2 = _extrap_ref(oracle, name)
+    gpu.extrapolation_mode(mode)
+    try:
+        g1, g2 = gpu.extrapolate_reference_map(X1, X2, phi, dx, dy, layers)
+        path = gpu.extrapolation_last_path(*phi.shape)
+    finally:
+        gpu.extrapolation_mode(0)
     _eq(g1, r1); _eq(g2, r2)
+    if mode == 0 and name in _CHAIN_CASES:
+        assert path == 0, "chain path fell back"
+    if mode != 0:
+        assert path == 1
+
+
+_EXTRAP_REF = {}
+
+
+def _extrap_ref(oracle, name):
+    if name not in _EXTRAP_REF:
+        X1, X2, phi, dx, dy, layers = _extrap_case(name)
+        _EXTRAP_REF[name] = oracle.extrapolate_reference_map(X1, X2, phi, dx, dy, layers)
+    return _EXTRAP_REF[name]
 
 
 def test_momentum_pure_fluid_bitwise(gpu, oracle):
