@@ -503,7 +503,8 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes) {
     w.dmark = (int *)take(maxt * 4);
     w.rej = (int *)take((size_t)ML * EX_MAXREJ * 4);
     w.ctl = (int *)take(EXC_WORDS * 4);
-    w.arena_bytes = maxt * 2560LL;   // ~2 KB per record on average at the bench sizes
+    // ~2 KB per record on average at the bench sizes; offsets are 25-bit in 64-B units
+    w.arena_bytes = std::min(maxt * 2560LL, (1LL << 31) - 65536);
     w.arena = take(w.arena_bytes);
     w.maxt = maxt;
     w.plane = plane;

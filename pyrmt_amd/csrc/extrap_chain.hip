@@ -259,8 +259,12 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
     const u64 th = ih & ~((qf >= 64) ? ((1ull << (qf - 64)) - 1) : 0ull);
     const int n = __popcll(tl) + __popcll(th), npad = (n + 7) & ~7;
     const int nd = __popcll(dl) + __popcll(dh);
-    const long long bytes = ((8LL * (CH_HDR + 6 * npad) + 8LL * nd) + 63) & ~63LL;
+    const long long bytes = ((8LL * (CH_HDR + 4 * nd + 6 * npad)) + 63) & ~63LL;
     unsigned long long off = 0;
+    if (nd > 64) {   // k_ex_chain forms one product per lane
+        if (lane == 0) { ws.ctl[EXC_FALLBACK] = 1; ws.recoff[id] = -1; }
+        return true;
+    }
     if (lane == 0) {
         off = atomicAdd((unsigned long long *)(ws.ctl + EXC_ARENA), (unsigned long long)bytes);
         if ((long long)(off + bytes) > ws.arena_bytes) ws.ctl[EXC_FALLBACK] = 1;
@@ -271,8 +275,8 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
         return true;   // (fallback sweep recomputes everything)
     }
     double *rec = (double *)(ws.arena + off);
-    double *tv = rec + CH_HDR;
-    int2 *dyn = (int2 *)(tv + 6 * npad);
+    double *dyn = rec + CH_HDR;           // nd entries {(k, src), w*1, w*x, w*y}
+    double *tv = dyn + 4 * nd;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const bool term = h ? ((th >> lane) & 1) && lane < 17 : (tl >> lane) & 1;
@@ -284,10 +288,9 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
             tv[2 * npad + k] = wa2 * b1[h]; tv[3 * npad + k] = wa0 * b2[h];
             tv[4 * npad + k] = wa1 * b2[h]; tv[5 * npad + k] = wa2 * b2[h];
         } else {
-            tv[0 * npad + k] = wa0; tv[1 * npad + k] = wa1; tv[2 * npad + k] = wa2;
-            tv[3 * npad + k] = wa0; tv[4 * npad + k] = wa1; tv[5 * npad + k] = wa2;
             const int dk = h ? __popcll(dl) + __popcll(dh & lt) : __popcll(dl & lt);
-            dyn[dk] = make_int2(k, src[h]);
+            dyn[4 * dk] = __longlong_as_double(((long long)src[h] << 32) | (unsigned)k);
+            dyn[4 * dk + 1] = wa0; dyn[4 * dk + 2] = wa1; dyn[4 * dk + 3] = wa2;
         }
     }
     if (lane < 6 * (npad - n)) tv[(lane / (npad - n)) * npad + n + lane % (npad - n)] = 0.0;
@@ -449,24 +452,31 @@ __global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, in
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(status, __popcll(b));
 }
 
-// record sources: fit ids -> chain indices; the ring needs every source < CH_R/2 back
+// record sources: fit ids -> chain indices (the ring needs every source < CH_R/2 back);
+// header word 23 <- (chain index, record) of the next accepted fit of the same chain wave
 __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
     if (ws.ctl[EXC_FALLBACK]) return;
-    const int id = blockIdx.x * 256 + threadIdx.x;
-    if (id >= ws.ctl[EXC_BASE + ML]) return;
+    const int id = blockIdx.x * 256 + threadIdx.x, total = ws.ctl[EXC_BASE + ML];
+    if (id >= total) return;
     const long long r = ws.recoff[id];
     if (r < 0) return;
     double *rec = (double *)(ws.arena + ((r & 0xffffffffLL) << 6));
     const long long meta = __double_as_longlong(rec[1]);
     const int npad = (int)(meta & 0xffffffff), nd = (int)(meta >> 32);
-    int2 *dyn = (int2 *)(rec + CH_HDR + 6 * npad);
+    int2 *dyn = (int2 *)(rec + CH_HDR);   // entry d at int2 index 2d: (k, src)
     const int x = ws.chain_of[id];
+    (void)npad;
     for (int d = 0; d < nd; ++d) {
-        const int xs = ws.chain_of[dyn[d].y];
-        dyn[d].y = xs;
+        const int xs = ws.chain_of[dyn[4 * d].y];
+        dyn[4 * d].y = xs;
         if (xs >= x) { ws.ctl[EXC_ABORT] = 1; atomicExch(ws.status + 1, 1); }   // a bug
         else if (x - xs >= CH_R / 2) ws.ctl[EXC_FALLBACK] = 1;
     }
+    int xn = x + CH_W;
+    while (xn < total && ws.rec_by_chain[xn] < 0) xn += CH_W;
+    const long long rn = xn < total ? ws.rec_by_chain[xn] : 0;   // (size64 << 32) | off64
+    const unsigned r32 = (unsigned)(rn & 0xffffffffLL) | ((unsigned)(rn >> 32) << 25);
+    rec[23] = __longlong_as_double(((long long)xn << 32) | r32);
 }
 
 // ------------------------------------------------------------------ 3. the chain ---
@@ -480,178 +490,242 @@ struct ChainArgs {
     int *status;
 };
 
-struct Rec5 { double2 v0, v1, v2, v3, v4; };   // one record, 16 B per lane per KB
+// record r (packed: 64-B units of offset | size << 25) -> five 16-B pieces per lane; every
+// lane issues the same 5 loads (lanes past the record re-read its last piece, same line).
+// Plain named registers, not an aggregate: an aggregate gets promoted to LDS, which turns the
+// prefetch into a synchronous copy.
+#define CH_LOAD(r)                                                                   \
+    do {                                                                             \
+        const double2 *p_ = (const double2 *)(arena + ((size_t)((r) & 0x1ffffff) << 6)); \
+        const int l_ = (int)(((r) >> 25) << 2) - 1;                                  \
+        d0 = p_[min(lane, l_)];        d1 = p_[min(64 + lane, l_)];                  \
+        d2 = p_[min(128 + lane, l_)];  d3 = p_[min(192 + lane, l_)];                 \
+        d4 = p_[min(256 + lane, l_)];                                                \
+    } while (0)
+#define CH_STAGE(r)                                                                  \
+    do {                                                                             \
+        const int n_ = (int)(((r) >> 25) << 2);                                      \
+        double2 *B2 = (double2 *)B;                                                  \
+        if (lane < n_) B2[lane] = d0;                                                \
+        if (64 + lane < n_) B2[64 + lane] = d1;                                      \
+        if (128 + lane < n_) B2[128 + lane] = d2;                                    \
+        if (192 + lane < n_) B2[192 + lane] = d3;                                    \
+        if (256 + lane < n_) B2[256 + lane] = d4;                                    \
+    } while (0)
 
-// this wave's LDS record buffer <- the prefetched registers
-__device__ __forceinline__ void ch_stage(double *B, long long r, int lane, Rec5 d) {
-    if (r < 0) return;
-    const int n16 = (int)((r >> 32) << 2);
-    double2 *B2 = (double2 *)B;
-    if (lane < n16) B2[lane] = d.v0;
-    if (64 + lane < n16) B2[64 + lane] = d.v1;
-    if (128 + lane < n16) B2[128 + lane] = d.v2;
-    if (192 + lane < n16) B2[192 + lane] = d.v3;
-    if (256 + lane < n16) B2[256 + lane] = d.v4;
-}
-
-__device__ __forceinline__ void ch_load(const char *arena, long long r, int lane, Rec5 &v) {
-    // rejected fits (r < 0) load piece 0 of the arena (never used); lanes past the record
-    // re-read its last piece (same line), so every lane issues the same 5 loads
-    const double2 *p = (const double2 *)(arena + (r < 0 ? 0 : (r & 0xffffffffLL) << 6));
-    const int last = r < 0 ? 0 : (int)((r >> 32) << 2) - 1;
-    v.v0 = p[min(lane, last)];
-    v.v1 = p[min(64 + lane, last)];
-    v.v2 = p[min(128 + lane, last)];
-    v.v3 = p[min(192 + lane, last)];
-    v.v4 = p[min(256 + lane, last)];
-}
-
-// one fit of the chain (chain index x, record r0 whose bytes are in d0); false on a timeout
-__device__ __forceinline__ bool ch_fit(double *X1e, double *X2e, int x, long long r0,
-                                       int lane, int wv, double *B,
-                                       double2 *val, int *tag, int *cur, int &wm) {
-    bool ok = true;
-    __hip_atomic_store(&cur[wv], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (r0 >= 0) {
-        // ring reuse: every fit < x - CH_R/2 is done (their readers are all < x)
-        long spins = 0;
-        while (x - CH_R / 2 >= wm) {
-            int m = 0x7fffffff;
-            for (int k = 0; k < CH_W; ++k)
-                m = min(m, __hip_atomic_load(&cur[k], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WORKGROUP));
-            wm = m;
-            if (x - CH_R / 2 >= wm) {
-                if (++spins > CH_SPIN_LIMIT) { ok = false; break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
+// One fit of the chain: chain index x whose record is staged in this wave's buffer B.
+// LDS hand-offs: a fit writes its value pair, then its tag; a reader that sees the tag reads
+// the values afterwards (one wave's LDS operations are performed in issue order), so no
+// fence is needed -- and none is wanted: a workgroup fence would also drain the record
+// prefetch in flight.  Returns false on a timeout (bug guard).
+#define CH_STAMP(k)                                                    \
+    if constexpr (PROF) {                                              \
+        const long long t_ = __builtin_amdgcn_s_memtime();             \
+        pr[k] += t_ - tl; tl = t_;                                     \
+    }
+// fold row[8*c0 .. 8*c1) into acc in order; two 8-term chunks of reads in flight
+__device__ __forceinline__ double ch_fold(double acc, const double *row, int c0, int c1) {
+    if (c0 >= c1) return acc;
+    const double2 *r2 = (const double2 *)row;
+    double2 a0 = r2[4 * c0], a1 = r2[4 * c0 + 1], a2 = r2[4 * c0 + 2], a3 = r2[4 * c0 + 3];
+    for (int c = c0; c < c1; ++c) {
+        double2 b0, b1, b2, b3;
+        const bool more = c + 1 < c1;
+        if (more) {
+            b0 = r2[4 * c + 4]; b1 = r2[4 * c + 5]; b2 = r2[4 * c + 6]; b3 = r2[4 * c + 7];
         }
-        if (!ok) return false;
+        acc += a0.x; acc += a0.y; acc += a1.x; acc += a1.y;
+        acc += a2.x; acc += a2.y; acc += a3.x; acc += a3.y;
+        if (more) { a0 = b0; a1 = b1; a2 = b2; a3 = b3; }
+    }
+    return acc;
+}
+
+__device__ __forceinline__ double dpp_shl(double v, int ctrl) {
+    // row_shl:1 = 0x101, row_shl:2 = 0x102 (lanes read lane + k within their 16-lane row)
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const int l2 = ctrl == 1 ? __builtin_amdgcn_update_dpp(0, lo, 0x101, 0xf, 0xf, false)
+                             : __builtin_amdgcn_update_dpp(0, lo, 0x102, 0xf, 0xf, false);
+    const int h2 = ctrl == 1 ? __builtin_amdgcn_update_dpp(0, hi, 0x101, 0xf, 0xf, false)
+                             : __builtin_amdgcn_update_dpp(0, hi, 0x102, 0xf, 0xf, false);
+    return __hiloint2double(h2, l2);
+}
+
+// One fit of the chain: chain index x whose record is staged in this wave's buffer B.
+// Everything that does not need the last-arriving source runs before waiting for it: the
+// products of sources already published, the fold of the terms before the first missing
+// one, and the solve constants.  LDS hand-offs: a fit writes its value pair, then its tag; a
+// reader that sees the tag reads the values afterwards (one wave's LDS operations are
+// performed in issue order), so no fence is needed -- and none is wanted: a workgroup fence
+// would also drain the record prefetch in flight.  Returns false on a timeout (bug guard).
+template <bool PROF>
+__device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
+                                       int *cur, int &wm, double &o_out, long &c_out,
+                                       long long *pr, long long &tl) {
+    // ring reuse: every fit < x - CH_R/2 is done (all their readers are < x)
+    long spins = 0;
+    while (x - CH_R / 2 >= wm) {
+        int m = 0x7fffffff;
+        for (int k = 0; k < CH_W; ++k)
+            m = min(m, __hip_atomic_load(&cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        wm = m;
+        if (x - CH_R / 2 >= wm) {
+            if (++spins > CH_SPIN_LIMIT) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    CH_STAMP(1);
+    const long long meta = __double_as_longlong(B[1]);
+    const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
+    const int nd = __builtin_amdgcn_readfirstlane((int)(meta >> 32));
+    if (npad > CH_TVS || nd > 64 || npad < 0 || nd < 0) return false;   // bug guard
+    const double *dyn = B + CH_HDR;
+    double *tv = B + CH_HDR + 4 * nd;
+    // solve constants (lanes 0, 3) and this lane's dynamic source with its coefficients
+    // wave-uniform solve constants, kept in SGPRs
+    auto U = [&](int k) {
+        const double v = B[k];
+        return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                                __builtin_amdgcn_readfirstlane(__double2loint(v)));
+    };
+    const double x0 = U(2), y0 = U(3), M0 = U(4), M1 = U(5), M2 = U(6), M3 = U(7), M4 = U(8);
+    const double M5 = U(9), M6 = U(10), M7 = U(11), M8 = U(12), C0 = U(13), C1 = U(14);
+    const double C2 = U(15), inv_det = U(16);
+    double acc = 0.0;
+    if (lane < 6) acc = B[17 + lane];
+    const bool has = lane < nd;
+    int2 e = make_int2(0, -1);
+    double cf[3] = {0.0, 0.0, 0.0};   // w*1, w*x, w*y (the same for the X1 and X2 sums)
+    if (has) {
+        const double2 q0 = ((const double2 *)dyn)[2 * lane], q1 = ((const double2 *)dyn)[2 * lane + 1];
+        const long long kk = __double_as_longlong(q0.x);
+        e = make_int2((int)(kk & 0xffffffff), (int)(kk >> 32));
+        cf[0] = q0.y; cf[1] = q1.x; cf[2] = q1.y;
+    }
+    const int slot = e.y & (CH_R - 1);
+    bool done = !has;   // product written
+    // pass 1: products of the sources already published; fold up to the first missing one
+    {
+        const bool ready = has && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
+        asm volatile("" ::: "memory");
+        if (ready) {
+            const double2 v = val[slot];
+#pragma unroll
+            for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+            done = true;
+        }
+    }
+    // first window term whose source is still missing: sources are listed in window order
+    const u64 pend = __ballot(!done);
+    const int kmiss = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : npad;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int c1 = kmiss >> 3, nch = npad >> 3;
+    if (lane < 6) acc = ch_fold(acc, tv + lane * npad, 0, c1);
+    CH_STAMP(3);
+    // pass 2: wait for the missing sources, then the rest of the fold
+    if (pend) {
+        long sp = 0;
+        for (;;) {
+            if (!done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
+                asm volatile("" ::: "memory");
+                const double2 v = val[slot];
+#pragma unroll
+                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+                done = true;
+            }
+            if (__ballot(!done) == 0) break;
+            if (++sp > CH_SPIN_LIMIT) return false;
+            if constexpr (PROF) pr[7] += 1;
+            __builtin_amdgcn_s_sleep(0);
+        }
+        CH_STAMP(2);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        const long long meta = __double_as_longlong(B[1]);
-        const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
-        const int nd = __builtin_amdgcn_readfirstlane((int)(meta >> 32));
-        double *tv = B + CH_HDR;
-        // dynamic sources: wait for their values, then form the products in place
-        if (nd > 0) {
-            const int2 *dyn = (const int2 *)(tv + 6 * npad);
-            for (int d0i = 0; d0i < nd; d0i += 64) {
-                const int d = d0i + lane;
-                int2 e = make_int2(0, -1);
-                if (d < nd) e = dyn[d];
-                const int slot = e.y & (CH_R - 1);
-                bool ready = d >= nd;
-                long sp = 0;
-                while (true) {
-                    if (!ready)
-                        ready = __hip_atomic_load(&tag[slot], __ATOMIC_ACQUIRE,
-                                                  __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
-                    if (__ballot(!ready) == 0) break;
-                    if (++sp > CH_SPIN_LIMIT) { ok = false; break; }
-                    __builtin_amdgcn_s_sleep(0);
-                }
-                if (!ok) return false;
-                if (d < nd) {
-                    const double2 v = val[slot];
-#pragma unroll
-                    for (int s = 0; s < 6; ++s) {
-                        double *p = tv + s * npad + e.x;
-                        *p = *p * (s < 3 ? v.x : v.y);
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        }
-        // the 6 ordered sums of functions.py:128-133 (lanes 0-5), from the static prefix
-        double acc = 0.0;
-        if (lane < 6) {
-            acc = B[17 + lane];
-            const double2 *row = (const double2 *)(tv + lane * npad);
-            const int nq = npad >> 2;   // 4-term quads
-            double2 a0, a1, b0, b1;
-            if (nq > 0) { a0 = row[0]; a1 = row[1]; }
-            for (int qd = 0; qd < nq; qd += 2) {
-                if (qd + 1 < nq) { b0 = row[2 * qd + 2]; b1 = row[2 * qd + 3]; }
-                acc += a0.x; acc += a0.y; acc += a1.x; acc += a1.y;
-                if (qd + 1 < nq) {
-                    if (qd + 2 < nq) { a0 = row[2 * qd + 4]; a1 = row[2 * qd + 5]; }
-                    acc += b0.x; acc += b0.y; acc += b1.x; acc += b1.y;
-                }
-            }
-        }
-        // utils.py:134-166 on lanes 0 (X1) and 3 (X2) with the precomputed cofactors
-        const double bb1 = __shfl(acc, lane + 1), bb2 = __shfl(acc, lane + 2);
-        if (lane == 0 || lane == 3) {
-            const double b[3] = {acc, bb1, bb2};
-            const double *M = B + 4;
-            const double C0 = B[13], C1 = B[14], C2 = B[15], inv_det = B[16];
-            const double xs = (b[0] * C0 - M[1] * (b[1] * M[8] - M[5] * b[2]) +
-                               M[2] * (b[1] * M[7] - M[4] * b[2])) * inv_det;
-            const double ys = (M[0] * (b[1] * M[8] - M[5] * b[2]) - b[0] * C1 +
-                               M[2] * (M[3] * b[2] - b[1] * M[6])) * inv_det;
-            const double zs = (M[0] * (M[4] * b[2] - b[1] * M[7]) -
-                               M[1] * (M[3] * b[2] - b[1] * M[6]) + b[0] * C2) * inv_det;
-            const double o = xs + ys * B[2] + zs * B[3];
-            const int slot = x & (CH_R - 1);
-            ((double *)&val[slot])[lane == 0 ? 0 : 1] = o;
-            const long c0 = __double_as_longlong(B[0]);
-            (lane == 0 ? X1e : X2e)[c0] = o;
-        }
-        if (lane == 0)
-            __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    return ok;
+    if (lane < 6) acc = ch_fold(acc, tv + lane * npad, c1, nch);
+    if constexpr (PROF) asm volatile("" : "+v"(acc));
+    CH_STAMP(4);
+    // utils.py:134-166 on lanes 0 (X1) and 3 (X2) with the precomputed cofactors
+    const double bb1 = dpp_shl(acc, 1), bb2 = dpp_shl(acc, 2);
+    if (lane == 0 || lane == 3) {
+        const double b0 = acc, b1 = bb1, b2 = bb2;
+        const double xs = (b0 * C0 - M1 * (b1 * M8 - M5 * b2) + M2 * (b1 * M7 - M4 * b2)) * inv_det;
+        const double ys = (M0 * (b1 * M8 - M5 * b2) - b0 * C1 + M2 * (M3 * b2 - b1 * M6)) * inv_det;
+        const double zs = (M0 * (M4 * b2 - b1 * M7) - M1 * (M3 * b2 - b1 * M6) + b0 * C2) * inv_det;
+        const double o = xs + ys * x0 + zs * y0;
+        ((double *)&val[x & (CH_R - 1)])[lane == 0 ? 0 : 1] = o;
+        o_out = o;
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0)
+        __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    c_out = __double_as_longlong(B[0]);
+    if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    CH_STAMP(5);
+    return true;
 }
 
-__global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C) {
+template <bool PROF>
+__global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *gprof) {
     __shared__ double2 val[CH_R];
     __shared__ int tag[CH_R];
     __shared__ __attribute__((aligned(16))) double buf[CH_W][CH_BUFD];
     __shared__ int cur[CH_W];
-    __shared__ int s_abort;
     const int *ctl = C.ws.ctl;
-    const long long *rbc = C.ws.rec_by_chain;
     const char *arena = C.ws.arena;
     double *X1e = C.X1e, *X2e = C.X2e;
     for (int s = threadIdx.x; s < CH_R; s += blockDim.x) tag[s] = -1;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (threadIdx.x < CH_W) cur[threadIdx.x] = 0;
-    if (threadIdx.x == 0) s_abort = 0;
     __syncthreads();
     if (ctl[EXC_FALLBACK] || ctl[EXC_ABORT]) return;
     const int total = ctl[EXC_BASE + C.ML];
     double *B = buf[wv];
-    // record pipeline: offsets two ahead, data one ahead
-    long long r0 = wv < total ? rbc[wv] : -1;
-    long long r1 = wv + CH_W < total ? rbc[wv + CH_W] : -1;
-    Rec5 d0, d1;
-    ch_load(arena, r0, lane, d0);
+    // this wave's first accepted fit; every record names the wave's next one (k_ex_relink)
+    int x = wv;
+    long long r0 = -1;
+    while (x < total && (r0 = C.ws.rec_by_chain[x]) < 0) x += CH_W;
+    unsigned r = (unsigned)(r0 & 0xffffffffLL) | (unsigned)((r0 >> 32) << 25);
+    double2 d0, d1, d2, d3, d4;
+    if (x < total) CH_LOAD(r);
     int wm = 0;
     bool ok = true;
-    for (int x = wv; x < total; x += 2 * CH_W) {
-        // two fits per trip so the prefetched bytes never move between registers
-        const long long r2 = x + 2 * CH_W < total ? rbc[x + 2 * CH_W] : -1;
-        ch_stage(B, r0, lane, d0);
-        ch_load(arena, r1, lane, d1);
-        if (!ch_fit(X1e, X2e, x, r0, lane, wv, B, val, tag, cur, wm)) { ok = false; break; }
-        const int x1 = x + CH_W;
-        if (x1 >= total) break;
-        const long long r3 = x1 + 2 * CH_W < total ? rbc[x1 + 2 * CH_W] : -1;
-        ch_stage(B, r1, lane, d1);
-        ch_load(arena, r2, lane, d0);
-        if (!ch_fit(X1e, X2e, x1, r1, lane, wv, B, val, tag, cur, wm)) { ok = false; break; }
-        r0 = r2; r1 = r3;
+    long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = 0;
+    if constexpr (PROF) tl = __builtin_amdgcn_s_memtime();
+    double o = 0.0;      // previous fit's value (lane 0: X1, lane 3: X2) and cell
+    long c = -1;
+    while (x < total) {
+        __hip_atomic_store(&cur[wv], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        CH_STAGE(r);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        CH_STAMP(0);
+        // the previous fit's stores go out BEFORE the prefetch, so that waiting for the
+        // prefetched record next trip never waits on a younger store
+        if (c >= 0 && (lane == 0 || lane == 3)) (lane == 0 ? X1e : X2e)[c] = o;
+        // prefetch the next record of this wave into the registers just staged
+        const long long nx = __double_as_longlong(B[23]);
+        const int x2 = __builtin_amdgcn_readfirstlane((int)(nx >> 32));
+        const unsigned r2 = (unsigned)__builtin_amdgcn_readfirstlane((int)(nx & 0xffffffff));
+        if (x2 <= x) { ok = false; break; }   // bug guard: the wave's sequence must advance
+        if (x2 < total) CH_LOAD(r2);
+        CH_STAMP(6);
+        if (!ch_fit<PROF>(x, lane, B, val, tag, cur, wm, o, c, pr, tl)) { ok = false; break; }
+        x = x2; r = r2;
     }
+    if constexpr (PROF)
+        if (lane == 0)
+            for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&gprof[k], pr[k]);
+    if (ok && c >= 0 && (lane == 0 || lane == 3)) (lane == 0 ? X1e : X2e)[c] = o;
     __hip_atomic_store(&cur[wv], 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (!ok && lane == 0) {
         C.ws.ctl[EXC_ABORT] = 1;
         atomicExch(&C.status[1], 1);
     }
 }
-
 // ------------------------------------------------------------------ host side ------
 bool extrap_chain_supported(int ny, int nx, int ML) {
     return ML >= 1 && ML <= EX_MAXL && ny >= 3 && nx >= 3;
@@ -680,8 +754,33 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status};
-    k_ex_chain<<<1, CH_W * 64, 0, st>>>(C);
-    RMT_LAUNCHED();
+    static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
+    if (!prof) {
+        k_ex_chain<false><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+        RMT_LAUNCHED();
+    } else {
+        // diagnostic: per-phase shader clocks summed over the chain waves
+        long long *gp = nullptr, hp[8];
+        RMT_HIP(hipMalloc(&gp, sizeof(hp)));
+        RMT_HIP(hipMemsetAsync(gp, 0, sizeof(hp), st));
+        hipEvent_t e0, e1;
+        RMT_HIP(hipEventCreate(&e0)); RMT_HIP(hipEventCreate(&e1));
+        RMT_HIP(hipEventRecord(e0, st));
+        k_ex_chain<true><<<1, CH_W * 64, 0, st>>>(C, gp);
+        RMT_LAUNCHED();
+        RMT_HIP(hipEventRecord(e1, st));
+        RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));
+        int hs[2];
+        RMT_HIP(hipMemcpyAsync(hs, ws.status, sizeof(hs), hipMemcpyDeviceToHost, st));
+        RMT_HIP(hipStreamSynchronize(st));
+        float ms = 0;
+        RMT_HIP(hipEventElapsedTime(&ms, e0, e1));
+        fprintf(stderr, "[chain-prof] %.3f ms fits=%d | stage %.3g throttle %.3g wait %.3g "
+                "products %.3g fold %.3g solve+publish %.3g store+prefetch %.3g (Mclk, all "
+                "waves) polls %lld\n", ms, hs[0], hp[0] / 1e6, hp[1] / 1e6, hp[2] / 1e6,
+                hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6, hp[6] / 1e6, hp[7]);
+        hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
+    }
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], st));
     return RMT_OK;
 }

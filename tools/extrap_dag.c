@@ -34,6 +34,7 @@ int main(int argc, char **argv) {
     double *fin1 = malloc(cap * 8);
     long s_inc = 0, s_after1 = 0, s_dyn1 = 0; int maxlev1[16] = {0}; double maxfin1[16] = {0};
     int nf = 0, maxlev = 0;
+    long *fkey = malloc(sizeof(long) * cap); int *pa = malloc(4 * (cap * 20)), *pb = malloc(4 * (cap * 20)); long np = 0;
     double maxfin = 0, SOLVE = 10;
     long hist[100] = {0};
     long ndyn = 0;
@@ -94,6 +95,8 @@ int main(int argc, char **argv) {
                     hist[after < 99 ? after : 99]++;
                 }
                 ndyn += nd;
+                for (int k = 0; k < nd && np < cap * 20; ++k) { pa[np] = nf; pb[np] = dsrc[k]; ++np; }
+                fkey[nf] = ((long)(j + 5 * L) * ML + L) * nx + i;
                 { int lv1 = 0, qf = 81, nd1 = 0; double f1 = 0;
                   for (int k = 0; k < nd; ++k) if (lay[dsrc[k]] == L) {
                       ++nd1; if (dq[k] < qf) qf = dq[k];
@@ -117,6 +120,14 @@ int main(int argc, char **argv) {
     printf("layer-sequential: avg included %.1f, avg same-layer deps %.1f, avg terms from first same-layer dep %.1f\n", (double)s_inc/nf, (double)s_dyn1/nf, (double)s_after1/nf);
     { int tot = 0; double tf = 0; for (int L = 0; L < ML; ++L) { printf("  layer %d depth %d weighted %.0f\n", L, maxlev1[L] + 1, maxfin1[L]); tot += maxlev1[L] + 1; tf += maxfin1[L]; }
       printf("  sum of layer depths %d, weighted %.0f\n", tot, tf); }
+    { /* chain order (j + 5L, L, i) over all targets: max distance fit -> source */
+      long *srt = malloc(sizeof(long) * nf); int *rank = malloc(4 * nf);
+      for (int k = 0; k < nf; ++k) srt[k] = fkey[k] * 65536L + k;
+      int cmp(const void *a, const void *b) { long x = *(long *)a, y = *(long *)b; return x < y ? -1 : x > y; }
+      qsort(srt, nf, sizeof(long), cmp);
+      for (int k = 0; k < nf; ++k) rank[srt[k] & 65535 ? srt[k] % 65536 : srt[k] % 65536] = k;
+      long md = 0; for (long p = 0; p < np; ++p) { long d = rank[pa[p]] - rank[pb[p]]; if (d > md) md = d; if (d <= 0) printf("non-topological!\n"); }
+      printf("max chain distance fit->source: %ld\n", md); }
     printf("suffix length after latest dependency (hist):");
     for (int k = 0; k < 60; ++k) if (hist[k]) printf(" %d:%ld", k, hist[k]);
     printf("\n");
