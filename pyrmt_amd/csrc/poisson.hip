@@ -1,11 +1,18 @@
 // poisson.hip -- functions.py:1091-1119 DCT-I Neumann Poisson solve on MI355X.
 //
 // p = idctn(dctn(rhs, type=1) / eig, type=1) - mean(p).  An unnormalised DCT-I of length
-// n is the real part of the length-M = 2(n-1) real DFT of the even extension
-// [x0 .. x_{n-1}, x_{n-2} .. x1] (the same construction pocketfft uses inside scipy).
-// Each 2D transform = two rounds of {even-extend rows -> rocFFT batched R2C -> take the
-// real part transposed through LDS}, so both rounds transform contiguous rows.  scipy's
-// inverse DCT-I is the forward one scaled by 1/(2(n-1)) per axis.
+// n is the length-M = 2(n-1) DFT of the even extension [x0 .. x_{n-1}, x_{n-2} .. x1]
+// (the construction pocketfft uses inside scipy); that DFT is real, so TWO rows packed as
+// the real and imaginary parts of one complex sequence come back separated in Re and Im.
+// scipy's inverse DCT-I is the forward one scaled by 1/(2(n-1)) per axis.
+//
+// Main path (M <= 8192 and M = product of radices 2..31): k_dct1 -- one workgroup per row
+// pair, the whole length-M complex sequence resident in LDS (<= 128 KB), a mixed-radix
+// Stockham FFT with register-staged passes (read every butterfly input -> barrier ->
+// twiddle + small DFT -> write -> barrier).  A 2D solve is five launches:
+//   rows (x)  ->  transpose  ->  columns: DCT, / eig, inverse DCT, fused  ->  transpose
+//   ->  rows (x, inverse).
+// HBM traffic: 10 planes per solve.  Other sizes: rocFFT R2C rounds (the previous path).
 #include "rmt_internal.hpp"
 #include <vector>
 
@@ -22,6 +29,11 @@ struct DctPlan {
     double *T = nullptr;      // transposed real plane
     double *lamx = nullptr, *lamy = nullptr;
     double dx = 0, dy = 0;
+    // LDS FFT path
+    bool lds = false;
+    int big = 0;                            // a radix above 13 present
+    double2 *Wx = nullptr, *Wy = nullptr;   // e^{-2 pi i t / M} tables
+    int radx[16] = {0}, rady[16] = {0}, npx = 0, npy = 0;
 };
 
 static bool g_rocfft_ready = false;
@@ -56,6 +68,7 @@ void dct_destroy(DctPlan *P) {
     if (P->info) rocfft_execution_info_destroy(P->info);
     hipFree(P->work); hipFree(P->E); hipFree(P->C); hipFree(P->T);
     hipFree(P->lamx); hipFree(P->lamy);
+    hipFree(P->Wx); hipFree(P->Wy);
     delete P;
 }
 
@@ -67,13 +80,52 @@ static void host_lambda(int n, double h, std::vector<double> &lam) {
     for (int k = 0; k < n; ++k) lam[k] = -2.0 * (1.0 - std::cos(M_PI * k / (n - 1))) / h2;
 }
 
+constexpr int DCT_T = 512;        // threads per row pair
+constexpr int DCT_MAXM = 8192;    // complex LDS entries (128 KB)
+
+// radices of M for the LDS FFT (4 for pairs of 2); false if a prime factor > 31 remains
+static bool factor(int M, int *rad, int *np) {
+    int n = 0, m = M;
+    while (m % 4 == 0) { rad[n++] = 4; m /= 4; }
+    for (int r : {2, 3, 5, 7, 11, 13, 17, 19, 23})
+        while (m % r == 0) { if (n >= 16) return false; rad[n++] = r; m /= r; }
+    *np = n;
+    return m == 1 && M >= 2 && M <= DCT_MAXM;
+}
+
+static int twiddles(int M, double2 **W) {
+    std::vector<double2> h(M);
+    for (int t = 0; t < M; ++t) {
+        long double a = 2.0L * 3.141592653589793238462643383279502884L * t / M;
+        h[t] = make_double2((double)cosl(a), (double)-sinl(a));
+    }
+    RMT_HIP(hipMalloc(W, M * sizeof(double2)));
+    RMT_HIP(hipMemcpy(*W, h.data(), M * sizeof(double2), hipMemcpyHostToDevice));
+    return RMT_OK;
+}
+
 static int dct_plan(rmt_ctx *ctx, double dx, double dy) {
     DctPlan *P = ctx->dct;
     if (P && P->dx == dx && P->dy == dy) return RMT_OK;
-    if (!g_rocfft_ready) { RMT_TRY(rf(rocfft_setup(), "setup")); g_rocfft_ready = true; }
     if (!P) {
         P = ctx->dct = new DctPlan;
         P->ny = ctx->ny; P->nx = ctx->nx;
+        const int Mx = 2 * (P->nx - 1), My = 2 * (P->ny - 1);
+        static const bool force_rocfft = getenv("RMT_DCT_ROCFFT") && atoi(getenv("RMT_DCT_ROCFFT"));
+        P->lds = !force_rocfft && factor(Mx, P->radx, &P->npx) && factor(My, P->rady, &P->npy);
+        for (int k = 0; k < P->npx; ++k) P->big |= P->radx[k] > 13;
+        for (int k = 0; k < P->npy; ++k) P->big |= P->rady[k] > 13;
+    }
+    if (!P->lds && !g_rocfft_ready) { RMT_TRY(rf(rocfft_setup(), "setup")); g_rocfft_ready = true; }
+    if (P->lds && !P->Wx) {
+        const size_t n = (size_t)P->ny * P->nx;
+        RMT_TRY(twiddles(2 * (P->nx - 1), &P->Wx));
+        RMT_TRY(twiddles(2 * (P->ny - 1), &P->Wy));
+        RMT_HIP(hipMalloc(&P->T, n * sizeof(double)));
+        RMT_HIP(hipMalloc(&P->lamx, P->nx * sizeof(double)));
+        RMT_HIP(hipMalloc(&P->lamy, P->ny * sizeof(double)));
+    }
+    if (!P->lds && !P->px) {
         size_t Mx = 2 * (size_t)(P->nx - 1), My = 2 * (size_t)(P->ny - 1);
         RMT_TRY(make_r2c(&P->px, Mx, P->ny));
         if (P->ny == P->nx) P->py = nullptr;
@@ -157,6 +209,223 @@ static int round_rows(rmt_ctx *ctx, DctPlan *P, rocfft_plan plan, const double *
     return RMT_OK;
 }
 
+// ---------------------------------------------------------------- LDS FFT path --
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(__builtin_fma(a.x, b.x, -a.y * b.y), __builtin_fma(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+
+// in-register DFT of length R (forward, e^{-2 pi i jm/R}); constants from the W table
+template <int R>
+__device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *__restrict__ W, int M) {
+    if constexpr (R == 2) {
+        const double2 a = v[0], b = v[1];
+        v[0] = cadd(a, b); v[1] = csub(a, b);
+    } else if constexpr (R == 4) {
+        const double2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+        const double2 t2 = cadd(v[1], v[3]), t3 = csub(v[1], v[3]);
+        v[0] = cadd(t0, t2); v[2] = csub(t0, t2);
+        v[1] = make_double2(t1.x + t3.y, t1.y - t3.x);   // t1 - i t3
+        v[3] = make_double2(t1.x - t3.y, t1.y + t3.x);   // t1 + i t3
+    } else {
+        constexpr int K = (R - 1) / 2;
+        double2 a[K], b[K];
+        double2 x0 = v[0];
+#pragma unroll
+        for (int j = 1; j <= K; ++j) {
+            a[j - 1] = cadd(v[j], v[R - j]);
+            b[j - 1] = csub(v[j], v[R - j]);
+            x0 = cadd(x0, a[j - 1]);
+        }
+        const int step = M / R;
+#pragma unroll
+        for (int m = 1; m <= K; ++m) {
+            double2 A = v[0], S = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int j = 1; j <= K; ++j) {
+                const double2 w = W[((j * m) % R) * step];   // (cos, -sin)
+                A.x = __builtin_fma(a[j - 1].x, w.x, A.x);
+                A.y = __builtin_fma(a[j - 1].y, w.x, A.y);
+                S.x = __builtin_fma(b[j - 1].x, -w.y, S.x);
+                S.y = __builtin_fma(b[j - 1].y, -w.y, S.y);
+            }
+            v[m] = make_double2(A.x + S.y, A.y - S.x);        // A - i S
+            v[R - m] = make_double2(A.x - S.y, A.y + S.x);    // A + i S
+        }
+        v[0] = x0;
+    }
+}
+
+// one Stockham pass of radix R over z[0..M) (Ns = product of the earlier radices)
+template <int R>
+__device__ __forceinline__ void fft_pass(double2 *z, int M, int Ns, const double2 *__restrict__ W) {
+    constexpr int BPT = (DCT_MAXM / DCT_T + R - 1) / R;   // butterflies per thread (max)
+    const int nb = M / R, tid = threadIdx.x;
+    double2 v[BPT][R];
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+        const int j = tid + b * DCT_T;
+        if (j < nb)
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[b][r] = z[j + r * nb];
+    }
+    __syncthreads();
+    const int tstep = M / (Ns * R);
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+        const int j = tid + b * DCT_T;
+        if (j < nb) {
+            const int k = j % Ns;
+            if (Ns > 1)
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], W[k * r * tstep]);
+            small_dft<R>(v[b], W, M);
+            const int o = (j / Ns) * Ns * R + k;
+#pragma unroll
+            for (int r = 0; r < R; ++r) z[o + r * Ns] = v[b][r];
+        }
+    }
+    __syncthreads();
+}
+
+struct Radices { int r[16]; int n; };
+
+// BIG = 0: radices 2..13 (192 VGPRs); BIG = 1: up to 23 (244 VGPRs; one kernel holding every
+// radix up to 31 spills, so 29 and 31 go to rocFFT)
+template <int BIG>
+__device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__restrict__ W) {
+    int Ns = 1;
+    for (int p = 0; p < rd.n; ++p) {
+        const int R = rd.r[p];
+        switch (R) {
+            case 2: fft_pass<2>(z, M, Ns, W); break;
+            case 3: fft_pass<3>(z, M, Ns, W); break;
+            case 4: fft_pass<4>(z, M, Ns, W); break;
+            case 5: fft_pass<5>(z, M, Ns, W); break;
+            case 7: fft_pass<7>(z, M, Ns, W); break;
+            case 11: fft_pass<11>(z, M, Ns, W); break;
+            case 13: fft_pass<13>(z, M, Ns, W); break;
+            default:
+                if constexpr (BIG) {
+                    switch (R) {
+                        case 17: fft_pass<17>(z, M, Ns, W); break;
+                        case 19: fft_pass<19>(z, M, Ns, W); break;
+                        case 23: fft_pass<23>(z, M, Ns, W); break;
+                    }
+                }
+        }
+        Ns *= R;
+    }
+}
+
+// even extension of the row pair (a, b) into z: z[j] = z[M - j] = (a_j, b_j)
+__device__ __forceinline__ void put_even(double2 *z, int n, int M, int j, double a, double b) {
+    z[j] = make_double2(a, b);
+    if (j >= 1 && j <= n - 2) z[M - j] = make_double2(a, b);
+}
+
+// DCT-I along the rows of src (rows x n) -> dst, row pairs per workgroup.  SOLVE: rows are
+// x-frequencies kx (transposed plane), and the column transform is forward DCT, / eig,
+// inverse DCT (the eig of functions.py:1091-1104: lam_x[kx] + lam_y[ky], (0,0) -> 1).
+template <bool SOLVE, int BIG>
+__global__ void __launch_bounds__(DCT_T) k_dct1(const double *__restrict__ src,
+                                                double *__restrict__ dst, int rows, int n,
+                                                const double2 *__restrict__ W, Radices rd,
+                                                double scale, const double *__restrict__ lamr,
+                                                const double *__restrict__ lamk) {
+    extern __shared__ double2 z[];
+    const int M = 2 * (n - 1), rA = 2 * blockIdx.x, rB = rA + 1, tid = threadIdx.x;
+    const bool hasB = rB < rows;
+    const double *sa = src + (long)rA * n, *sb = src + (long)rB * n;
+    for (int j = tid; j < n; j += DCT_T) put_even(z, n, M, j, sa[j], hasB ? sb[j] : 0.0);
+    __syncthreads();
+    fft_lds<BIG>(z, M, rd, W);
+    if constexpr (SOLVE) {
+        constexpr int PER = 4096 / DCT_T + 1;
+        double2 q[PER];
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int k = tid + t * DCT_T;
+            if (k < n) {
+                const double2 Z = z[k];
+                const double eA = (rA == 0 && k == 0) ? 1.0 : lamr[rA] + lamk[k];
+                const double eB = hasB ? lamr[rB] + lamk[k] : 1.0;
+                q[t] = make_double2(Z.x / eA, hasB ? Z.y / eB : 0.0);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int k = tid + t * DCT_T;
+            if (k < n) put_even(z, n, M, k, q[t].x, q[t].y);
+        }
+        __syncthreads();
+        fft_lds<BIG>(z, M, rd, W);
+    }
+    double *da = dst + (long)rA * n, *db = dst + (long)rB * n;
+    for (int k = tid; k < n; k += DCT_T) {
+        const double2 Z = z[k];
+        da[k] = Z.x * scale;
+        if (hasB) db[k] = Z.y * scale;
+    }
+}
+
+// out (C x R) = in (R x C) transposed, 64 x 64 tiles through LDS
+__global__ void __launch_bounds__(256) k_transpose(const double *__restrict__ in, int R, int C,
+                                                   double *__restrict__ out) {
+    __shared__ double t[64][65];
+    const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int rr = ty; rr < 64; rr += 4) {
+        const int r = r0 + rr, c = c0 + tx;
+        if (r < R && c < C) t[rr][tx] = in[(long)r * C + c];
+    }
+    __syncthreads();
+    for (int cc = ty; cc < 64; cc += 4) {
+        const int c = c0 + cc, r = r0 + tx;
+        if (r < R && c < C) out[(long)c * R + r] = t[tx][cc];
+    }
+}
+
+static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p) {
+    const int ny = P->ny, nx = P->nx;
+    hipStream_t st = ctx->stream;
+    static bool attr = false;
+    if (!attr) {
+        const void *fs[4] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
+                             (const void *)k_dct1<false, 1>, (const void *)k_dct1<true, 1>};
+        for (auto f : fs)
+            RMT_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        DCT_MAXM * 16));
+        attr = true;
+    }
+    Radices rx{}, ry{};
+    for (int k = 0; k < 16; ++k) { rx.r[k] = P->radx[k]; ry.r[k] = P->rady[k]; }
+    rx.n = P->npx; ry.n = P->npy;
+    const size_t lx = 2 * (size_t)(nx - 1) * sizeof(double2), ly = 2 * (size_t)(ny - 1) * sizeof(double2);
+    auto rows = [&](bool solve, const double *src, double *dst, int nr, int n, const double2 *W,
+                    const Radices &rd, double scale, size_t lds) {
+        const unsigned g = (nr + 1) / 2;
+        if (solve) {
+            if (P->big) k_dct1<true, 1><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, P->lamx, P->lamy);
+            else k_dct1<true, 0><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, P->lamx, P->lamy);
+        } else {
+            if (P->big) k_dct1<false, 1><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, nullptr, nullptr);
+            else k_dct1<false, 0><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, nullptr, nullptr);
+        }
+    };
+    // forward along x: p <- DCT_x(rhs) (p doubles as scratch), then T <- p^T (nx x ny)
+    rows(false, rhs, p, ny, nx, P->Wx, rx, 1.0, lx);
+    k_transpose<<<dim3((nx + 63) / 64, (ny + 63) / 64), 256, 0, st>>>(p, ny, nx, P->T);
+    // columns: DCT_y, / eig, inverse DCT_y (scaled), in place on T
+    rows(true, P->T, P->T, nx, ny, P->Wy, ry, 1.0 / (2.0 * (ny - 1)), ly);
+    k_transpose<<<dim3((ny + 63) / 64, (nx + 63) / 64), 256, 0, st>>>(P->T, nx, ny, p);
+    // inverse along x, in place
+    rows(false, p, p, ny, nx, P->Wx, rx, 1.0 / (2.0 * (nx - 1)), lx);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
 __global__ void k_sub_mean(double *__restrict__ x, long n, const double *__restrict__ s) {
     long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (k < n) x[k] = x[k] - *s;
@@ -168,13 +437,17 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
     RMT_TRY(dct_plan(ctx, dx, dy));
     DctPlan *P = ctx->dct;
     const int ny = P->ny, nx = P->nx;
-    rocfft_plan px = P->px, py = P->py ? P->py : P->px;
-    // forward: along x (rows of rhs) -> T[ki][j]; along y -> p[kj][ki] / eig
-    RMT_TRY(round_rows(ctx, P, px, rhs, ny, nx, 1.0, nullptr, nullptr, P->T));
-    RMT_TRY(round_rows(ctx, P, py, P->T, nx, ny, 1.0, P->lamx, P->lamy, p));
-    // inverse: same transform, scaled by 1/(2(n-1)) per axis
-    RMT_TRY(round_rows(ctx, P, px, p, ny, nx, 1.0 / (2.0 * (nx - 1)), nullptr, nullptr, P->T));
-    RMT_TRY(round_rows(ctx, P, py, P->T, nx, ny, 1.0 / (2.0 * (ny - 1)), nullptr, nullptr, p));
+    if (P->lds) {
+        RMT_TRY(dct_lds_solve(ctx, P, rhs, p));
+    } else {
+        rocfft_plan px = P->px, py = P->py ? P->py : P->px;
+        // forward: along x (rows of rhs) -> T[ki][j]; along y -> p[kj][ki] / eig
+        RMT_TRY(round_rows(ctx, P, px, rhs, ny, nx, 1.0, nullptr, nullptr, P->T));
+        RMT_TRY(round_rows(ctx, P, py, P->T, nx, ny, 1.0, P->lamx, P->lamy, p));
+        // inverse: same transform, scaled by 1/(2(n-1)) per axis
+        RMT_TRY(round_rows(ctx, P, px, p, ny, nx, 1.0 / (2.0 * (nx - 1)), nullptr, nullptr, P->T));
+        RMT_TRY(round_rows(ctx, P, py, P->T, nx, ny, 1.0 / (2.0 * (ny - 1)), nullptr, nullptr, p));
+    }
     const long n = (long)ny * nx;
     double *mean = ctx->red + RED_BLOCKS + 8;
     RMT_TRY(reduce_mean(ctx, p, n, mean));

@@ -188,6 +188,24 @@ def test_momentum_solid_tolerance(gpu):
     np.testing.assert_allclose(m[1], o["mband_v"], rtol=0, atol=1e-14)
 
 
+@pytest.mark.parametrize("shape", [(49, 49), (65, 65), (257, 129), (256, 256), (130, 200),
+                                   (300, 4096), (1024, 1024), (4096, 4096)])
+def test_dct_solve_sizes(gpu, oracle, shape):
+    """functions.py:1107-1119 against scipy's pocketfft (the reference's own call) on random
+    right-hand sides.  Covers the LDS FFT's radix sets (2..13: 49, 65, 129, 4096; up to 23:
+    256, 300) and the rocFFT fallback (130, 200, 1024: a prime factor > 23 in 2(n-1)).
+    Bar: |p_gpu - p_ref| <= 1e-13 * max|p_ref| (different FFT algorithms round differently)."""
+    ny, nx = shape
+    dx, dy = 1.0 / (nx - 1), 1.0 / (ny - 1)
+    rng = np.random.default_rng(ny * 7 + nx)
+    rhs = rng.standard_normal((ny, nx))
+    eig = oracle._precompute_poisson_eigenvalues(nx, ny, dx, dy)
+    ref = oracle._solve_poisson_dct(rhs, eig)
+    got = gpu._solve_poisson_dct(rhs, eig)
+    err = np.abs(got - ref).max() / np.abs(ref).max()
+    assert err <= 1e-13, err
+
+
 def test_projection_pieces(gpu):
     o = golden("operators")
     dx, dy = float(o["dx"]), float(o["dy"])
