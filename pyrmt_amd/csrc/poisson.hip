@@ -82,6 +82,7 @@ static void host_lambda(int n, double h, std::vector<double> &lam) {
 
 constexpr int DCT_T = 512;        // threads per row pair
 constexpr int DCT_MAXM = 8192;    // complex LDS entries (128 KB)
+constexpr int DCT_RCS = 98;       // 3 + 5 + 7 + 11 + 13 + 17 + 19 + 23 radix constants
 
 // radices of M for the LDS FFT (4 for pairs of 2); false if a prime factor > 31 remains
 static bool factor(int M, int *rad, int *np) {
@@ -93,14 +94,29 @@ static bool factor(int M, int *rad, int *np) {
     return m == 1 && M >= 2 && M <= DCT_MAXM;
 }
 
+// radix constants e^{-2 pi i t/R} for every supported odd radix, at these offsets
+static const int kRcR[8] = {3, 5, 7, 11, 13, 17, 19, 23};
+static int rc_offset(int R) {
+    int o = 0;
+    for (int r : kRcR) { if (r == R) return o; o += r; }
+    return 0;
+}
+
 static int twiddles(int M, double2 **W) {
-    std::vector<double2> h(M);
+    const long double PI = 3.141592653589793238462643383279502884L;
+    std::vector<double2> h(M + DCT_RCS);
     for (int t = 0; t < M; ++t) {
-        long double a = 2.0L * 3.141592653589793238462643383279502884L * t / M;
+        long double a = 2.0L * PI * t / M;
         h[t] = make_double2((double)cosl(a), (double)-sinl(a));
     }
-    RMT_HIP(hipMalloc(W, M * sizeof(double2)));
-    RMT_HIP(hipMemcpy(*W, h.data(), M * sizeof(double2), hipMemcpyHostToDevice));
+    int o = M;
+    for (int R : kRcR)
+        for (int t = 0; t < R; ++t, ++o) {
+            long double a = 2.0L * PI * t / R;
+            h[o] = make_double2((double)cosl(a), (double)-sinl(a));
+        }
+    RMT_HIP(hipMalloc(W, h.size() * sizeof(double2)));
+    RMT_HIP(hipMemcpy(*W, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice));
     return RMT_OK;
 }
 
@@ -218,7 +234,7 @@ __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_doub
 
 // in-register DFT of length R (forward, e^{-2 pi i jm/R}); constants from the W table
 template <int R>
-__device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *__restrict__ W, int M) {
+__device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *rc) {
     if constexpr (R == 2) {
         const double2 a = v[0], b = v[1];
         v[0] = cadd(a, b); v[1] = csub(a, b);
@@ -238,13 +254,12 @@ __device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *__rest
             b[j - 1] = csub(v[j], v[R - j]);
             x0 = cadd(x0, a[j - 1]);
         }
-        const int step = M / R;
 #pragma unroll
         for (int m = 1; m <= K; ++m) {
             double2 A = v[0], S = make_double2(0.0, 0.0);
 #pragma unroll
             for (int j = 1; j <= K; ++j) {
-                const double2 w = W[((j * m) % R) * step];   // (cos, -sin)
+                const double2 w = rc[(j * m) % R];   // (cos, -sin) of 2 pi jm / R
                 A.x = __builtin_fma(a[j - 1].x, w.x, A.x);
                 A.y = __builtin_fma(a[j - 1].y, w.x, A.y);
                 S.x = __builtin_fma(b[j - 1].x, -w.y, S.x);
@@ -257,11 +272,21 @@ __device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *__rest
     }
 }
 
-// one Stockham pass of radix R over z[0..M) (Ns = product of the earlier radices)
+// Twiddles e^{-2 pi i t/M} as Wh[t >> 7] * Wl[t & 127] (both tables in LDS, <= 2 ulp)
+struct Tw { const double2 *hi, *lo; };
+__device__ __forceinline__ double2 tw(const Tw &T, int t) { return cmul(T.hi[t >> 7], T.lo[t & 127]); }
+
+// Per pass: radix, Ns (product of the earlier radices), and 1/Ns for divide-free index math
+struct Pass { int R, Ns; float inv; int rc; };   // rc: offset of this radix's constants
+struct Radices { Pass p[16]; int n; };
+
+// one Stockham pass of radix R over z[0..M)
 template <int R>
-__device__ __forceinline__ void fft_pass(double2 *z, int M, int Ns, const double2 *__restrict__ W) {
+__device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps, const Tw &T,
+                                         const double2 *rcs) {
     constexpr int BPT = (DCT_MAXM / DCT_T + R - 1) / R;   // butterflies per thread (max)
-    const int nb = M / R, tid = threadIdx.x;
+    const int nb = M / R, tid = threadIdx.x, Ns = ps.Ns;
+    const double2 *rc = rcs + ps.rc;
     double2 v[BPT][R];
 #pragma unroll
     for (int b = 0; b < BPT; ++b) {
@@ -276,12 +301,13 @@ __device__ __forceinline__ void fft_pass(double2 *z, int M, int Ns, const double
     for (int b = 0; b < BPT; ++b) {
         const int j = tid + b * DCT_T;
         if (j < nb) {
-            const int k = j % Ns;
+            int g = (int)((float)j * ps.inv), k = j - g * Ns;   // j = g Ns + k
+            if (k < 0) { --g; k += Ns; } else if (k >= Ns) { ++g; k -= Ns; }
             if (Ns > 1)
 #pragma unroll
-                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], W[k * r * tstep]);
-            small_dft<R>(v[b], W, M);
-            const int o = (j / Ns) * Ns * R + k;
+                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw(T, k * r * tstep));
+            small_dft<R>(v[b], rc);
+            const int o = g * Ns * R + k;
 #pragma unroll
             for (int r = 0; r < R; ++r) z[o + r * Ns] = v[b][r];
         }
@@ -289,33 +315,29 @@ __device__ __forceinline__ void fft_pass(double2 *z, int M, int Ns, const double
     __syncthreads();
 }
 
-struct Radices { int r[16]; int n; };
-
-// BIG = 0: radices 2..13 (192 VGPRs); BIG = 1: up to 23 (244 VGPRs; one kernel holding every
-// radix up to 31 spills, so 29 and 31 go to rocFFT)
+// BIG = 0: radices 2..13; BIG = 1: up to 23 (one kernel holding every radix up to 31 spills,
+// so 29 and 31 go to rocFFT)
 template <int BIG>
-__device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__restrict__ W) {
-    int Ns = 1;
-    for (int p = 0; p < rd.n; ++p) {
-        const int R = rd.r[p];
-        switch (R) {
-            case 2: fft_pass<2>(z, M, Ns, W); break;
-            case 3: fft_pass<3>(z, M, Ns, W); break;
-            case 4: fft_pass<4>(z, M, Ns, W); break;
-            case 5: fft_pass<5>(z, M, Ns, W); break;
-            case 7: fft_pass<7>(z, M, Ns, W); break;
-            case 11: fft_pass<11>(z, M, Ns, W); break;
-            case 13: fft_pass<13>(z, M, Ns, W); break;
+__device__ void fft_lds(double2 *z, int M, const Radices &rd, const Tw &T, const double2 *rcs) {
+    for (int q = 0; q < rd.n; ++q) {
+        const Pass &ps = rd.p[q];
+        switch (ps.R) {
+            case 2: fft_pass<2>(z, M, ps, T, rcs); break;
+            case 3: fft_pass<3>(z, M, ps, T, rcs); break;
+            case 4: fft_pass<4>(z, M, ps, T, rcs); break;
+            case 5: fft_pass<5>(z, M, ps, T, rcs); break;
+            case 7: fft_pass<7>(z, M, ps, T, rcs); break;
+            case 11: fft_pass<11>(z, M, ps, T, rcs); break;
+            case 13: fft_pass<13>(z, M, ps, T, rcs); break;
             default:
                 if constexpr (BIG) {
-                    switch (R) {
-                        case 17: fft_pass<17>(z, M, Ns, W); break;
-                        case 19: fft_pass<19>(z, M, Ns, W); break;
-                        case 23: fft_pass<23>(z, M, Ns, W); break;
+                    switch (ps.R) {
+                        case 17: fft_pass<17>(z, M, ps, T, rcs); break;
+                        case 19: fft_pass<19>(z, M, ps, T, rcs); break;
+                        case 23: fft_pass<23>(z, M, ps, T, rcs); break;
                     }
                 }
         }
-        Ns *= R;
     }
 }
 
@@ -335,14 +357,20 @@ __global__ void __launch_bounds__(DCT_T) k_dct1(const double *__restrict__ src,
                                                 double scale, const double *__restrict__ lamr,
                                                 const double *__restrict__ lamk) {
     extern __shared__ double2 z[];
+    __shared__ double2 twh[DCT_MAXM / 128], twl[128], rcs[DCT_RCS];
     const int M = 2 * (n - 1), rA = 2 * blockIdx.x, rB = rA + 1, tid = threadIdx.x;
+    // tables: W has M + 192 entries: [0, M) e^{-2 pi i t/M}, then at M the small-radix constants
+    if (tid < DCT_MAXM / 128) twh[tid] = (tid << 7) < M ? W[tid << 7] : make_double2(1.0, 0.0);
+    if (tid < 128) twl[tid] = tid < M ? W[tid] : make_double2(1.0, 0.0);
+    if (tid < DCT_RCS) rcs[tid] = W[M + tid];
+    const Tw T{twh, twl};
     const bool hasB = rB < rows;
     const double *sa = src + (long)rA * n, *sb = src + (long)rB * n;
     for (int j = tid; j < n; j += DCT_T) put_even(z, n, M, j, sa[j], hasB ? sb[j] : 0.0);
     __syncthreads();
-    fft_lds<BIG>(z, M, rd, W);
+    fft_lds<BIG>(z, M, rd, T, rcs);
     if constexpr (SOLVE) {
-        constexpr int PER = 4096 / DCT_T + 1;
+        constexpr int PER = (4096 + DCT_T) / DCT_T;
         double2 q[PER];
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
@@ -361,7 +389,7 @@ __global__ void __launch_bounds__(DCT_T) k_dct1(const double *__restrict__ src,
             if (k < n) put_even(z, n, M, k, q[t].x, q[t].y);
         }
         __syncthreads();
-        fft_lds<BIG>(z, M, rd, W);
+        fft_lds<BIG>(z, M, rd, T, rcs);
     }
     double *da = dst + (long)rA * n, *db = dst + (long)rB * n;
     for (int k = tid; k < n; k += DCT_T) {
@@ -399,9 +427,17 @@ static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p)
                                         DCT_MAXM * 16));
         attr = true;
     }
-    Radices rx{}, ry{};
-    for (int k = 0; k < 16; ++k) { rx.r[k] = P->radx[k]; ry.r[k] = P->rady[k]; }
-    rx.n = P->npx; ry.n = P->npy;
+    auto passes = [](const int *rad, int np) {
+        Radices rd{};
+        int Ns = 1;
+        for (int k = 0; k < np; ++k) {
+            rd.p[k] = Pass{rad[k], Ns, (float)(1.0 / Ns), rc_offset(rad[k])};
+            Ns *= rad[k];
+        }
+        rd.n = np;
+        return rd;
+    };
+    const Radices rx = passes(P->radx, P->npx), ry = passes(P->rady, P->npy);
     const size_t lx = 2 * (size_t)(nx - 1) * sizeof(double2), ly = 2 * (size_t)(ny - 1) * sizeof(double2);
     auto rows = [&](bool solve, const double *src, double *dst, int nr, int n, const double2 *W,
                     const Radices &rd, double scale, size_t lds) {
