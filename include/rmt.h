@@ -204,6 +204,43 @@ int rmt_sim_phase_times(rmt_sim *sim, double *ms8, long *calls8);
 /* Copy the diagnostics of all completed steps since creation (blocks). */
 int rmt_sim_diagnostics(rmt_sim *sim, rmt_diag *out, int max_records, int *n_records);
 
+/* ---- slab-decomposed step (the fused step over G GPUs, 1D row slabs) ----
+ * One rmt_slab = rows [r0, r1) of the global ny x nx grid (row_splits[rank] ..
+ * row_splits[rank+1]) plus RMT_SLAB_HALO resident rows on each side, and the column block
+ * [col_splits[rank], col_splits[rank+1]) of the transposed DCT pass.  The caller
+ * (pyrmt_amd/distributed.py) runs the phases below on every slab, in this order, and
+ * performs the collectives named between them (torch.distributed over RCCL, or in-process
+ * copies); the result is bit-identical to rmt_sim_step when every slab holds 2^m rows at a
+ * multiple of 2^m (the row-tree means), and equal to rounding otherwise.
+ * The ctx must be created for the GLOBAL grid; splits must be even and slabs >= HALO rows.
+ * Replaces the loop body of soft_disc_in_lid_driven.py:206-235 (semi-Lagrangian, one disc).
+ *   buffers: 0-6 u v p X1 X2 phi J (resident (hi-lo) x nx planes), 7 p_c plane,
+ *            8 known bits (ny x W u64), 9 rim entries (3 doubles each), 10 DCT slab buffer
+ *            (owned x nx), 11 DCT column buffer (ny x nc), 12 scalars (16 doubles:
+ *            [0] max|u|^2 owned, [1..10] diag partials, [11] flags (1 non-finite velocity,
+ *            2 halo overrun, 4 extrapolation abort), [12] rim count, [13] row-tree root,
+ *            [14] cells fitted)
+ *   info: r0, r1, lo, hi, c0, c1, W (64-cell words per row), HALO; and the constant dt. */
+#define RMT_SLAB_HALO 12
+typedef struct rmt_slab rmt_slab;
+int rmt_slab_create(rmt_ctx *ctx, const rmt_sim_params *prm, int G, int rank,
+                    const int *row_splits, const int *col_splits, rmt_slab **out);
+int rmt_slab_destroy(rmt_slab *slab);
+int rmt_slab_info(rmt_slab *slab, int *ints8, double *dt_const);
+int rmt_slab_buffer(rmt_slab *slab, int id, void **dev_ptr);
+int rmt_slab_begin(rmt_slab *slab);                      /* scal[0] of the initial state  */
+int rmt_slab_advect(rmt_slab *slab, double dt);          /* then: allgather known bit rows */
+int rmt_slab_rim_pack(rmt_slab *slab);                   /* then: allgather rim entries    */
+int rmt_slab_extrapolate(rmt_slab *slab, const double *gathered, const long long *counts,
+                         long long cap);                 /* gathered: G x cap x 3 (device) */
+int rmt_slab_momentum(rmt_slab *slab, double dt);
+int rmt_slab_project_rows(rmt_slab *slab, double dt);    /* then: all_to_all 10 -> 11      */
+int rmt_slab_project_cols(rmt_slab *slab);               /* then: all_to_all 11 -> 10      */
+int rmt_slab_project_unrows(rmt_slab *slab);             /* then: allgather scal[13]       */
+int rmt_slab_sub_mean(rmt_slab *slab, int which, const double *roots_dev);  /* 0 p_c, 1 p */
+int rmt_slab_project_correct(rmt_slab *slab, double dt); /* after halo(p_c); then roots   */
+int rmt_slab_finish(rmt_slab *slab);                     /* then: allgather scal          */
+
 #ifdef __cplusplus
 }
 #endif

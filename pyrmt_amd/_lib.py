@@ -81,6 +81,23 @@ SIGNATURES = {
     "rmt_sim_diagnostics": (_I, [_P, ctypes.POINTER(rmt_diag), _I, ctypes.POINTER(_I)]),
     "rmt_sim_set_profiling": (_I, [_P, _I]),
     "rmt_sim_phase_times": (_I, [_P, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
+    # slab-decomposed step (distributed.py)
+    "rmt_slab_create": (_I, [_P, ctypes.POINTER(rmt_sim_params), _I, _I, ctypes.POINTER(_I),
+                             ctypes.POINTER(_I), ctypes.POINTER(_P)]),
+    "rmt_slab_destroy": (_I, [_P]),
+    "rmt_slab_info": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_D)]),
+    "rmt_slab_buffer": (_I, [_P, _I, ctypes.POINTER(_P)]),
+    "rmt_slab_begin": (_I, [_P]),
+    "rmt_slab_advect": (_I, [_P, _D]),
+    "rmt_slab_rim_pack": (_I, [_P]),
+    "rmt_slab_extrapolate": (_I, [_P, _P, ctypes.POINTER(ctypes.c_longlong), ctypes.c_longlong]),
+    "rmt_slab_momentum": (_I, [_P, _D]),
+    "rmt_slab_project_rows": (_I, [_P, _D]),
+    "rmt_slab_project_cols": (_I, [_P]),
+    "rmt_slab_project_unrows": (_I, [_P]),
+    "rmt_slab_sub_mean": (_I, [_P, _I, _P]),
+    "rmt_slab_project_correct": (_I, [_P, _D]),
+    "rmt_slab_finish": (_I, [_P]),
 }
 
 _lib = None

@@ -52,11 +52,13 @@ __global__ void __launch_bounds__(256) k_ex_bits(const double *__restrict__ phi,
                                                  const double *__restrict__ X1,
                                                  const double *__restrict__ X2,
                                                  double *__restrict__ X1o,
-                                                 double *__restrict__ X2o, int copy) {
+                                                 double *__restrict__ X2o, int copy,
+                                                 const u64 *__restrict__ kin) {
     const int j = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
     const long c = (long)j * nx + i;
     const bool in = i < nx;
-    const bool k = in && phi[c] < 0;
+    // kin: the known plane given directly (slab-decomposed step: gathered bit rows)
+    const bool k = in && (kin ? ((kin[(long)j * W + (i >> 6)] >> (i & 63)) & 1) : phi[c] < 0);
     if (in && copy) { X1o[c] = X1[c]; X2o[c] = X2[c]; }
     const u64 m = __ballot(k);
     if ((threadIdx.x & 63) == 0 && (i >> 6) < W) {
@@ -519,7 +521,8 @@ size_t extrap_workspace(int ny, int nx, int max_layers) {
 }
 
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
-                double dy, int max_layers, double *X1o, double *X2o, int *dev_status) {
+                double dy, int max_layers, double *X1o, double *X2o, int *dev_status,
+                const u64 *kin) {
     const int ny = ctx->ny, nx = ctx->nx;
     const long n = (long)ny * nx;
     const int W = (nx + 63) / 64;
@@ -540,7 +543,7 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
     const int copy = (X1o != X1) || (X2o != X2);
     k_ex_bits<<<dim3((nx + 255) / 256, ny), 256, 0, ctx->stream>>>(
         phi, ny, nx, W, max_layers, ws.kbits, ws.Kold, ws.rowcand, ws.jrange, X1, X2, X1o, X2o,
-        copy);
+        copy, kin);
     RMT_HIP(hipMemsetAsync(ws.status, 0, 4 * sizeof(int), ctx->stream));
     if (chain) {
         RMT_HIP(hipMemsetAsync(ws.ctl, 0, EXC_WORDS * sizeof(int), ctx->stream));

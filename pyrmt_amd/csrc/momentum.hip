@@ -6,6 +6,7 @@
 // s2 -> k3, acc += 2 k3; s3 -> u* = u + dt/6 (acc + k4) (pre-BC), i.e. exactly the
 // reference's left-to-right (((k1 + 2 k2) + 2 k3) + k4).
 #include "rmt_internal.hpp"
+#include <algorithm>
 
 namespace rmt {
 
@@ -15,9 +16,10 @@ __global__ void k_mom_prep(const double *__restrict__ X1, const double *__restri
                            double rho_s, double rho_f, double *__restrict__ sxx,
                            double *__restrict__ sxy, double *__restrict__ syy,
                            double *__restrict__ J, double *__restrict__ H,
-                           double *__restrict__ rho, unsigned char *__restrict__ solid) {
-    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)ny * nx) return;
+                           double *__restrict__ rho, unsigned char *__restrict__ solid,
+                           int jb, int je) {
+    long c = (long)jb * nx + blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)je * nx) return;
     int j = (int)(c / nx), i = (int)(c % nx);
     Stress s{0.0, 0.0, 0.0, 1.0};
     if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1)
@@ -143,11 +145,11 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     double rho_f, const double *__restrict__ p, double dt6, double dx, double dy, int ny, int nx,
     int tiles_x, int ntiles, double *__restrict__ ku, double *__restrict__ kv,
     double *__restrict__ accu, double *__restrict__ accv, double *__restrict__ outu,
-    double *__restrict__ outv) {
+    double *__restrict__ outv, RowWin rw) {
     __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
     __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
     const int tile = xcd_tile(blockIdx.x, ntiles);
-    const int i0 = (tile % tiles_x) * MS_TX, j0 = (tile / tiles_x) * MS_TY;
+    const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
     const double h2x = 2 * dx, h2y = 2 * dy;
     // 1. stage velocity (functions.py:714), BC applied; all loads issued before the LDS stores
     {
@@ -158,10 +160,10 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
         for (int it = 0; it < MS_NU; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q % MS_UX;
             const int j = j0 - 3 + ry, i = i0 - 3 + rx;
-            ok[it] = q < MS_UX * MS_UY && j >= 0 && j < ny && i >= 0 && i < nx;
+            ok[it] = q < MS_UX * MS_UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
             const BCSrc s = bc_source(bc, lid, ok[it] ? j : 1, ok[it] ? i : 1, ny, nx);
             uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
-            const long cu = ok[it] ? s.u_src : 0, cv = ok[it] ? s.v_src : 0;
+            const long cu = ok[it] ? s.u_src : (long)rw.lo * nx, cv = ok[it] ? s.v_src : (long)rw.lo * nx;
             a[it] = u[cu]; b[it] = v[cv];
             ka[it] = stage ? kpu[cu] : 0.0; kb[it] = stage ? kpv[cv] : 0.0;
         }
@@ -184,8 +186,8 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
         for (int it = 0; it < MS_NG; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
             const int j = j0 - 2 + ry, i = i0 - 2 + rx;
-            ok[it] = q < MS_GX * MS_GY && j >= 0 && j < ny && i >= 0 && i < nx;
-            const long c = ok[it] ? (long)j * nx + i : 0;
+            ok[it] = q < MS_GX * MS_GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
+            const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
             ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh[it] = H[c];
             sol[it] = solid[c] != 0;
         }
@@ -223,8 +225,8 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
         for (int it = 0; it < MS_NO; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
             const int j = j0 + ry, i = i0 + rx;
-            ok[it] = q < MS_TX * MS_TY && j < ny && i < nx;
-            const long c = ok[it] ? (long)j * nx + i : 0;
+            ok[it] = q < MS_TX * MS_TY && j < rw.je && i < nx;
+            const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
             // grad2(p) operands (functions.py:941): centred inside, one-sided at the edges
             // (inside: c+1 / c-1; i == 0: c+1; i == nx-1: c-1 as the "+s" operand; the "-s"
             // operand only inside) -- every index stays in the grid
@@ -282,14 +284,17 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     }
 }
 
-// Final BC (functions.py:760) on the boundary cells only: 2(nx + ny) threads.
-__global__ void k_bc_edges(int kind, double lid, double *u, double *v, int ny, int nx) {
-    int q = blockIdx.x * blockDim.x + threadIdx.x;
+// Final BC (functions.py:760) on the boundary cells of rows [jb, je) only: the bottom / top
+// rows when the window holds them, then the side columns.
+__global__ void k_bc_edges(int kind, double lid, double *u, double *v, int ny, int nx, int jb,
+                           int je) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int ra = max(jb, 1), rb = min(je, ny - 1), nr = max(rb - ra, 0);
     int j, i;
-    if (q < nx) { j = 0; i = q; }
-    else if (q < 2 * nx) { j = ny - 1; i = q - nx; }
-    else if (q < 2 * nx + ny - 2) { j = q - 2 * nx + 1; i = 0; }
-    else if (q < 2 * nx + 2 * (ny - 2)) { j = q - 2 * nx - (ny - 2) + 1; i = nx - 1; }
+    if (q < nx) { if (jb > 0) return; j = 0; i = q; }
+    else if (q < 2 * nx) { if (je < ny) return; j = ny - 1; i = q - nx; }
+    else if (q < 2 * nx + nr) { j = ra + (q - 2 * nx); i = 0; }
+    else if (q < 2 * nx + 2 * nr) { j = ra + (q - 2 * nx - nr); i = nx - 1; }
     else return;
     BCSrc s = bc_source(kind, lid, j, i, ny, nx);   // edge cells read interior cells only
     double uu = s.u_const ? s.u_val : u[s.u_src];
@@ -300,14 +305,21 @@ __global__ void k_bc_edges(int kind, double lid, double *u, double *v, int ny, i
 int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                  const double *p, const double *X1, const double *X2, const double *phi,
                  double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
-                 const MomWork &W) {
+                 const MomWork &W, const RowWin *win) {
     const int ny = ctx->ny, nx = ctx->nx;
     const long n = (long)ny * nx;
     RMT_CHECK(P->bc_kind >= 0 && P->bc_kind <= 2, RMT_EINVAL, "unknown velocity bc kind");
+    // rows of each pass: the final u*, v* on [jb, je); stage s reads stage s-1 two rows out
+    // (upwind3 / grad2 of the blended stress), the prep pass one more row
+    const RowWin w0 = win ? *win : RowWin{0, ny, 0, ny};
+    auto grow = [&](int m) { return RowWin{std::max(w0.jb - m, 0), std::min(w0.je + m, ny), w0.lo, w0.hi}; };
+    RMT_CHECK(w0.lo <= grow(9).jb && grow(9).je <= w0.hi, RMT_EINVAL,
+              "momentum window: resident rows must cover the RK4 halo (9 rows)");
     double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
-    k_mom_prep<<<grid1d(n, 256), 256, 0, ctx->stream>>>(
+    const RowWin wp = grow(7);
+    k_mom_prep<<<grid1d((long)(wp.je - wp.jb) * nx, 256), 256, 0, ctx->stream>>>(
         X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
-        P->rho_f, sxx, sxy, syy, J, W.H, W.rho, W.solid);
+        P->rho_f, sxx, sxy, syy, J, W.H, W.rho, W.solid, wp.jb, wp.je);
     RMT_LAUNCHED();
     // visc = eta_s > 0 and any(solid): cells with no solid contribute nothing anyway, so
     // the per-cell solid test reproduces the reference's np.any guard.
@@ -317,15 +329,18 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     double *kbu[2] = {W.k1u, W.k2u}, *kbv[2] = {W.k1v, W.k2v};
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
     static const bool unfused = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED"));
-    const int tiles_x = (nx + MS_TX - 1) / MS_TX, ntiles = tiles_x * ((ny + MS_TY - 1) / MS_TY);
+    const int tiles_x = (nx + MS_TX - 1) / MS_TX;
     for (int s = 0; s < 4 && !unfused; ++s) {
         const double *kpu = s ? kbu[(s - 1) & 1] : u, *kpv = s ? kbv[(s - 1) & 1] : v;
+        const RowWin ws = grow(2 * (3 - s));
+        const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         k_mom_stage<<<ntiles, MS_T, 0, ctx->stream>>>(
             u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid, visc,
             P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx, tiles_x, ntiles,
-            kbu[s & 1], kbv[s & 1], W.accu, W.accv, u_new, v_new);
+            kbu[s & 1], kbv[s & 1], W.accu, W.accv, u_new, v_new, ws);
         RMT_LAUNCHED();
     }
+    RMT_CHECK(!unfused || !win, RMT_ENOTSUP, "RMT_MOM_UNFUSED: single-domain only");
     for (int s = 0; s < 4 && unfused; ++s) {
         // stage 0 reads only u, v; kp* still point at valid planes
         const double *kpu = s ? kbu[(s - 1) & 1] : u, *kpv = s ? kbv[(s - 1) & 1] : v;
@@ -344,7 +359,7 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     }
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
     k_bc_edges<<<grid1d(2 * (nx + ny), 256), 256, 0, ctx->stream>>>(P->bc_kind, P->lid, u_new,
-                                                                     v_new, ny, nx);
+                                                                     v_new, ny, nx, w0.jb, w0.je);
     RMT_LAUNCHED();
     return RMT_OK;
 }

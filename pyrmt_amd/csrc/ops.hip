@@ -96,6 +96,88 @@ int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double
 int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *o) {
     return reduce_impl(ctx, 0, x, x, n, o, 1.0 / (double)n);
 }
+// Row-tree sums (means of the projection): a fixed-order sum per row, then an aligned
+// pairwise tree over the rows (level l node k covers rows [k 2^l, (k+1) 2^l)).  A slab of 2^m
+// rows starting at a multiple of 2^m is one node of that tree, so the slab-decomposed step
+// (slab.hip) combines its per-slab roots with the same tree and gets the same bits.
+__global__ void __launch_bounds__(256) k_rowsum(const double *__restrict__ x, int nx,
+                                                double *__restrict__ rs) {
+    __shared__ double s[256];
+    const double *r = x + (long)blockIdx.x * nx;
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < nx; i += 256) acc += r[i];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) s[threadIdx.x] = s[threadIdx.x] + s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rs[blockIdx.x] = s[0];
+}
+constexpr int TREE_MAX = 8192, TREE_T = 1024;
+__global__ void __launch_bounds__(TREE_T) k_rowtree(const double *__restrict__ rs, int m,
+                                                    double *__restrict__ out) {
+    __shared__ double s[TREE_MAX];
+    for (int k = threadIdx.x; k < m; k += TREE_T) s[k] = rs[k];
+    __syncthreads();
+    while (m > 1) {
+        const int h = (m + 1) / 2;
+        double v[TREE_MAX / 2 / TREE_T];
+#pragma unroll
+        for (int q = 0; q < TREE_MAX / 2 / TREE_T; ++q) {
+            const int k = threadIdx.x + q * TREE_T;
+            if (k < h) v[q] = 2 * k + 1 < m ? s[2 * k] + s[2 * k + 1] : s[2 * k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < TREE_MAX / 2 / TREE_T; ++q) {
+            const int k = threadIdx.x + q * TREE_T;
+            if (k < h) s[k] = v[q];
+        }
+        __syncthreads();
+        m = h;
+    }
+    if (threadIdx.x == 0) *out = s[0];
+}
+// the same aligned tree over G <= 64 slab roots (every thread folds it)
+__device__ __forceinline__ double tree_roots(const double *__restrict__ roots, int G) {
+    double v[64];
+    for (int k = 0; k < G; ++k) v[k] = roots[k];
+    int m = G;
+    while (m > 1) {
+        const int h = (m + 1) / 2;
+        for (int k = 0; k < h; ++k) v[k] = 2 * k + 1 < m ? v[2 * k] + v[2 * k + 1] : v[2 * k];
+        m = h;
+    }
+    return v[0];
+}
+// x -= tree(roots) / count over n cells (numpy mean: sum / count)
+__global__ void k_sub_tree_mean(double *__restrict__ x, long n, const double *__restrict__ roots,
+                                int G, double count) {
+    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double m = tree_roots(roots, G) / count;
+    x[k] = x[k] - m;
+}
+int rowtree_root(rmt_ctx *ctx, const double *x, int nrows, int nx, double *dev_root) {
+    RMT_CHECK(nrows >= 1 && nrows <= TREE_MAX && nrows <= ctx->rsum_len, RMT_EINVAL,
+              "rowtree_root: rows out of range");
+    k_rowsum<<<nrows, 256, 0, ctx->stream>>>(x, nx, ctx->rsum);
+    k_rowtree<<<1, TREE_T, 0, ctx->stream>>>(ctx->rsum, nrows, dev_root);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int G, double count) {
+    RMT_CHECK(G >= 1 && G <= 64, RMT_EINVAL, "sub_tree_mean: 1..64 roots");
+    if (n > 0) k_sub_tree_mean<<<grid1d(n, 256), 256, 0, ctx->stream>>>(x, n, dev_roots, G, count);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int sub_mean_rows(rmt_ctx *ctx, double *x, int ny, int nx) {
+    double *root = ctx->red + RED_BLOCKS + 16;
+    RMT_TRY(rowtree_root(ctx, x, ny, nx, root));
+    return sub_tree_mean(ctx, x, (long)ny * nx, root, 1, (double)ny * nx);
+}
 int read_scalar(rmt_ctx *ctx, const double *dev, double *host) {
     RMT_HIP(hipMemcpyAsync(host, dev, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     RMT_HIP(hipStreamSynchronize(ctx->stream));
@@ -220,9 +302,9 @@ __global__ void k_apply_bc(int kind, double lid, double *u, double *v, int ny, i
 // -------------------------------------------------------------------- projection ----
 __global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
                                 const double *__restrict__ p, int ny, int nx, double d_f,
-                                double dx, double dy, double *__restrict__ divU) {
-    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)ny * nx) return;
+                                double dx, double dy, double *__restrict__ divU, int jb, int je) {
+    long c = (long)jb * nx + blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)je * nx) return;
     int j = (int)(c / nx), i = (int)(c % nx);
     if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) { divU[c] = 0.0; return; }
     const double h2x = 2.0 * dx, h2y = 2.0 * dy;
@@ -287,18 +369,14 @@ __global__ void k_project_correct(const double *__restrict__ a_s, const double *
                                   const double *__restrict__ pc, const double *__restrict__ p_prev,
                                   int ny, int nx, double dx, double dy, double dt_rho, int bc,
                                   double lid, double *__restrict__ a, double *__restrict__ b,
-                                  double *__restrict__ p) {
-    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)ny * nx) return;
+                                  double *__restrict__ p, int jb, int je) {
+    long c = (long)jb * nx + blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)je * nx) return;
     int j = (int)(c / nx), i = (int)(c % nx);
     BCSrc s = bc_source(bc, lid, j, i, ny, nx);
     a[c] = s.u_const ? s.u_val : corrected(a_s, pc, s.u_src, ny, nx, dx, dy, dt_rho, 0);
     b[c] = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, dx, dy, dt_rho, 1);
     p[c] = p_prev ? p_prev[c] + pc[c] : pc[c];
-}
-__global__ void k_sub_scalar(double *__restrict__ x, long n, const double *__restrict__ s) {
-    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (k < n) x[k] = x[k] - *s;
 }
 __global__ void k_scale_copy(const double *__restrict__ x, long n, double s,
                              double *__restrict__ y) {
@@ -309,6 +387,24 @@ __global__ void k_div_scalar(const double *__restrict__ x, long n, double s,
                              double *__restrict__ y) {
     long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (k < n) y[k] = x[k] / s;
+}
+// Row-window launches for the slab-decomposed step (global cell indices, rows [jb, je))
+int divergence_rc_rows(rmt_ctx *ctx, const double *a, const double *b, const double *p,
+                       double d_f, double dx, double dy, double *divU, int jb, int je) {
+    if (je > jb)
+        k_divergence_rc<<<grid1d((long)(je - jb) * ctx->nx, 256), 256, 0, ctx->stream>>>(
+            a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU, jb, je);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int project_correct_rows(rmt_ctx *ctx, const double *a_s, const double *b_s, const double *pc,
+                         const double *p_prev, double dx, double dy, double dt_rho, int bc,
+                         double lid, double *a, double *b, double *p, int jb, int je) {
+    if (je > jb)
+        k_project_correct<<<grid1d((long)(je - jb) * ctx->nx, 256), 256, 0, ctx->stream>>>(
+            a_s, b_s, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt_rho, bc, lid, a, b, p, jb, je);
+    RMT_LAUNCHED();
+    return RMT_OK;
 }
 }  // namespace rmt
 
@@ -326,6 +422,8 @@ int rmt_ctx_create(int ny, int nx, int device, void *stream, rmt_ctx **out) {
     rmt_ctx *c = new rmt_ctx;
     c->ny = ny; c->nx = nx; c->device = device; c->stream = (hipStream_t)stream;
     RMT_HIP(hipMalloc(&c->red, (RED_BLOCKS + 64) * sizeof(double)));
+    c->rsum_len = ny > 8192 ? ny : 8192;
+    RMT_HIP(hipMalloc(&c->rsum, c->rsum_len * sizeof(double)));
     *out = c;
     return RMT_OK;
 }
@@ -343,6 +441,7 @@ int rmt_ctx_destroy(rmt_ctx *ctx) {
     hipSetDevice(ctx->device);
     if (ctx->scratch) hipFree(ctx->scratch);
     if (ctx->red) hipFree(ctx->red);
+    if (ctx->rsum) hipFree(ctx->rsum);
     if (ctx->bytes) hipFree(ctx->bytes);
     if (ctx->dct) dct_destroy(ctx->dct);
     delete ctx;
@@ -444,7 +543,7 @@ int rmt_apply_velocity_bc(rmt_ctx *ctx, int bc_kind, double lid, double *u, doub
 }
 int rmt_divergence_rc(rmt_ctx *ctx, const double *a, const double *b, const double *p,
                       double d_f, double dx, double dy, double *divU) {
-    k_divergence_rc<<<LAUNCH1D(N_CELLS)>>>(a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU);
+    k_divergence_rc<<<LAUNCH1D(N_CELLS)>>>(a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU, 0, ctx->ny);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -477,12 +576,9 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
     k_div_scalar<<<LAUNCH1D(n)>>>(rhs, n, dt, rhs);
     RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc));
     k_project_correct<<<LAUNCH1D(n)>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy,
-                                       dt / rho, bc_kind, lid, a, b, p);
+                                       dt / rho, bc_kind, lid, a, b, p, 0, ctx->ny);
     RMT_LAUNCHED();
-    double *mean = ctx->red + RED_BLOCKS;
-    RMT_TRY(reduce_mean(ctx, p, n, mean));
-    k_sub_scalar<<<LAUNCH1D(n)>>>(p, n, mean);
-    RMT_LAUNCHED();
+    RMT_TRY(sub_mean_rows(ctx, p, ctx->ny, ctx->nx));
     return RMT_OK;
 }
 int rmt_compute_timestep(rmt_ctx *ctx, const double *a, const double *b, double dx, double dy,

@@ -120,7 +120,7 @@ static int twiddles(int M, double2 **W) {
     return RMT_OK;
 }
 
-static int dct_plan(rmt_ctx *ctx, double dx, double dy) {
+int dct_plan(rmt_ctx *ctx, double dx, double dy) {
     DctPlan *P = ctx->dct;
     if (P && P->dx == dx && P->dy == dy) return RMT_OK;
     if (!P) {
@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(DCT_T) k_dct1(const double *__restrict__ src,
                                                 double *__restrict__ dst, int rows, int n,
                                                 const double2 *__restrict__ W, Radices rd,
                                                 double scale, const double *__restrict__ lamr,
-                                                const double *__restrict__ lamk) {
+                                                const double *__restrict__ lamk, int row0) {
     extern __shared__ double2 z[];
     __shared__ double2 twh[DCT_MAXM / 128], twl[128], rcs[DCT_RCS];
     const int M = 2 * (n - 1), rA = 2 * blockIdx.x, rB = rA + 1, tid = threadIdx.x;
@@ -377,8 +377,9 @@ __global__ void __launch_bounds__(DCT_T) k_dct1(const double *__restrict__ src,
             const int k = tid + t * DCT_T;
             if (k < n) {
                 const double2 Z = z[k];
-                const double eA = (rA == 0 && k == 0) ? 1.0 : lamr[rA] + lamk[k];
-                const double eB = hasB ? lamr[rB] + lamk[k] : 1.0;
+                // row0: global frequency of local row 0 (slab-decomposed solves)
+                const double eA = (row0 + rA == 0 && k == 0) ? 1.0 : lamr[row0 + rA] + lamk[k];
+                const double eB = hasB ? lamr[row0 + rB] + lamk[k] : 1.0;
                 q[t] = make_double2(Z.x / eA, hasB ? Z.y / eB : 0.0);
             }
         }
@@ -415,9 +416,24 @@ __global__ void __launch_bounds__(256) k_transpose(const double *__restrict__ in
     }
 }
 
-static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p) {
-    const int ny = P->ny, nx = P->nx;
-    hipStream_t st = ctx->stream;
+static Radices radices(const int *rad, int np) {
+    Radices rd{};
+    int Ns = 1;
+    for (int k = 0; k < np; ++k) {
+        rd.p[k] = Pass{rad[k], Ns, (float)(1.0 / Ns), rc_offset(rad[k])};
+        Ns *= rad[k];
+    }
+    rd.n = np;
+    return rd;
+}
+
+// One LDS DCT-I pass over nrows rows of length n (axis 0: n = nx, axis 1: n = ny).  SOLVE
+// (axis 1 only): forward, / eig, inverse, with rows = x-frequencies row0 .. row0 + nrows.
+int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
+             int row0, double scale) {
+    DctPlan *P = ctx->dct;
+    RMT_CHECK(P && P->lds, RMT_ENOTSUP, "dct_pass: no LDS DCT plan for this grid");
+    RMT_CHECK(!solve || axis == 1, RMT_EINVAL, "dct_pass: the solve pass runs along y");
     static bool attr = false;
     if (!attr) {
         const void *fs[4] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
@@ -427,44 +443,43 @@ static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p)
                                         DCT_MAXM * 16));
         attr = true;
     }
-    auto passes = [](const int *rad, int np) {
-        Radices rd{};
-        int Ns = 1;
-        for (int k = 0; k < np; ++k) {
-            rd.p[k] = Pass{rad[k], Ns, (float)(1.0 / Ns), rc_offset(rad[k])};
-            Ns *= rad[k];
-        }
-        rd.n = np;
-        return rd;
-    };
-    const Radices rx = passes(P->radx, P->npx), ry = passes(P->rady, P->npy);
-    const size_t lx = 2 * (size_t)(nx - 1) * sizeof(double2), ly = 2 * (size_t)(ny - 1) * sizeof(double2);
-    auto rows = [&](bool solve, const double *src, double *dst, int nr, int n, const double2 *W,
-                    const Radices &rd, double scale, size_t lds) {
-        const unsigned g = (nr + 1) / 2;
-        if (solve) {
-            if (P->big) k_dct1<true, 1><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, P->lamx, P->lamy);
-            else k_dct1<true, 0><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, P->lamx, P->lamy);
-        } else {
-            if (P->big) k_dct1<false, 1><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, nullptr, nullptr);
-            else k_dct1<false, 0><<<g, DCT_T, lds, st>>>(src, dst, nr, n, W, rd, scale, nullptr, nullptr);
-        }
-    };
-    // forward along x: p <- DCT_x(rhs) (p doubles as scratch), then T <- p^T (nx x ny)
-    rows(false, rhs, p, ny, nx, P->Wx, rx, 1.0, lx);
-    k_transpose<<<dim3((nx + 63) / 64, (ny + 63) / 64), 256, 0, st>>>(p, ny, nx, P->T);
-    // columns: DCT_y, / eig, inverse DCT_y (scaled), in place on T
-    rows(true, P->T, P->T, nx, ny, P->Wy, ry, 1.0 / (2.0 * (ny - 1)), ly);
-    k_transpose<<<dim3((ny + 63) / 64, (nx + 63) / 64), 256, 0, st>>>(P->T, nx, ny, p);
-    // inverse along x, in place
-    rows(false, p, p, ny, nx, P->Wx, rx, 1.0 / (2.0 * (nx - 1)), lx);
+    if (nrows <= 0) return RMT_OK;
+    const int n = axis == 0 ? P->nx : P->ny;
+    const Radices rd = axis == 0 ? radices(P->radx, P->npx) : radices(P->rady, P->npy);
+    const double2 *W = axis == 0 ? P->Wx : P->Wy;
+    const size_t lds = 2 * (size_t)(n - 1) * sizeof(double2);
+    const unsigned g = (nrows + 1) / 2;
+    hipStream_t st = ctx->stream;
+    if (solve) {
+        if (P->big) k_dct1<true, 1><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0);
+        else k_dct1<true, 0><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0);
+    } else {
+        if (P->big) k_dct1<false, 1><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0);
+        else k_dct1<false, 0><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0);
+    }
     RMT_LAUNCHED();
     return RMT_OK;
 }
 
-__global__ void k_sub_mean(double *__restrict__ x, long n, const double *__restrict__ s) {
-    long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (k < n) x[k] = x[k] - *s;
+bool dct_lds_ready(rmt_ctx *ctx) { return ctx->dct && ctx->dct->lds; }
+
+void transpose(hipStream_t st, const double *in, int R, int C, double *out) {
+    k_transpose<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out);
+}
+
+static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p) {
+    const int ny = P->ny, nx = P->nx;
+    hipStream_t st = ctx->stream;
+    // forward along x: p <- DCT_x(rhs) (p doubles as scratch), then T <- p^T (nx x ny)
+    RMT_TRY(dct_pass(ctx, false, 0, rhs, p, ny, 0, 1.0));
+    transpose(st, p, ny, nx, P->T);
+    // columns: DCT_y, / eig, inverse DCT_y (scaled), in place on T
+    RMT_TRY(dct_pass(ctx, true, 1, P->T, P->T, nx, 0, 1.0 / (2.0 * (ny - 1))));
+    transpose(st, P->T, nx, ny, p);
+    // inverse along x, in place
+    RMT_TRY(dct_pass(ctx, false, 0, p, p, ny, 0, 1.0 / (2.0 * (nx - 1))));
+    RMT_LAUNCHED();
+    return RMT_OK;
 }
 
 int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
@@ -484,11 +499,7 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
         RMT_TRY(round_rows(ctx, P, px, p, ny, nx, 1.0 / (2.0 * (nx - 1)), nullptr, nullptr, P->T));
         RMT_TRY(round_rows(ctx, P, py, P->T, nx, ny, 1.0 / (2.0 * (ny - 1)), nullptr, nullptr, p));
     }
-    const long n = (long)ny * nx;
-    double *mean = ctx->red + RED_BLOCKS + 8;
-    RMT_TRY(reduce_mean(ctx, p, n, mean));
-    k_sub_mean<<<grid1d(n, 256), 256, 0, ctx->stream>>>(p, n, mean);
-    RMT_LAUNCHED();
+    RMT_TRY(sub_mean_rows(ctx, p, ny, nx));
     return RMT_OK;
 }
 

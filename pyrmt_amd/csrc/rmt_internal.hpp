@@ -52,6 +52,8 @@ struct rmt_ctx {
     double *scratch = nullptr;
     size_t scratch_bytes = 0;
     double *red = nullptr;      // reduction partials (host-visible results copied out)
+    double *rsum = nullptr;     // per-row sums of the row-tree reductions
+    int rsum_len = 0;
     unsigned char *bytes = nullptr;
     size_t bytes_len = 0;
     rmt::DctPlan *dct = nullptr;
@@ -92,9 +94,13 @@ __device__ __forceinline__ double upwind3(const double *f, long s, int k, int n,
     return 0.0;
 }
 
-// interpolators.py:4-61 bilinear_interpolate at one query point.
-__device__ __forceinline__ double bilinear(const double *__restrict__ u, double xq, double yq,
-                                           double dx, double dy, int nx, int ny) {
+// interpolators.py:4-61 bilinear_interpolate at one query point.  CHK (slab-decomposed
+// step): the two rows read must be resident, rows [lo, hi); otherwise *oob is set and the
+// result is NaN (a departure point farther than the halo: never at CFL <= 1).
+template <bool CHK>
+__device__ __forceinline__ double bilinear_t(const double *__restrict__ u, double xq, double yq,
+                                             double dx, double dy, int nx, int ny, int lo,
+                                             int hi, bool *oob) {
     double x = xq / dx, y = yq / dy;
     if (!(isfinite(x) && isfinite(y))) return __builtin_nan("");
     if (x < 0.0) x = 0.0; else if (x > nx - 1.0) x = nx - 1.0;
@@ -102,27 +108,42 @@ __device__ __forceinline__ double bilinear(const double *__restrict__ u, double 
     int ix = (int)floor(x), iy = (int)floor(y);
     if (ix >= nx - 1) ix = nx - 2;
     if (iy >= ny - 1) iy = ny - 2;
+    if (CHK && (iy < lo || iy + 1 >= hi)) { *oob = true; return __builtin_nan(""); }
     double fx = x - ix, fy = y - iy;
     const double *r0 = u + (long)iy * nx, *r1 = r0 + nx;
     return (1 - fx) * (1 - fy) * r0[ix] + fx * (1 - fy) * r0[ix + 1] +
            (1 - fx) * fy * r1[ix] + fx * fy * r1[ix + 1];
 }
+__device__ __forceinline__ double bilinear(const double *__restrict__ u, double xq, double yq,
+                                           double dx, double dy, int nx, int ny) {
+    return bilinear_t<false>(u, xq, yq, dx, dy, nx, ny, 0, ny, nullptr);
+}
 
 // functions.py:194-227: RK4 backtrace of one point; returns the foot (xb, yb).
+template <bool CHK>
+__device__ __forceinline__ void sl_backtrace_t(const double *__restrict__ a,
+                                               const double *__restrict__ b, double x, double y,
+                                               double dt, double dx, double dy, int nx, int ny,
+                                               int lo, int hi, bool *oob, double &xb,
+                                               double &yb) {
+#define BL_(f, X, Y) bilinear_t<CHK>(f, X, Y, dx, dy, nx, ny, lo, hi, oob)
+    const double hdt = 0.5 * dt, dt6 = dt / 6.0;
+    double k1x = BL_(a, x, y), k1y = BL_(b, x, y);
+    double x2 = x - hdt * k1x, y2 = y - hdt * k1y;
+    double k2x = BL_(a, x2, y2), k2y = BL_(b, x2, y2);
+    double x3 = x - hdt * k2x, y3 = y - hdt * k2y;
+    double k3x = BL_(a, x3, y3), k3y = BL_(b, x3, y3);
+    double x4 = x - dt * k3x, y4 = y - dt * k3y;
+    double k4x = BL_(a, x4, y4), k4y = BL_(b, x4, y4);
+#undef BL_
+    xb = x - dt6 * (k1x + 2 * k2x + 2 * k3x + k4x);
+    yb = y - dt6 * (k1y + 2 * k2y + 2 * k3y + k4y);
+}
 __device__ __forceinline__ void sl_backtrace(const double *__restrict__ a,
                                              const double *__restrict__ b, double x, double y,
                                              double dt, double dx, double dy, int nx, int ny,
                                              double &xb, double &yb) {
-    const double hdt = 0.5 * dt, dt6 = dt / 6.0;
-    double k1x = bilinear(a, x, y, dx, dy, nx, ny), k1y = bilinear(b, x, y, dx, dy, nx, ny);
-    double x2 = x - hdt * k1x, y2 = y - hdt * k1y;
-    double k2x = bilinear(a, x2, y2, dx, dy, nx, ny), k2y = bilinear(b, x2, y2, dx, dy, nx, ny);
-    double x3 = x - hdt * k2x, y3 = y - hdt * k2y;
-    double k3x = bilinear(a, x3, y3, dx, dy, nx, ny), k3y = bilinear(b, x3, y3, dx, dy, nx, ny);
-    double x4 = x - dt * k3x, y4 = y - dt * k3y;
-    double k4x = bilinear(a, x4, y4, dx, dy, nx, ny), k4y = bilinear(b, x4, y4, dx, dy, nx, ny);
-    xb = x - dt6 * (k1x + 2 * k2x + 2 * k3x + k4x);
-    yb = y - dt6 * (k1y + 2 * k2y + 2 * k3y + k4y);
+    sl_backtrace_t<false>(a, b, x, y, dt, dx, dy, nx, ny, 0, ny, nullptr, xb, yb);
 }
 
 // benchmarks/common.py:55-57 disc signed distance, numpy order: sqrt(dx*dx + dy*dy) - R.
@@ -271,6 +292,31 @@ int reduce_max(rmt_ctx *ctx, const double *x, long n, double *dev_out);
 int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double *dev_out);
 int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *dev_out);
 int read_scalar(rmt_ctx *ctx, const double *dev, double *host);
+// row-tree sums (ops.hip): root of rows [0, nrows) of x (row length nx) into *dev_root;
+// x -= tree(G roots) / count; and both for a whole (ny, nx) plane
+int rowtree_root(rmt_ctx *ctx, const double *x, int nrows, int nx, double *dev_root);
+int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int G, double count);
+int sub_mean_rows(rmt_ctx *ctx, double *x, int ny, int nx);
+
+// Row window of a slab-decomposed call (slab.hip): planes are addressed with GLOBAL cell
+// indices j*nx + i (the caller offsets its pointers by -lo*nx), rows [lo, hi) are resident,
+// rows [jb, je) are computed, and ny stays the global row count, so every boundary test
+// of the reference sees the true domain edge.  A single-domain call is {0, ny, 0, ny}.
+struct RowWin { int jb, je, lo, hi; };
+
+int divergence_rc_rows(rmt_ctx *ctx, const double *a, const double *b, const double *p,
+                       double d_f, double dx, double dy, double *divU, int jb, int je);
+int project_correct_rows(rmt_ctx *ctx, const double *a_s, const double *b_s, const double *pc,
+                         const double *p_prev, double dx, double dy, double dt_rho, int bc,
+                         double lid, double *a, double *b, double *p, int jb, int je);
+
+// sim.hip: the fused step's diagnostic partials (centroid sums, J range, energies) over rows
+// [jb, je); part holds DIAG_PART doubles, out receives 10
+constexpr int DIAG_PART = 512 * 10;
+int diag_rows(rmt_ctx *ctx, const double *phi, const double *J, const double *xs,
+              const double *ys, const double *u, const double *v, const double *X1,
+              const double *X2, const rmt_sim_params &P, int jb, int je, double *part,
+              double *out);
 
 // --------------------------------------------------------------------- momentum --
 constexpr int MOM_WORK_PLANES = 13;
@@ -286,17 +332,24 @@ inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
 int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                  const double *p, const double *X1, const double *X2, const double *phi,
                  double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
-                 const MomWork &W);
+                 const MomWork &W, const RowWin *win = nullptr);
 
 // ---------------------------------------------------------------------- poisson --
 int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
               const double *dev_mean_sub = nullptr);
+int dct_plan(rmt_ctx *ctx, double dx, double dy);
+bool dct_lds_ready(rmt_ctx *ctx);
+int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
+             int row0, double scale);
+void transpose(hipStream_t st, const double *in, int R, int C, double *out);
 void dct_destroy(DctPlan *);
 
 // ------------------------------------------------------------------ extrapolate --
 // dev_status (optional, device): receives {cells fitted, aborted} after the sweep
+// kin (optional): the known plane (phi < 0) as 64-cell words, ny x ceil(nx/64); phi unused then
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
-                double dy, int max_layers, double *X1o, double *X2o, int *dev_status = nullptr);
+                double dy, int max_layers, double *X1o, double *X2o, int *dev_status = nullptr,
+                const unsigned long long *kin = nullptr);
 size_t extrap_workspace(int ny, int nx, int max_layers);   // bytes of ctx->bytes it uses
 
 }  // namespace rmt

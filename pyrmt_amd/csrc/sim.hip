@@ -127,13 +127,15 @@ struct DiagArgs {
     const double *phi, *J, *xs, *ys, *u, *v, *X1, *X2;
     int ny, nx, energies;
     double dx, dy, w_t, rho_s, rho_f, mu_f, eta_s, mu_s, kappa;
+    int jb, je;   // rows reduced (global indices; the whole grid: 0, ny)
 };
 // partial [sx, sy, cnt, Jmin, Jmax, ke, se, diss, ymin, ymax] per block
 __global__ void __launch_bounds__(DIAG_T) k_diag_p1(DiagArgs A, double *__restrict__ part) {
     __shared__ double s[DIAG_VALS][DIAG_T];
     double v[DIAG_VALS] = {0, 0, 0, INFINITY, -INFINITY, 0, 0, 0, INFINITY, -INFINITY};
-    const long n = (long)A.ny * A.nx;
-    for (long c = blockIdx.x * (long)DIAG_T + threadIdx.x; c < n; c += (long)DIAG_BLOCKS * DIAG_T) {
+    const long n = (long)A.je * A.nx;
+    for (long c = (long)A.jb * A.nx + blockIdx.x * (long)DIAG_T + threadIdx.x; c < n;
+         c += (long)DIAG_BLOCKS * DIAG_T) {
         int j = (int)(c / A.nx), i = (int)(c % A.nx);
         double ph = A.phi[c];
         bool solid = ph <= 0.0;
@@ -188,6 +190,19 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p2(const double *__restrict__ p
         __syncthreads();
     }
     if (threadIdx.x < DIAG_VALS) out[threadIdx.x] = s[threadIdx.x][0];
+}
+
+// slab-decomposed step: the 10 diagnostic partials of rows [jb, je) into out (device)
+int diag_rows(rmt_ctx *ctx, const double *phi, const double *J, const double *xs,
+              const double *ys, const double *u, const double *v, const double *X1,
+              const double *X2, const rmt_sim_params &P, int jb, int je, double *part,
+              double *out) {
+    DiagArgs D{phi, J, xs, ys, u, v, X1, X2, P.ny, P.nx, P.energies, P.dx, P.dy, P.w_t,
+               P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa, jb, je};
+    k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, ctx->stream>>>(D, part);
+    k_diag_p2<<<1, DIAG_T, 0, ctx->stream>>>(part, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
 }
 
 }  // namespace rmt
@@ -339,7 +354,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[5], st));
         // 7. diagnostics
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
-                   P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa};
+                   P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa, 0, ny};
         k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, S->dscr);
         k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, sc + 2);
         RMT_LAUNCHED();

@@ -1,0 +1,421 @@
+"""Slab-decomposed RMT step over G GPUs.
+
+The reference runs one NumPy/Numba process (benchmarks/soft_disc_in_lid_driven.py:206-235);
+this module splits the same loop body into 1D row slabs, one per GPU, with librmt's slab
+phases (include/rmt.h, rmt_slab_*) doing all arithmetic and the collectives between them
+done here:
+
+* ``TorchComm`` -- one slab per process over ``torch.distributed``: RCCL (backend "nccl")
+  moves device tensors directly over xGMI; "gloo" stages through host memory (CPU tests,
+  and two processes sharing one GPU).
+* ``LocalComm`` -- G virtual slabs in one process on one GPU, exchanges are device copies.
+  Same phases, same data movement pattern: the bit-exactness tests of the decomposition
+  run on a single GPU with it.
+
+Per step: one halo exchange of (u, v, p, X1, X2) (RMT_SLAB_HALO rows; the stencils of the
+SL backtrace and the 4 RK4 stages are recomputed on the overlap instead of exchanged per
+stage), an allgather of the known bit rows and of the narrow band's rim (index, X1, X2)
+for the exact raster-order extrapolation replicated on every slab, two all-to-all
+transposes around the fused column DCT -> / eig -> inverse DCT, a 2-row halo of p_c, and
+small allgathers of row-tree roots and per-slab scalars (the means and diagnostics).
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib as L
+from . import functions as F
+from .simulation import _wrap_device
+
+HALO = 12           # RMT_SLAB_HALO
+SC_N = 16           # scalar block: [0] max|u|^2, [1..10] diag partials, [11] flags,
+SC_M2, SC_DIAG, SC_FLAGS, SC_COUNT, SC_ROOT, SC_FIT = 0, 1, 11, 12, 13, 14
+BUF = {"u": 0, "v": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5, "J": 6, "pc": 7, "bits": 8,
+       "rim": 9, "A": 10, "B": 11, "scal": 12}
+
+
+def even_splits(n, G, minsz=2):
+    """Split range(n) into G contiguous parts with even boundaries (row / column pairs of
+    the DCT stay together) as balanced as possible."""
+    if G < 1 or n < G * minsz:
+        raise ValueError(f"cannot split {n} into {G} parts of >= {minsz}")
+    s = [0]
+    for k in range(1, G):
+        b = int(round(k * n / G))
+        b -= b & 1
+        s.append(b)
+    s.append(n)
+    for k in range(G):
+        if s[k + 1] - s[k] < minsz:
+            raise ValueError(f"split {s} has a part smaller than {minsz}")
+    return s
+
+
+# ------------------------------------------------------------------ communicators --
+class LocalComm:
+    """G virtual ranks in this process (one GPU): every collective is device copies over
+    the list of local slabs, in rank order."""
+
+    def __init__(self, G):
+        self.G = G
+        self.ranks = list(range(G))
+
+    def halo(self, slabs, planes, nrows):
+        import torch
+        with torch.no_grad():
+            for k, s in enumerate(slabs):
+                for name in planes:
+                    dst = s.view(name)
+                    if k > 0:                      # rows [r0 - n, r0) from slab k - 1
+                        o = slabs[k - 1]
+                        a = max(s.r0 - nrows, s.lo)
+                        dst[a - s.lo:s.r0 - s.lo].copy_(o.view(name)[a - o.lo:s.r0 - o.lo])
+                    if k + 1 < len(slabs):         # rows [r1, r1 + n) from slab k + 1
+                        o = slabs[k + 1]
+                        b = min(s.r1 + nrows, s.hi)
+                        dst[s.r1 - s.lo:b - s.lo].copy_(o.view(name)[s.r1 - o.lo:b - o.lo])
+
+    def allgather_rows(self, slabs, name):
+        for s in slabs:
+            dst = s.view(name)
+            for o in slabs:
+                if o is not s:
+                    dst[o.r0:o.r1].copy_(o.view(name)[o.r0:o.r1])
+
+    def allgather(self, tensors):
+        import torch
+        g = torch.stack([t.reshape(-1) for t in tensors])
+        return [g] * len(tensors)
+
+    def allgather_padded(self, tensors, counts, width):
+        """tensors[k][:counts[k] * width] of every rank -> (G, cap * width) on every rank."""
+        import torch
+        cap = max(counts) if counts else 0
+        g = torch.zeros((self.G, max(cap, 1) * width), dtype=tensors[0].dtype,
+                        device=tensors[0].device)
+        for k, t in enumerate(tensors):
+            g[k, :counts[k] * width].copy_(t.reshape(-1)[:counts[k] * width])
+        return [g] * len(tensors), cap
+
+    def all_to_all(self, sends, recvs, send_splits, recv_splits):
+        for m, r in enumerate(recvs):
+            ro = 0
+            for k, s in enumerate(sends):
+                so = sum(send_splits[k][:m])
+                n = send_splits[k][m]
+                assert n == recv_splits[m][k]
+                r.reshape(-1)[ro:ro + n].copy_(s.reshape(-1)[so:so + n])
+                ro += n
+
+
+class TorchComm:
+    """One slab per process over torch.distributed (RANK / WORLD_SIZE from the process
+    group).  Backend "nccl" is RCCL on ROCm and moves device tensors directly; "gloo"
+    stages every exchange through host memory."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.G = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.ranks = [self.rank]
+        self.staged = dist.get_backend(group) != "nccl"
+
+    def _host(self, t):
+        return t.cpu() if self.staged else t
+
+    def _back(self, dst, src):
+        if src is not dst:
+            dst.copy_(src)
+
+    def halo(self, slabs, planes, nrows):
+        (s,) = slabs
+        dist, k = self.dist, self.rank
+        ops, post = [], []
+        for name in planes:
+            v = s.view(name)
+            if k > 0:
+                a = max(s.r0 - nrows, s.lo)
+                snd = self._host(v[s.r0 - s.lo:s.r0 - s.lo + (s.r0 - a)].contiguous())
+                rcv = v[a - s.lo:s.r0 - s.lo]
+                rb = rcv.cpu() if self.staged else rcv
+                ops += [(dist.isend, snd, k - 1), (dist.irecv, rb, k - 1)]
+                post.append((rcv, rb))
+            if k + 1 < self.G:
+                b = min(s.r1 + nrows, s.hi)
+                snd = self._host(v[s.r1 - s.lo - (b - s.r1):s.r1 - s.lo].contiguous())
+                rcv = v[s.r1 - s.lo:b - s.lo]
+                rb = rcv.cpu() if self.staged else rcv
+                ops += [(dist.isend, snd, k + 1), (dist.irecv, rb, k + 1)]
+                post.append((rcv, rb))
+        if not ops:
+            return
+        if self.staged:
+            reqs = [f(t, peer, group=self.group) for f, t, peer in ops]
+            for r in reqs:
+                r.wait()
+        else:
+            p2p = [dist.P2POp(f, t, peer, group=self.group) for f, t, peer in ops]
+            for r in dist.batch_isend_irecv(p2p):
+                r.wait()
+        for rcv, rb in post:
+            self._back(rcv, rb)
+
+    def allgather_rows(self, slabs, name):
+        import torch
+        (s,) = slabs
+        v = s.view(name)
+        sizes = [s.splits[k + 1] - s.splits[k] for k in range(self.G)]
+        mx = max(sizes)
+        mine = torch.zeros((mx,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+        mine[:s.r1 - s.r0].copy_(v[s.r0:s.r1])
+        mine = self._host(mine)
+        out = torch.empty(self.G * mine.numel(), dtype=v.dtype, device=mine.device)
+        self.dist.all_gather_into_tensor(out, mine.reshape(-1), group=self.group)
+        out = out.view((self.G,) + tuple(mine.shape))
+        for k in range(self.G):
+            if k != self.rank:
+                v[s.splits[k]:s.splits[k + 1]].copy_(out[k, :sizes[k]])
+
+    def allgather(self, tensors):
+        import torch
+        (t,) = tensors
+        src = self._host(t.reshape(-1).contiguous())
+        out = torch.empty(self.G * src.numel(), dtype=src.dtype, device=src.device)
+        self.dist.all_gather_into_tensor(out, src, group=self.group)
+        out = out.view(self.G, src.numel())
+        return [out.to(t.device) if self.staged else out]
+
+    def allgather_padded(self, tensors, counts, width):
+        import torch
+        (t,) = tensors
+        cap = max(counts) if counts else 0
+        mine = torch.zeros(max(cap, 1) * width, dtype=t.dtype, device=t.device)
+        n = counts[self.rank] * width
+        mine[:n].copy_(t.reshape(-1)[:n])
+        mine = self._host(mine)
+        out = torch.empty(self.G * mine.numel(), dtype=t.dtype, device=mine.device)
+        self.dist.all_gather_into_tensor(out, mine, group=self.group)
+        out = out.view(self.G, mine.numel())
+        return [out.to(t.device) if self.staged else out], cap
+
+    def all_to_all(self, sends, recvs, send_splits, recv_splits):
+        (snd,), (rcv,) = sends, recvs
+        src = self._host(snd.reshape(-1)[:sum(send_splits[0])])
+        dst = rcv.reshape(-1)[:sum(recv_splits[0])]
+        db = dst.cpu() if self.staged else dst
+        self.dist.all_to_all_single(db, src, output_split_sizes=list(recv_splits[0]),
+                                    input_split_sizes=list(send_splits[0]), group=self.group)
+        self._back(dst, db)
+
+
+# ---------------------------------------------------------------------- one slab --
+class Slab:
+    """One rmt_slab: rows [r0, r1) resident as [lo, hi); zero-copy torch views of its
+    buffers (device memory owned by librmt)."""
+
+    def __init__(self, ctx, params, G, rank, rsplits, csplits):
+        self.lib = L.lib()
+        rs = (ctypes.c_int * (G + 1))(*rsplits)
+        cs = (ctypes.c_int * (G + 1))(*csplits)
+        h = ctypes.c_void_p()
+        L.check(self.lib.rmt_slab_create(ctx.bind(), ctypes.byref(params), G, rank, rs, cs,
+                                         ctypes.byref(h)), "rmt_slab_create")
+        self.h = h
+        info = (ctypes.c_int * 8)()
+        dtc = ctypes.c_double()
+        L.check(self.lib.rmt_slab_info(h, info, ctypes.byref(dtc)))
+        self.r0, self.r1, self.lo, self.hi, self.c0, self.c1, self.W, _ = list(info)
+        self.dt_const = dtc.value
+        self.G, self.rank, self.splits, self.csplits = G, rank, list(rsplits), list(csplits)
+        self.NY, self.NX = params.ny, params.nx
+        self._views = {}
+
+    def __del__(self):
+        try:
+            self.lib.rmt_slab_destroy(self.h)
+        except Exception:
+            pass
+
+    def _ptr(self, bid):
+        p = ctypes.c_void_p()
+        L.check(self.lib.rmt_slab_buffer(self.h, bid, ctypes.byref(p)))
+        return p.value
+
+    def view(self, name):
+        if name not in self._views:
+            torch = F._torch()
+            nl, no = self.hi - self.lo, self.r1 - self.r0
+            nc = self.c1 - self.c0
+            shape = {"bits": (self.NY, self.W), "rim": (no * self.NX, 3), "A": (no * self.NX,),
+                     "B": (self.NY * nc,), "scal": (SC_N,)}.get(name, (nl, self.NX))
+            t = _wrap_device(torch, self._ptr(BUF[name]), shape)
+            if name == "bits":
+                t = t.view(torch.int64)
+            self._views[name] = t
+        return self._views[name]
+
+    def a2a_splits(self):
+        """element counts: forward send (to m: rows_me x nc_m), forward recv (from k:
+        rows_k x nc_me); the backward transpose swaps them"""
+        rows = self.r1 - self.r0
+        nc = self.c1 - self.c0
+        snd = [rows * (self.csplits[m + 1] - self.csplits[m]) for m in range(self.G)]
+        rcv = [(self.splits[k + 1] - self.splits[k]) * nc for k in range(self.G)]
+        return snd, rcv
+
+
+# ------------------------------------------------------------------ the whole step --
+class DistributedSim:
+    """The fused RMT step of rmt_sim (sim.hip), decomposed into G row slabs.
+
+    ``comm`` is a LocalComm (G slabs here) or a TorchComm (this process's slab).  The
+    physics parameters are those of ``simulation.Simulation`` (semi-Lagrangian, one disc).
+    """
+
+    def __init__(self, N, comm, *, bc_kind, lid, disc, mu_s, kappa, rho_s, eta_s, mu_f,
+                 rho_f, w_t, layers, cfl, dt_cap, stress_band=False, detg_clamp=3.0):
+        torch = F._torch()
+        self.torch, self.comm, self.N, self.G = torch, comm, N, comm.G
+        self.X, self.Y, self.dx, self.dy = F.create_grid(N, N, 1.0, 1.0)
+        self.xs = np.ascontiguousarray(self.X[0, :])
+        self.ys = np.ascontiguousarray(self.Y[:, 0])
+        P = L.rmt_sim_params()
+        P.ny = P.nx = N; P.dx = self.dx; P.dy = self.dy
+        P.xs = self.xs.ctypes.data; P.ys = self.ys.ctypes.data
+        P.scheme = 0; P.bc_kind = bc_kind; P.lid = lid; P.shape = 1
+        P.x0, P.y0, P.R = disc
+        P.mu_s, P.kappa, P.rho_s, P.eta_s, P.mu_f, P.rho_f = mu_s, kappa, rho_s, eta_s, mu_f, rho_f
+        P.w_t = w_t; P.layers = layers; P.cfl = cfl; P.dt_cap = dt_cap
+        P.stress_band = int(bool(stress_band)); P.detg_clamp = detg_clamp; P.energies = 0
+        self.params, self.cfl = P, cfl
+        self.rsplits = even_splits(N, self.G, HALO)
+        self.csplits = even_splits(N, self.G, 2)
+        self.ctx = F.ctx_for(N, N)
+        self.slabs = [Slab(self.ctx, P, self.G, r, self.rsplits, self.csplits)
+                      for r in comm.ranks]
+        self.dt_const = self.slabs[0].dt_const
+        self.t = 0.0
+        self.m2 = None
+        self.records = []
+        self._counts = (ctypes.c_longlong * self.G)()
+
+    # -------------------------------------------------------------- state in / out --
+    def set_state(self, **fields):
+        """Full (N, N) host arrays -> every slab's resident rows."""
+        torch = self.torch
+        for name, arr in fields.items():
+            a = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float64))
+            for s in self.slabs:
+                s.view(name).copy_(a[s.lo:s.hi].to(s.view(name).device))
+        self.m2 = None
+
+    def gather(self, name):
+        """The owned rows of every slab assembled into a full (N, N) host array."""
+        torch = self.torch
+        torch.cuda.synchronize()
+        views = [s.view(name)[s.r0 - s.lo:s.r1 - s.lo].contiguous() for s in self.slabs]
+        if isinstance(self.comm, LocalComm):
+            return torch.cat(views).cpu().numpy()
+        mx = max(self.rsplits[k + 1] - self.rsplits[k] for k in range(self.G))
+        pad = torch.zeros((mx, self.N), dtype=torch.float64, device=views[0].device)
+        pad[:views[0].shape[0]].copy_(views[0])
+        (g,) = self.comm.allgather([pad])
+        g = g.reshape(self.G, mx, self.N).cpu().numpy()
+        return np.concatenate([g[k, :self.rsplits[k + 1] - self.rsplits[k]]
+                               for k in range(self.G)])
+
+    def _call(self, fn, *args):
+        for s in self.slabs:
+            L.check(getattr(s.lib, fn)(s.h, *args), fn)
+
+    def _scalars(self):
+        """(G, SC_N) host array of every slab's scalar block (one host sync)."""
+        g = self.comm.allgather([s.view("scal") for s in self.slabs])[0]
+        return g.cpu().numpy().reshape(self.G, SC_N)
+
+    # ----------------------------------------------------------------------- step --
+    def step(self, nsteps=1, t_end=math.inf):
+        self.ctx.bind()
+        comm, S = self.comm, self.slabs
+        if self.m2 is None:
+            self._call("rmt_slab_begin")
+            self.m2 = float(self._scalars()[:, SC_M2].max())
+        for _ in range(nsteps):
+            if not (self.t < t_end):
+                break
+            comm.halo(S, ("u", "v", "p", "X1", "X2"), HALO)
+            m2 = self.m2
+            dt = min(self.dt_const, self.cfl * self.dx / (math.sqrt(m2) + 1e-6))
+            if self.t + dt > t_end:
+                dt = t_end - self.t
+            # advection + exact extrapolation (band replicated on every slab)
+            self._call("rmt_slab_advect", dt)
+            comm.allgather_rows(S, "bits")
+            self._call("rmt_slab_rim_pack")
+            counts = [int(c) for c in self._scalars()[:, SC_COUNT]]
+            gathered, cap = comm.allgather_padded([s.view("rim") for s in S], counts, 3)
+            for k, c in enumerate(counts):
+                self._counts[k] = c
+            for s, g in zip(S, gathered):
+                L.check(s.lib.rmt_slab_extrapolate(s.h, g.data_ptr(), self._counts, cap),
+                        "rmt_slab_extrapolate")
+            # momentum, projection
+            self._call("rmt_slab_momentum", dt)
+            self._call("rmt_slab_project_rows", dt)
+            sp = [s.a2a_splits() for s in S]
+            comm.all_to_all([s.view("A") for s in S], [s.view("B") for s in S],
+                            [x[0] for x in sp], [x[1] for x in sp])
+            self._call("rmt_slab_project_cols")
+            comm.all_to_all([s.view("B") for s in S], [s.view("A") for s in S],
+                            [x[1] for x in sp], [x[0] for x in sp])
+            self._call("rmt_slab_project_unrows")
+            self._sub_mean(0)
+            comm.halo(S, ("pc",), 2)
+            self._call("rmt_slab_project_correct", dt)
+            self._sub_mean(1)
+            self._call("rmt_slab_finish")
+            sc = self._scalars()
+            self.t += dt
+            self._record(sc, dt, m2)
+
+    def _sub_mean(self, which):
+        roots = self.comm.allgather([s.view("scal")[SC_ROOT:SC_ROOT + 1] for s in self.slabs])
+        for s, r in zip(self.slabs, roots):
+            L.check(s.lib.rmt_slab_sub_mean(s.h, which, r.data_ptr()), "rmt_slab_sub_mean")
+
+    def _record(self, sc, dt, m2):
+        fl = int(np.bitwise_or.reduce(sc[:, SC_FLAGS].astype(np.int64)))
+        if fl & 1:
+            raise FloatingPointError("advect_reference_map: non-finite velocity (the "
+                                     "simulation diverged)")
+        if fl & 2:
+            raise L.RMTError("slab step: a departure point left the halo rows")
+        if fl & 4:
+            raise L.RMTError("extrapolation sweep aborted (progress wait timed out)")
+        d = sc[:, SC_DIAG:SC_DIAG + 10]
+        sx, sy, cnt = (float(sum(d[:, k])) for k in (0, 1, 2))
+        self.m2 = float(sc[:, SC_M2].max())
+        self.records.append({
+            "t": self.t, "dt": dt, "cx": sx / cnt if cnt > 0 else math.nan,
+            "cy": sy / cnt if cnt > 0 else math.nan, "minJ": float(d[:, 3].min()),
+            "maxJ": float(d[:, 4].max()), "umax": math.sqrt(m2),
+            "fitted": int(sc[0, SC_FIT])})
+
+    def diagnostics(self):
+        keys = self.records[0].keys() if self.records else ()
+        return {k: np.array([r[k] for r in self.records]) for k in keys}
+
+
+def soft_disc_in_lid_driven(N, comm):
+    """Configs 2/4 physics (soft_disc_in_lid_driven.py:165-199), decomposed over comm.G
+    slabs, from the driver's initial condition."""
+    from .simulation import soft_disc_params, initial_disc_map
+    kw = soft_disc_params(N)
+    sim = DistributedSim(N, comm, **kw)
+    X1, X2 = initial_disc_map(N, *kw["disc"], kw["layers"])
+    z = np.zeros((N, N))
+    sim.set_state(u=z, v=z, p=z, X1=X1, X2=X2)
+    return sim

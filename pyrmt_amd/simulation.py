@@ -121,18 +121,31 @@ def _init_disc_map(sim, x0, y0, R, layers):
     sim.set_field("X2", X2)
 
 
+def soft_disc_params(N, stress_band=False, detg_clamp=3.0):
+    """Configs 2 and 4 physics (soft_disc_in_lid_driven.py:165-199 parameters): neo-Hookean
+    disc (0.6, 0.5, R=0.2) in the lid cavity, semi-Lagrangian map advection."""
+    w_t = 2.0 * np.linspace(0, 1, N)[1]
+    layers = max(3, int(np.ceil(w_t / (np.linspace(0, 1, N)[1]))) + 1)
+    return dict(bc_kind=NOSLIP_LID, lid=1.0, disc=(0.6, 0.5, 0.2), mu_s=0.1, kappa=0.0,
+                rho_s=1.0, eta_s=0.01, mu_f=0.01, rho_f=1.0, w_t=w_t, layers=layers, cfl=0.2,
+                dt_cap=1e-3, stress_band=stress_band, detg_clamp=detg_clamp)
+
+
+def initial_disc_map(N, x0, y0, R, layers):
+    """The drivers' initial reference map (soft_disc_in_lid_driven.py:177-193): phi0 with
+    apply_phi_BCs, xi = x * mask, then the narrow-band extrapolation (on the GPU)."""
+    X, Y, dx, dy = F.create_grid(N, N, 1.0, 1.0)
+    phi = F.apply_phi_BCs(np.sqrt((X - x0) ** 2 + (Y - y0) ** 2) - R)
+    m = (phi <= 0).astype(float)
+    return F.extrapolate_reference_map(X * m, Y * m, phi, dx, dy, layers)
+
+
 def soft_disc_in_lid_driven(N=128, scheme="semilagrangian", stress_band=False, detg_clamp=3.0):
     """Configs 2 and 4: neo-Hookean disc (0.6, 0.5, R=0.2) in the lid cavity
     (soft_disc_in_lid_driven.py:165-199 parameters)."""
-    dx = 1.0 / (N - 1)
-    w_t = 2.0 * np.linspace(0, 1, N)[1]
-    layers = max(3, int(np.ceil(w_t / (np.linspace(0, 1, N)[1]))) + 1)
-    sim = Simulation(N, scheme=scheme, bc_kind=NOSLIP_LID, lid=1.0, disc=(0.6, 0.5, 0.2),
-                     mu_s=0.1, kappa=0.0, rho_s=1.0, eta_s=0.01, mu_f=0.01, rho_f=1.0, w_t=w_t,
-                     layers=layers, cfl=0.2, dt_cap=1e-3, stress_band=stress_band,
-                     detg_clamp=detg_clamp)
-    _init_disc_map(sim, 0.6, 0.5, 0.2, layers)
-    _ = dx
+    kw = soft_disc_params(N, stress_band, detg_clamp)
+    sim = Simulation(N, scheme=scheme, **kw)
+    _init_disc_map(sim, 0.6, 0.5, 0.2, kw["layers"])
     return sim
 
 

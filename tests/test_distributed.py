@@ -1,0 +1,103 @@
+"""Slab-decomposed step (pyrmt_amd/distributed.py, librmt rmt_slab_*).
+
+CPU (gloo): every TorchComm collective against the in-process LocalComm on the same data,
+world sizes 2 and 3 (uneven slabs).  GPU: the decomposed step over G virtual slabs is
+bit-identical to the fused single-domain step (rmt_sim) when every slab holds 2^m rows at
+a multiple of 2^m; with uneven slabs (N=129, G=3) it agrees to rounding; and two
+processes sharing the GPU over gloo reproduce the single-domain step (the TorchComm path).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(nproc, script, *args, timeout=240, env=None):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={_port()}",
+           os.path.join(ROOT, "tests", "workers", script), *map(str, args)]
+    e = dict(os.environ, OMP_NUM_THREADS="1", HSA_ENABLE_IPC_MODE_LEGACY="0", **(env or {}))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def test_even_splits():
+    from pyrmt_amd.distributed import even_splits
+    assert even_splits(4096, 8, 12) == [512 * k for k in range(9)]
+    s = even_splits(129, 3, 12)
+    assert s[0] == 0 and s[-1] == 129 and all(x % 2 == 0 for x in s[:-1])
+    assert all(b - a >= 12 for a, b in zip(s, s[1:]))
+    with pytest.raises(ValueError):
+        even_splits(20, 2, 12)
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_torchcomm_gloo_matches_localcomm(G):
+    out = _torchrun(G, "dist_comm.py")
+    assert f"dist_comm ok {G}" in out
+
+
+# ------------------------------------------------------------------------------ GPU --
+def _fused(gpu, N, steps):
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    sim = soft_disc_in_lid_driven(N)
+    sim.step(steps)
+    return sim
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 2, 4])
+def test_slab_step_bitexact_vs_fused(gpu, G):
+    """N=256: slabs of 256/G rows (aligned row-tree nodes) -> identical bits to rmt_sim."""
+    from pyrmt_amd import distributed as D
+    N, K = 256, 4
+    ref = _fused(gpu, N, K)
+    sim = D.soft_disc_in_lid_driven(N, D.LocalComm(G))
+    sim.step(K)
+    d, r = sim.diagnostics(), ref.diagnostics()
+    np.testing.assert_array_equal(d["dt"], r["dt"])
+    for f in ("u", "v", "p", "X1", "X2"):
+        np.testing.assert_array_equal(sim.gather(f), ref.get(f), err_msg=f)
+    np.testing.assert_array_equal(d["minJ"], r["minJ"])
+    np.testing.assert_array_equal(d["maxJ"], r["maxJ"])
+    np.testing.assert_allclose(d["cx"], r["cx"], rtol=1e-13)
+    np.testing.assert_allclose(d["cy"], r["cy"], rtol=1e-13)
+    assert d["fitted"][-1] > 0
+
+
+@pytest.mark.gpu
+def test_slab_step_uneven_slabs(gpu):
+    """N=129 over 3 slabs (58/58/13-ish rows, not tree-aligned): the means differ in the
+    last bits only, so fields agree to rounding and the centroid to 1e-12."""
+    from pyrmt_amd import distributed as D
+    N, K = 129, 5
+    ref = _fused(gpu, N, K)
+    sim = D.soft_disc_in_lid_driven(N, D.LocalComm(3))
+    sim.step(K)
+    d, r = sim.diagnostics(), ref.diagnostics()
+    np.testing.assert_allclose(d["cx"], r["cx"], rtol=1e-12)
+    np.testing.assert_allclose(d["cy"], r["cy"], rtol=1e-12)
+    for f in ("u", "v", "X1", "X2"):
+        np.testing.assert_allclose(sim.gather(f), ref.get(f), rtol=0, atol=1e-10, err_msg=f)
+
+
+@pytest.mark.gpu
+def test_slab_step_two_processes_gloo(gpu):
+    """The TorchComm path: two processes on cuda:0 over gloo (host-staged collectives)
+    match the fused single-domain step."""
+    out = _torchrun(2, "dist_step.py", 129, 4, "gloo", timeout=300)
+    assert "dist_step ok" in out
