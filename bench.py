@@ -8,9 +8,10 @@ reference-map advection, narrow-band extrapolation, level-set rebuild, RK4 momen
 Rhie-Chow + DCT-I projection, centroid/J diagnostics) on synthetic state of that shape
 (the driver's own initial condition: disc (0.6, 0.5, 0.2), fluid at rest, lid U=1).
 
-Multi-GPU: the fused step is not domain-decomposed yet, so N > 1 runs N independent
-replicas of the full N=4096 problem, one per rank (DESIGN.md, "replicas only");
-`value` counts the cells all ranks updated, timed by the max over ranks.
+Multi-GPU (--gpus N > 1, one process per GPU under torch.distributed.run): the SAME
+N=4096 problem decomposed into N row slabs (pyrmt_amd/distributed.py, librmt rmt_slab_*),
+RCCL halo exchanges / all-to-all transposes / allgathers over xGMI -- strong scaling;
+`value` = the problem's cell-updates per second, timed by the max over ranks.
 """
 import argparse
 import json
@@ -67,7 +68,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--grid", "--n", dest="n", type=int, default=4096)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -75,15 +76,25 @@ def main():
     ws, rank, local = _dist()
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local)
+    # RMT_DIST_BACKEND=gloo: rehearsal of the multi-rank path with every rank on the visible
+    # GPUs round-robin (host-staged collectives); the default is RCCL, one rank per GPU
+    backend = os.environ.get("RMT_DIST_BACKEND", "nccl")
+    dev = local % torch.cuda.device_count() if backend == "gloo" else local
+    torch.cuda.set_device(dev)
     if ws > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import sys
     sys.path.insert(0, ROOT)
-    from pyrmt_amd.simulation import soft_disc_in_lid_driven
-
     N = args.n
-    sim = soft_disc_in_lid_driven(N)
+    if ws > 1:
+        from pyrmt_amd import distributed as D
+        sim = D.soft_disc_in_lid_driven(N, D.TorchComm())
+    else:
+        from pyrmt_amd.simulation import soft_disc_in_lid_driven
+        sim = soft_disc_in_lid_driven(N)
     sim.step(args.warmup)
     torch.cuda.synchronize()
     sim.set_profiling(True)
@@ -105,41 +116,47 @@ def main():
     assert np.all(np.isfinite(d["cx"])) and np.all(np.isfinite(d["umax"])), "non-finite state"
 
     if rank == 0:
-        cells = N * N * args.steps * ws
+        cells = N * N * args.steps          # one problem (strong scaling when ws > 1)
         value = cells / elapsed
-        rk_ms, rk_launches = ph["rk4_stage_kernels"]
+        rk_ms, rk_intervals = ph["rk4_stage_kernels"]
+        rk_launches = rk_intervals if ws == 1 else 4 * rk_intervals
         per_launch_s = rk_ms / 1e3 / rk_launches
         # achieved: SURVEY 8(d)'s algorithmic bytes of the stress + RK4 pass (7 planes per cell
-        # for the 4 stage launches) spread over the launches, / the HIP-event launch time
-        alg_per_launch = RK4_ALG_BYTES_PER_CELL * N * N / 4
+        # for the 4 stage launches) spread over the launches, / the HIP-event launch time;
+        # a slab's cell-updates are its owned rows (the recomputed halo rows are overhead)
+        own = N * N if ws == 1 else (sim.slabs[0].r1 - sim.slabs[0].r0) * N
+        alg_per_launch = RK4_ALG_BYTES_PER_CELL * own / 4
         achieved = alg_per_launch / per_launch_s / 1e9
-        ex_ms, ex_calls = ph["extrap_sweep_kernel"]
+        ex_ms, ex_calls = ph["extrap_sweep_kernel" if ws == 1 else "extrap_chain_kernel"]
         out = {
             "metric": "cell-updates/s (full RMT step) at N=4096; achieved HBM GB/s vs peak",
             "value": value, "unit": "cell-updates/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if ws > 1 else "weak",
+            "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (driver initial condition: disc at rest, lid U=1)",
             "config": {"workload": f"soft_disc_in_lid_driven N={N} semilagrangian "
                                    "(configs 2/4 loop body)", "grid": N,
-                       "parallelism": "replicas" if ws > 1 else "single-gpu"},
+                       "parallelism": f"slab{ws} (row slabs, RCCL)" if ws > 1 else "single-gpu"},
             # the dominant HBM-bound kernel: the fused RK4 stage (4 launches per step)
             "roofline": {"bound": "hbm", "kernel": "k_mom_stage (fused RK4 stage, 4 launches/step)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": TRAFFIC_PER_LAUNCH if N == 4096 else None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": TRAFFIC_PER_LAUNCH if N == 4096 and ws == 1 else None,
                          "launch_ms": per_launch_s * 1e3,
                          "alg_bytes_per_launch": alg_per_launch},
             # the dominant kernel by time is not HBM-bound: the exact raster-order extrapolation
             # chain runs on one workgroup, bounded by its dependency depth
-            "latency_bound": {"kernel": "k_ex_sweep (exact serial-order extrapolation chain)",
+            "latency_bound": {"kernel": "k_ex_chain (exact serial-order extrapolation chain)",
                               "ms_per_step": ex_ms / max(1, ex_calls),
                               "critical_path_fits": CHAIN_DEPTH_4096 if N == 4096 else None},
             "step_roofline": {"alg_bytes_per_cell": STEP_ALG_BYTES_PER_CELL,
+                              "per_gpu": True,
                               "achieved_GBs": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9,
                               "frac": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9 / HBM_PEAK_GBS},
             "phase_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ph.items()},
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and ws == 1:
             out["cpu_baseline"] = cpu_baseline(N, args.cpu_steps)
         print(json.dumps(out), flush=True)
     if ws > 1:

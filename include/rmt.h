@@ -63,6 +63,11 @@ int rmt_ctx_create(int ny, int nx, int device, void *stream, rmt_ctx **out);
 int rmt_ctx_set_stream(rmt_ctx *ctx, void *stream);
 int rmt_ctx_destroy(rmt_ctx *ctx);
 int rmt_ctx_sync(rmt_ctx *ctx);
+/* HIP-event kernel timers on the ctx stream: after each momentum / extrapolation call,
+ * ms2[0] = the four RK4 stage kernels of the last momentum call, ms2[1] = the last
+ * extrapolation chain (0 if none was recorded).  Blocks until the events complete. */
+int rmt_ctx_set_profiling(rmt_ctx *ctx, int on);
+int rmt_ctx_kernel_ms(rmt_ctx *ctx, double *ms2);
 
 /* ---- finite-difference helpers (pyRMT/utils.py) ----------------------------------- */
 /* utils.py:4-14 grad_central_x_2nd / utils.py:16-25 grad_central_y_2nd */

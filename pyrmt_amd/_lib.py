@@ -50,6 +50,8 @@ SIGNATURES = {
     "rmt_ctx_set_stream": (_I, [_P, _P]),
     "rmt_ctx_destroy": (_I, [_P]),
     "rmt_ctx_sync": (_I, [_P]),
+    "rmt_ctx_set_profiling": (_I, [_P, _I]),
+    "rmt_ctx_kernel_ms": (_I, [_P, ctypes.POINTER(_D)]),
     "rmt_grad_x_2nd": (_I, [_P, _P, _D, _P]),
     "rmt_grad_y_2nd": (_I, [_P, _P, _D, _P]),
     "rmt_diff_upwind_3rd": (_I, [_P, _P, _P, _D, _I, _P]),

@@ -436,6 +436,26 @@ int rmt_ctx_sync(rmt_ctx *ctx) {
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     return RMT_OK;
 }
+int rmt_ctx_set_profiling(rmt_ctx *ctx, int on) {
+    RMT_CHECK(ctx, RMT_EINVAL, "null ctx");
+    if (on && !ctx->ev[0])
+        for (auto &e : ctx->ev) RMT_HIP(hipEventCreate(&e));
+    ctx->prof = on != 0;
+    return RMT_OK;
+}
+int rmt_ctx_kernel_ms(rmt_ctx *ctx, double *ms2) {
+    RMT_CHECK(ctx && ms2 && ctx->ev[0], RMT_EINVAL, "profiling not enabled");
+    float f = 0;
+    RMT_HIP(hipEventSynchronize(ctx->ev[1]));
+    RMT_HIP(hipEventElapsedTime(&f, ctx->ev[0], ctx->ev[1]));
+    ms2[0] = f;
+    ms2[1] = 0;
+    if (hipEventQuery(ctx->ev[3]) == hipSuccess &&
+        hipEventElapsedTime(&f, ctx->ev[2], ctx->ev[3]) == hipSuccess)
+        ms2[1] = f;
+    return RMT_OK;
+}
+
 int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (!ctx) return RMT_OK;
     hipSetDevice(ctx->device);

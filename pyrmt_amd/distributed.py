@@ -337,6 +337,26 @@ class DistributedSim:
         return g.cpu().numpy().reshape(self.G, SC_N)
 
     # ----------------------------------------------------------------------- step --
+    PHASES = ("halo", "advect", "extrapolate", "momentum", "projection", "finish",
+              "rk4_stage_kernels", "extrap_chain_kernel")
+
+    def set_profiling(self, on=True):
+        """HIP events (torch.cuda.Event on the stream librmt uses) around each phase, and
+        librmt's own kernel timers; read with phase_times()."""
+        L.check(L.lib().rmt_ctx_set_profiling(self.ctx.h, int(bool(on))))
+        self._prof = bool(on)
+        self._ms = {k: 0.0 for k in self.PHASES}
+        self._nprof = 0
+
+    def phase_times(self):
+        return {k: (v, self._nprof) for k, v in self._ms.items()}
+
+    def _mark(self, ev):
+        if getattr(self, "_prof", False):
+            e = self.torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append(e)
+
     def step(self, nsteps=1, t_end=math.inf):
         self.ctx.bind()
         comm, S = self.comm, self.slabs
@@ -346,13 +366,17 @@ class DistributedSim:
         for _ in range(nsteps):
             if not (self.t < t_end):
                 break
+            ev = []
+            self._mark(ev)
             comm.halo(S, ("u", "v", "p", "X1", "X2"), HALO)
             m2 = self.m2
             dt = min(self.dt_const, self.cfl * self.dx / (math.sqrt(m2) + 1e-6))
             if self.t + dt > t_end:
                 dt = t_end - self.t
+            self._mark(ev)
             # advection + exact extrapolation (band replicated on every slab)
             self._call("rmt_slab_advect", dt)
+            self._mark(ev)
             comm.allgather_rows(S, "bits")
             self._call("rmt_slab_rim_pack")
             counts = [int(c) for c in self._scalars()[:, SC_COUNT]]
@@ -362,8 +386,10 @@ class DistributedSim:
             for s, g in zip(S, gathered):
                 L.check(s.lib.rmt_slab_extrapolate(s.h, g.data_ptr(), self._counts, cap),
                         "rmt_slab_extrapolate")
+            self._mark(ev)
             # momentum, projection
             self._call("rmt_slab_momentum", dt)
+            self._mark(ev)
             self._call("rmt_slab_project_rows", dt)
             sp = [s.a2a_splits() for s in S]
             comm.all_to_all([s.view("A") for s in S], [s.view("B") for s in S],
@@ -376,10 +402,20 @@ class DistributedSim:
             comm.halo(S, ("pc",), 2)
             self._call("rmt_slab_project_correct", dt)
             self._sub_mean(1)
+            self._mark(ev)
             self._call("rmt_slab_finish")
+            self._mark(ev)
             sc = self._scalars()
             self.t += dt
             self._record(sc, dt, m2)
+            if ev:
+                for k, name in enumerate(self.PHASES[:6]):
+                    self._ms[name] += ev[k].elapsed_time(ev[k + 1])
+                ms2 = (ctypes.c_double * 2)()
+                L.check(L.lib().rmt_ctx_kernel_ms(self.ctx.h, ms2))
+                self._ms["rk4_stage_kernels"] += ms2[0]
+                self._ms["extrap_chain_kernel"] += ms2[1]
+                self._nprof += 1
 
     def _sub_mean(self, which):
         roots = self.comm.allgather([s.view("scal")[SC_ROOT:SC_ROOT + 1] for s in self.slabs])
