@@ -1,0 +1,193 @@
+"""mac_oracle -- CPU restatement of pyRMT's MAC path, config 5 (TEST INFRASTRUCTURE ONLY).
+
+Only tests/ and bench.py's cpu_baseline leg may import this module, as the checker.
+pyRMT/mac.py is pure NumPy in the reference; it is restated here with the same NumPy
+operations in the same order (so bit-exact with the reference), the DCT-II through
+scipy.fft like mac.py:118-123.  The per-disc reference-map advection / extrapolation /
+stress reuse the C restatement in oracle.py.  Pinned by tests/golden/mac_ops.npz and
+mac_trace.npz (tests/test_oracle_golden.py).
+"""
+import numpy as np
+
+from .oracle import (advect_reference_map, extrapolate_reference_map, grad_central_x_2nd,
+                     grad_central_y_2nd, rebuild_phi_disc, smoothed_heaviside,
+                     solid_cauchy_stress)
+
+
+def mac_grid(Nx, Ny, Lx=1.0, Ly=1.0):
+    """mac.py:22-23: cell sizes of an Nx x Ny cell grid."""
+    return Lx / Nx, Ly / Ny
+
+
+def divergence(u, v, dx, dy):
+    """mac.py:81-84: cell-centred divergence of the face velocities."""
+    return (u[:, 1:] - u[:, :-1]) / dx + (v[1:, :] - v[:-1, :]) / dy
+
+
+def gradient_p_u(p, dx):
+    """mac.py:87-93: dp/dx on the interior u faces, wall faces 0."""
+    g = np.zeros((p.shape[0], p.shape[1] + 1))
+    g[:, 1:-1] = (p[:, 1:] - p[:, :-1]) / dx
+    return g
+
+
+def gradient_p_v(p, dy):
+    """mac.py:96-101: dp/dy on the interior v faces, wall faces 0."""
+    g = np.zeros((p.shape[0] + 1, p.shape[1]))
+    g[1:-1, :] = (p[1:, :] - p[:-1, :]) / dy
+    return g
+
+
+def poisson_eigs_neumann(Nx, Ny, dx, dy):
+    """mac.py:104-115: DCT-II symbol of the cell-centred Neumann Laplacian, (0,0) -> 1."""
+    lx = -2.0 * (1.0 - np.cos(np.pi * np.arange(Nx) / Nx)) / dx ** 2
+    ly = -2.0 * (1.0 - np.cos(np.pi * np.arange(Ny) / Ny)) / dy ** 2
+    eig = (lx[np.newaxis, :] + ly[:, np.newaxis]).copy()
+    eig[0, 0] = 1.0
+    return eig
+
+
+def solve_poisson_neumann(rhs, eig):
+    """mac.py:118-123: orthonormal DCT-II both ways, constant mode zeroed."""
+    from scipy.fft import dctn, idctn
+    h = dctn(rhs, type=2, norm='ortho') / eig
+    h[0, 0] = 0.0
+    return idctn(h, type=2, norm='ortho')
+
+
+def project(u_star, v_star, dx, dy, dt, rho, eig):
+    """mac.py:126-139: exact projection of the face velocities."""
+    rhs = (rho / dt) * divergence(u_star, v_star, dx, dy)
+    rhs = rhs - rhs.mean()
+    phi = solve_poisson_neumann(rhs, eig)
+    return (u_star - (dt / rho) * gradient_p_u(phi, dx),
+            v_star - (dt / rho) * gradient_p_v(phi, dy), phi)
+
+
+def momentum_predictor(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0):
+    """mac.py:196-232 (+ ghosts :147-166, face averages :168-177): explicit central
+    advection + diffusion, lid / no-slip by reflected ghosts, face forces / rho."""
+    Ny, Nx = u.shape[0], u.shape[1] - 1
+    ug = np.empty((Ny + 2, Nx + 1)); ug[1:-1] = u
+    ug[0] = -u[0]; ug[-1] = 2.0 * U_lid - u[-1]
+    vg = np.empty((Ny + 1, Nx + 2)); vg[:, 1:-1] = v
+    vg[:, 0] = -v[:, 0]; vg[:, -1] = -v[:, -1]
+    uc = u[:, 1:-1]
+    vu = 0.25 * (v[:-1, :-1] + v[:-1, 1:] + v[1:, :-1] + v[1:, 1:])
+    ru = (-(uc * ((u[:, 2:] - u[:, :-2]) / (2 * dx))
+            + vu * ((ug[2:, 1:-1] - ug[:-2, 1:-1]) / (2 * dy)))
+          + nu * ((u[:, 2:] - 2 * uc + u[:, :-2]) / dx ** 2
+                  + (ug[2:, 1:-1] - 2 * ug[1:-1, 1:-1] + ug[:-2, 1:-1]) / dy ** 2))
+    if fu is not None:
+        ru = ru + fu[:, 1:-1] / rho
+    us = u.copy(); us[:, 1:-1] = uc + dt * ru
+    us[:, 0] = 0.0; us[:, -1] = 0.0
+    vc = v[1:-1, :]
+    uv = 0.25 * (u[:-1, :-1] + u[:-1, 1:] + u[1:, :-1] + u[1:, 1:])
+    rv = (-(uv * ((vg[1:-1, 2:] - vg[1:-1, :-2]) / (2 * dx))
+            + vc * ((v[2:, :] - v[:-2, :]) / (2 * dy)))
+          + nu * ((vg[1:-1, 2:] - 2 * vg[1:-1, 1:-1] + vg[1:-1, :-2]) / dx ** 2
+                  + (v[2:, :] - 2 * vc + v[:-2, :]) / dy ** 2))
+    if fv is not None:
+        rv = rv + fv[1:-1, :] / rho
+    vs = v.copy(); vs[1:-1, :] = vc + dt * rv
+    vs[0, :] = 0.0; vs[-1, :] = 0.0
+    return us, vs
+
+
+def contact_stress(phi_a, phi_b, eta, Gsum, eps, dx, dy):
+    """mac.py:729-749: trace-free pair contact stress (Rycroft et al. 2018)."""
+    f = [np.where(q < eps, 0.5 * (1.0 - q / eps), 0.0) for q in (phi_a, phi_b)]
+    fc = np.minimum(f[0], f[1])
+    d = phi_a - phi_b
+    gx = np.zeros_like(d); gy = np.zeros_like(d)
+    gx[:, 1:-1] = (d[:, 2:] - d[:, :-2]) / (2 * dx)
+    gy[1:-1, :] = (d[2:, :] - d[:-2, :]) / (2 * dy)
+    mag = np.sqrt(gx * gx + gy * gy) + 1e-12
+    nx_, ny_ = gx / mag, gy / mag
+    s = -eta * fc * Gsum
+    return s * (nx_ * nx_ - 0.5), s * (nx_ * ny_), s * (ny_ * ny_ - 0.5)
+
+
+def place_discs(n, seed, Rrange=(0.07, 0.12), box=(0.18, 0.82)):
+    """mac_multi_disc_lid.py:22-33: rejection-sampled non-overlapping discs (R, cx, cy)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(2000):
+        if len(out) == n:
+            break
+        R = rng.uniform(*Rrange)
+        cx = rng.uniform(box[0] + R, box[1] - R); cy = rng.uniform(box[0] + R, box[1] - R)
+        if all((cx - d[1]) ** 2 + (cy - d[2]) ** 2 > (R + d[0] + 0.03) ** 2 for d in out):
+            out.append((R, cx, cy))
+    return out
+
+
+class MacMultiDisc:
+    """benchmarks/mac_multi_disc_lid.py:36-111 (config 5) loop body: K discs, each with
+    its own reference map advected on the cell-centre velocity, blended solid stress +
+    pair contact stress -> face force, explicit MAC predictor, exact DCT-II projection."""
+
+    def __init__(self, N, n_discs=3, seed=3, U_lid=1.0, mu_s=0.3, mu_f=0.01, rho=1.0, eta=2.0):
+        dx, dy = mac_grid(N, N)
+        self.N, self.dx, self.dy = N, dx, dy
+        xc = (np.arange(N) + 0.5) * dx
+        self.Xc, self.Yc = np.meshgrid(xc, xc)
+        self.Xg, self.Yg = np.meshgrid(np.arange(N) * dx, np.arange(N) * dy)
+        self.w_t, self.nu, self.eps = 2.0 * dx, mu_f / rho, 3.0 * dx
+        self.U, self.mu_s, self.rho, self.eta = U_lid, mu_s, rho, eta
+        self.specs = place_discs(n_discs, seed)
+        self.refs = []
+        for (R, cx, cy) in self.specs:
+            phi = rebuild_phi_disc(self.Xc, self.Yc, cx, cy, R)
+            m = (phi <= 0).astype(float)
+            self.refs.append(list(extrapolate_reference_map(self.Xc * m, self.Yc * m, phi,
+                                                            dx, dy, 3)))
+        self.u = np.zeros((N, N + 1)); self.v = np.zeros((N + 1, N)); self.p = None
+        self.eig = poisson_eigs_neumann(N, N, dx, dy)
+        cs = np.sqrt(mu_s / rho)
+        self.dt = min(0.3 * dx / U_lid, 0.2 * dx * dx / self.nu, 0.3 * dx / (cs + 1e-9))
+        self.t = 0.0
+
+    def step(self, t_end=np.inf):
+        N, dx, dy = self.N, self.dx, self.dy
+        dt = self.dt
+        if self.t + dt > t_end:
+            dt = t_end - self.t
+        u_c = 0.5 * (self.u[:, :-1] + self.u[:, 1:]); v_c = 0.5 * (self.v[:-1, :] + self.v[1:, :])
+        phis = []
+        for k, (R, cx, cy) in enumerate(self.specs):
+            X1, X2 = self.refs[k]
+            phi = rebuild_phi_disc(X1, X2, cx, cy, R); m = (phi <= 0).astype(float)
+            X1 = advect_reference_map(X1, u_c, v_c, self.Xg, self.Yg, dt, dx, dy, phi) * m
+            X2 = advect_reference_map(X2, u_c, v_c, self.Xg, self.Yg, dt, dx, dy, phi) * m
+            X1, X2 = extrapolate_reference_map(X1, X2, phi, dx, dy, 3)
+            self.refs[k] = [X1, X2]
+            phis.append(rebuild_phi_disc(X1, X2, cx, cy, R))
+        S = [np.zeros((N, N)) for _ in range(3)]
+        Jmin = Jmax = 1.0
+        for k in range(len(self.refs)):
+            sxx, sxy, syy, J = solid_cauchy_stress(self.refs[k][0], self.refs[k][1], dx, dy,
+                                                   self.mu_s, 0.0, phis[k])
+            H = smoothed_heaviside(phis[k], self.w_t)
+            S[0] += (1 - H) * sxx; S[1] += (1 - H) * sxy; S[2] += (1 - H) * syy
+            Jmin = min(Jmin, J.min()); Jmax = max(Jmax, J.max())
+        if self.eta > 0:
+            for i in range(len(phis)):
+                for j in range(i + 1, len(phis)):
+                    t3 = contact_stress(phis[i], phis[j], self.eta, 2 * self.mu_s, self.eps,
+                                        dx, dy)
+                    for q in range(3):
+                        S[q] += t3[q]
+        divx = grad_central_x_2nd(S[0], dx) + grad_central_y_2nd(S[1], dy)
+        divy = grad_central_x_2nd(S[1], dx) + grad_central_y_2nd(S[2], dy)
+        fu = np.zeros((N, N + 1)); fu[:, 1:-1] = 0.5 * (divx[:, 1:] + divx[:, :-1])
+        fv = np.zeros((N + 1, N)); fv[1:-1, :] = 0.5 * (divy[1:, :] + divy[:-1, :])
+        us, vs = momentum_predictor(self.u, self.v, self.nu, dx, dy, dt, self.U,
+                                    fu=fu, fv=fv, rho=self.rho)
+        self.u, self.v, self.p = project(us, vs, dx, dy, dt, self.rho, self.eig)
+        self.t += dt
+        self.phis = phis
+        cents = [(self.Xc[q <= 0].mean(), self.Yc[q <= 0].mean()) for q in phis]
+        return dict(t=self.t, dt=dt, minJ=Jmin, maxJ=Jmax,
+                    cx=np.array([c[0] for c in cents]), cy=np.array([c[1] for c in cents]))

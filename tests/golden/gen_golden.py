@@ -446,7 +446,74 @@ def gen_mac():
          pu=pu, pv=pv, pp=pp, pa=pa, pb=pb, txx=txx, txy=txy, tyy=tyy)
 
 
+def gen_mac_trace(N=64, nsteps=8, n_discs=3, seed=3):
+    """Config 5 loop body (benchmarks/mac_multi_disc_lid.py:36-98) with the reference's
+    own functions, no I/O: per-step centroids / J range and the final state."""
+    import importlib
+    drv = importlib.import_module("benchmarks.mac_multi_disc_lid")
+    U_lid, mu_s, mu_f, rho, eta = 1.0, 0.3, 0.01, 1.0, 2.0
+    dx, dy = M.mac_grid(N, N)
+    xc = (np.arange(N) + 0.5) * dx
+    Xc, Yc = np.meshgrid(xc, xc)
+    Xg, Yg = np.meshgrid(np.arange(N) * dx, np.arange(N) * dy)
+    w_t = 2.0 * dx; nu = mu_f / rho; eps = 3.0 * dx
+    specs = drv._place_discs(n_discs, seed)
+    inits = [(lambda X, Y, cx=cx, cy=cy, R=R: np.sqrt((X-cx)**2 + (Y-cy)**2) - R)
+             for (R, cx, cy) in specs]
+    refs = []
+    for pin in inits:
+        phi = pin(Xc, Yc); m = (phi <= 0).astype(float)
+        refs.append(list(F.extrapolate_reference_map(Xc * m, Yc * m, phi, dx, dy, 3)))
+    init_refs = [[a.copy() for a in r] for r in refs]
+    u = np.zeros((N, N + 1)); v = np.zeros((N + 1, N))
+    eig = M.poisson_eigs_neumann(N, N, dx, dy)
+    cs = np.sqrt(mu_s / rho)
+    dt = min(0.3 * dx / U_lid, 0.2 * dx * dx / nu, 0.3 * dx / (cs + 1e-9))
+    rec = {k: [] for k in ("cx", "cy", "minJ", "maxJ")}
+    for _ in range(nsteps):
+        u_c = 0.5 * (u[:, :-1] + u[:, 1:]); v_c = 0.5 * (v[:-1, :] + v[1:, :])
+        phis = []
+        for k, pin in enumerate(inits):
+            X1, X2 = refs[k]
+            phi = F.rebuild_phi_from_reference_map(X1, X2, pin); m = (phi <= 0).astype(float)
+            X1 = F.advect_reference_map(X1, u_c, v_c, Xg, Yg, dt, dx, dy, phi, 'semilagrangian', 0.0) * m
+            X2 = F.advect_reference_map(X2, u_c, v_c, Xg, Yg, dt, dx, dy, phi, 'semilagrangian', 0.0) * m
+            X1, X2 = F.extrapolate_reference_map(X1, X2, phi, dx, dy, 3)
+            refs[k] = [X1, X2]
+            phis.append(F.rebuild_phi_from_reference_map(X1, X2, pin))
+        Sxx = np.zeros((N, N)); Sxy = np.zeros((N, N)); Syy = np.zeros((N, N))
+        Jmin = 1.0; Jmax = 1.0
+        for k in range(len(refs)):
+            sxx, sxy, syy, J = F.solid_cauchy_stress(refs[k][0], refs[k][1], dx, dy, mu_s, 0.0, phis[k])
+            H = F.smoothed_heaviside(phis[k], w_t)
+            Sxx += (1 - H) * sxx; Sxy += (1 - H) * sxy; Syy += (1 - H) * syy
+            Jmin = min(Jmin, J.min()); Jmax = max(Jmax, J.max())
+        for i in range(len(phis)):
+            for j in range(i + 1, len(phis)):
+                txx, txy, tyy = M.contact_stress(phis[i], phis[j], eta, 2 * mu_s, eps, dx, dy)
+                Sxx += txx; Sxy += txy; Syy += tyy
+        divx = U.grad_central_x_2nd(Sxx, dx) + U.grad_central_y_2nd(Sxy, dy)
+        divy = U.grad_central_x_2nd(Sxy, dx) + U.grad_central_y_2nd(Syy, dy)
+        fu = np.zeros((N, N + 1)); fu[:, 1:-1] = 0.5 * (divx[:, 1:] + divx[:, :-1])
+        fv = np.zeros((N + 1, N)); fv[1:-1, :] = 0.5 * (divy[1:, :] + divy[:-1, :])
+        ustar, vstar = M.momentum_predictor(u, v, nu, dx, dy, dt, U_lid, fu=fu, fv=fv, rho=rho)
+        u, v, p = M.project(ustar, vstar, dx, dy, dt, rho, eig)
+        cents = [(Xc[pp <= 0].mean(), Yc[pp <= 0].mean()) for pp in phis]
+        rec["cx"].append([c[0] for c in cents]); rec["cy"].append([c[1] for c in cents])
+        rec["minJ"].append(Jmin); rec["maxJ"].append(Jmax)
+    save("mac_trace", N=N, nsteps=nsteps, specs=np.array(specs), dt=dt, u=u, v=v, p=p,
+         X1_0=init_refs[0][0], X2_0=init_refs[0][1],
+         **{f"X{c}_{k}_end": refs[k][c - 1] for k in range(len(refs)) for c in (1, 2)},
+         **{f"phi_{k}": phis[k] for k in range(len(phis))},
+         Sxx=Sxx, Sxy=Sxy, Syy=Syy, fu=fu, fv=fv, ustar=ustar, vstar=vstar,
+         **{k: np.array(val) for k, val in rec.items()})
+
+
 if __name__ == "__main__":
+    if "--only" in sys.argv:     # regenerate the named fixtures only
+        for name in sys.argv[sys.argv.index("--only") + 1:]:
+            globals()[f"gen_{name}"]()
+        sys.exit(0)
     t0 = time.time()
     gen_primitives()
     gen_operator_cases()
