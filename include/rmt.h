@@ -246,6 +246,54 @@ int rmt_slab_sub_mean(rmt_slab *slab, int which, const double *roots_dev);  /* 0
 int rmt_slab_project_correct(rmt_slab *slab, double dt); /* after halo(p_c); then roots   */
 int rmt_slab_finish(rmt_slab *slab);                     /* then: allgather scal          */
 
+/* ---- MAC path (config 5): pyRMT/mac.py operators on an N x N cell grid -----------
+ * ctx created for (N, N) cells; u is (N, N+1) x-faces, v (N+1, N) y-faces, p / phi (N, N). */
+int rmt_mac_divergence(rmt_ctx *ctx, const double *u, const double *v, double dx, double dy,
+                       double *out);                                       /* mac.py:81-84  */
+int rmt_mac_gradient_p(rmt_ctx *ctx, const double *p, double dx, double dy, double *gu,
+                       double *gv);                                        /* mac.py:87-101 */
+/* lamx (nx) / lamy (ny): HOST per-axis eigenvalues (eig = lamx[None,:] + lamy[:,None], the
+ * (0,0) mode zeroed), or both NULL for poisson_eigs_neumann's own (mac.py:104-115) */
+int rmt_mac_solve_poisson_neumann(rmt_ctx *ctx, const double *rhs, double dx, double dy,
+                                  const double *lamx, const double *lamy,
+                                  double *out);                           /* mac.py:118-123 */
+int rmt_mac_project(rmt_ctx *ctx, const double *u_star, const double *v_star, double dx,
+                    double dy, double dt, double rho, const double *lamx, const double *lamy,
+                    double *u, double *v, double *phi);                   /* mac.py:126-139 */
+/* fu / fv: face forces or both NULL                                       mac.py:196-232 */
+int rmt_mac_momentum_predictor(rmt_ctx *ctx, const double *u, const double *v, double nu,
+                               double dx, double dy, double dt, double U_lid, const double *fu,
+                               const double *fv, double rho, double *u_star, double *v_star);
+int rmt_mac_contact_stress(rmt_ctx *ctx, const double *phi_a, const double *phi_b, double eta,
+                           double Gsum, double eps, double dx, double dy, double *txx,
+                           double *txy, double *tyy);                     /* mac.py:729-749 */
+
+/* The loop body of benchmarks/mac_multi_disc_lid.py:62-98 (K soft discs with contact, lid
+ * U_lid, fixed dt), device-resident.  Fields: 0 u, 1 v, 2 p (disc ignored); 3 X1, 4 X2,
+ * 5 phi of disc `disc`. */
+#define RMT_MAC_MAXD 8
+typedef struct {
+    int N;                   /* cells per side, dx = 1 / N                               */
+    double dx;
+    int n_discs;
+    double R[RMT_MAC_MAXD], cx[RMT_MAC_MAXD], cy[RMT_MAC_MAXD];
+    double U_lid, mu_s, mu_f, rho, eta;
+    int layers;              /* extrapolation layers (3 in the driver)                   */
+    double dt;               /* the driver's fixed step (mac_multi_disc_lid.py:58)        */
+} rmt_mac_params;
+typedef struct {
+    double t, dt, minJ, maxJ, umax;
+    int n_discs;
+    double cx[RMT_MAC_MAXD], cy[RMT_MAC_MAXD];   /* centroid of phi_k <= 0 (:104)        */
+} rmt_mac_diag;
+typedef struct rmt_mac_sim rmt_mac_sim;
+int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **out);
+int rmt_mac_sim_destroy(rmt_mac_sim *sim);
+int rmt_mac_sim_field(rmt_mac_sim *sim, int field, int disc, double **dev_ptr);
+int rmt_mac_sim_step(rmt_mac_sim *sim, int nsteps, double t_end);
+int rmt_mac_sim_diagnostics(rmt_mac_sim *sim, rmt_mac_diag *out, int max_records,
+                            int *n_records);
+
 #ifdef __cplusplus
 }
 #endif

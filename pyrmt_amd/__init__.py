@@ -11,6 +11,7 @@ from .functions import (_precompute_poisson_eigenvalues, _solve_poisson_dct,  # 
                         _compute_divergence_rc, _compute_divergence, _compute_pressure_gradient,
                         _weno5_rhs)
 from . import simulation
+from . import mac
 
 __version__ = "0.1.0"
 

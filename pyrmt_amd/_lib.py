@@ -42,6 +42,20 @@ class rmt_diag(ctypes.Structure):
                 ("t", "dt", "cx", "cy", "minJ", "maxJ", "umax", "ke", "se", "diss", "integ", "ry")]
 
 
+class rmt_mac_params(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int), ("dx", ctypes.c_double), ("n_discs", ctypes.c_int),
+                ("R", ctypes.c_double * 8), ("cx", ctypes.c_double * 8),
+                ("cy", ctypes.c_double * 8), ("U_lid", ctypes.c_double),
+                ("mu_s", ctypes.c_double), ("mu_f", ctypes.c_double), ("rho", ctypes.c_double),
+                ("eta", ctypes.c_double), ("layers", ctypes.c_int), ("dt", ctypes.c_double)]
+
+
+class rmt_mac_diag(ctypes.Structure):
+    _fields_ = [("t", ctypes.c_double), ("dt", ctypes.c_double), ("minJ", ctypes.c_double),
+                ("maxJ", ctypes.c_double), ("umax", ctypes.c_double), ("n_discs", ctypes.c_int),
+                ("cx", ctypes.c_double * 8), ("cy", ctypes.c_double * 8)]
+
+
 _P, _D, _I, _L = ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_long
 SIGNATURES = {
     "rmt_last_error": (ctypes.c_char_p, []),
@@ -100,6 +114,18 @@ SIGNATURES = {
     "rmt_slab_sub_mean": (_I, [_P, _I, _P]),
     "rmt_slab_project_correct": (_I, [_P, _D]),
     "rmt_slab_finish": (_I, [_P]),
+    # MAC path (mac.py)
+    "rmt_mac_divergence": (_I, [_P, _P, _P, _D, _D, _P]),
+    "rmt_mac_gradient_p": (_I, [_P, _P, _D, _D, _P, _P]),
+    "rmt_mac_solve_poisson_neumann": (_I, [_P, _P, _D, _D, _P, _P, _P]),
+    "rmt_mac_project": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _P, _P, _P, _P]),
+    "rmt_mac_momentum_predictor": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _P, _P, _D, _P, _P]),
+    "rmt_mac_contact_stress": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _P, _P, _P]),
+    "rmt_mac_sim_create": (_I, [_P, ctypes.POINTER(rmt_mac_params), ctypes.POINTER(_P)]),
+    "rmt_mac_sim_destroy": (_I, [_P]),
+    "rmt_mac_sim_field": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
+    "rmt_mac_sim_step": (_I, [_P, _I, _D]),
+    "rmt_mac_sim_diagnostics": (_I, [_P, ctypes.POINTER(rmt_mac_diag), _I, ctypes.POINTER(_I)]),
 }
 
 _lib = None

@@ -464,6 +464,7 @@ int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (ctx->rsum) hipFree(ctx->rsum);
     if (ctx->bytes) hipFree(ctx->bytes);
     if (ctx->dct) dct_destroy(ctx->dct);
+    if (ctx->dct2) dct2_destroy(ctx->dct2);
     delete ctx;
     return RMT_OK;
 }

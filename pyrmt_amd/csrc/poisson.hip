@@ -503,4 +503,226 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
     return RMT_OK;
 }
 
+
+// ============================================================ DCT-II (MAC grid) ====
+// mac.py:118-123 solves the cell-centred Neumann Poisson problem with an orthonormal
+// DCT-II both ways.  The orthonormal scalings cancel between the forward and the inverse
+// transform (they are diagonal per axis), so the solve runs the unnormalised pair
+// y = D x (y_k = 2 sum_n x_n cos(pi k (2n+1) / 2N)) and x = D^-1 y: equal to rounding,
+// like every FFT-based DCT against pocketfft's.  Makhoul's method: D x is 2 Re(w_k V_k),
+// V = FFT_N of the even/odd-reordered x, w_k = e^{-i pi k/2N}; D^-1 builds
+// V_k = 1/2 conj(w_k) (y_k - i y_{N-k}) and inverts the FFT.  Two rows share one complex
+// FFT (their spectra separate by conjugate symmetry), the whole row resident in LDS.
+//   MODE 0: forward along rows; 1: forward, / eig ((0,0) -> 0), inverse (fused column
+//   solve); 2: inverse along rows.
+__device__ __forceinline__ int mk_src(int m, int n) { return m < n / 2 ? 2 * m : 2 * (n - 1 - m) + 1; }
+
+template <int MODE, int BIG>
+__global__ void __launch_bounds__(DCT_T) k_dct2(const double *__restrict__ src,
+                                                double *__restrict__ dst, int rows, int n,
+                                                const double2 *__restrict__ W,
+                                                const double2 *__restrict__ Wq, Radices rd,
+                                                const double *__restrict__ lamr,
+                                                const double *__restrict__ lamk, int row0,
+                                                double scale) {
+    extern __shared__ double2 z[];
+    __shared__ double2 twh[DCT_MAXM / 128], twl[128], rcs[DCT_RCS];
+    constexpr int PER = DCT_MAXM / DCT_T;
+    const int rA = 2 * blockIdx.x, rB = rA + 1, tid = threadIdx.x;
+    if (tid < DCT_MAXM / 128) twh[tid] = (tid << 7) < n ? W[tid << 7] : make_double2(1.0, 0.0);
+    if (tid < 128) twl[tid] = tid < n ? W[tid] : make_double2(1.0, 0.0);
+    if (tid < DCT_RCS) rcs[tid] = W[n + tid];
+    const Tw T{twh, twl};
+    const bool hasB = rB < rows;
+    const double *sa = src + (long)rA * n, *sb = src + (long)rB * n;
+    double *da = dst + (long)rA * n, *db = dst + (long)rB * n;
+    if constexpr (MODE != 2) {
+        for (int m = tid; m < n; m += DCT_T) {
+            const int q = mk_src(m, n);
+            z[m] = make_double2(sa[q], hasB ? sb[q] : 0.0);
+        }
+        __syncthreads();
+        fft_lds<BIG>(z, n, rd, T, rcs);
+        double2 y[PER];
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int k = tid + t * DCT_T;
+            if (k < n) {
+                const double2 Zk = z[k], Zm = z[k ? n - k : 0], w = Wq[k];
+                y[t].x = w.x * (Zk.x + Zm.x) - w.y * (Zk.y - Zm.y);
+                y[t].y = w.x * (Zk.y + Zm.y) + w.y * (Zk.x - Zm.x);
+                if constexpr (MODE == 1) {
+                    y[t].x = (row0 + rA == 0 && k == 0) ? 0.0 : y[t].x / (lamr[row0 + rA] + lamk[k]);
+                    y[t].y = hasB ? y[t].y / (lamr[row0 + rB] + lamk[k]) : 0.0;
+                }
+            }
+        }
+        if constexpr (MODE == 0) {
+#pragma unroll
+            for (int t = 0; t < PER; ++t) {
+                const int k = tid + t * DCT_T;
+                if (k < n) { da[k] = y[t].x * scale; if (hasB) db[k] = y[t].y * scale; }
+            }
+            return;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int k = tid + t * DCT_T;
+            if (k < n) z[k] = y[t];
+        }
+    } else {
+        for (int k = tid; k < n; k += DCT_T) z[k] = make_double2(sa[k], hasB ? sb[k] : 0.0);
+    }
+    __syncthreads();
+    // inverse: conj(Z), Z_k = V^a_k + i V^b_k, V_k = 1/2 conj(w_k) (y_k - i y_{n-k})
+    {
+        double2 c[PER];
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int k = tid + t * DCT_T;
+            if (k < n) {
+                const double2 Y = z[k], Ym = k ? z[n - k] : make_double2(0.0, 0.0);
+                const double2 w = Wq[k];   // (cos, -sin); conj(w) = (cos, sin)
+                const double cs = w.x, sn = -w.y;
+                const double vax = 0.5 * (cs * Y.x + sn * Ym.x), vay = 0.5 * (sn * Y.x - cs * Ym.x);
+                const double vbx = 0.5 * (cs * Y.y + sn * Ym.y), vby = 0.5 * (sn * Y.y - cs * Ym.y);
+                c[t] = make_double2(vax - vby, -(vay + vbx));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int k = tid + t * DCT_T;
+            if (k < n) z[k] = c[t];
+        }
+    }
+    __syncthreads();
+    fft_lds<BIG>(z, n, rd, T, rcs);
+    const double s = scale / n;
+    for (int m = tid; m < n; m += DCT_T) {
+        const double2 R = z[m];
+        const int q = mk_src(m, n);
+        da[q] = R.x * s;
+        if (hasB) db[q] = -R.y * s;
+    }
+}
+
+struct Dct2Plan {
+    int ny = 0, nx = 0, big = 0;
+    double dx = 0, dy = 0;
+    int radx[16] = {0}, rady[16] = {0}, npx = 0, npy = 0;
+    double2 *Wx = nullptr, *Wy = nullptr, *Qx = nullptr, *Qy = nullptr;
+    double *lamx = nullptr, *lamy = nullptr, *T = nullptr;
+};
+
+void dct2_destroy(Dct2Plan *P) {
+    if (!P) return;
+    hipFree(P->Wx); hipFree(P->Wy); hipFree(P->Qx); hipFree(P->Qy);
+    hipFree(P->lamx); hipFree(P->lamy); hipFree(P->T);
+    delete P;
+}
+
+static int quarter_twiddles(int n, double2 **Q) {
+    const long double PI = 3.141592653589793238462643383279502884L;
+    std::vector<double2> h(n);
+    for (int k = 0; k < n; ++k) {
+        long double a = PI * k / (2.0L * n);
+        h[k] = make_double2((double)cosl(a), (double)-sinl(a));
+    }
+    RMT_HIP(hipMalloc(Q, n * sizeof(double2)));
+    RMT_HIP(hipMemcpy(*Q, h.data(), n * sizeof(double2), hipMemcpyHostToDevice));
+    return RMT_OK;
+}
+
+// mac.py:104-115 eigenvalues per axis: -2 (1 - cos(pi k / n)) / h**2 (h**2: libm pow, as a
+// Python float)
+static void mac_lambda(int n, double h, std::vector<double> &lam) {
+    lam.resize(n);
+    const double h2 = std::pow(h, 2.0);
+    for (int k = 0; k < n; ++k) lam[k] = -2.0 * (1.0 - std::cos(M_PI * k / n)) / h2;
+}
+
+int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
+    Dct2Plan *P = ctx->dct2;
+    if (P && P->ny == ny && P->nx == nx && P->dx == dx && P->dy == dy) return RMT_OK;
+    if (P) { dct2_destroy(P); ctx->dct2 = nullptr; }
+    P = new Dct2Plan;
+    P->ny = ny; P->nx = nx; P->dx = dx; P->dy = dy;
+    if ((nx & 1) || (ny & 1) || !factor(nx, P->radx, &P->npx) || !factor(ny, P->rady, &P->npy)) {
+        delete P;
+        set_error("DCT-II solve: N must be even, <= 8192, and factor into radices <= 23");
+        return RMT_ENOTSUP;
+    }
+    for (int k = 0; k < P->npx; ++k) P->big |= P->radx[k] > 13;
+    for (int k = 0; k < P->npy; ++k) P->big |= P->rady[k] > 13;
+    ctx->dct2 = P;
+    RMT_TRY(twiddles(nx, &P->Wx));
+    RMT_TRY(twiddles(ny, &P->Wy));
+    RMT_TRY(quarter_twiddles(nx, &P->Qx));
+    RMT_TRY(quarter_twiddles(ny, &P->Qy));
+    std::vector<double> lx, ly;
+    mac_lambda(nx, dx, lx);
+    mac_lambda(ny, dy, ly);
+    RMT_HIP(hipMalloc(&P->lamx, nx * sizeof(double)));
+    RMT_HIP(hipMalloc(&P->lamy, ny * sizeof(double)));
+    RMT_HIP(hipMemcpy(P->lamx, lx.data(), nx * 8, hipMemcpyHostToDevice));
+    RMT_HIP(hipMemcpy(P->lamy, ly.data(), ny * 8, hipMemcpyHostToDevice));
+    RMT_HIP(hipMalloc(&P->T, (size_t)nx * ny * sizeof(double)));
+    static bool attr = false;
+    if (!attr) {
+        const void *fs[6] = {(const void *)k_dct2<0, 0>, (const void *)k_dct2<1, 0>,
+                             (const void *)k_dct2<2, 0>, (const void *)k_dct2<0, 1>,
+                             (const void *)k_dct2<1, 1>, (const void *)k_dct2<2, 1>};
+        for (auto f : fs)
+            RMT_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        DCT_MAXM * 16));
+        attr = true;
+    }
+    return RMT_OK;
+}
+
+// one DCT-II pass over nrows rows along axis (0: length nx, 1: length ny; MODE 1 needs 1)
+static int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst,
+                     int nrows, int row0) {
+    Dct2Plan *P = ctx->dct2;
+    const int n = axis == 0 ? P->nx : P->ny;
+    const Radices rd = axis == 0 ? radices(P->radx, P->npx) : radices(P->rady, P->npy);
+    const double2 *W = axis == 0 ? P->Wx : P->Wy, *Q = axis == 0 ? P->Qx : P->Qy;
+    const size_t lds = (size_t)n * sizeof(double2);
+    const unsigned g = (nrows + 1) / 2;
+    hipStream_t st = ctx->stream;
+#define DCT2_L(M, B) k_dct2<M, B><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0)
+    if (P->big) {
+        if (mode == 0) DCT2_L(0, 1); else if (mode == 1) DCT2_L(1, 1); else DCT2_L(2, 1);
+    } else {
+        if (mode == 0) DCT2_L(0, 0); else if (mode == 1) DCT2_L(1, 0); else DCT2_L(2, 0);
+    }
+#undef DCT2_L
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+// the caller's eigenvalues (eig = lam_x[None, :] + lam_y[:, None] of mac.py:104-115)
+int dct2_set_lambda(rmt_ctx *ctx, const double *lamx, const double *lamy) {
+    Dct2Plan *P = ctx->dct2;
+    RMT_CHECK(P, RMT_EINVAL, "dct2_set_lambda: no plan");
+    RMT_HIP(hipMemcpyAsync(P->lamx, lamx, P->nx * 8, hipMemcpyHostToDevice, ctx->stream));
+    RMT_HIP(hipMemcpyAsync(P->lamy, lamy, P->ny * 8, hipMemcpyHostToDevice, ctx->stream));
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    P->dx = P->dy = -1.0;   // next dct2_plan call recomputes the reference's own values
+    return RMT_OK;
+}
+
+// mac.py:118-123: p = D^-1 (D rhs / eig), (0,0) -> 0; rhs and p are (ny, nx), may alias
+int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p) {
+    Dct2Plan *P = ctx->dct2;
+    RMT_CHECK(P, RMT_EINVAL, "dct2_solve: no plan");
+    const int ny = P->ny, nx = P->nx;
+    RMT_TRY(dct2_pass(ctx, 0, 0, rhs, p, ny, 0));
+    transpose(ctx->stream, p, ny, nx, P->T);
+    RMT_TRY(dct2_pass(ctx, 1, 1, P->T, P->T, nx, 0));
+    transpose(ctx->stream, P->T, nx, ny, p);
+    return dct2_pass(ctx, 2, 0, p, p, ny, 0);
+}
 }  // namespace rmt

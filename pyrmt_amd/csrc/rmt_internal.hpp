@@ -41,7 +41,8 @@ void set_error(const std::string &msg);
 #define RMT_TRY(expr)                                                                   \
     do { int s_ = (expr); if (s_ != RMT_OK) return s_; } while (0)
 
-struct DctPlan;  // poisson.hip
+struct DctPlan;   // poisson.hip (DCT-I, collocated grid)
+struct Dct2Plan;  // poisson.hip (DCT-II, MAC grid)
 
 }  // namespace rmt
 
@@ -57,6 +58,7 @@ struct rmt_ctx {
     unsigned char *bytes = nullptr;
     size_t bytes_len = 0;
     rmt::DctPlan *dct = nullptr;
+    rmt::Dct2Plan *dct2 = nullptr;
     // optional kernel timers (rmt_sim profiling): [0,1] around the four RK4 stage kernels,
     // [2,3] around the extrapolation sweep kernel
     bool prof = false;
@@ -318,6 +320,11 @@ int diag_rows(rmt_ctx *ctx, const double *phi, const double *J, const double *xs
               const double *X2, const rmt_sim_params &P, int jb, int je, double *part,
               double *out);
 
+int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
+                const double *b, const double *xs, const double *ys, double dt, double dx,
+                double dy, double x0, double y0, double R, double *X1n, double *X2n,
+                double *phi_pre, int *bad);
+
 // --------------------------------------------------------------------- momentum --
 constexpr int MOM_WORK_PLANES = 13;
 struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + flag
@@ -342,6 +349,11 @@ bool dct_lds_ready(rmt_ctx *ctx);
 int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
              int row0, double scale);
 void transpose(hipStream_t st, const double *in, int R, int C, double *out);
+// MAC grid (mac.py:104-123): DCT-II Neumann solve on a (ny, nx) cell grid, (0,0) -> 0
+int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);
+int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p);
+int dct2_set_lambda(rmt_ctx *ctx, const double *lamx, const double *lamy);
+void dct2_destroy(Dct2Plan *P);
 void dct_destroy(DctPlan *);
 
 // ------------------------------------------------------------------ extrapolate --

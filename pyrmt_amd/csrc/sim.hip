@@ -192,6 +192,19 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p2(const double *__restrict__ p
     if (threadIdx.x < DIAG_VALS) out[threadIdx.x] = s[threadIdx.x][0];
 }
 
+// k_sim_sl for other drivers (mac.hip: one disc's map on the MAC cell-centre velocity)
+int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
+                const double *b, const double *xs, const double *ys, double dt, double dx,
+                double dy, double x0, double y0, double R, double *X1n, double *X2n,
+                double *phi_pre, int *bad) {
+    const long n = (long)ctx->ny * ctx->nx;
+    k_sim_sl<<<grid1d(n, 256), 256, 0, ctx->stream>>>(X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt,
+                                                      dx, dy, RMT_SHAPE_DISC, x0, y0, R, X1n,
+                                                      X2n, phi_pre, bad);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
 // slab-decomposed step: the 10 diagnostic partials of rows [jb, je) into out (device)
 int diag_rows(rmt_ctx *ctx, const double *phi, const double *J, const double *xs,
               const double *ys, const double *u, const double *v, const double *X1,

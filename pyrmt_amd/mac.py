@@ -1,0 +1,218 @@
+"""Staggered (MAC) operators of pyRMT/mac.py and the config-5 loop body on MI355X.
+
+Same names, arguments and return values as the reference module (mac.py:22-139,
+196-232, 729-749); the arrays go through librmt's HIP kernels (include/rmt.h, rmt_mac_*).
+Layout as the reference: p / phi (Ny, Nx) cell centres, u (Ny, Nx+1) x-faces,
+v (Ny+1, Nx) y-faces (square grids: Nx == Ny).  ``MacMultiDisc`` is the device-resident
+loop body of benchmarks/mac_multi_disc_lid.py:36-98 (K soft discs with pair contact).
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib as L
+from .functions import _IO, _p, ctx_for, extrapolate_reference_map
+from .simulation import _wrap_device
+
+
+def mac_grid(Nx, Ny, Lx=1.0, Ly=1.0):
+    """mac.py:22-23."""
+    return Lx / Nx, Ly / Ny
+
+
+def poisson_eigs_neumann(Nx, Ny, dx, dy):
+    """mac.py:104-115 (setup, host): DCT-II symbol, (0,0) pinned to 1."""
+    lx = -2.0 * (1.0 - np.cos(np.pi * np.arange(Nx) / Nx)) / dx ** 2
+    ly = -2.0 * (1.0 - np.cos(np.pi * np.arange(Ny) / Ny)) / dy ** 2
+    eig = (lx[np.newaxis, :] + ly[:, np.newaxis]).copy()
+    eig[0, 0] = 1.0
+    return eig
+
+
+def _axis_eigs(eig):
+    """Per-axis eigenvalues of a separable eig table (row 0 and column 0; the reference's
+    lam[0] is -0.0, so eig[0, k] == lam_x[k] exactly).  Raises if eig is not separable."""
+    eig = np.asarray(eig, dtype=np.float64)
+    lx = eig[0, :].copy(); ly = eig[:, 0].copy()
+    lx[0] = ly[0] = -0.0
+    chk = lx[np.newaxis, :] + ly[:, np.newaxis]
+    chk[0, 0] = eig[0, 0]
+    if not np.array_equal(chk, eig):
+        raise NotImplementedError("eig is not a separable per-axis symbol (DCT-II solve)")
+    return np.ascontiguousarray(lx), np.ascontiguousarray(ly)
+
+
+def _ctx(N):
+    return ctx_for(N, N).bind()
+
+
+def divergence(u, v, dx, dy):
+    """mac.py:81-84."""
+    io = _IO(u, v); u = io.dev(u); v = io.dev(v)
+    N = u.shape[0]
+    out = io.empty((N, N))
+    L.check(L.lib().rmt_mac_divergence(_ctx(N), _p(u), _p(v), dx, dy, _p(out)), "divergence")
+    return io.out(out)
+
+
+def _gradients(p, dx, dy):
+    io = _IO(p); p = io.dev(p)
+    N = p.shape[0]
+    gu = io.empty((N, N + 1)); gv = io.empty((N + 1, N))
+    L.check(L.lib().rmt_mac_gradient_p(_ctx(N), _p(p), dx, dy, _p(gu), _p(gv)), "gradient_p")
+    return io, gu, gv
+
+
+def gradient_p_u(p, dx):
+    """mac.py:87-93."""
+    io, gu, _ = _gradients(p, dx, dx)
+    return io.out(gu)
+
+
+def gradient_p_v(p, dy):
+    """mac.py:96-101."""
+    io, _, gv = _gradients(p, dy, dy)
+    return io.out(gv)
+
+
+def solve_poisson_neumann(rhs, eig):
+    """mac.py:118-123 (orthonormal DCT-II both ways, constant mode zeroed)."""
+    lx, ly = _axis_eigs(eig)
+    io = _IO(rhs); r = io.dev(rhs)
+    N = r.shape[0]
+    out = io.empty((N, N))
+    L.check(L.lib().rmt_mac_solve_poisson_neumann(
+        _ctx(N), _p(r), 1.0 / N, 1.0 / N, lx.ctypes.data_as(ctypes.c_void_p),
+        ly.ctypes.data_as(ctypes.c_void_p), _p(out)), "solve_poisson_neumann")
+    return io.out(out)
+
+
+def project(u_star, v_star, dx, dy, dt, rho, eig):
+    """mac.py:126-139: returns (u, v, phi)."""
+    lx, ly = _axis_eigs(eig)
+    io = _IO(u_star, v_star); us = io.dev(u_star); vs = io.dev(v_star)
+    N = us.shape[0]
+    u = io.empty(us.shape); v = io.empty(vs.shape); phi = io.empty((N, N))
+    L.check(L.lib().rmt_mac_project(_ctx(N), _p(us), _p(vs), dx, dy, dt, float(rho),
+                                    lx.ctypes.data_as(ctypes.c_void_p),
+                                    ly.ctypes.data_as(ctypes.c_void_p), _p(u), _p(v), _p(phi)),
+            "project")
+    return io.out(u), io.out(v), io.out(phi)
+
+
+def momentum_predictor(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0):
+    """mac.py:196-232."""
+    if (fu is None) != (fv is None):
+        raise NotImplementedError("momentum_predictor: give both face forces or neither")
+    io = _IO(u, v); ud = io.dev(u); vd = io.dev(v)
+    fud, fvd = io.dev(fu), io.dev(fv)
+    us = io.empty(ud.shape); vs = io.empty(vd.shape)
+    L.check(L.lib().rmt_mac_momentum_predictor(_ctx(ud.shape[0]), _p(ud), _p(vd), nu, dx, dy,
+                                               dt, U_lid, _p(fud), _p(fvd), float(rho), _p(us),
+                                               _p(vs)), "momentum_predictor")
+    return io.out(us), io.out(vs)
+
+
+def contact_stress(phi_a, phi_b, eta, Gsum, eps, dx, dy):
+    """mac.py:729-749: (txx, txy, tyy)."""
+    io = _IO(phi_a, phi_b); a = io.dev(phi_a); b = io.dev(phi_b)
+    out = [io.empty(a.shape) for _ in range(3)]
+    L.check(L.lib().rmt_mac_contact_stress(_ctx(a.shape[0]), _p(a), _p(b), eta, Gsum, eps, dx,
+                                           dy, *map(_p, out)), "contact_stress")
+    return tuple(io.out(t) for t in out)
+
+
+# ------------------------------------------------------------------ config 5 loop --
+def place_discs(n, seed, Rrange=(0.07, 0.12), box=(0.18, 0.82)):
+    """mac_multi_disc_lid.py:22-33 (setup, host): non-overlapping random discs (R, cx, cy)."""
+    rng = np.random.default_rng(seed)
+    discs = []
+    for _ in range(2000):
+        if len(discs) == n:
+            break
+        R = rng.uniform(*Rrange)
+        cx = rng.uniform(box[0] + R, box[1] - R); cy = rng.uniform(box[0] + R, box[1] - R)
+        if all((cx - d[1]) ** 2 + (cy - d[2]) ** 2 > (R + d[0] + 0.03) ** 2 for d in discs):
+            discs.append((R, cx, cy))
+    return discs
+
+
+class MacMultiDisc:
+    """benchmarks/mac_multi_disc_lid.py:36-98 on the GPU (rmt_mac_sim_*): state (u, v, p and
+    every disc's X1, X2, phi) stays in HBM; one host sync per step reads the diagnostics."""
+
+    FIELDS = {"u": 0, "v": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5}
+
+    def __init__(self, N=128, n_discs=3, seed=3, U_lid=1.0, mu_s=0.3, mu_f=0.01, rho=1.0,
+                 eta=2.0, specs=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("pyrmt_amd needs a visible MI355X")
+        self.torch, self.N = torch, N
+        dx, dy = mac_grid(N, N)
+        self.dx = dx
+        self.specs = list(specs) if specs is not None else place_discs(n_discs, seed)
+        if not 1 <= len(self.specs) <= 8:
+            raise ValueError("1..8 discs")
+        cs = np.sqrt(mu_s / rho)
+        self.dt = min(0.3 * dx / U_lid, 0.2 * dx * dx / (mu_f / rho), 0.3 * dx / (cs + 1e-9))
+        P = L.rmt_mac_params()
+        P.N = N; P.dx = dx; P.n_discs = len(self.specs)
+        for k, (R, cx, cy) in enumerate(self.specs):
+            P.R[k], P.cx[k], P.cy[k] = R, cx, cy
+        P.U_lid, P.mu_s, P.mu_f, P.rho, P.eta = U_lid, mu_s, mu_f, rho, eta
+        P.layers = 3
+        P.dt = float(self.dt)
+        self.ctx = ctx_for(N, N)
+        h = ctypes.c_void_p()
+        L.check(L.lib().rmt_mac_sim_create(self.ctx.bind(), ctypes.byref(P), ctypes.byref(h)),
+                "rmt_mac_sim_create")
+        self.h, self.params = h, P
+        self._views = {}
+        # initial maps (mac_multi_disc_lid.py:51-56): xi = x_c * mask, then extrapolated
+        xc = (np.arange(N) + 0.5) * dx
+        Xc, Yc = np.meshgrid(xc, xc)
+        for k, (R, cx, cy) in enumerate(self.specs):
+            phi = np.sqrt((Xc - cx) ** 2 + (Yc - cy) ** 2) - R
+            m = (phi <= 0).astype(float)
+            X1, X2 = extrapolate_reference_map(Xc * m, Yc * m, phi, dx, dy, 3)
+            self.field("X1", k).copy_(torch.as_tensor(X1))
+            self.field("X2", k).copy_(torch.as_tensor(X2))
+            self.field("phi", k).copy_(torch.as_tensor(np.sqrt((X1 - cx) ** 2 + (X2 - cy) ** 2) - R))
+
+    def __del__(self):
+        try:
+            L.lib().rmt_mac_sim_destroy(self.h)
+        except Exception:
+            pass
+
+    def field(self, name, disc=0):
+        key = (name, disc if name in ("X1", "X2", "phi") else 0)
+        if key not in self._views:
+            ptr = ctypes.c_void_p()
+            L.check(L.lib().rmt_mac_sim_field(self.h, self.FIELDS[name], key[1], ctypes.byref(ptr)))
+            N = self.N
+            shape = {"u": (N, N + 1), "v": (N + 1, N)}.get(name, (N, N))
+            self._views[key] = _wrap_device(self.torch, ptr.value, shape)
+        return self._views[key]
+
+    def get(self, name, disc=0):
+        self.torch.cuda.synchronize()
+        return self.field(name, disc).cpu().numpy()
+
+    def step(self, nsteps=1, t_end=math.inf):
+        self.ctx.bind()
+        L.check(L.lib().rmt_mac_sim_step(self.h, int(nsteps), float(t_end)), "rmt_mac_sim_step")
+
+    def diagnostics(self):
+        n = ctypes.c_int()
+        L.check(L.lib().rmt_mac_sim_diagnostics(self.h, None, 0, ctypes.byref(n)))
+        buf = (L.rmt_mac_diag * max(n.value, 1))()
+        L.check(L.lib().rmt_mac_sim_diagnostics(self.h, buf, n.value, ctypes.byref(n)))
+        K = len(self.specs)
+        out = {k: np.array([getattr(buf[i], k) for i in range(n.value)])
+               for k in ("t", "dt", "minJ", "maxJ", "umax")}
+        out["cx"] = np.array([[buf[i].cx[k] for k in range(K)] for i in range(n.value)])
+        out["cy"] = np.array([[buf[i].cy[k] for k in range(K)] for i in range(n.value)])
+        return out

@@ -1,0 +1,96 @@
+"""GPU parity of the MAC path (config 5): pyrmt_amd.mac (librmt rmt_mac_*) against the
+reference's fixtures (tests/golden/mac_ops.npz, mac_trace.npz) and the oracle.
+
+Bars: bit-exact for the predictor, divergence, face gradients and contact stress (IEEE
+arithmetic in the reference's order); the DCT-II projection to 1e-12 relative (FFT
+rounding differs from pocketfft's) and machine-zero divergence (tests/test_mac.py:97-113);
+the 8-step multi-disc loop at N=64 to 1e-9 (centroids, J range, fields).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def M(gpu):
+    from pyrmt_amd import mac
+    return mac
+
+
+def test_mac_predictor_bitwise(M):
+    g = golden("mac_ops")
+    dx, dy = float(g["dx"]), float(g["dy"])
+    us, vs = M.momentum_predictor(g["u"], g["v"], 0.01, dx, dy, 1e-3, 1.0, fu=g["fu"],
+                                  fv=g["fv"], rho=1.0)
+    np.testing.assert_array_equal(us, g["us"])
+    np.testing.assert_array_equal(vs, g["vs"])
+
+
+def test_mac_contact_stress_bitwise(M):
+    g = golden("mac_ops")
+    dx, dy = float(g["dx"]), float(g["dy"])
+    for a, b in zip(M.contact_stress(g["pa"], g["pb"], 2.0, 0.6, 3 * dx, dx, dy),
+                    (g["txx"], g["txy"], g["tyy"])):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_mac_divergence_gradient_bitwise(M, oracle):
+    from oracle import mac_oracle as MO
+    g = golden("mac_ops")
+    dx, dy = float(g["dx"]), float(g["dy"])
+    np.testing.assert_array_equal(M.divergence(g["us"], g["vs"], dx, dy),
+                                  MO.divergence(g["us"], g["vs"], dx, dy))
+    np.testing.assert_array_equal(M.gradient_p_u(g["pp"], dx), MO.gradient_p_u(g["pp"], dx))
+    np.testing.assert_array_equal(M.gradient_p_v(g["pp"], dy), MO.gradient_p_v(g["pp"], dy))
+
+
+def test_mac_projection(M):
+    g = golden("mac_ops")
+    N, dx, dy = int(g["N"]), float(g["dx"]), float(g["dy"])
+    eig = M.poisson_eigs_neumann(N, N, dx, dy)
+    u, v, phi = M.project(g["us"], g["vs"], dx, dy, 1e-3, 1.0, eig)
+    sc = np.abs(g["pp"]).max()
+    np.testing.assert_allclose(phi, g["pp"], rtol=0, atol=1e-12 * sc)
+    np.testing.assert_allclose(u, g["pu"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(v, g["pv"], rtol=0, atol=1e-12)
+    # the headline property of mac.py: machine-zero divergence after the projection
+    assert np.abs(M.divergence(u, v, dx, dy)).max() < 1e-9
+
+
+@pytest.mark.parametrize("N", [64, 256, 1024])
+def test_mac_poisson_roundtrip(M, N):
+    """tests/test_mac.py:82-95: solve(lap(p)) == p - mean(p), through the DCT-II solve."""
+    from oracle import mac_oracle as MO
+    dx = dy = 1.0 / N
+    rng = np.random.default_rng(N)
+    p = rng.standard_normal((N, N))
+    eig = M.poisson_eigs_neumann(N, N, dx, dy)
+    rhs = MO.divergence(MO.gradient_p_u(p, dx), MO.gradient_p_v(p, dy), dx, dy)
+    got = M.solve_poisson_neumann(rhs, eig)
+    np.testing.assert_allclose(got, p - p.mean(), rtol=0, atol=1e-9)
+    ref = MO.solve_poisson_neumann(rhs, eig)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-11)
+
+
+def test_mac_multi_disc_trace(M):
+    """mac_multi_disc_lid.py loop body, N=64, 3 discs (seed 3), 8 steps vs the reference."""
+    g = golden("mac_trace")
+    N, K = int(g["N"]), int(g["nsteps"])
+    sim = M.MacMultiDisc(N, n_discs=3, seed=3)
+    np.testing.assert_array_equal(np.array(sim.specs), g["specs"])
+    assert sim.dt == float(g["dt"])
+    np.testing.assert_array_equal(sim.get("X1", 0), g["X1_0"])
+    sim.step(K)
+    d = sim.diagnostics()
+    np.testing.assert_allclose(d["cx"], g["cx"], rtol=1e-10)
+    np.testing.assert_allclose(d["cy"], g["cy"], rtol=1e-10)
+    np.testing.assert_allclose(d["minJ"], g["minJ"], rtol=1e-9)
+    np.testing.assert_allclose(d["maxJ"], g["maxJ"], rtol=1e-9)
+    np.testing.assert_allclose(sim.get("u"), g["u"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(sim.get("v"), g["v"], rtol=0, atol=1e-9)
+    for k in range(3):
+        np.testing.assert_allclose(sim.get("X1", k), g[f"X1_{k}_end"], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(sim.get("X2", k), g[f"X2_{k}_end"], rtol=0, atol=1e-9)
