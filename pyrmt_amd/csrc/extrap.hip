@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits
                                                    unsigned char *__restrict__ rowcand,
                                                    int *__restrict__ jrange,
                                                    const int *__restrict__ ctl) {
-    if (ctl && !ctl[EXC_FALLBACK]) return;   // the chain path handled this call
+    if (ctl && (!ctl[EXC_FALLBACK] || ctl[EXC_NOOP])) return;   // chain path / no-op call
     const long t = blockIdx.x * 256L + threadIdx.x;
     if (t >= (long)ny * W) return;
     const int j = (int)(t / W), w = (int)(t % W);
@@ -107,6 +107,84 @@ __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits
         atomicMin(&jrange[0], j);
         atomicMax(&jrange[1], j);
     }
+}
+
+// k_ex_none: can ANY first-layer target be accepted when it sees only the original known
+// set?  If not, none is accepted in the serial order either (by induction: the first target
+// sees exactly that set, is rejected, so the next sees it too ...), the known set never
+// grows, every later layer has the same targets and the same fits, and the whole call is
+// the identity -- exactly (functions.py:95-161).  This is the N = 8192 case of config 5,
+// where det(Aw) ~ 1e-14 < 1e-10 for every fit.  One wave per row;
+// the window sums keep the reference's order (raster within the clipped 9x9 window).
+__global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, int ny, int nx,
+                                                 int W, double dx, double dy, double r2,
+                                                 int *__restrict__ ctl) {
+    __shared__ double tb[4][6][96];
+    __shared__ u64 tab[256];
+    for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int j = blockIdx.x * 4 + wv;
+    if (j < 1 || j > ny - 2) return;
+    double (*t)[96] = tb[wv];
+    auto K = [&](int jj, int w) -> u64 {
+        return (jj < 0 || jj >= ny || w < 0 || w >= W) ? 0 : kbits[(long)jj * W + w];
+    };
+    for (int w0 = 0; w0 < W; ++w0) {
+        if (__hip_atomic_load(ctl + EXC_ANY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        u64 d = 0;
+        for (int jj = j - 1; jj <= j + 1; ++jj) {
+            const u64 a = K(jj, w0 - 1), b = K(jj, w0), e = K(jj, w0 + 1);
+            d |= b | (b << 1) | (a >> 63) | (b >> 1) | (e << 63);
+        }
+        const int i0 = 64 * w0, lo = max(1, i0) - i0, hi = min(nx - 2, i0 + 63) - i0;
+        if (hi < lo) continue;
+        u64 cand = d & ~K(j, w0) & (~0ull >> (63 - hi)) & (~0ull << lo);
+        while (cand) {
+            const int i = i0 + __builtin_ctzll(cand);
+            cand &= cand - 1;
+            const double x0 = dx * i, y0 = dy * j;
+            int inc_n = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
+                bool inc = false;
+                double xi = 0.0, yi = 0.0, w = 0.0;
+                if (q < EX_WIN && jj >= 0 && jj < ny && ii >= 0 && ii < nx &&
+                    ((K(jj, ii >> 6) >> (ii & 63)) & 1)) {
+                    xi = dx * ii; yi = dy * jj;
+                    const double ax = xi - x0, ay = yi - y0, d2 = ax * ax + ay * ay;
+                    if (d2 <= r2) { inc = true; w = exp_glibc_tab(-d2 / r2, tab); }
+                }
+                inc_n += __popcll(__ballot(inc));
+                if (q < 96) {
+                    const double wa0 = w * 1.0, wa1 = w * xi, wa2 = w * yi;
+                    t[0][q] = inc ? wa0 * 1.0 : 0.0;  t[1][q] = inc ? wa0 * xi : 0.0;
+                    t[2][q] = inc ? wa0 * yi : 0.0;   t[3][q] = inc ? wa1 * xi : 0.0;
+                    t[4][q] = inc ? wa1 * yi : 0.0;   t[5][q] = inc ? wa2 * yi : 0.0;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            double acc = 0.0;
+            if (lane < 6)
+                for (int q = 0; q < EX_WIN; ++q) acc += t[lane][q];
+            __builtin_amdgcn_wave_barrier();
+            const double A00 = __shfl(acc, 0), A01 = __shfl(acc, 1), A02 = __shfl(acc, 2);
+            const double A11 = __shfl(acc, 3), A12 = __shfl(acc, 4), A22 = __shfl(acc, 5);
+            const double M[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
+            const double det = (M[0] * (M[4] * M[8] - M[5] * M[7])
+                              - M[1] * (M[3] * M[8] - M[5] * M[6])
+                              + M[2] * (M[3] * M[7] - M[4] * M[6]));
+            if (inc_n >= 3 && fabs(det) > 1e-10) {
+                if (lane == 0) atomicOr(ctl + EXC_ANY, 1);
+                return;
+            }
+        }
+    }
+}
+__global__ void k_ex_none_fin(int *ctl) {
+    if (!ctl[EXC_ANY]) { ctl[EXC_FALLBACK] = 1; ctl[EXC_NOOP] = 1; }
 }
 
 __device__ __forceinline__ u64 ld_sc1_u64(const u64 *p) {
@@ -367,7 +445,7 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A, long long *gpr
     __shared__ __attribute__((aligned(16))) double term[EXW][12 * EXS];
     __shared__ u64 tab[256];
     __shared__ int s_ticket, s_abort;
-    if (A.ctl && !A.ctl[EXC_FALLBACK]) return;   // the chain path handled this call
+    if (A.ctl && (!A.ctl[EXC_FALLBACK] || A.ctl[EXC_NOOP])) return;   // chain path / no-op
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int s = threadIdx.x; s < EX_RING; s += blockDim.x)
         ring[s] = ((u64)(unsigned)(s - EX_RING) << 32) | EX_DONE;   // virtual done tickets
@@ -552,6 +630,12 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
             RMT_HIP(hipMemcpyAsync(ws.ctl + EXC_FALLBACK, &one, sizeof(int),
                                    hipMemcpyHostToDevice, ctx->stream));
         }
+        // exact shortcut: no target can be accepted -> identity (k_ex_none)
+        const double r = 4 * std::sqrt(dx * dx + dy * dy);
+        k_ex_none<<<grid1d(ny, 4), 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, dx, dy, r * r,
+                                                           ws.ctl);
+        k_ex_none_fin<<<1, 1, 0, ctx->stream>>>(ws.ctl);
+        RMT_LAUNCHED();
         RMT_TRY(extrap_chain_launch(ctx, ws, X1o, X2o, dx, dy, max_layers));
     }
     const int *ctl = chain ? ws.ctl : nullptr;
@@ -613,12 +697,14 @@ extern "C" int rmt_extrap_last_path(rmt_ctx *ctx, int *path) {
     RMT_CHECK(ctx && path, RMT_EINVAL, "null argument");
     RMT_CHECK(ctx->bytes, RMT_EINVAL, "no extrapolation has run on this context");
     const rmt::ExWs ws = rmt::extrap_layout(ctx->bytes, ctx->ny, ctx->nx, ctx->ex_layers, nullptr);
-    int fb = 1;
+    int fb[2] = {1, 0};   // EXC_FALLBACK, EXC_NOOP
     if (ctx->ex_chain) {
-        RMT_HIP(hipMemcpyAsync(&fb, ws.ctl + rmt::EXC_FALLBACK, sizeof(int),
+        RMT_HIP(hipMemcpyAsync(&fb[0], ws.ctl + rmt::EXC_FALLBACK, sizeof(int),
+                               hipMemcpyDeviceToHost, ctx->stream));
+        RMT_HIP(hipMemcpyAsync(&fb[1], ws.ctl + rmt::EXC_NOOP, sizeof(int),
                                hipMemcpyDeviceToHost, ctx->stream));
         RMT_HIP(hipStreamSynchronize(ctx->stream));
     }
-    *path = fb ? 1 : 0;
+    *path = fb[1] ? 2 : fb[0] ? 1 : 0;
     return RMT_OK;
 }

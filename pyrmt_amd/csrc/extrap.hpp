@@ -18,8 +18,10 @@ constexpr int EX_MAXREJ = 4096;     // rejected fits per layer the fix-up handle
 constexpr int EX_DCAP = 8192;       // fix-up dirty-list capacity
 
 // ctl words (int): fallback flag, abort flag, accepted count, and 64-bit arena cursor
+// EXC_ANY / EXC_NOOP: k_ex_none's proof that no target can be accepted (both paths skip)
 enum { EXC_FALLBACK = 0, EXC_ABORT = 1, EXC_FILLED = 2, EXC_ARENA = 4, EXC_REJ = 8,
-       EXC_BASE = 8 + EX_MAXL, EXC_WORDS = 8 + 2 * EX_MAXL + 8 };
+       EXC_BASE = 8 + EX_MAXL, EXC_ANY = 8 + 2 * EX_MAXL, EXC_NOOP = EXC_ANY + 1,
+       EXC_WORDS = 8 + 2 * EX_MAXL + 8 };
 
 struct ExWs {
     // band detection (both paths) and the fallback sweep

@@ -101,13 +101,14 @@ def _extrap_case(name):
                       "discs3": (700, 640, 2), "rect_l1": (200, 300, 1),
                       "rect_l6": (200, 300, 6), "wide": (96, 4500, 3),
                       "corner": (257, 257, 3), "empty": (64, 80, 3), "full": (64, 80, 3),
+                      "tiny": (96, 96, 3),
                       "disc4096": (4096, 4096, 3)}[name]
     x = np.linspace(0.0, 1.0, nx); y = np.linspace(0.0, 1.0, ny)
     X, Y = np.meshgrid(x, y)
     X1 = X + 0.05 * np.sin(2 * np.pi * Y) * np.cos(np.pi * X)
     X2 = Y + 0.03 * np.sin(2 * np.pi * X)
     disc = lambda cx, cy, R: np.sqrt((X1 - cx) ** 2 + (X2 - cy) ** 2) - R
-    if name in ("disc1024", "disc4096", "rect_l1", "rect_l6", "wide"):
+    if name in ("disc1024", "disc4096", "rect_l1", "rect_l6", "wide", "tiny"):
         phi = disc(0.6, 0.5, 0.2)
     elif name == "slab":
         phi = X2 - 0.4 - 0.02 * np.sin(6 * X1)
@@ -120,15 +121,19 @@ def _extrap_case(name):
     else:
         phi = -np.ones((ny, nx))
     solid = (phi < 0).astype(float)
+    if name == "tiny":   # the spacing of N = 8192: det(Aw) < 1e-10 for every fit (config 5)
+        return X1 * solid, X2 * solid, phi, 1.0 / 8192, 1.0 / 8192, layers
     return X1 * solid, X2 * solid, phi, 1.0 / (nx - 1), 1.0 / (ny - 1), layers
 
 
 # cases the chain path must take itself (the others exceed its ring distance and fall back)
-_CHAIN_CASES = {"disc1024", "discs3", "rect_l1", "rect_l6", "corner", "empty", "full", "disc4096"}
+_CHAIN_CASES = {"disc1024", "discs3", "rect_l1", "rect_l6", "corner", "disc4096"}
+# cases where no fit can be accepted: k_ex_none proves the call is the identity (path 2)
+_NOOP_CASES = {"empty", "full", "tiny"}
 
 
 @pytest.mark.parametrize("name", ["disc1024", "slab", "discs3", "rect_l1", "rect_l6", "wide",
-                                  "corner", "empty", "full", "disc4096"])
+                                  "corner", "empty", "full", "tiny", "disc4096"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_extrapolation_vs_oracle(gpu, oracle, name, mode):
     """Both extrapolation paths reproduce the serial raster-order chain bit for bit, at the
@@ -145,7 +150,10 @@ def test_extrapolation_vs_oracle(gpu, oracle, name, mode):
     _eq(g1, r1); _eq(g2, r2)
     if mode == 0 and name in _CHAIN_CASES:
         assert path == 0, "chain path fell back"
-    if mode != 0:
+    if mode != 1 and name in _NOOP_CASES:
+        assert path == 2, "no-op proof not taken"
+        _eq(g1, X1); _eq(g2, X2)
+    elif mode != 0:
         assert path == 1
 
 
