@@ -43,7 +43,8 @@ typedef enum {
 typedef enum {
     RMT_BC_NONE = 0,          /* identity                                            */
     RMT_BC_NOSLIP_LID = 1,    /* no_slip_lid_bc: walls 0, top row u = lid, corners 0  */
-    RMT_BC_FREESLIP_BOX = 2   /* free_slip_box_bc: normal 0, tangential copied        */
+    RMT_BC_FREESLIP_BOX = 2,  /* free_slip_box_bc: normal 0, tangential copied        */
+    RMT_BC_PERIODIC = 3       /* overlap grid: last column / row copy column / row 0  */
 } rmt_bc_kind;
 
 /* Reference-map advection schemes (functions.py:501-542). */
@@ -208,6 +209,23 @@ int rmt_sim_set_profiling(rmt_sim *sim, int on);
 int rmt_sim_phase_times(rmt_sim *sim, double *ms8, long *calls8);
 /* Copy the diagnostics of all completed steps since creation (blocks). */
 int rmt_sim_diagnostics(rmt_sim *sim, rmt_diag *out, int max_records, int *n_records);
+
+/* ---- periodic branch (functions.py:1177-1290; tests/test_poisson.py:24-78) -----------
+ * Overlap grid (x[-1] == x[0]): operators on the reduced (N-1)^2 sub-grid, tiled back.
+ * lamx / lamy: HOST per-axis symbols -(sin(2 pi k / m) / h)^2, length m = N - 1. */
+int rmt_divergence_periodic(rmt_ctx *ctx, const double *a, const double *b, double dx, double dy,
+                            double *divU);                           /* functions.py:1236 */
+int rmt_pressure_gradient_periodic(rmt_ctx *ctx, const double *p, double dx, double dy,
+                                   double *gx, double *gy);          /* functions.py:1246 */
+int rmt_solve_poisson_fft(rmt_ctx *ctx, const double *rhs, const double *lamx,
+                          const double *lamy, double *p);            /* functions.py:1216 */
+/* pressure_projection_amg(bc_type='periodic') (functions.py:1277-1290): rho_bar = mean rho
+ * in the Poisson rhs; rho_cells (device, nullable) the local density of the correction */
+int rmt_pressure_projection_periodic(rmt_ctx *ctx, const double *a_star, const double *b_star,
+                                     double dx, double dy, double dt, double rho_bar,
+                                     const double *rho_cells, int bc_kind, double lid,
+                                     const double *lamx, const double *lamy,
+                                     const double *p_prev, double *a, double *b, double *p);
 
 /* ---- slab-decomposed step (the fused step over G GPUs, 1D row slabs) ----
  * One rmt_slab = rows [r0, r1) of the global ny x nx grid (row_splits[rank] ..

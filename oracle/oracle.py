@@ -244,6 +244,66 @@ def pressure_projection(a_star, b_star, dx, dy, dt, rho, bc_kind, lid, p_prev, e
     return a, b, p
 
 
+# ── periodic branch (functions.py:1171-1252, 1277-1290): NumPy in the reference ─────
+def _precompute_poisson_eigenvalues_periodic(Nx, Ny, dx, dy):
+    mx, my = Nx - 1, Ny - 1
+    lx = -(np.sin(2.0 * np.pi * np.arange(mx) / mx) / dx) ** 2
+    ly = -(np.sin(2.0 * np.pi * np.arange(my) / my) / dy) ** 2
+    eig = lx[np.newaxis, :] + ly[:, np.newaxis]
+    null = np.abs(eig) < 1e-12
+    eig = eig.copy()
+    eig[null] = 1.0
+    return eig, null
+
+
+def _tile_overlap(red, Ny, Nx):
+    out = np.empty((Ny, Nx))
+    out[:-1, :-1] = red
+    out[-1, :-1] = red[0, :]
+    out[:-1, -1] = red[:, 0]
+    out[-1, -1] = red[0, 0]
+    return out
+
+
+def _solve_poisson_fft(rhs_full, eigenvalues_periodic):
+    eig, null = eigenvalues_periodic
+    Ny, Nx = rhs_full.shape
+    r = rhs_full[:-1, :-1].copy()
+    r -= np.mean(r)
+    h = np.fft.fft2(r) / eig
+    h[null] = 0.0
+    p = _tile_overlap(np.real(np.fft.ifft2(h)), Ny, Nx)
+    p -= np.mean(p)
+    return p
+
+
+def _wrap_d(f, axis, h):
+    return (np.roll(f, -1, axis=axis) - np.roll(f, 1, axis=axis)) / (2.0 * h)
+
+
+def _compute_divergence_periodic(a, b, dx, dy):
+    Ny, Nx = a.shape
+    return _tile_overlap(_wrap_d(a[:-1, :-1], 1, dx) + _wrap_d(b[:-1, :-1], 0, dy), Ny, Nx)
+
+
+def _compute_pressure_gradient_periodic(p, dx, dy):
+    Ny, Nx = p.shape
+    r = p[:-1, :-1]
+    return _tile_overlap(_wrap_d(r, 1, dx), Ny, Nx), _tile_overlap(_wrap_d(r, 0, dy), Ny, Nx)
+
+
+def pressure_projection_periodic(a_star, b_star, dx, dy, dt, rho, bc_kind, lid, p_prev, eig):
+    """functions.py:1277-1290 (bc_kind 3 = the overlap-grid periodic copy)."""
+    divU = _compute_divergence_periodic(a_star, b_star, dx, dy)
+    rho_bar = float(np.mean(rho)) if isinstance(rho, np.ndarray) else float(rho)
+    pc = _solve_poisson_fft(rho_bar * divU / dt, eig)
+    gx, gy = _compute_pressure_gradient_periodic(pc, dx, dy)
+    a, b = apply_bc(bc_kind, lid, a_star - (dt / rho) * gx, b_star - (dt / rho) * gy)
+    p = (p_prev + pc) if p_prev is not None else pc
+    p -= np.mean(p)
+    return a, b, p
+
+
 def compute_timestep(a, b, dx, dy, CFL, dt_min_cap, mu_s, rho_s, gamma, rho_f, mu_f=0.0,
                      eta_s=0.0, kappa=0.0):
     """functions.py:165-192."""

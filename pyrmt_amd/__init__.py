@@ -5,11 +5,13 @@ operators run as hand-written HIP kernels for gfx950 in librmt.so (include/rmt.h
 a device-resident fused step (pyrmt_amd.simulation) for the benchmark loop bodies.
 """
 from . import _lib
-from .bc import NoSlipLid, FreeSlipBox, Disc
+from .bc import NoSlipLid, FreeSlipBox, Periodic, Disc
 from .functions import *  # noqa: F401,F403  (the reference's operator names)
 from .functions import (_precompute_poisson_eigenvalues, _solve_poisson_dct,  # noqa: F401
                         _compute_divergence_rc, _compute_divergence, _compute_pressure_gradient,
-                        _weno5_rhs)
+                        _weno5_rhs, _precompute_poisson_eigenvalues_periodic,
+                        _tile_overlap, _solve_poisson_fft, _compute_divergence_periodic,
+                        _compute_pressure_gradient_periodic)
 from . import simulation
 from . import mac
 

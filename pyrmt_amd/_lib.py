@@ -97,6 +97,12 @@ SIGNATURES = {
     "rmt_sim_diagnostics": (_I, [_P, ctypes.POINTER(rmt_diag), _I, ctypes.POINTER(_I)]),
     "rmt_sim_set_profiling": (_I, [_P, _I]),
     "rmt_sim_phase_times": (_I, [_P, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
+    # periodic branch
+    "rmt_divergence_periodic": (_I, [_P, _P, _P, _D, _D, _P]),
+    "rmt_pressure_gradient_periodic": (_I, [_P, _P, _D, _D, _P, _P]),
+    "rmt_solve_poisson_fft": (_I, [_P, _P, _P, _P, _P]),
+    "rmt_pressure_projection_periodic": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _I, _D, _P, _P,
+                                              _P, _P, _P, _P]),
     # slab-decomposed step (distributed.py)
     "rmt_slab_create": (_I, [_P, ctypes.POINTER(rmt_sim_params), _I, _I, ctypes.POINTER(_I),
                              ctypes.POINTER(_I), ctypes.POINTER(_P)]),

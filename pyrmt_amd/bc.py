@@ -9,7 +9,7 @@ otherwise NotImplementedError is raised (no silent host path).
 """
 import numpy as np
 
-NONE, NOSLIP_LID, FREESLIP_BOX = 0, 1, 2
+NONE, NOSLIP_LID, FREESLIP_BOX, PERIODIC = 0, 1, 2, 3
 
 
 class VelocityBC:
@@ -29,6 +29,11 @@ class VelocityBC:
             v[:, 0] = v[:, 1]; v[:, -1] = v[:, -2]
             v[0, :] = 0.0; v[-1, :] = 0.0
             u[0, :] = u[1, :]; u[-1, :] = u[-2, :]
+        elif self.kind == PERIODIC:
+            for a in (u, v):
+                a[:, -1] = a[:, 0]
+            for a in (u, v):
+                a[-1, :] = a[0, :]
         return u, v
 
 
@@ -43,6 +48,11 @@ class NoSlipLid(VelocityBC):
 class FreeSlipBox(VelocityBC):
     """benchmarks/common.py:40-50 free_slip_box_bc(u, v)."""
     kind = FREESLIP_BOX
+
+
+class Periodic(VelocityBC):
+    """tests/test_poisson.py:57-61 _periodic_bc (overlap grid: last column / row wrap)."""
+    kind = PERIODIC
 
 
 class Identity(VelocityBC):
@@ -61,12 +71,12 @@ def resolve_bc(bc):
     ru, rv = bc(u.copy(), v.copy())
     ru = np.asarray(ru); rv = np.asarray(rv)
     lid = float(ru[-1, 4])
-    for cand in (NoSlipLid(lid), FreeSlipBox(), Identity()):
+    for cand in (NoSlipLid(lid), FreeSlipBox(), Periodic(), Identity()):
         cu, cv = cand(u, v)
         if np.array_equal(cu, ru) and np.array_equal(cv, rv):
             return cand.kind, cand.lid
     raise NotImplementedError(
-        "velocity_bc callable does not match no_slip_lid_bc / free_slip_box_bc; "
+        "velocity_bc callable does not match no_slip_lid_bc / free_slip_box_bc / periodic; "
         "pass a pyrmt_amd.bc descriptor")
 
 

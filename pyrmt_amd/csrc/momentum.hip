@@ -308,7 +308,7 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
                  const MomWork &W, const RowWin *win) {
     const int ny = ctx->ny, nx = ctx->nx;
     const long n = (long)ny * nx;
-    RMT_CHECK(P->bc_kind >= 0 && P->bc_kind <= 2, RMT_EINVAL, "unknown velocity bc kind");
+    RMT_CHECK(P->bc_kind >= 0 && P->bc_kind <= 3, RMT_EINVAL, "unknown velocity bc kind");
     // rows of each pass: the final u*, v* on [jb, je); stage s reads stage s-1 two rows out
     // (upwind3 / grad2 of the blended stress), the prep pass one more row
     const RowWin w0 = win ? *win : RowWin{0, ny, 0, ny};

@@ -465,6 +465,7 @@ int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (ctx->bytes) hipFree(ctx->bytes);
     if (ctx->dct) dct_destroy(ctx->dct);
     if (ctx->dct2) dct2_destroy(ctx->dct2);
+    if (ctx->per) per_destroy(ctx->per);
     delete ctx;
     return RMT_OK;
 }
@@ -557,7 +558,7 @@ int rmt_smoothed_heaviside(rmt_ctx *ctx, const double *x, long n, double w_t, do
     return RMT_OK;
 }
 int rmt_apply_velocity_bc(rmt_ctx *ctx, int bc_kind, double lid, double *u, double *v) {
-    RMT_CHECK(bc_kind >= 0 && bc_kind <= 2, RMT_EINVAL, "unknown velocity bc kind");
+    RMT_CHECK(bc_kind >= 0 && bc_kind <= 3, RMT_EINVAL, "unknown velocity bc kind");
     k_apply_bc<<<LAUNCH1D(N_CELLS)>>>(bc_kind, lid, u, v, ctx->ny, ctx->nx);
     RMT_LAUNCHED();
     return RMT_OK;
@@ -586,7 +587,7 @@ int rmt_solve_poisson_dct(rmt_ctx *ctx, const double *rhs, double dx, double dy,
 int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_star,
                             double dx, double dy, double dt, double rho, int bc_kind,
                             double lid, const double *p_prev, double *a, double *b, double *p) {
-    RMT_CHECK(bc_kind >= 0 && bc_kind <= 2, RMT_EINVAL, "unknown velocity bc kind");
+    RMT_CHECK(bc_kind >= 0 && bc_kind <= 3, RMT_EINVAL, "unknown velocity bc kind");
     long n = N_CELLS;
     RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
     double *rhs = ctx->scratch, *pc = rhs + n;

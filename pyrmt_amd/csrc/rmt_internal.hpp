@@ -43,6 +43,7 @@ void set_error(const std::string &msg);
 
 struct DctPlan;   // poisson.hip (DCT-I, collocated grid)
 struct Dct2Plan;  // poisson.hip (DCT-II, MAC grid)
+struct PerPlan;   // periodic.hip (reduced-grid 2D FFT)
 
 }  // namespace rmt
 
@@ -59,6 +60,7 @@ struct rmt_ctx {
     size_t bytes_len = 0;
     rmt::DctPlan *dct = nullptr;
     rmt::Dct2Plan *dct2 = nullptr;
+    rmt::PerPlan *per = nullptr;
     // optional kernel timers (rmt_sim profiling): [0,1] around the four RK4 stage kernels,
     // [2,3] around the extrapolation sweep kernel
     bool prof = false;
@@ -276,6 +278,9 @@ __device__ __forceinline__ BCSrc bc_source(int kind, double lid, int j, int i, i
             s.u_const = s.v_const = true;
             s.u_val = (j == ny - 1 && i != 0 && i != nx - 1) ? lid : 0.0;
         }
+    } else if (kind == RMT_BC_PERIODIC) {
+        // test_poisson.py _periodic_bc: last column <- column 0, then last row <- row 0
+        s.u_src = s.v_src = (long)(j == ny - 1 ? 0 : j) * nx + (i == nx - 1 ? 0 : i);
     } else if (kind == RMT_BC_FREESLIP_BOX) {
         if (i == 0 || i == nx - 1) s.u_const = true;
         else if (j == 0) s.u_src = c + nx;
@@ -354,6 +359,7 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);
 int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p);
 int dct2_set_lambda(rmt_ctx *ctx, const double *lamx, const double *lamy);
 void dct2_destroy(Dct2Plan *P);
+void per_destroy(PerPlan *P);
 void dct_destroy(DctPlan *);
 
 // ------------------------------------------------------------------ extrapolate --

@@ -229,7 +229,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     RMT_CHECK(prm->ny == ctx->ny && prm->nx == ctx->nx, RMT_EINVAL, "sim grid != ctx grid");
     RMT_CHECK(prm->scheme == RMT_SCHEME_SEMILAGRANGIAN || prm->scheme == RMT_SCHEME_WENO5,
               RMT_EINVAL, "unknown advection scheme");
-    RMT_CHECK(prm->bc_kind >= 0 && prm->bc_kind <= 2, RMT_EINVAL, "unknown bc kind");
+    RMT_CHECK(prm->bc_kind >= 0 && prm->bc_kind <= 3, RMT_EINVAL, "unknown bc kind");
     RMT_CHECK(prm->shape == RMT_SHAPE_NONE || prm->shape == RMT_SHAPE_DISC, RMT_EINVAL,
               "unknown shape");
     RMT_CHECK(prm->shape == RMT_SHAPE_NONE || prm->rho_s == prm->rho_f, RMT_ENOTSUP,

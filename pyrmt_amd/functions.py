@@ -341,10 +341,115 @@ def _solve_poisson_dct(rhs_2d, eigenvalues):
     return io.out(out)
 
 
+# ── periodic branch (functions.py:1171-1252, 1277-1290) ────────────────────────────
+def _periodic_axis(n, h):
+    m = n - 1
+    return -(np.sin(2.0 * np.pi * np.arange(m) / m) / h) ** 2
+
+
+def _precompute_poisson_eigenvalues_periodic(Nx, Ny, dx, dy):
+    """functions.py:1177-1202 (setup, host): (eig, null) on the reduced grid."""
+    eig = _periodic_axis(Nx, dx)[np.newaxis, :] + _periodic_axis(Ny, dy)[:, np.newaxis]
+    null = np.abs(eig) < 1e-12
+    eig = eig.copy()
+    eig[null] = 1.0
+    return eig, null
+
+
+def _periodic_axes_of(eigenvalues_periodic, dx=None, dy=None):
+    """Per-axis symbols behind an (eig, null) pair: recomputed from the grid spacing (given,
+    or recovered from eig[0, 1] / eig[1, 0] and nudged by ulps) and checked bit for bit."""
+    eig, null = (np.asarray(a) for a in eigenvalues_periodic)
+    my, mx = eig.shape
+
+    def cands(n, e):
+        h = float(np.sin(2.0 * np.pi / n) / np.sqrt(-e))
+        return [h] + [np.nextafter(h, np.inf), np.nextafter(h, -np.inf),
+                      np.nextafter(np.nextafter(h, np.inf), np.inf),
+                      np.nextafter(np.nextafter(h, -np.inf), -np.inf)]
+
+    hxs = [dx] if dx is not None else cands(mx, eig[0, 1])
+    hys = [dy] if dy is not None else cands(my, eig[1, 0])
+    for hx in hxs:
+        for hy in hys:
+            e2, n2 = _precompute_poisson_eigenvalues_periodic(mx + 1, my + 1, hx, hy)
+            if np.array_equal(e2, eig) and np.array_equal(n2, null):
+                return (np.ascontiguousarray(_periodic_axis(mx + 1, hx)),
+                        np.ascontiguousarray(_periodic_axis(my + 1, hy)))
+    raise NotImplementedError("eigenvalues are not the periodic symbol of a uniform grid")
+
+
+def _tile_overlap(field_reduced, Ny, Nx):
+    """functions.py:1205-1213 (host helper)."""
+    out = np.empty((Ny, Nx))
+    out[:-1, :-1] = field_reduced
+    out[-1, :-1] = field_reduced[0, :]
+    out[:-1, -1] = field_reduced[:, 0]
+    out[-1, -1] = field_reduced[0, 0]
+    return out
+
+
+def _solve_poisson_fft(rhs_full, eigenvalues_periodic):
+    """functions.py:1216-1233: reduced-grid 2D FFT solve, null modes zeroed."""
+    lx, ly = _periodic_axes_of(eigenvalues_periodic)
+    io = _IO(rhs_full); r = io.dev(rhs_full); out = io.empty(r.shape)
+    c = ctx_for(*r.shape)
+    L.check(L.lib().rmt_solve_poisson_fft(c.bind(), _p(r), lx.ctypes.data_as(ctypes.c_void_p),
+                                          ly.ctypes.data_as(ctypes.c_void_p), _p(out)),
+            "_solve_poisson_fft")
+    return io.out(out)
+
+
+def _compute_divergence_periodic(a_star, b_star, dx, dy):
+    """functions.py:1236-1243."""
+    io = _IO(a_star, b_star); a = io.dev(a_star); b = io.dev(b_star); out = io.empty(a.shape)
+    c = ctx_for(*a.shape)
+    L.check(L.lib().rmt_divergence_periodic(c.bind(), _p(a), _p(b), dx, dy, _p(out)),
+            "_compute_divergence_periodic")
+    return io.out(out)
+
+
+def _compute_pressure_gradient_periodic(p, dx, dy):
+    """functions.py:1246-1252."""
+    io = _IO(p); pd = io.dev(p); gx = io.empty(pd.shape); gy = io.empty(pd.shape)
+    c = ctx_for(*pd.shape)
+    L.check(L.lib().rmt_pressure_gradient_periodic(c.bind(), _p(pd), dx, dy, _p(gx), _p(gy)),
+            "_compute_pressure_gradient_periodic")
+    return io.out(gx), io.out(gy)
+
+
+def _projection_periodic(a_star, b_star, dx, dy, dt, rho, velocity_bc, A, ml, p_prev,
+                         eigenvalues):
+    """functions.py:1277-1290."""
+    Ny, Nx = np.shape(a_star)
+    if eigenvalues is None:
+        eigenvalues = _precompute_poisson_eigenvalues_periodic(Nx, Ny, dx, dy)
+    lx, ly = _periodic_axes_of(eigenvalues, dx, dy)
+    kind, lid = resolve_bc(velocity_bc)
+    torch = _torch()
+    io = _IO(a_star, b_star, p_prev)
+    a_s, b_s, pp = map(io.dev, (a_star, b_star, p_prev))
+    if isinstance(rho, np.ndarray) or isinstance(rho, torch.Tensor):
+        rho_bar = float(np.mean(np.asarray(rho.cpu() if isinstance(rho, torch.Tensor) else rho)))
+        rc = io.dev(rho)
+    else:
+        rho_bar, rc = float(rho), None
+    a = io.empty(a_s.shape); b = io.empty(a_s.shape); p = io.empty(a_s.shape)
+    c = ctx_for(*a_s.shape)
+    L.check(L.lib().rmt_pressure_projection_periodic(
+        c.bind(), _p(a_s), _p(b_s), dx, dy, dt, rho_bar, _p(rc), kind, lid,
+        lx.ctypes.data_as(ctypes.c_void_p), ly.ctypes.data_as(ctypes.c_void_p), _p(pp), _p(a),
+        _p(b), _p(p)), "pressure_projection_amg(periodic)")
+    return io.out(a), io.out(b), io.out(p), A, ml
+
+
 def pressure_projection_amg(a_star, b_star, dx, dy, dt, rho, velocity_bc, A=None, ml=None,
                             p_prev=None, eigenvalues=None, bc_type='neumann'):
-    """functions.py:1255-1364, Neumann branch with the DCT direct solve and constant
-    density.  Returns (a, b, p, A, ml) like the reference."""
+    """functions.py:1255-1364: the Neumann branch (DCT direct solve, constant density) and
+    the periodic branch (reduced-grid FFT).  Returns (a, b, p, A, ml) like the reference."""
+    if bc_type == 'periodic':
+        return _projection_periodic(a_star, b_star, dx, dy, dt, rho, velocity_bc, A, ml,
+                                    p_prev, eigenvalues)
     if bc_type != 'neumann':
         raise NotImplementedError("bc_type %r is outside this build's path" % (bc_type,))
     if eigenvalues is None:

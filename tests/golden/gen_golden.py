@@ -446,6 +446,33 @@ def gen_mac():
          pu=pu, pv=pv, pp=pp, pa=pa, pb=pb, txx=txx, txy=txy, tyy=tyy)
 
 
+def gen_periodic(N=65):
+    """functions.py:1177-1290 periodic branch on tests/test_poisson.py:24-78's fields."""
+    X, Y, dx, dy = F.create_grid(N, N, 1.0, 1.0)
+    k = 2 * np.pi
+    p_true = np.cos(k * X) * np.sin(k * Y) + 0.5 * np.sin(2 * k * X)
+    gx, gy = F._compute_pressure_gradient_periodic(p_true, dx, dy)
+    lap = F._compute_divergence_periodic(gx, gy, dx, dy)
+    eig, null = F._precompute_poisson_eigenvalues_periodic(N, N, dx, dy)
+    p = F._solve_poisson_fft(lap, (eig, null))
+
+    def periodic_bc(u, v):
+        u = u.copy(); v = v.copy()
+        u[:, -1] = u[:, 0]; v[:, -1] = v[:, 0]
+        u[-1, :] = u[0, :]; v[-1, :] = v[0, :]
+        return u, v
+    a = np.sin(k * X) * np.cos(k * Y) + 0.3 * np.cos(k * X)
+    b = -np.cos(k * X) * np.sin(k * Y) + 0.2 * np.sin(k * Y)
+    a, b = periodic_bc(a, b)
+    rng = np.random.default_rng(5)
+    p_prev = rng.standard_normal((N, N))
+    an, bn, pn, _, _ = F.pressure_projection_amg(a, b, dx, dy, 1e-2, 1.0, periodic_bc,
+                                                 p_prev=p_prev, eigenvalues=(eig, null),
+                                                 bc_type='periodic')
+    save("periodic", N=N, dx=dx, dy=dy, p_true=p_true, gx=gx, gy=gy, lap=lap, eig=eig,
+         null=null, p=p, a=a, b=b, p_prev=p_prev, an=an, bn=bn, pn=pn)
+
+
 def gen_mac_trace(N=64, nsteps=8, n_discs=3, seed=3):
     """Config 5 loop body (benchmarks/mac_multi_disc_lid.py:36-98) with the reference's
     own functions, no I/O: per-step centroids / J range and the final state."""
