@@ -187,6 +187,41 @@ __global__ void k_ex_none_fin(int *ctl) {
     if (!ctl[EXC_ANY]) { ctl[EXC_FALLBACK] = 1; ctl[EXC_NOOP] = 1; }
 }
 
+// Tiles (MOM_TX x MOM_TY) whose momentum may depend on an extrapolated value (sim.hip runs
+// the momentum speculatively, concurrently with the chain, then re-runs these tiles): a tile
+// qualifies if the box of `margin` cells around it holds an unknown interior cell and the box
+// of margin + ML holds a known one -- every target lies within ML cells of the known set.
+// One wave per tile, one box row per lane.
+__global__ void __launch_bounds__(256) k_fix_tiles(const u64 *__restrict__ kbits, int ny, int nx,
+                                                   int W, int reach, int margin, int tiles_x,
+                                                   int ntiles, int *__restrict__ list,
+                                                   int *__restrict__ count) {
+    const int lane = threadIdx.x & 63, t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= ntiles) return;
+    const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY, w0 = i0 >> 6;
+    auto cols = [&](int ww, int a, int b) -> u64 {   // bits of word ww for columns [a, b)
+        if (ww < 0 || ww >= W) return 0;
+        const int lo = max(a - 64 * ww, 0), hi = min(b - 64 * ww, 64);
+        if (hi <= lo) return 0;
+        const u64 m = hi == 64 ? ~0ull : ((1ull << hi) - 1);
+        return m & ~((1ull << lo) - 1);
+    };
+    bool kn = false, un = false;
+    const int j = j0 - reach + lane;   // reach = margin + ML <= 31 rows each side
+    if (lane < MOM_TY + 2 * reach && j >= 0 && j < ny) {
+        const bool inner = j >= j0 - margin && j < j0 + MOM_TY + margin && j >= 1 && j <= ny - 2;
+        for (int d = -1; d <= 1; ++d) {
+            const int ww = w0 + d;
+            if (ww < 0 || ww >= W) continue;
+            const u64 k = kbits[(long)j * W + ww];
+            kn |= (k & cols(ww, max(i0 - reach, 0), min(i0 + MOM_TX + reach, nx))) != 0;
+            if (inner)
+                un |= (~k & cols(ww, max(i0 - margin, 1), min(i0 + MOM_TX + margin, nx - 1))) != 0;
+        }
+    }
+    if (__ballot(kn) && __ballot(un) && lane == 0) list[atomicAdd(count, 1)] = t;
+}
+
 __device__ __forceinline__ u64 ld_sc1_u64(const u64 *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -675,6 +710,7 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
     if (dev_status)
         RMT_HIP(hipMemcpyAsync(dev_status, ws.status, 2 * sizeof(int), hipMemcpyDeviceToDevice,
                                ctx->stream));
+    if (ctx->ev_chain && !chain) RMT_HIP(hipEventRecord(ctx->ev_chain, ctx->stream));
     return RMT_OK;
 }
 
@@ -692,6 +728,20 @@ extern "C" int rmt_extrap_set_mode(int mode) {
     rmt::g_ex_mode = mode;
     return RMT_OK;
 }
+
+namespace rmt {
+int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *count) {
+    const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
+    const int tiles_x = (nx + MOM_TX - 1) / MOM_TX, ntiles = tiles_x * ((ny + MOM_TY - 1) / MOM_TY);
+    RMT_CHECK(margin + max_layers <= 24 && margin >= 0, RMT_EINVAL, "fix-tile reach");
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
+    RMT_HIP(hipMemsetAsync(count, 0, sizeof(int), ctx->stream));
+    k_fix_tiles<<<grid1d(ntiles, 4), 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, margin + max_layers,
+                                                             margin, tiles_x, ntiles, list, count);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+}  // namespace rmt
 
 extern "C" int rmt_extrap_last_path(rmt_ctx *ctx, int *path) {
     RMT_CHECK(ctx && path, RMT_EINVAL, "null argument");

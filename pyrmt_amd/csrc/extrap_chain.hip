@@ -558,7 +558,9 @@ __device__ __forceinline__ double dpp_shl(double v, int ctrl) {
 // reader that sees the tag reads the values afterwards (one wave's LDS operations are
 // performed in issue order), so no fence is needed -- and none is wanted: a workgroup fence
 // would also drain the record prefetch in flight.  Returns false on a timeout (bug guard).
-template <bool PROF>
+// VAR (experiment knob, RMT_CH_VARIANT): bit 0 = wave priorities (low while polling, high
+// from the last source's arrival through the publish); bit 1 = poll without s_sleep
+template <bool PROF, int VAR>
 __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                        int *cur, int &wm, double &o_out, long &c_out,
                                        long long *pr, long long &tl) {
@@ -627,6 +629,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     // pass 2: wait for the missing sources, then the rest of the fold
     if (pend) {
         long sp = 0;
+        if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
         for (;;) {
             if (!done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
@@ -639,8 +642,9 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             if (__ballot(!done) == 0) break;
             if (++sp > CH_SPIN_LIMIT) return false;
             if constexpr (PROF) pr[7] += 1;
-            __builtin_amdgcn_s_sleep(0);
+            if constexpr (!(VAR & 2)) __builtin_amdgcn_s_sleep(0);
         }
+        if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(3);
         CH_STAMP(2);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -662,13 +666,14 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     asm volatile("" ::: "memory");
     if (lane == 0)
         __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
     c_out = __double_as_longlong(B[0]);
     if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     CH_STAMP(5);
     return true;
 }
 
-template <bool PROF>
+template <bool PROF, int VAR>
 __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *gprof) {
     __shared__ double2 val[CH_R];
     __shared__ int tag[CH_R];
@@ -713,7 +718,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         if (x2 <= x) { ok = false; break; }   // bug guard: the wave's sequence must advance
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
-        if (!ch_fit<PROF>(x, lane, B, val, tag, cur, wm, o, c, pr, tl)) { ok = false; break; }
+        if (!ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl)) { ok = false; break; }
         x = x2; r = r2;
     }
     if constexpr (PROF)
@@ -753,10 +758,17 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
+    if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
+    static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 0;
     if (!prof) {
-        k_ex_chain<false><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+        switch (var) {
+            case 1: k_ex_chain<false, 1><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
+            case 2: k_ex_chain<false, 2><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
+            case 3: k_ex_chain<false, 3><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
+            default: k_ex_chain<false, 0><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+        }
         RMT_LAUNCHED();
     } else {
         // diagnostic: per-phase shader clocks summed over the chain waves
@@ -766,7 +778,7 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
         hipEvent_t e0, e1;
         RMT_HIP(hipEventCreate(&e0)); RMT_HIP(hipEventCreate(&e1));
         RMT_HIP(hipEventRecord(e0, st));
-        k_ex_chain<true><<<1, CH_W * 64, 0, st>>>(C, gp);
+        k_ex_chain<true, 0><<<1, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, st));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));

@@ -31,6 +31,32 @@ __global__ void k_mom_prep(const double *__restrict__ X1, const double *__restri
     solid[c] = pc <= 0.0;
 }
 
+// k_mom_prep over the listed 64 x 16 tiles (momentum_fixup)
+__global__ void __launch_bounds__(256) k_mom_prep_tiles(
+    const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ phi,
+    int ny, int nx, double dx, double dy, double mu_s, double kappa, double w_cut, double clamp,
+    double w_t, double rho_s, double rho_f, double *__restrict__ sxx, double *__restrict__ sxy,
+    double *__restrict__ syy, double *__restrict__ J, double *__restrict__ H,
+    double *__restrict__ rho, unsigned char *__restrict__ solid, const int *__restrict__ tiles,
+    const int *__restrict__ count, int tiles_x) {
+    if ((int)blockIdx.x >= *count) return;
+    const int t = tiles[blockIdx.x];
+    const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
+    for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
+        const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
+        if (j >= ny || i >= nx) continue;
+        const long c = (long)j * nx + i;
+        Stress s{0.0, 0.0, 0.0, 1.0};
+        if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1)
+            solid_stress_cell(X1, X2, phi, c, nx, dx, dy, mu_s, kappa, w_cut, clamp, false, s);
+        sxx[c] = s.sxx; sxy[c] = s.sxy; syy[c] = s.syy; J[c] = s.J;
+        const double pc = phi[c], h = heaviside(pc, w_t);
+        H[c] = h;
+        rho[c] = (1 - h) * rho_s + h * rho_f;
+        solid[c] = pc <= 0.0;
+    }
+}
+
 // Stage pass, three per-cell kernels (round-1 structure: simple and verifiable).
 // 1. k_stage_vel: BC'd stage velocity us = BC(u + coef k_prev)   (functions.py:714)
 // 2. k_stage_sigma: blended stress H sigma_f + (1-H)(sigma_el + solid viscous)
@@ -144,11 +170,14 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     const unsigned char *__restrict__ solid, int visc, double mu_f, double eta_s, double rho_s,
     double rho_f, const double *__restrict__ p, double dt6, double dx, double dy, int ny, int nx,
     int tiles_x, int ntiles, double *__restrict__ ku, double *__restrict__ kv,
-    double *__restrict__ accu, double *__restrict__ accv, double *__restrict__ outu,
-    double *__restrict__ outv, RowWin rw) {
+    const double *__restrict__ ainu, const double *__restrict__ ainv, double *__restrict__ accu,
+    double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
+    const int *__restrict__ tlist, const int *__restrict__ tcount) {
     __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
     __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
-    const int tile = xcd_tile(blockIdx.x, ntiles);
+    // tlist: the listed tiles only (momentum_fixup); otherwise every tile of rows [jb, je)
+    if (tlist && (int)blockIdx.x >= *tcount) return;
+    const int tile = tlist ? tlist[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
     const double h2x = 2 * dx, h2y = 2 * dy;
     // 1. stage velocity (functions.py:714), BC applied; all loads issued before the LDS stores
@@ -237,8 +266,8 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !ey ? p[c - nx] : 0.0;
             hh[it] = H[c];
             // accumulation operands
-            x0[it] = stage == 1 ? kpu[c] : (stage >= 2 ? accu[c] : 0.0);
-            y0[it] = stage == 1 ? kpv[c] : (stage >= 2 ? accv[c] : 0.0);
+            x0[it] = stage == 1 ? kpu[c] : (stage >= 2 ? ainu[c] : 0.0);
+            y0[it] = stage == 1 ? kpv[c] : (stage >= 2 ? ainv[c] : 0.0);
             x1[it] = stage == 3 ? u[c] : 0.0;
             y1[it] = stage == 3 ? v[c] : 0.0;
         }
@@ -282,6 +311,26 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             }
         }
     }
+}
+
+// One fused stage launch: k_{s+1} -> (k1 | k2 | k3)[s], acc1 / acc2 / u* (see MomWork)
+static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const double *u,
+                     const double *v, const double *p, const double *sxx, const double *sxy,
+                     const double *syy, const MomWork &W, double *u_new, double *v_new,
+                     RowWin ws, int ntiles, const int *tlist, const int *tcount) {
+    const int nx = ctx->nx, ny = ctx->ny, tiles_x = (nx + MS_TX - 1) / MS_TX;
+    const double coef[4] = {0.0, 0.5 * P->dt, 0.5 * P->dt, P->dt}, dt6 = P->dt / 6.0;
+    double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
+    const double *kpu = s ? ku[s - 1] : u, *kpv = s ? kv[s - 1] : v;
+    const double *ainu = s == 3 ? W.acc2u : W.accu, *ainv = s == 3 ? W.acc2v : W.accv;
+    double *aou = s == 2 ? W.acc2u : W.accu, *aov = s == 2 ? W.acc2v : W.accv;
+    k_mom_stage<<<ntiles, MS_T, 0, ctx->stream>>>(
+        u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid,
+        P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx,
+        tiles_x, ntiles, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, ainu, ainv, aou, aov,
+        u_new, v_new, ws, tlist, tcount);
+    RMT_LAUNCHED();
+    return RMT_OK;
 }
 
 // Final BC (functions.py:760) on the boundary cells of rows [jb, je) only: the bottom / top
@@ -331,14 +380,10 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     static const bool unfused = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED"));
     const int tiles_x = (nx + MS_TX - 1) / MS_TX;
     for (int s = 0; s < 4 && !unfused; ++s) {
-        const double *kpu = s ? kbu[(s - 1) & 1] : u, *kpv = s ? kbv[(s - 1) & 1] : v;
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
-        k_mom_stage<<<ntiles, MS_T, 0, ctx->stream>>>(
-            u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid, visc,
-            P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx, tiles_x, ntiles,
-            kbu[s & 1], kbv[s & 1], W.accu, W.accv, u_new, v_new, ws);
-        RMT_LAUNCHED();
+        RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
+                          nullptr, nullptr));
     }
     RMT_CHECK(!unfused || !win, RMT_ENOTSUP, "RMT_MOM_UNFUSED: single-domain only");
     for (int s = 0; s < 4 && unfused; ++s) {
@@ -360,6 +405,28 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
     k_bc_edges<<<grid1d(2 * (nx + ny), 256), 256, 0, ctx->stream>>>(P->bc_kind, P->lid, u_new,
                                                                      v_new, ny, nx, w0.jb, w0.je);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
+                   const double *p, const double *X1, const double *X2, const double *phi,
+                   double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
+                   const MomWork &W, const int *tiles, const int *count, int max_tiles) {
+    const int ny = ctx->ny, nx = ctx->nx;
+    static_assert(MOM_TX == MS_TX && MOM_TY == MS_TY, "fixup tiles are the stage tiles");
+    const double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
+    const int tiles_x = (nx + MS_TX - 1) / MS_TX;
+    k_mom_prep_tiles<<<max_tiles, 256, 0, ctx->stream>>>(
+        X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
+        P->rho_f, sxx, sxy, syy, J, W.H, W.rho, W.solid, tiles, count, tiles_x);
+    RMT_LAUNCHED();
+    const RowWin all{0, ny, 0, ny};
+    for (int s = 0; s < 4; ++s)
+        RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, all, max_tiles,
+                          tiles, count));
+    k_bc_edges<<<grid1d(2 * (nx + ny), 256), 256, 0, ctx->stream>>>(P->bc_kind, P->lid, u_new,
+                                                                     v_new, ny, nx, 0, ny);
     RMT_LAUNCHED();
     return RMT_OK;
 }

@@ -445,14 +445,12 @@ int rmt_ctx_set_profiling(rmt_ctx *ctx, int on) {
 }
 int rmt_ctx_kernel_ms(rmt_ctx *ctx, double *ms2) {
     RMT_CHECK(ctx && ms2 && ctx->ev[0], RMT_EINVAL, "profiling not enabled");
-    float f = 0;
-    RMT_HIP(hipEventSynchronize(ctx->ev[1]));
-    RMT_HIP(hipEventElapsedTime(&f, ctx->ev[0], ctx->ev[1]));
-    ms2[0] = f;
-    ms2[1] = 0;
-    if (hipEventQuery(ctx->ev[3]) == hipSuccess &&
-        hipEventElapsedTime(&f, ctx->ev[2], ctx->ev[3]) == hipSuccess)
-        ms2[1] = f;
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    for (int k = 0; k < 2; ++k) {   // an interval never recorded reads as 0
+        float f = 0;
+        ms2[k] = hipEventElapsedTime(&f, ctx->ev[2 * k], ctx->ev[2 * k + 1]) == hipSuccess ? f : 0.0;
+    }
+    (void)hipGetLastError();
     return RMT_OK;
 }
 

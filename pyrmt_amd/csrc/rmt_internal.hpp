@@ -67,6 +67,9 @@ struct rmt_ctx {
     int ex_layers = 0;          // last extrapolation call (rmt_extrap_last_path)
     bool ex_chain = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // optional (sim.hip overlap): recorded on the stream right before the extrapolation's
+    // serial chain kernel starts (or after the call when no chain kernel runs)
+    hipEvent_t ev_chain = nullptr;
 };
 
 namespace rmt {
@@ -331,20 +334,31 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 double *phi_pre, int *bad);
 
 // --------------------------------------------------------------------- momentum --
-constexpr int MOM_WORK_PLANES = 13;
+// every stage keeps its own k and accumulation planes (k1, k2, k3, acc1 = k1 + 2 k2,
+// acc2 = acc1 + 2 k3), so a tile-list re-run of any stage (momentum_fixup) finds its inputs
+constexpr int MOM_WORK_PLANES = 17;
 struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + flag
     double *H, *rho, *k1u, *k1v, *k2u, *k2v, *accu, *accv, *us, *vs, *gxx, *gxy, *gyy;
+    double *k3u, *k3v, *acc2u, *acc2v;
     unsigned char *solid;
     int *any_solid;
 };
 inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
-    return MomWork{w,         w + n,     w + 2 * n, w + 3 * n,  w + 4 * n,  w + 5 * n, w + 6 * n,
-                   w + 7 * n, w + 8 * n, w + 9 * n, w + 10 * n, w + 11 * n, w + 12 * n, solid, flag};
+    return MomWork{w,          w + n,      w + 2 * n,  w + 3 * n,  w + 4 * n,  w + 5 * n,
+                   w + 6 * n,  w + 7 * n,  w + 8 * n,  w + 9 * n,  w + 10 * n, w + 11 * n,
+                   w + 12 * n, w + 13 * n, w + 14 * n, w + 15 * n, w + 16 * n, solid, flag};
 }
 int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                  const double *p, const double *X1, const double *X2, const double *phi,
                  double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
                  const MomWork &W, const RowWin *win = nullptr);
+// re-run prep + the 4 stages on the 64 x 16 tiles listed in tiles[0 .. *count) (device) after
+// a speculative momentum_rk4 whose inputs changed only inside them (sim.hip overlap)
+constexpr int MOM_TX = 64, MOM_TY = 16;
+int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
+                   const double *p, const double *X1, const double *X2, const double *phi,
+                   double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
+                   const MomWork &W, const int *tiles, const int *count, int max_tiles);
 
 // ---------------------------------------------------------------------- poisson --
 int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
@@ -369,5 +383,8 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 double dy, int max_layers, double *X1o, double *X2o, int *dev_status = nullptr,
                 const unsigned long long *kin = nullptr);
 size_t extrap_workspace(int ny, int nx, int max_layers);   // bytes of ctx->bytes it uses
+// after extrapolate(): the MOM_TX x MOM_TY tiles within `margin` cells of a possible target
+// (device list + count); the momentum of every other cell ignores the extrapolated values
+int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *count);
 
 }  // namespace rmt

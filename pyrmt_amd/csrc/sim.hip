@@ -35,6 +35,10 @@ struct rmt_sim {
     double dt_const = 0, t = 0, integ = 0;
     std::vector<rmt_diag> diag;
     void *block = nullptr;
+    // overlap of the (one-CU) extrapolation chain with a speculative momentum pass
+    hipStream_t st2 = nullptr;
+    hipEvent_t e_sl = nullptr, e_mom = nullptr;
+    int *tiles = nullptr, *tcount = nullptr, max_tiles = 0;
     bool prof = false;
     hipEvent_t pev[7] = {};
     double ms[8] = {};
@@ -98,6 +102,28 @@ __global__ void k_phi_rebuild(const double *__restrict__ X1n, const double *__re
         phi[c] = disc_phi(a, b, x0, y0, R);
     } else {
         phi[c] = 1.0;
+    }
+}
+
+// k_phi_rebuild on the listed tiles (after the chain: the targets all lie inside them)
+__global__ void __launch_bounds__(256) k_phi_tiles(const double *__restrict__ X1n,
+                                                   const double *__restrict__ X2n, int ny, int nx,
+                                                   double x0, double y0, double R,
+                                                   double *__restrict__ phi,
+                                                   double *__restrict__ X1,
+                                                   double *__restrict__ X2,
+                                                   const int *__restrict__ tiles,
+                                                   const int *__restrict__ count, int tiles_x) {
+    if ((int)blockIdx.x >= *count) return;
+    const int t = tiles[blockIdx.x];
+    const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
+    for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
+        const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
+        if (j >= ny || i >= nx) continue;
+        const long c = (long)j * nx + i;
+        const double a = X1n[c], b = X2n[c];
+        X1[c] = a; X2[c] = b;
+        phi[c] = disc_phi(a, b, x0, y0, R);
     }
 }
 
@@ -270,6 +296,15 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     // byte workspace, so nothing is reallocated while kernels are queued
     RMT_TRY(ensure_scratch(ctx, 3 * n * sizeof(double)));
     RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, prm->layers)));
+    if (prm->shape == RMT_SHAPE_DISC && prm->scheme == RMT_SCHEME_SEMILAGRANGIAN &&
+        prm->layers >= 1 && prm->layers <= 12) {
+        RMT_HIP(hipStreamCreateWithFlags(&S->st2, hipStreamNonBlocking));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_sl, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_mom, hipEventDisableTiming));
+        S->max_tiles = ((nx + MOM_TX - 1) / MOM_TX) * ((ny + MOM_TY - 1) / MOM_TY);
+        RMT_HIP(hipMalloc(&S->tiles, (S->max_tiles + 64) * sizeof(int)));
+        S->tcount = S->tiles + S->max_tiles;
+    }
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
     return RMT_OK;
@@ -278,6 +313,10 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
 int rmt_sim_destroy(rmt_sim *S) {
     if (!S) return RMT_OK;
     hipFree(S->block);
+    if (S->tiles) hipFree(S->tiles);
+    if (S->e_sl) hipEventDestroy(S->e_sl);
+    if (S->e_mom) hipEventDestroy(S->e_mom);
+    if (S->st2) hipStreamDestroy(S->st2);
     for (auto e : S->pev) if (e) hipEventDestroy(e);
     S->ctx->prof = false;
     delete S;
@@ -313,6 +352,17 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         double dt = hv[1];
         if (S->t + dt > t_end) dt = t_end - S->t;
         const bool solid = P.shape != RMT_SHAPE_NONE;
+        rmt_momentum_params M{};
+        M.bc_kind = P.bc_kind; M.lid = P.lid; M.mu_s = P.mu_s; M.kappa = P.kappa;
+        M.eta_s = P.eta_s; M.rho_s = P.rho_s; M.rho_f = P.rho_f; M.mu_f = P.mu_f; M.w_t = P.w_t;
+        M.dx = P.dx; M.dy = P.dy; M.dt = dt; M.stress_band = P.stress_band;
+        M.detg_clamp = P.detg_clamp;
+        MomWork W = mom_work(S->mw, n, S->mbytes, S->flag + 1);
+        // the extrapolation chain occupies one CU for milliseconds; everything it does not
+        // feed runs beside it: the momentum of every cell, from the pre-extrapolation map, on
+        // a second stream, re-run afterwards on the tiles within reach of a target
+        static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
+        const bool overlap = solid && S->st2 && !no_overlap;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
             // 2. advect the reference map with the pre-advection level set and mask
@@ -332,9 +382,27 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             }
             RMT_LAUNCHED();
             if (S->prof) RMT_HIP(hipEventRecord(S->pev[2], st));
-            // 3. narrow-band extrapolation (exact raster-order semantics), in place
-            RMT_TRY(extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers, S->X1n,
-                                S->X2n, S->flag + 2));
+            // 3. narrow-band extrapolation (exact raster-order semantics), in place; with the
+            // overlap, the speculative phi + momentum start on the second stream once the
+            // chip-wide passes are done and the one-workgroup chain kernel is launched
+            if (overlap) ctx->ev_chain = S->e_sl;
+            const int es = extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
+                                       S->X1n, S->X2n, S->flag + 2);
+            ctx->ev_chain = nullptr;
+            RMT_TRY(es);
+            if (overlap) {
+                RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
+                k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R,
+                                                      S->phi, S->X1, S->X2);
+                RMT_LAUNCHED();
+                ctx->stream = S->st2;
+                const int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi,
+                                            S->us, S->vs, S->sxx, S->sxy, S->syy, S->J, W);
+                ctx->stream = st;
+                RMT_TRY(ms);
+                RMT_HIP(hipEventRecord(S->e_mom, S->st2));
+            }
+            if (overlap) RMT_TRY(extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount));
             if (S->prof) RMT_HIP(hipEventRecord(S->pev[3], st));
             int fl[4] = {0, 0, 0, 0};   // non-finite, (momentum), fitted, sweep aborted
             RMT_HIP(hipMemcpyAsync(fl, S->flag, sizeof(fl), hipMemcpyDeviceToHost, st));
@@ -347,19 +415,25 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_HIP(hipEventRecord(S->pev[2], st));
             RMT_HIP(hipEventRecord(S->pev[3], st));
         }
-        // 4. phi from the advected + extrapolated map
-        k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R, S->phi,
-                                          S->X1, S->X2);
-        // 5. momentum (RK4)
-        rmt_momentum_params M{};
-        M.bc_kind = P.bc_kind; M.lid = P.lid; M.mu_s = P.mu_s; M.kappa = P.kappa;
-        M.eta_s = P.eta_s; M.rho_s = P.rho_s; M.rho_f = P.rho_f; M.mu_f = P.mu_f; M.w_t = P.w_t;
-        M.dx = P.dx; M.dy = P.dy; M.dt = dt; M.stress_band = P.stress_band;
-        M.detg_clamp = P.detg_clamp;
-        double *w = S->mw;
-        MomWork W = mom_work(w, n, S->mbytes, S->flag + 1);
-        RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
-                             S->sxx, S->sxy, S->syy, S->J, W));
+        if (overlap) {
+            // 4 + 5 on the tiles the extrapolation can reach
+            RMT_HIP(hipStreamWaitEvent(st, S->e_mom, 0));
+            const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
+            k_phi_tiles<<<S->max_tiles, 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
+                                                       S->phi, S->X1, S->X2, S->tiles, S->tcount,
+                                                       tiles_x);
+            RMT_LAUNCHED();
+            RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
+                                   S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,
+                                   S->max_tiles));
+        } else {
+            // 4. phi from the advected + extrapolated map
+            k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R, S->phi,
+                                              S->X1, S->X2);
+            // 5. momentum (RK4)
+            RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
+                                 S->sxx, S->sxy, S->syy, S->J, W));
+        }
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[4], st));
         // 6. projection (constant density rho_f; Neumann DCT-I)
         RMT_TRY(rmt_pressure_projection(ctx, S->us, S->vs, P.dx, P.dy, dt, P.rho_f, P.bc_kind,
