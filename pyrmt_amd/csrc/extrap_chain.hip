@@ -558,8 +558,9 @@ __device__ __forceinline__ double dpp_shl(double v, int ctrl) {
 // reader that sees the tag reads the values afterwards (one wave's LDS operations are
 // performed in issue order), so no fence is needed -- and none is wanted: a workgroup fence
 // would also drain the record prefetch in flight.  Returns false on a timeout (bug guard).
-// VAR (experiment knob, RMT_CH_VARIANT): bit 0 = wave priorities (low while polling, high
-// from the last source's arrival through the publish); bit 1 = poll without s_sleep
+// VAR (RMT_CH_VARIANT, default 3): bit 0 = wave priorities (low while polling, high from the
+// last source's arrival through the publish); bit 1 = poll without s_sleep.  Measured on the
+// 4096^2 disc: 0 -> 4.66 ms, 1 -> 4.50, 2 -> 4.74, 3 -> 4.45 (profiles/r01s3/chain_variants.log)
 template <bool PROF, int VAR>
 __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                        int *cur, int &wm, double &o_out, long &c_out,
@@ -761,13 +762,13 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
-    static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 0;
+    static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 3;
     if (!prof) {
         switch (var) {
+            case 0: k_ex_chain<false, 0><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 1: k_ex_chain<false, 1><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 2: k_ex_chain<false, 2><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 3: k_ex_chain<false, 3><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
-            default: k_ex_chain<false, 0><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+            default: k_ex_chain<false, 3><<<1, CH_W * 64, 0, st>>>(C, nullptr);
         }
         RMT_LAUNCHED();
     } else {
@@ -778,7 +779,7 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
         hipEvent_t e0, e1;
         RMT_HIP(hipEventCreate(&e0)); RMT_HIP(hipEventCreate(&e1));
         RMT_HIP(hipEventRecord(e0, st));
-        k_ex_chain<true, 0><<<1, CH_W * 64, 0, st>>>(C, gp);
+        k_ex_chain<true, 3><<<1, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, st));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));

@@ -298,7 +298,11 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, prm->layers)));
     if (prm->shape == RMT_SHAPE_DISC && prm->scheme == RMT_SCHEME_SEMILAGRANGIAN &&
         prm->layers >= 1 && prm->layers <= 12) {
-        RMT_HIP(hipStreamCreateWithFlags(&S->st2, hipStreamNonBlocking));
+        // the speculative momentum stream at the lowest priority: the extrapolation's own
+        // kernels (chip-wide passes, then the chain) are dispatched first when both are ready
+        int least = 0, greatest = 0;
+        RMT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        RMT_HIP(hipStreamCreateWithPriority(&S->st2, hipStreamNonBlocking, least));
         RMT_HIP(hipEventCreateWithFlags(&S->e_sl, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_mom, hipEventDisableTiming));
         S->max_tiles = ((nx + MOM_TX - 1) / MOM_TX) * ((ny + MOM_TY - 1) / MOM_TY);
