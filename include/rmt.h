@@ -50,7 +50,10 @@ typedef enum {
 /* Reference-map advection schemes (functions.py:501-542). */
 typedef enum {
     RMT_SCHEME_SEMILAGRANGIAN = 0,  /* advect_semilagrangian_rk4 (bilinear)            */
-    RMT_SCHEME_WENO5 = 1            /* advect_weno5_rk3                               */
+    RMT_SCHEME_WENO5 = 1,           /* advect_weno5_rk3                               */
+    RMT_SCHEME_CENTRAL2 = 2,        /* advect_central2_rk3                            */
+    RMT_SCHEME_CONSERVATIVE = 3,    /* advect_conservative_rk3 (Jain 2019 eq. 26)      */
+    RMT_SCHEME_SEMILAGRANGIAN_CUBIC = 4 /* advect_semilagrangian_cubic_rk4 (bicubic)  */
 } rmt_scheme;
 
 typedef struct rmt_ctx rmt_ctx;
@@ -93,6 +96,19 @@ int rmt_advect_weno5_rk3(rmt_ctx *ctx, const double *q, const double *a, const d
                          double dx, double dy, double dt, const double *phi, double w_cut,
                          double *out);
 /* functions.py:524-526 guard: sets *finite (host) to 1 if every a, b is finite.  Blocks. */
+/* functions.py:420-495 _central2_rhs / _conservative_rhs and the SSP-RK3 drivers
+ * advect_central2_rk3 / advect_conservative_rk3 (conservative = 0 / 1) */
+int rmt_central_rhs(rmt_ctx *ctx, const double *q, const double *a, const double *b, double dx,
+                    double dy, const double *phi, double w_cut, int conservative, double *rhs);
+int rmt_advect_central_rk3(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                           double dx, double dy, double dt, const double *phi, double w_cut,
+                           int conservative, double *out);
+/* interpolators.py:64-156 bicubic_interpolate; functions.py:228-251 the bicubic SL-RK4 */
+int rmt_bicubic_interpolate(rmt_ctx *ctx, const double *u, const double *xq, const double *yq,
+                            long nq, double dx, double dy, double *out);
+int rmt_advect_sl_cubic_rk4(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                            const double *X, const double *Y, double dt, double dx, double dy,
+                            double *out);
 int rmt_all_finite2(rmt_ctx *ctx, const double *a, const double *b, int *finite);
 
 /* functions.py:48-163 extrapolate_reference_map: exact raster-order (Gauss-Seidel)

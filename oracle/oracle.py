@@ -57,6 +57,10 @@ def _load():
         "rmto_divergence_central": (None, [P, P, I, I, D, D, P]),
         "rmto_pressure_gradient": (None, [P, I, I, D, D, P, P]),
         "rmto_pairwise_sum": (D, [P, L]),
+        "rmto_bicubic": (None, [P, P, P, L, D, D, I, I, P]),
+        "rmto_set_pow_mode": (None, [I]),
+        "rmto_advect_sl_cubic_rk4": (None, [P, P, P, P, P, I, I, D, D, D, P]),
+        "rmto_central_rhs": (None, [P, P, P, I, I, D, D, P, D, I, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -142,6 +146,56 @@ def advect_weno5_rk3(q, a, b, dx, dy, dt, phi, w_cut=0.0):
     return out
 
 
+def set_pow_mode(on):
+    """Pure-Python semantics for cubic_convolution's x**2 / x**3 (libm pow, as the golden
+    generator runs it) instead of Numba's multiplications (the default)."""
+    _lib.rmto_set_pow_mode(int(bool(on)))
+
+
+def bicubic_interpolate(u, xq, yq, dx, dy, Nx, Ny):
+    """interpolators.py:64-142."""
+    u, xq, yq = map(_c, (u, xq, yq)); out = _e(xq.shape)
+    _lib.rmto_bicubic(_p(u), _p(xq), _p(yq), xq.size, dx, dy, Nx, Ny, _p(out)); return out
+
+
+def advect_semilagrangian_cubic_rk4(q, a, b, X, Y, dt, dx, dy):
+    """functions.py:228-251."""
+    q, a, b, X, Y = map(_c, (q, a, b, X, Y)); out = _e(q.shape)
+    _lib.rmto_advect_sl_cubic_rk4(_p(q), _p(a), _p(b), _p(X), _p(Y), q.shape[0], q.shape[1], dt,
+                                  dx, dy, _p(out))
+    return out
+
+
+def _central_rhs(q, a, b, dx, dy, phi, w_cut, mode):
+    q, a, b, phi = map(_c, (q, a, b, phi)); out = _e(q.shape)
+    _lib.rmto_central_rhs(_p(q), _p(a), _p(b), q.shape[0], q.shape[1], dx, dy, _p(phi), w_cut,
+                          mode, _p(out))
+    return out
+
+
+def _central2_rhs(q, a, b, dx, dy, phi, w_cut):
+    return _central_rhs(q, a, b, dx, dy, phi, w_cut, 0)
+
+
+def _conservative_rhs(q, a, b, dx, dy, phi, w_cut):
+    return _central_rhs(q, a, b, dx, dy, phi, w_cut, 1)
+
+
+def _ssprk3(q, dt, rhs):
+    """functions.py:447-463 / 492-498: Shu-Osher SSP-RK3 with NumPy combinations."""
+    q1 = q + dt * rhs(q)
+    q2 = 0.75 * q + 0.25 * (q1 + dt * rhs(q1))
+    return (1.0 / 3.0) * q + (2.0 / 3.0) * (q2 + dt * rhs(q2))
+
+
+def advect_central2_rk3(q, a, b, dx, dy, dt, phi, w_cut=0.0):
+    return _ssprk3(_c(q), dt, lambda s: _central2_rhs(s, a, b, dx, dy, phi, w_cut))
+
+
+def advect_conservative_rk3(q, a, b, dx, dy, dt, phi, w_cut=0.0):
+    return _ssprk3(_c(q), dt, lambda s: _conservative_rhs(s, a, b, dx, dy, phi, w_cut))
+
+
 def advect_reference_map(q, a, b, X, Y, dt, dx, dy, phi, scheme='semilagrangian', w_cut=0.0):
     """functions.py:501-542 dispatcher (the two schemes on the hot path)."""
     if not (np.all(np.isfinite(a)) and np.all(np.isfinite(b))):
@@ -150,6 +204,12 @@ def advect_reference_map(q, a, b, X, Y, dt, dx, dy, phi, scheme='semilagrangian'
         return advect_semilagrangian_rk4(q, a, b, X, Y, dt, dx, dy)
     if scheme == 'weno5':
         return advect_weno5_rk3(q, a, b, dx, dy, dt, phi, w_cut)
+    if scheme == 'semilagrangian_cubic':
+        return advect_semilagrangian_cubic_rk4(q, a, b, X, Y, dt, dx, dy)
+    if scheme == 'central2':
+        return advect_central2_rk3(q, a, b, dx, dy, dt, phi, w_cut)
+    if scheme == 'conservative':
+        return advect_conservative_rk3(q, a, b, dx, dy, dt, phi, w_cut)
     raise ValueError("Unknown advection scheme %r" % (scheme,))
 
 

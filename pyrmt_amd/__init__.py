@@ -11,7 +11,8 @@ from .functions import (_precompute_poisson_eigenvalues, _solve_poisson_dct,  # 
                         _compute_divergence_rc, _compute_divergence, _compute_pressure_gradient,
                         _weno5_rhs, _precompute_poisson_eigenvalues_periodic,
                         _tile_overlap, _solve_poisson_fft, _compute_divergence_periodic,
-                        _compute_pressure_gradient_periodic)
+                        _compute_pressure_gradient_periodic, _central2_rhs,
+                        _conservative_rhs)
 from . import simulation
 from . import mac
 

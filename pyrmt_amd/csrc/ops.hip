@@ -254,6 +254,46 @@ __global__ void k_weno5_rhs(const double *__restrict__ q, const double *__restri
     }
     rhs[c] = r;
 }
+// functions.py:420-444 _central2_rhs (mode 0) and :466-489 _conservative_rhs (mode 1):
+// interior cells with phi <= w_cut, +/-1 central stencils, zero elsewhere
+__global__ void k_central_rhs(const double *__restrict__ q, const double *__restrict__ a,
+                              const double *__restrict__ b, int ny, int nx, double dx, double dy,
+                              const double *__restrict__ phi, double w_cut, int mode,
+                              double *__restrict__ rhs) {
+    const long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    const int j = (int)(c / nx), i = (int)(c % nx);
+    double r = 0.0;
+    if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1 && !(phi[c] > w_cut)) {
+        const double ix2 = 0.5 / dx, iy2 = 0.5 / dy;
+        if (mode == 0) {
+            const double dqdx = (q[c + 1] - q[c - 1]) * ix2, dqdy = (q[c + nx] - q[c - nx]) * iy2;
+            r = -(a[c] * dqdx + b[c] * dqdy);
+        } else {
+            const double dux = (a[c + 1] * q[c + 1] - a[c - 1] * q[c - 1]) * ix2;
+            const double dvy = (b[c + nx] * q[c + nx] - b[c - nx] * q[c - nx]) * iy2;
+            r = -(dux + dvy);
+        }
+    }
+    rhs[c] = r;
+}
+__global__ void k_bicubic(const double *__restrict__ u, const double *__restrict__ xq,
+                          const double *__restrict__ yq, long nq, double dx, double dy, int nx,
+                          int ny, double *__restrict__ out) {
+    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < nq) out[k] = bicubic(u, xq[k], yq[k], dx, dy, nx, ny);
+}
+__global__ void k_sl_cubic(const double *__restrict__ q, const double *__restrict__ a,
+                           const double *__restrict__ b, const double *__restrict__ X,
+                           const double *__restrict__ Y, int ny, int nx, double dt, double dx,
+                           double dy, double *__restrict__ out) {
+    const long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    double xb, yb;
+    sl_backtrace_cubic(a, b, X[c], Y[c], dt, dx, dy, nx, ny, xb, yb);
+    out[c] = bicubic(q, xb, yb, dx, dy, nx, ny);
+}
+
 // SSP-RK3 stage combinations (functions.py:407-413); stage 0: q + dt r,
 // stage 1: 0.75 q + 0.25 (q1 + dt r), stage 2: (1/3) q + (2/3) (q2 + dt r).
 __global__ void k_ssprk3_combine(const double *__restrict__ q, const double *__restrict__ qs,
@@ -537,6 +577,42 @@ int rmt_advect_weno5_rk3(rmt_ctx *ctx, const double *q, const double *a, const d
     k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q1, r, n, dt, 1, q2);
     RMT_TRY(rmt_weno5_rhs(ctx, q2, a, b, dx, dy, phi, w_cut, r));
     k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q2, r, n, dt, 2, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_central_rhs(rmt_ctx *ctx, const double *q, const double *a, const double *b, double dx,
+                    double dy, const double *phi, double w_cut, int conservative, double *rhs) {
+    k_central_rhs<<<LAUNCH1D(N_CELLS)>>>(q, a, b, ctx->ny, ctx->nx, dx, dy, phi, w_cut,
+                                         conservative ? 1 : 0, rhs);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_advect_central_rk3(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                           double dx, double dy, double dt, const double *phi, double w_cut,
+                           int conservative, double *out) {
+    long n = N_CELLS;
+    RMT_TRY(ensure_scratch(ctx, 3 * n * sizeof(double)));
+    double *r = ctx->scratch, *q1 = r + n, *q2 = q1 + n;
+    RMT_TRY(rmt_central_rhs(ctx, q, a, b, dx, dy, phi, w_cut, conservative, r));
+    k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q, r, n, dt, 0, q1);
+    RMT_TRY(rmt_central_rhs(ctx, q1, a, b, dx, dy, phi, w_cut, conservative, r));
+    k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q1, r, n, dt, 1, q2);
+    RMT_TRY(rmt_central_rhs(ctx, q2, a, b, dx, dy, phi, w_cut, conservative, r));
+    k_ssprk3_combine<<<LAUNCH1D(n)>>>(q, q2, r, n, dt, 2, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_bicubic_interpolate(rmt_ctx *ctx, const double *u, const double *xq, const double *yq,
+                            long nq, double dx, double dy, double *out) {
+    if (nq <= 0) return RMT_OK;
+    k_bicubic<<<LAUNCH1D(nq)>>>(u, xq, yq, nq, dx, dy, ctx->nx, ctx->ny, out);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+int rmt_advect_sl_cubic_rk4(rmt_ctx *ctx, const double *q, const double *a, const double *b,
+                            const double *X, const double *Y, double dt, double dx, double dy,
+                            double *out) {
+    k_sl_cubic<<<LAUNCH1D(N_CELLS)>>>(q, a, b, X, Y, ctx->ny, ctx->nx, dt, dx, dy, out);
     RMT_LAUNCHED();
     return RMT_OK;
 }

@@ -153,6 +153,60 @@ __device__ __forceinline__ void sl_backtrace(const double *__restrict__ a,
     sl_backtrace_t<false>(a, b, x, y, dt, dx, dy, nx, ny, 0, ny, nullptr, xb, yb);
 }
 
+// interpolators.py:144-156 cubic_convolution (Catmull-Rom); Numba's x**3 = x * (x * x)
+__device__ __forceinline__ double cubic_conv(double v0, double v1, double v2, double v3, double x) {
+    const double a0 = -0.5 * v0 + 1.5 * v1 - 1.5 * v2 + 0.5 * v3;
+    const double a1 = v0 - 2.5 * v1 + 2.0 * v2 - 0.5 * v3;
+    const double a2 = -0.5 * v0 + 0.5 * v2;
+    const double x2 = x * x, x3 = x * x2;
+    return a0 * x3 + a1 * x2 + a2 * x + v1;
+}
+// interpolators.py:64-142 bicubic_interpolate at one query point: clamped 4x4 stencil,
+// Catmull-Rom in x then y, result clamped to the stencil's min / max
+__device__ __forceinline__ double bicubic(const double *__restrict__ u, double xq, double yq,
+                                          double dx, double dy, int nx, int ny) {
+    double x = xq / dx, y = yq / dy;
+    if (!(isfinite(x) && isfinite(y))) return __builtin_nan("");
+    if (x < 0.0) x = 0.0; else if (x > nx - 1.0) x = nx - 1.0;
+    if (y < 0.0) y = 0.0; else if (y > ny - 1.0) y = ny - 1.0;
+    const int ix = (int)floor(x), iy = (int)floor(y);
+    const double fx = x - ix, fy = y - iy;
+    double rv[4], lo = 1e18, hi = -1e18;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int yg = min(max(iy - 1 + m, 0), ny - 1);
+        double cv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double v = u[(long)yg * nx + min(max(ix - 1 + q, 0), nx - 1)];
+            cv[q] = v;
+            if (v < lo) lo = v;
+            if (v > hi) hi = v;
+        }
+        rv[m] = cubic_conv(cv[0], cv[1], cv[2], cv[3], fx);
+    }
+    double r = cubic_conv(rv[0], rv[1], rv[2], rv[3], fy);
+    if (r < lo) r = lo;
+    if (r > hi) r = hi;
+    return r;
+}
+// functions.py:228-251 RK4 backtrace with the bicubic interpolant
+__device__ __forceinline__ void sl_backtrace_cubic(const double *__restrict__ a,
+                                                   const double *__restrict__ b, double x,
+                                                   double y, double dt, double dx, double dy,
+                                                   int nx, int ny, double &xb, double &yb) {
+    const double hdt = 0.5 * dt, dt6 = dt / 6.0;
+    double k1x = bicubic(a, x, y, dx, dy, nx, ny), k1y = bicubic(b, x, y, dx, dy, nx, ny);
+    double x2 = x - hdt * k1x, y2 = y - hdt * k1y;
+    double k2x = bicubic(a, x2, y2, dx, dy, nx, ny), k2y = bicubic(b, x2, y2, dx, dy, nx, ny);
+    double x3 = x - hdt * k2x, y3 = y - hdt * k2y;
+    double k3x = bicubic(a, x3, y3, dx, dy, nx, ny), k3y = bicubic(b, x3, y3, dx, dy, nx, ny);
+    double x4 = x - dt * k3x, y4 = y - dt * k3y;
+    double k4x = bicubic(a, x4, y4, dx, dy, nx, ny), k4y = bicubic(b, x4, y4, dx, dy, nx, ny);
+    xb = x - dt6 * (k1x + 2 * k2x + 2 * k3x + k4x);
+    yb = y - dt6 * (k1y + 2 * k2y + 2 * k3y + k4y);
+}
+
 // benchmarks/common.py:55-57 disc signed distance, numpy order: sqrt(dx*dx + dy*dy) - R.
 __device__ __forceinline__ double disc_phi(double X1, double X2, double x0, double y0,
                                            double R) {

@@ -68,6 +68,27 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
     X2n[c] = bilinear(X2, xb, yb, dx, dy, nx, ny) * m;
 }
 
+// k_sim_sl with the bicubic interpolant (functions.py:228-251, scheme semilagrangian_cubic)
+__global__ void k_sim_sl_cubic(const double *__restrict__ X1, const double *__restrict__ X2,
+                               const double *__restrict__ a, const double *__restrict__ b,
+                               const double *__restrict__ xs, const double *__restrict__ ys,
+                               int ny, int nx, double dt, double dx, double dy, double x0,
+                               double y0, double R, double *__restrict__ X1n,
+                               double *__restrict__ X2n, double *__restrict__ phi_pre, int *bad) {
+    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    int j = (int)(c / nx), i = (int)(c % nx);
+    bool fin = isfinite(a[c]) && isfinite(b[c]);
+    if (__any(!fin) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+    double ph = disc_phi(X1[c], X2[c], x0, y0, R);
+    phi_pre[c] = ph;
+    double m = ph <= 0 ? 1.0 : 0.0;
+    double xb, yb;
+    sl_backtrace_cubic(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, xb, yb);
+    X1n[c] = bicubic(X1, xb, yb, dx, dy, nx, ny) * m;
+    X2n[c] = bicubic(X2, xb, yb, dx, dy, nx, ny) * m;
+}
+
 __global__ void k_sim_phi_mask(const double *__restrict__ X1, const double *__restrict__ X2,
                                const double *__restrict__ a, const double *__restrict__ b,
                                long n, double x0, double y0, double R,
@@ -253,7 +274,8 @@ extern "C" {
 int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     RMT_CHECK(ctx && prm && out, RMT_EINVAL, "null argument");
     RMT_CHECK(prm->ny == ctx->ny && prm->nx == ctx->nx, RMT_EINVAL, "sim grid != ctx grid");
-    RMT_CHECK(prm->scheme == RMT_SCHEME_SEMILAGRANGIAN || prm->scheme == RMT_SCHEME_WENO5,
+    RMT_CHECK(prm->scheme >= RMT_SCHEME_SEMILAGRANGIAN &&
+                  prm->scheme <= RMT_SCHEME_SEMILAGRANGIAN_CUBIC,
               RMT_EINVAL, "unknown advection scheme");
     RMT_CHECK(prm->bc_kind >= 0 && prm->bc_kind <= 3, RMT_EINVAL, "unknown bc kind");
     RMT_CHECK(prm->shape == RMT_SHAPE_NONE || prm->shape == RMT_SHAPE_DISC, RMT_EINVAL,
@@ -375,13 +397,25 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 k_sim_sl<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt,
                                             P.dx, P.dy, P.shape, P.x0, P.y0, P.R, S->X1n, S->X2n,
                                             S->phi_pre, S->flag);
+            } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN_CUBIC) {
+                k_sim_sl_cubic<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx,
+                                                  dt, P.dx, P.dy, P.x0, P.y0, P.R, S->X1n,
+                                                  S->X2n, S->phi_pre, S->flag);
             } else {
+                // Eulerian schemes on the pre-advection level set, w_cut = 0 as the drivers
                 k_sim_phi_mask<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, n, P.x0, P.y0, P.R,
                                                   S->phi_pre, S->flag);
-                RMT_TRY(rmt_advect_weno5_rk3(ctx, S->X1, S->u, S->v, P.dx, P.dy, dt, S->phi_pre,
-                                             0.0, S->X1n));
-                RMT_TRY(rmt_advect_weno5_rk3(ctx, S->X2, S->u, S->v, P.dx, P.dy, dt, S->phi_pre,
-                                             0.0, S->X2n));
+                for (int comp = 0; comp < 2; ++comp) {
+                    const double *q = comp ? S->X2 : S->X1;
+                    double *o = comp ? S->X2n : S->X1n;
+                    if (P.scheme == RMT_SCHEME_WENO5)
+                        RMT_TRY(rmt_advect_weno5_rk3(ctx, q, S->u, S->v, P.dx, P.dy, dt,
+                                                     S->phi_pre, 0.0, o));
+                    else
+                        RMT_TRY(rmt_advect_central_rk3(ctx, q, S->u, S->v, P.dx, P.dy, dt,
+                                                       S->phi_pre, 0.0,
+                                                       P.scheme == RMT_SCHEME_CONSERVATIVE, o));
+                }
                 k_mask_mul<<<g, 256, 0, st>>>(S->X1n, S->X2n, S->phi_pre, n);
             }
             RMT_LAUNCHED();

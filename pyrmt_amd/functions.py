@@ -203,10 +203,69 @@ def advect_weno5_rk3(q, a, b, dx, dy, dt, phi, w_cut=0.0):
     return io.out(out)
 
 
+def bicubic_interpolate(u, xq, yq, dx, dy, Nx, Ny):
+    """interpolators.py:64-142 (monotone Catmull-Rom bicubic)."""
+    io = _IO(u, xq, yq); u = io.dev(u); xq = io.dev(xq); yq = io.dev(yq)
+    if u.shape != (Ny, Nx):
+        raise ValueError("bicubic_interpolate: u must have shape (Ny, Nx)")
+    out = io.empty(xq.shape)
+    c = ctx_for(Ny, Nx)
+    L.check(L.lib().rmt_bicubic_interpolate(c.bind(), _p(u), _p(xq), _p(yq), xq.numel(), dx, dy,
+                                            _p(out)), "bicubic_interpolate")
+    return io.out(out)
+
+
+def advect_semilagrangian_cubic_rk4(q, a, b, X, Y, dt, dx, dy):
+    """functions.py:228-251."""
+    io = _IO(q, a, b, X, Y); q, a, b, X, Y = map(io.dev, (q, a, b, X, Y))
+    out = io.empty(q.shape)
+    c = ctx_for(*q.shape)
+    L.check(L.lib().rmt_advect_sl_cubic_rk4(c.bind(), _p(q), _p(a), _p(b), _p(X), _p(Y), dt, dx,
+                                            dy, _p(out)), "advect_semilagrangian_cubic_rk4")
+    return io.out(out)
+
+
+def _central_rhs(q, a, b, dx, dy, phi, w_cut, conservative):
+    io = _IO(q, a, b, phi); q, a, b, phi = map(io.dev, (q, a, b, phi))
+    out = io.empty(q.shape)
+    c = ctx_for(*q.shape)
+    L.check(L.lib().rmt_central_rhs(c.bind(), _p(q), _p(a), _p(b), dx, dy, _p(phi), w_cut,
+                                    int(conservative), _p(out)), "_central_rhs")
+    return io.out(out)
+
+
+def _central2_rhs(q, a, b, dx, dy, phi, w_cut):
+    """functions.py:420-444."""
+    return _central_rhs(q, a, b, dx, dy, phi, w_cut, False)
+
+
+def _conservative_rhs(q, a, b, dx, dy, phi, w_cut):
+    """functions.py:466-489 (Jain, Kamrin & Mani 2019, eq. 26)."""
+    return _central_rhs(q, a, b, dx, dy, phi, w_cut, True)
+
+
+def _advect_central(q, a, b, dx, dy, dt, phi, w_cut, conservative, name):
+    io = _IO(q, a, b, phi); q, a, b, phi = map(io.dev, (q, a, b, phi))
+    out = io.empty(q.shape)
+    c = ctx_for(*q.shape)
+    L.check(L.lib().rmt_advect_central_rk3(c.bind(), _p(q), _p(a), _p(b), dx, dy, dt, _p(phi),
+                                           w_cut, int(conservative), _p(out)), name)
+    return io.out(out)
+
+
+def advect_central2_rk3(q, a, b, dx, dy, dt, phi, w_cut=0.0):
+    """functions.py:447-463."""
+    return _advect_central(q, a, b, dx, dy, dt, phi, w_cut, False, "advect_central2_rk3")
+
+
+def advect_conservative_rk3(q, a, b, dx, dy, dt, phi, w_cut=0.0):
+    """functions.py:492-498."""
+    return _advect_central(q, a, b, dx, dy, dt, phi, w_cut, True, "advect_conservative_rk3")
+
+
 def advect_reference_map(q, a, b, X, Y, dt, dx, dy, phi, scheme='semilagrangian', w_cut=0.0):
     """functions.py:501-542: raises FloatingPointError on non-finite velocity, ValueError
-    on an unknown scheme; 'semilagrangian_cubic', 'central2', 'conservative' are the
-    next tier and raise NotImplementedError."""
+    on an unknown scheme."""
     io = _IO(q, a, b, X, Y, phi)
     ad, bd = io.dev(a), io.dev(b)
     c = ctx_for(*ad.shape)
@@ -216,10 +275,14 @@ def advect_reference_map(q, a, b, X, Y, dt, dx, dy, phi, scheme='semilagrangian'
         raise FloatingPointError("advect_reference_map: non-finite velocity (the simulation diverged)")
     if scheme == 'semilagrangian':
         return advect_semilagrangian_rk4(q, a, b, X, Y, dt, dx, dy)
+    if scheme == 'semilagrangian_cubic':
+        return advect_semilagrangian_cubic_rk4(q, a, b, X, Y, dt, dx, dy)
+    if scheme == 'central2':
+        return advect_central2_rk3(q, a, b, dx, dy, dt, phi, w_cut)
     if scheme == 'weno5':
         return advect_weno5_rk3(q, a, b, dx, dy, dt, phi, w_cut)
-    if scheme in ('semilagrangian_cubic', 'central2', 'conservative'):
-        raise NotImplementedError(f"advection scheme {scheme!r} is outside this build's path")
+    if scheme == 'conservative':
+        return advect_conservative_rk3(q, a, b, dx, dy, dt, phi, w_cut)
     raise ValueError("Unknown advection scheme %r (expected 'semilagrangian', "
                      "'central2', 'weno5' or 'conservative')" % (scheme,))
 

@@ -446,6 +446,32 @@ def gen_mac():
          pu=pu, pv=pv, pp=pp, pa=pa, pb=pb, txx=txx, txy=txy, tyy=tyy)
 
 
+def gen_schemes(N=41):
+    """The other advection schemes behind advect_reference_map (functions.py:228-251,
+    420-498; interpolators.py:64-156) on a deformed disc map."""
+    rng = np.random.default_rng(77)
+    X, Y, dx, dy = F.create_grid(N, N, 1.0, 1.0)
+    f = rng.standard_normal((N, N))
+    xq = rng.uniform(-0.2, 1.2, (N, N)); yq = rng.uniform(-0.2, 1.2, (N, N))
+    xq[0, 0] = np.nan; yq[1, 1] = np.inf; xq[3, 3] = 1e200; xq[5, 5] = 1.0; yq[5, 5] = 1.0
+    bic = I.bicubic_interpolate(f, xq, yq, dx, dy, N, N)
+    a = 0.3 * np.sin(2 * np.pi * Y) * np.cos(np.pi * X) + 0.1
+    b = -0.2 * np.cos(2 * np.pi * X) * np.sin(np.pi * Y)
+    X1 = X + 0.02 * np.sin(2 * np.pi * Y); X2 = Y + 0.03 * np.sin(2 * np.pi * X)
+    phi = np.sqrt((X1 - 0.5) ** 2 + (X2 - 0.5) ** 2) - 0.3
+    dt = 0.2 * dx / 0.4
+    out = dict(N=N, dx=dx, dy=dy, f=f, xq=xq, yq=yq, bic=bic, a=a, b=b, X1=X1, X2=X2, phi=phi,
+               dt=dt)
+    out["sl_cubic"] = F.advect_reference_map(X1, a, b, X, Y, dt, dx, dy, phi, 'semilagrangian_cubic')
+    for name in ("central2", "conservative"):
+        for wc in (0.0, 2 * dx):
+            out[f"{name}_{int(wc > 0)}"] = F.advect_reference_map(X1, a, b, X, Y, dt, dx, dy, phi,
+                                                                 name, wc)
+    out["c2_rhs"] = F._central2_rhs(X1, a, b, dx, dy, phi, 0.0)
+    out["cons_rhs"] = F._conservative_rhs(X1, a, b, dx, dy, phi, 2 * dx)
+    save("schemes", **out)
+
+
 def gen_periodic(N=65):
     """functions.py:1177-1290 periodic branch on tests/test_poisson.py:24-78's fields."""
     X, Y, dx, dy = F.create_grid(N, N, 1.0, 1.0)
