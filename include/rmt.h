@@ -328,6 +328,35 @@ int rmt_mac_sim_step(rmt_mac_sim *sim, int nsteps, double t_end);
 int rmt_mac_sim_diagnostics(rmt_mac_sim *sim, rmt_mac_diag *out, int max_records,
                             int *n_records);
 
+/* The MAC step decomposed into row slabs (config 5 on several GPUs).
+ * No reference interface: pyRMT runs mac_multi_disc_lid.py:62-98 in one process.  Slab
+ * `rank` of G owns cell rows [row_splits[rank], row_splits[rank+1]) (even, > RMT_SLAB_HALO
+ * rows each) and column block [col_splits[rank], col_splits[rank+1]) of the transposed
+ * Poisson solve; ctx is the global N x N context.  The caller drives the phases and the
+ * collectives between them (order in mac.hip; pyrmt_amd/distributed.py MacDistributedSim).
+ * Buffers (rmt_mac_slab_buffer ids): 0 u ((hi-lo) x (N+1)), 1 v ((hi-lo+1) x N, face rows
+ * lo..hi), 2 p, 3 X1[disc], 4 X2[disc], 5 phi[disc] ((hi-lo) x N), 6 known bits[disc]
+ * (N x W words), 7 rim[disc] (owned cells x 3), 8 A, 9 B (transpose blocks), 10 scalars
+ * (RMT_MAC_SLAB_SCALARS doubles: [0] flags 1 non-finite / 2 halo / 4 extrapolation abort,
+ * [1] min J, [2] max J, [3] max|u|, [4 + 3k ..] disc k centroid sums (x, y, count),
+ * [28 + k] rim count of disc k, [36] row-tree root, [37] cells fitted). */
+#define RMT_MAC_SLAB_SCALARS 40
+typedef struct rmt_mac_slab rmt_mac_slab;
+int rmt_mac_slab_create(rmt_ctx *ctx, const rmt_mac_params *prm, int G, int rank,
+                        const int *row_splits, const int *col_splits, rmt_mac_slab **out);
+int rmt_mac_slab_destroy(rmt_mac_slab *slab);
+int rmt_mac_slab_info(rmt_mac_slab *slab, int *ints8);   /* r0 r1 lo hi c0 c1 W halo */
+int rmt_mac_slab_buffer(rmt_mac_slab *slab, int id, int disc, void **dev_ptr);
+int rmt_mac_slab_advect(rmt_mac_slab *slab, double dt);
+int rmt_mac_slab_rim_pack(rmt_mac_slab *slab);
+int rmt_mac_slab_extrapolate(rmt_mac_slab *slab, int disc, const double *gathered_rims,
+                             const long long *counts, long long cap);
+int rmt_mac_slab_predict(rmt_mac_slab *slab, double dt);
+int rmt_mac_slab_project_rows(rmt_mac_slab *slab, const double *dev_roots);
+int rmt_mac_slab_project_cols(rmt_mac_slab *slab);
+int rmt_mac_slab_project_unrows(rmt_mac_slab *slab);
+int rmt_mac_slab_correct(rmt_mac_slab *slab, double dt);
+
 #ifdef __cplusplus
 }
 #endif

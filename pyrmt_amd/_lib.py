@@ -124,6 +124,21 @@ SIGNATURES = {
     "rmt_slab_sub_mean": (_I, [_P, _I, _P]),
     "rmt_slab_project_correct": (_I, [_P, _D]),
     "rmt_slab_finish": (_I, [_P]),
+    # MAC slabs (distributed.py MacDistributedSim)
+    "rmt_mac_slab_create": (_I, [_P, ctypes.POINTER(rmt_mac_params), _I, _I, ctypes.POINTER(_I),
+                                 ctypes.POINTER(_I), ctypes.POINTER(_P)]),
+    "rmt_mac_slab_destroy": (_I, [_P]),
+    "rmt_mac_slab_info": (_I, [_P, ctypes.POINTER(_I)]),
+    "rmt_mac_slab_buffer": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
+    "rmt_mac_slab_advect": (_I, [_P, _D]),
+    "rmt_mac_slab_rim_pack": (_I, [_P]),
+    "rmt_mac_slab_extrapolate": (_I, [_P, _I, _P, ctypes.POINTER(ctypes.c_longlong),
+                                      ctypes.c_longlong]),
+    "rmt_mac_slab_predict": (_I, [_P, _D]),
+    "rmt_mac_slab_project_rows": (_I, [_P, _P]),
+    "rmt_mac_slab_project_cols": (_I, [_P]),
+    "rmt_mac_slab_project_unrows": (_I, [_P]),
+    "rmt_mac_slab_correct": (_I, [_P, _D]),
     # MAC path (mac.py)
     "rmt_mac_divergence": (_I, [_P, _P, _P, _D, _D, _P]),
     "rmt_mac_gradient_p": (_I, [_P, _P, _D, _D, _P, _P]),

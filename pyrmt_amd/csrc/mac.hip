@@ -16,6 +16,7 @@
 // Every formula keeps the reference's NumPy operation order; only sin (H), the DCT and the
 // reductions' summation order differ from the reference in the last bits.
 #include "rmt_internal.hpp"
+#include "extrap.hpp"
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -28,10 +29,13 @@ struct DiscSet {
     int K;
 };
 
+// Every kernel takes global row ranges and global-index plane pointers (pointer - lo * row
+// length), so the slab-decomposed step (rmt_mac_slab below) runs the same per-element code.
 __global__ void k_mac_centres(const double *__restrict__ u, const double *__restrict__ v, int N,
-                              double *__restrict__ uc, double *__restrict__ vc, int *bad) {
-    const long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)N * N) return;
+                              double *__restrict__ uc, double *__restrict__ vc, int *bad, int jb,
+                              int je) {
+    const long c = (long)jb * N + blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)je * N) return;
     const int j = (int)(c / N), i = (int)(c % N);
     const double a = 0.5 * (u[(long)j * (N + 1) + i] + u[(long)j * (N + 1) + i + 1]);
     const double b = 0.5 * (v[c] + v[c + N]);
@@ -89,12 +93,16 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
                                                        double eps, double *__restrict__ Sxx,
                                                        double *__restrict__ Sxy,
                                                        double *__restrict__ Syy,
-                                                       double *__restrict__ part) {
+                                                       double *__restrict__ part, int jb, int je,
+                                                       int jr0, int jr1) {
+    // S on rows [jb, je); the J range over rows [jr0, jr1)
     __shared__ double smin[MS_TPB], smax[MS_TPB];
     double jmin = 1.0, jmax = 1.0;
-    const long n = (long)N * N;
-    for (long c = blockIdx.x * (long)MS_TPB + threadIdx.x; c < n; c += (long)MS_BLOCKS * MS_TPB) {
+    const long n = (long)je * N;
+    for (long c = (long)jb * N + blockIdx.x * (long)MS_TPB + threadIdx.x; c < n;
+         c += (long)MS_BLOCKS * MS_TPB) {
         const int j = (int)(c / N), i = (int)(c % N);
+        const bool own = j >= jr0 && j < jr1;
         double axx = 0.0, axy = 0.0, ayy = 0.0;
         for (int k = 0; k < D.K; ++k) {
             Stress s{0.0, 0.0, 0.0, 1.0};
@@ -103,7 +111,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
                                   false, s);
             const double omh = 1 - heaviside(D.phi[k][c], w_t);
             axx = axx + omh * s.sxx; axy = axy + omh * s.sxy; ayy = ayy + omh * s.syy;
-            jmin = fmin(jmin, s.J); jmax = fmax(jmax, s.J);
+            if (own) { jmin = fmin(jmin, s.J); jmax = fmax(jmax, s.J); }
         }
         if (eta > 0)
             for (int a = 0; a < D.K; ++a)
@@ -140,18 +148,25 @@ __device__ __forceinline__ double divy_at(const double *Sxy, const double *Syy, 
 }
 
 // mac.py:196-232 with fu / fv of mac_multi_disc_lid.py:91-94 (S == nullptr: no force).
-// Threads [0, N(N+1)) take u faces, [N(N+1), 2N(N+1)) v faces.
+// Faces: u rows [F.u0, F.u1) (stride N + 1) then v rows [F.v0, F.v1) (stride N), one thread
+// each.
+struct FaceRows {
+    int u0, u1, v0, v1;
+};
+__host__ __device__ inline long face_count(const FaceRows &F, int N) {
+    return (long)(F.u1 - F.u0) * (N + 1) + (long)(F.v1 - F.v0) * N;
+}
 __global__ void k_mac_predict(const double *__restrict__ u, const double *__restrict__ v,
                               const double *__restrict__ Sxx, const double *__restrict__ Sxy,
                               const double *__restrict__ Syy, const double *__restrict__ fu,
                               const double *__restrict__ fv, int N, double nu, double dx,
                               double dy, double dx2, double dy2, double dt, double U, double rho,
-                              double *__restrict__ us, double *__restrict__ vs) {
+                              double *__restrict__ us, double *__restrict__ vs, FaceRows F) {
     // dx2, dy2: the reference's dx**2 on a Python float (libm pow), computed on the host
-    const long q = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    const long nf = (long)N * (N + 1);
+    const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
     const int W = N + 1;
-    if (q < nf) {   // u face (j, i), row stride N + 1
+    const long nuf = (long)(F.u1 - F.u0) * W, q = (long)F.u0 * W + t;
+    if (t < nuf) {   // u face (j, i), row stride N + 1
         const int j = (int)(q / W), i = (int)(q % W);
         if (i == 0 || i == N) { us[q] = 0.0; return; }
         const double uc = u[q], ul = u[q - 1], ur = u[q + 1];
@@ -166,8 +181,8 @@ __global__ void k_mac_predict(const double *__restrict__ u, const double *__rest
         if (Sxx) r = r + 0.5 * (divx_at(Sxx, Sxy, j, i, N, dx, dy) + divx_at(Sxx, Sxy, j, i - 1, N, dx, dy)) / rho;
         else if (fu) r = r + fu[q] / rho;
         us[q] = uc + dt * r;
-    } else if (q < 2 * nf) {   // v face (j, i), row stride N
-        const long p = q - nf;
+    } else if (t < nuf + (long)(F.v1 - F.v0) * N) {   // v face (j, i), row stride N
+        const long p = (long)F.v0 * N + (t - nuf);
         const int j = (int)(p / N), i = (int)(p % N);
         if (j == 0 || j == N) { vs[p] = 0.0; return; }
         const double vc = v[p], vd = v[p - N], vup = v[p + N];
@@ -187,9 +202,10 @@ __global__ void k_mac_predict(const double *__restrict__ u, const double *__rest
 
 // rhs = (rho / dt) * div(u*, v*)  (mac.py:81-84, 133-134)
 __global__ void k_mac_rhs(const double *__restrict__ u, const double *__restrict__ v, int N,
-                          double dx, double dy, double coef, double *__restrict__ rhs) {
-    const long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)N * N) return;
+                          double dx, double dy, double coef, double *__restrict__ rhs, int jb,
+                          int je) {
+    const long c = (long)jb * N + blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)je * N) return;
     const int j = (int)(c / N), i = (int)(c % N);
     const long cu = (long)j * (N + 1) + i;
     const double d = (u[cu + 1] - u[cu]) / dx + (v[c + N] - v[c]) / dy;
@@ -199,16 +215,17 @@ __global__ void k_mac_rhs(const double *__restrict__ u, const double *__restrict
 // u = u* - (dt/rho) grad_p_u(phi), v likewise (mac.py:87-101, 137-138)
 __global__ void k_mac_correct(const double *__restrict__ us, const double *__restrict__ vs,
                               const double *__restrict__ phi, int N, double dx, double dy,
-                              double c0, double *__restrict__ u, double *__restrict__ v) {
-    const long q = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    const long nf = (long)N * (N + 1);
-    if (q < nf) {
+                              double c0, double *__restrict__ u, double *__restrict__ v,
+                              FaceRows F) {
+    const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    const long nuf = (long)(F.u1 - F.u0) * (N + 1), q = (long)F.u0 * (N + 1) + t;
+    if (t < nuf) {
         const int j = (int)(q / (N + 1)), i = (int)(q % (N + 1));
         const double g = (i == 0 || i == N) ? 0.0 : (phi[(long)j * N + i] - phi[(long)j * N + i - 1]) / dx;
         u[q] = us[q] - c0 * g;
-    } else if (q < 2 * nf) {
-        const long p = q - nf;
-        const int j = (int)(p / N), i = (int)(p % N);
+    } else if (t < nuf + (long)(F.v1 - F.v0) * N) {
+        const long p = (long)F.v0 * N + (t - nuf);
+        const int j = (int)(p / N);
         const double g = (j == 0 || j == N) ? 0.0 : (phi[p] - phi[p - N]) / dy;
         v[p] = vs[p] - c0 * g;
     }
@@ -216,15 +233,18 @@ __global__ void k_mac_correct(const double *__restrict__ us, const double *__res
 
 // per-disc centroid sums over phi <= 0 (x, y, count) and max|u| partials
 constexpr int MD_VALS = 3 * MAC_MAXD + 1;
+// (rows [jb, je): cells and u faces)
 __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__restrict__ u,
-                                                     int N, double dx, double *__restrict__ part) {
+                                                     int N, double dx, double *__restrict__ part,
+                                                     int jb, int je) {
     __shared__ double s[MS_TPB];
     double acc[MD_VALS];
     for (int k = 0; k < MD_VALS; ++k) acc[k] = 0.0;
-    const long n = (long)N * N, nf = (long)N * (N + 1);
-    for (long c = blockIdx.x * (long)MS_TPB + threadIdx.x; c < nf; c += (long)MS_BLOCKS * MS_TPB) {
-        acc[3 * MAC_MAXD] = fmax(acc[3 * MAC_MAXD], fabs(u[c]));
-        if (c < n) {
+    const long n = (long)(je - jb) * N, nf = (long)(je - jb) * (N + 1);
+    for (long t = blockIdx.x * (long)MS_TPB + threadIdx.x; t < nf; t += (long)MS_BLOCKS * MS_TPB) {
+        acc[3 * MAC_MAXD] = fmax(acc[3 * MAC_MAXD], fabs(u[(long)jb * (N + 1) + t]));
+        if (t < n) {
+            const long c = (long)jb * N + t;
             const int j = (int)(c / N), i = (int)(c % N);
             const double xc = (i + 0.5) * dx, yc = (j + 0.5) * dx;
             for (int k = 0; k < D.K; ++k)
@@ -251,12 +271,12 @@ static int mac_project_impl(rmt_ctx *ctx, const double *us, const double *vs, do
     const int N = ctx->nx;
     const long n = (long)N * N, nf = (long)N * (N + 1);
     if (plan) RMT_TRY(dct2_plan(ctx, N, N, dx, dy));
-    k_mac_rhs<<<grid1d(n, 256), 256, 0, ctx->stream>>>(us, vs, N, dx, dy, rho / dt, rhs);
+    k_mac_rhs<<<grid1d(n, 256), 256, 0, ctx->stream>>>(us, vs, N, dx, dy, rho / dt, rhs, 0, N);
     RMT_LAUNCHED();
     RMT_TRY(sub_mean_rows(ctx, rhs, N, N));     // rhs - rhs.mean() (mac.py:135)
     RMT_TRY(dct2_solve(ctx, rhs, phi));
     k_mac_correct<<<grid1d(2 * nf, 256), 256, 0, ctx->stream>>>(us, vs, phi, N, dx, dy, dt / rho,
-                                                                u, v);
+                                                                u, v, FaceRows{0, N, 0, N + 1});
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -284,7 +304,8 @@ int rmt_mac_divergence(rmt_ctx *ctx, const double *u, const double *v, double dx
                        double *out) {
     RMT_CHECK(ctx && u && v && out && ctx->nx == ctx->ny, RMT_EINVAL, "bad argument");
     const long n = (long)ctx->nx * ctx->nx;
-    k_mac_rhs<<<grid1d(n, 256), 256, 0, ctx->stream>>>(u, v, ctx->nx, dx, dy, 1.0, out);
+    k_mac_rhs<<<grid1d(n, 256), 256, 0, ctx->stream>>>(u, v, ctx->nx, dx, dy, 1.0, out, 0,
+                                                       ctx->nx);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -298,7 +319,8 @@ int rmt_mac_gradient_p(rmt_ctx *ctx, const double *p, double dx, double dy, doub
     RMT_TRY(ensure_scratch(ctx, nf * sizeof(double)));
     RMT_HIP(hipMemsetAsync(ctx->scratch, 0, nf * sizeof(double), ctx->stream));
     k_mac_correct<<<grid1d(2 * nf, 256), 256, 0, ctx->stream>>>(ctx->scratch, ctx->scratch, p, N,
-                                                                dx, dy, -1.0, gu, gv);
+                                                                dx, dy, -1.0, gu, gv,
+                                                                FaceRows{0, N, 0, N + 1});
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -332,7 +354,7 @@ int rmt_mac_momentum_predictor(rmt_ctx *ctx, const double *u, const double *v, d
     const long nf = (long)N * (N + 1);
     k_mac_predict<<<grid1d(2 * nf, 256), 256, 0, ctx->stream>>>(
         u, v, nullptr, nullptr, nullptr, fu, fv, N, nu, dx, dy, std::pow(dx, 2.0),
-        std::pow(dy, 2.0), dt, U_lid, rho, us, vs);
+        std::pow(dy, 2.0), dt, U_lid, rho, us, vs, FaceRows{0, N, 0, N + 1});
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -416,7 +438,8 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         double dt = P.dt;
         if (S->t + dt > t_end) dt = t_end - S->t;
         RMT_HIP(hipMemsetAsync(S->flags, 0, 4 * sizeof(int), st));
-        k_mac_centres<<<grid1d(n, 256), 256, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags);
+        k_mac_centres<<<grid1d(n, 256), 256, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags, 0,
+                                                      N);
         RMT_LAUNCHED();
         for (int k = 0; k < K; ++k) {
             // phi from the current map (already S->phi[k]), advect with the pre-advection mask
@@ -430,17 +453,18 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
             RMT_LAUNCHED();
         }
         k_mac_stress<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, N, dx, dx, P.mu_s, w_t, P.eta, eps, S->Sxx,
-                                                    S->Sxy, S->Syy, S->part);
+                                                    S->Sxy, S->Syy, S->part, 0, N, 0, N);
         RMT_LAUNCHED();
         double jr[2 * MS_BLOCKS];
         RMT_HIP(hipMemcpyAsync(jr, S->part, sizeof(jr), hipMemcpyDeviceToHost, st));
         k_mac_predict<<<grid1d(2 * nf, 256), 256, 0, st>>>(S->u, S->v, S->Sxx, S->Sxy, S->Syy,
                                                             nullptr, nullptr, N, nu, dx, dx, dx2,
-                                                            dx2, dt, P.U_lid, P.rho, S->us, S->vs);
+                                                            dx2, dt, P.U_lid, P.rho, S->us, S->vs,
+                                                            FaceRows{0, N, 0, N + 1});
         RMT_LAUNCHED();
         RMT_TRY(mac_project_impl(ctx, S->us, S->vs, dx, dx, dt, P.rho, S->u, S->v, S->p,
                                  S->X1n));
-        k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, S->u, N, dx, S->part + 2 * MS_BLOCKS);
+        k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, S->u, N, dx, S->part + 2 * MS_BLOCKS, 0, N);
         RMT_LAUNCHED();
         std::vector<double> dp((size_t)MS_BLOCKS * MD_VALS);
         RMT_HIP(hipMemcpyAsync(dp.data(), S->part + 2 * MS_BLOCKS, dp.size() * 8,
@@ -490,6 +514,322 @@ int rmt_mac_contact_stress(rmt_ctx *ctx, const double *phi_a, const double *phi_
     const long n = (long)N * N;
     k_contact<<<grid1d(n, 256), 256, 0, ctx->stream>>>(phi_a, phi_b, N, eta, Gsum, eps, dx, dy,
                                                        txx, txy, tyy);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ MAC slabs (config 5) --
+// rmt_mac_sim's step decomposed into row slabs, as rmt_slab (slab.hip) decomposes the
+// cell-centred step.  Slab `rank` owns cell rows [r0, r1), u face rows [r0, r1) and v face
+// rows [r0, r1] (the face row r1 is computed by both neighbours, from the same inputs), and
+// keeps RMT_SLAB_HALO rows on either side resident.  Planes are addressed with GLOBAL
+// indices (pointer - lo * row length) so every kernel above runs unchanged on a row range.
+// Phases (collectives between them: pyrmt_amd/distributed.py, MacDistributedSim):
+//   halo(u, v, X1_k, X2_k)
+//   advect        centres on the resident rows; per disc SL-RK4 on rows r0-3 .. r1+3 and
+//                 the known bits of the owned rows
+//   allgather(bits_k); rim_pack (all discs); allgather(scalars); allgather(rim_k)
+//   extrapolate   per disc: dense replica, exact extrapolation, rim write-back, phi rebuilt
+//   predict       stress on rows r0-2 .. r1+2 (J range of the owned rows), predictor,
+//                 rhs of the owned rows and its row-tree root
+//   allgather(roots); project_rows (mean removed, DCT-II along x, column blocks packed)
+//   all_to_all; project_cols (DCT-II solve along y of the column block); all_to_all
+//   project_unrows (inverse DCT-II along x into p)
+//   halo(p, 1 row); correct (+ diagnostics partials -> scalar block); allgather(scalars)
+// With every slab holding 2^m rows at a multiple of 2^m the fields are bit-identical to
+// rmt_mac_sim's (the row-tree mean); the centroid sums differ in summation order only.
+namespace rmt {
+constexpr int MSL_MAXG = 64;
+enum { MS_FLAGS = 0, MS_JMIN = 1, MS_JMAX = 2, MS_UMAX = 3, MS_CEN = 4,
+       MS_COUNT = MS_CEN + 3 * MAC_MAXD, MS_ROOT = MS_COUNT + MAC_MAXD, MS_FIT = MS_ROOT + 1,
+       MS_N = MS_FIT + 3 };
+static_assert(MS_N == RMT_MAC_SLAB_SCALARS, "rmt.h scalar block size");
+
+// J range and diagnostics partials -> the scalar block; flags folded in
+__global__ void __launch_bounds__(256) k_mac_slab_scal(const double *__restrict__ part,
+                                                       const int *__restrict__ flags, int K,
+                                                       double *__restrict__ scal) {
+    __shared__ double s[256];
+    const int t = threadIdx.x;
+    const double *dp = part + 2 * MS_BLOCKS;
+    for (int v = 0; v < 2 + 3 * K + 1; ++v) {
+        // v: 0 J min, 1 J max, 2 .. 2+3K centroid sums, last max|u|
+        const int kind = v == 0 ? 0 : (v == 1 || v == 2 + 3 * K) ? 1 : 2;
+        double a = kind == 2 ? 0.0 : (kind == 0 ? 1.0 : (v == 1 ? 1.0 : 0.0));
+        for (int b = t; b < MS_BLOCKS; b += 256) {
+            const double x = v == 0 ? part[2 * b] : v == 1 ? part[2 * b + 1]
+                           : v == 2 + 3 * K ? dp[(long)b * MD_VALS + 3 * MAC_MAXD]
+                                            : dp[(long)b * MD_VALS + (v - 2)];
+            a = kind == 0 ? fmin(a, x) : kind == 1 ? fmax(a, x) : a + x;
+        }
+        s[t] = a;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (t < w) {
+                const double x = s[t + w];
+                s[t] = kind == 0 ? fmin(s[t], x) : kind == 1 ? fmax(s[t], x) : s[t] + x;
+            }
+            __syncthreads();
+        }
+        if (t == 0) {
+            const int o = v == 0 ? MS_JMIN : v == 1 ? MS_JMAX : v == 2 + 3 * K ? MS_UMAX
+                                                                               : MS_CEN + v - 2;
+            scal[o] = s[0];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        int fl = flags[0], fit = 0;
+        for (int k = 0; k < K; ++k) { fit += flags[4 + 2 * k]; fl |= flags[5 + 2 * k] ? 4 : 0; }
+        scal[MS_FLAGS] = (double)fl;
+        scal[MS_FIT] = (double)fit;
+    }
+}
+}  // namespace rmt
+
+struct rmt_mac_slab {
+    rmt_ctx *ctx = nullptr;
+    rmt_mac_params P{};
+    int G = 1, rank = 0, N = 0, W = 0, r0 = 0, r1 = 0, lo = 0, hi = 0, c0 = 0, c1 = 0;
+    int rs[rmt::MSL_MAXG + 1], cs[rmt::MSL_MAXG + 1];
+    void *block = nullptr;
+    double *u, *us;            // (hi - lo) x (N + 1)
+    double *v, *vs;            // (hi - lo + 1) x N: face rows lo .. hi
+    double *p, *uc, *vc, *Sxx, *Sxy, *Syy;
+    double *X1[RMT_MAC_MAXD], *X2[RMT_MAC_MAXD], *phi[RMT_MAC_MAXD];
+    double *X1n[RMT_MAC_MAXD], *X2n[RMT_MAC_MAXD], *phi_pre[RMT_MAC_MAXD];
+    double *X1d, *X2d;         // dense N x N extrapolation replica (shared by the discs)
+    u64 *bits[RMT_MAC_MAXD];   // N x W known planes
+    u64 *rimw;
+    int *rowcnt;
+    double *rim[RMT_MAC_MAXD]; // 3 doubles per owned cell
+    double *rhs, *A, *Y, *B, *T, *xs, *scal, *part;
+    int *flags;                // [0] flags, [4 + 2k, 5 + 2k] disc k {fitted, aborted}
+    double *gc(double *q) const { return q - (long)lo * N; }         // cells, v faces
+    double *gu(double *q) const { return q - (long)lo * (N + 1); }   // u faces
+    rmt::DiscSet discs() const {
+        rmt::DiscSet D{};
+        D.K = P.n_discs;
+        for (int k = 0; k < D.K; ++k) {
+            D.X1[k] = X1[k] - (long)lo * N; D.X2[k] = X2[k] - (long)lo * N;
+            D.phi[k] = phi[k] - (long)lo * N;
+        }
+        return D;
+    }
+};
+
+extern "C" {
+
+int rmt_mac_slab_create(rmt_ctx *ctx, const rmt_mac_params *prm, int G, int rank,
+                        const int *row_splits, const int *col_splits, rmt_mac_slab **out) {
+    RMT_CHECK(ctx && prm && row_splits && col_splits && out, RMT_EINVAL, "null argument");
+    RMT_CHECK(G >= 1 && G <= MSL_MAXG && rank >= 0 && rank < G, RMT_EINVAL, "slab: bad G/rank");
+    RMT_CHECK(prm->n_discs >= 1 && prm->n_discs <= RMT_MAC_MAXD, RMT_EINVAL, "1..8 discs");
+    const int N = prm->N;
+    RMT_CHECK(ctx->nx == N && ctx->ny == N, RMT_EINVAL, "slab: ctx must be the global N x N");
+    RMT_CHECK(N <= 8192, RMT_ENOTSUP, "MAC slab step: N <= 8192");
+    for (int k = 0; k < G; ++k) {
+        RMT_CHECK(row_splits[k + 1] - row_splits[k] >= RMT_SLAB_HALO + 1 && !(row_splits[k] & 1),
+                  RMT_EINVAL, "slab: row splits must be even, > RMT_SLAB_HALO rows each");
+        RMT_CHECK(col_splits[k + 1] - col_splits[k] >= 2 && !(col_splits[k] & 1), RMT_EINVAL,
+                  "slab: column splits must be even, >= 2 columns each");
+    }
+    RMT_CHECK(row_splits[0] == 0 && row_splits[G] == N && col_splits[0] == 0 &&
+                  col_splits[G] == N, RMT_EINVAL, "slab: splits must cover 0 .. N");
+    RMT_TRY(dct2_plan(ctx, N, N, prm->dx, prm->dx));
+    rmt_mac_slab *S = new rmt_mac_slab;
+    S->ctx = ctx; S->P = *prm; S->G = G; S->rank = rank; S->N = N; S->W = (N + 63) / 64;
+    for (int k = 0; k <= G; ++k) { S->rs[k] = row_splits[k]; S->cs[k] = col_splits[k]; }
+    S->r0 = row_splits[rank]; S->r1 = row_splits[rank + 1];
+    S->c0 = col_splits[rank]; S->c1 = col_splits[rank + 1];
+    S->lo = std::max(0, S->r0 - RMT_SLAB_HALO); S->hi = std::min(N, S->r1 + RMT_SLAB_HALO);
+    const int K = prm->n_discs, rows = S->r1 - S->r0;
+    const long nl = (long)(S->hi - S->lo) * N, nu = (long)(S->hi - S->lo) * (N + 1);
+    const long nv = (long)(S->hi - S->lo + 1) * N, no = (long)rows * N, nd = (long)N * N;
+    const long nc = S->c1 - S->c0, W = S->W;
+    const size_t dbl = 2 * nu + 2 * nv + 6 * nl + 6 * K * nl + 2 * nd + 3 * K * no + 3 * no +
+                       2 * nc * N + N + MS_N + (2 + MD_VALS) * MS_BLOCKS + 16;
+    const size_t bytes = dbl * 8 + (size_t)(K * N + rows) * W * 8 + (rows + 64) * 4 + 256;
+    RMT_HIP(hipMalloc(&S->block, bytes));
+    RMT_HIP(hipMemsetAsync(S->block, 0, bytes, ctx->stream));
+    double *q = (double *)S->block;
+    S->u = q; q += nu; S->us = q; q += nu;
+    S->v = q; q += nv; S->vs = q; q += nv;
+    double **pl[] = {&S->p, &S->uc, &S->vc, &S->Sxx, &S->Sxy, &S->Syy};
+    for (auto pp : pl) { *pp = q; q += nl; }
+    for (int k = 0; k < K; ++k) {
+        double **dk[] = {&S->X1[k], &S->X2[k], &S->phi[k], &S->X1n[k], &S->X2n[k],
+                         &S->phi_pre[k]};
+        for (auto pp : dk) { *pp = q; q += nl; }
+    }
+    S->X1d = q; q += nd;
+    S->X2d = q; q += nd;
+    for (int k = 0; k < K; ++k) { S->rim[k] = q; q += 3 * no; }
+    S->rhs = q; q += no;
+    S->A = q; q += no;
+    S->Y = q; q += no;
+    S->B = q; q += nc * N;
+    S->T = q; q += nc * N;
+    S->xs = q; q += N;
+    S->scal = q; q += MS_N;
+    S->part = q; q += (2 + MD_VALS) * MS_BLOCKS + 16;
+    u64 *b = (u64 *)q;
+    for (int k = 0; k < K; ++k) { S->bits[k] = b; b += (long)N * W; }
+    S->rimw = b; b += (long)rows * W;
+    S->rowcnt = (int *)b;
+    S->flags = S->rowcnt + rows + 32;
+    std::vector<double> g(N);
+    for (int i = 0; i < N; ++i) g[i] = i * prm->dx;   // mac_multi_disc_lid.py:41
+    RMT_HIP(hipMemcpyAsync(S->xs, g.data(), N * 8, hipMemcpyHostToDevice, ctx->stream));
+    RMT_TRY(ensure_bytes(ctx, extrap_workspace(N, N, prm->layers)));
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    *out = S;
+    return RMT_OK;
+}
+
+int rmt_mac_slab_destroy(rmt_mac_slab *S) {
+    if (!S) return RMT_OK;
+    hipFree(S->block);
+    delete S;
+    return RMT_OK;
+}
+
+int rmt_mac_slab_info(rmt_mac_slab *S, int *ints8) {
+    RMT_CHECK(S && ints8, RMT_EINVAL, "null argument");
+    const int v[8] = {S->r0, S->r1, S->lo, S->hi, S->c0, S->c1, S->W, RMT_SLAB_HALO};
+    for (int k = 0; k < 8; ++k) ints8[k] = v[k];
+    return RMT_OK;
+}
+
+int rmt_mac_slab_buffer(rmt_mac_slab *S, int id, int disc, void **ptr) {
+    RMT_CHECK(S && ptr, RMT_EINVAL, "null argument");
+    const bool per_disc = id == 3 || id == 4 || id == 5 || id == 6 || id == 7;
+    RMT_CHECK(id >= 0 && id <= 10 && (!per_disc || (disc >= 0 && disc < S->P.n_discs)),
+              RMT_EINVAL, "unknown buffer id / disc");
+    void *b[] = {S->u, S->v, S->p, per_disc ? S->X1[disc] : nullptr,
+                 per_disc ? S->X2[disc] : nullptr, per_disc ? S->phi[disc] : nullptr,
+                 per_disc ? (void *)S->bits[disc] : nullptr, per_disc ? S->rim[disc] : nullptr,
+                 S->A, S->B, S->scal};
+    *ptr = b[id];
+    return RMT_OK;
+}
+
+int rmt_mac_slab_advect(rmt_mac_slab *S, double dt) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    rmt_ctx *ctx = S->ctx;
+    const rmt_mac_params &P = S->P;
+    const int N = S->N;
+    RMT_HIP(hipMemsetAsync(S->flags, 0, 32 * sizeof(int), ctx->stream));
+    k_mac_centres<<<grid1d((long)(S->hi - S->lo) * N, 256), 256, 0, ctx->stream>>>(
+        S->gu(S->u), S->gc(S->v), N, S->gc(S->uc), S->gc(S->vc), S->flags, S->lo, S->hi);
+    RMT_LAUNCHED();
+    const int jb = std::max(0, S->r0 - 3), je = std::min(N, S->r1 + 3);
+    for (int k = 0; k < P.n_discs; ++k) {
+        RMT_TRY(slab_sl(ctx, S->gc(S->X1[k]), S->gc(S->X2[k]), S->gc(S->uc), S->gc(S->vc), S->xs,
+                        S->xs, N, N, dt, P.dx, P.dx, P.cx[k], P.cy[k], P.R[k], S->gc(S->X1n[k]),
+                        S->gc(S->X2n[k]), S->gc(S->phi_pre[k]), S->flags, jb, je, S->lo, S->hi));
+        RMT_TRY(slab_bits(ctx, S->gc(S->phi_pre[k]), N, S->W, S->bits[k], S->r0, S->r1));
+    }
+    return RMT_OK;
+}
+
+int rmt_mac_slab_rim_pack(rmt_mac_slab *S) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    for (int k = 0; k < S->P.n_discs; ++k)
+        RMT_TRY(slab_rim_pack(S->ctx, S->bits[k], S->N, S->N, S->W, S->r0, S->r1, S->rimw,
+                              S->rowcnt, S->gc(S->X1n[k]), S->gc(S->X2n[k]), S->rim[k],
+                              S->scal + MS_COUNT + k));
+    return RMT_OK;
+}
+
+int rmt_mac_slab_extrapolate(rmt_mac_slab *S, int disc, const double *gathered,
+                             const long long *counts, long long cap) {
+    RMT_CHECK(S && counts && (gathered || cap == 0) && disc >= 0 && disc < S->P.n_discs,
+              RMT_EINVAL, "bad argument");
+    rmt_ctx *ctx = S->ctx;
+    const rmt_mac_params &P = S->P;
+    const int N = S->N, k = disc;
+    RMT_TRY(slab_rim_extrapolate(ctx, gathered, counts, S->G, cap, S->X1d, S->X2d, S->bits[k],
+                                 P.dx, P.dx, P.layers, S->flags + 4 + 2 * k, S->gc(S->X1n[k]),
+                                 S->gc(S->X2n[k]), (long)S->lo * N, (long)S->hi * N));
+    const int jb = std::max(0, S->r0 - 3), je = std::min(N, S->r1 + 3);
+    const long o = (long)jb * N, n = (long)(je - jb) * N;
+    k_mac_phi<<<grid1d(n, 256), 256, 0, ctx->stream>>>(
+        S->gc(S->X1n[k]) + o, S->gc(S->X2n[k]) + o, n, P.cx[k], P.cy[k], P.R[k],
+        S->gc(S->X1[k]) + o, S->gc(S->X2[k]) + o, S->gc(S->phi[k]) + o);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int rmt_mac_slab_predict(rmt_mac_slab *S, double dt) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    rmt_ctx *ctx = S->ctx;
+    const rmt_mac_params &P = S->P;
+    const int N = S->N, rows = S->r1 - S->r0;
+    const double dx = P.dx, w_t = 2.0 * dx, eps = 3.0 * dx, nu = P.mu_f / P.rho;
+    const double dx2 = std::pow(dx, 2.0);
+    const DiscSet D = S->discs();
+    k_mac_stress<<<MS_BLOCKS, MS_TPB, 0, ctx->stream>>>(
+        D, N, dx, dx, P.mu_s, w_t, P.eta, eps, S->gc(S->Sxx), S->gc(S->Sxy), S->gc(S->Syy),
+        S->part, std::max(0, S->r0 - 2), std::min(N, S->r1 + 2), S->r0, S->r1);
+    RMT_LAUNCHED();
+    const FaceRows F{S->r0, S->r1, S->r0, std::min(S->r1 + 1, N + 1)};
+    k_mac_predict<<<grid1d(face_count(F, N), 256), 256, 0, ctx->stream>>>(
+        S->gu(S->u), S->gc(S->v), S->gc(S->Sxx), S->gc(S->Sxy), S->gc(S->Syy), nullptr, nullptr,
+        N, nu, dx, dx, dx2, dx2, dt, P.U_lid, P.rho, S->gu(S->us), S->gc(S->vs), F);
+    RMT_LAUNCHED();
+    double *rhs_g = S->rhs - (long)S->r0 * N;
+    k_mac_rhs<<<grid1d((long)rows * N, 256), 256, 0, ctx->stream>>>(
+        S->gu(S->us), S->gc(S->vs), N, dx, dx, P.rho / dt, rhs_g, S->r0, S->r1);
+    RMT_LAUNCHED();
+    return rowtree_root(ctx, S->rhs, rows, N, S->scal + MS_ROOT);
+}
+
+int rmt_mac_slab_project_rows(rmt_mac_slab *S, const double *roots) {
+    RMT_CHECK(S && roots, RMT_EINVAL, "null argument");
+    rmt_ctx *ctx = S->ctx;
+    const int N = S->N, rows = S->r1 - S->r0;
+    RMT_TRY(sub_tree_mean(ctx, S->rhs, (long)rows * N, roots, S->G, (double)N * N));
+    RMT_TRY(dct2_plan(ctx, N, N, S->P.dx, S->P.dx));
+    RMT_TRY(dct2_pass(ctx, 0, 0, S->rhs, S->Y, rows, 0));
+    return slab_cols(ctx, true, S->Y, rows, N, S->cs, S->G, S->A);
+}
+
+int rmt_mac_slab_project_cols(rmt_mac_slab *S) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    rmt_ctx *ctx = S->ctx;
+    const int nc = S->c1 - S->c0;
+    transpose(ctx->stream, S->B, S->N, nc, S->T);
+    RMT_TRY(dct2_pass(ctx, 1, 1, S->T, S->T, nc, S->c0));
+    transpose(ctx->stream, S->T, nc, S->N, S->B);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int rmt_mac_slab_project_unrows(rmt_mac_slab *S) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    rmt_ctx *ctx = S->ctx;
+    const int N = S->N, rows = S->r1 - S->r0;
+    RMT_TRY(slab_cols(ctx, false, S->Y, rows, N, S->cs, S->G, S->A));
+    return dct2_pass(ctx, 2, 0, S->Y, S->gc(S->p) + (long)S->r0 * N, rows, 0);
+}
+
+int rmt_mac_slab_correct(rmt_mac_slab *S, double dt) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    rmt_ctx *ctx = S->ctx;
+    const rmt_mac_params &P = S->P;
+    const int N = S->N;
+    const FaceRows F{S->r0, S->r1, S->r0, std::min(S->r1 + 1, N + 1)};
+    k_mac_correct<<<grid1d(face_count(F, N), 256), 256, 0, ctx->stream>>>(
+        S->gu(S->us), S->gc(S->vs), S->gc(S->p), N, P.dx, P.dx, dt / P.rho, S->gu(S->u),
+        S->gc(S->v), F);
+    RMT_LAUNCHED();
+    k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, ctx->stream>>>(S->discs(), S->gu(S->u), N, P.dx,
+                                                     S->part + 2 * MS_BLOCKS, S->r0, S->r1);
+    RMT_LAUNCHED();
+    k_mac_slab_scal<<<1, 256, 0, ctx->stream>>>(S->part, S->flags, P.n_discs, S->scal);
     RMT_LAUNCHED();
     return RMT_OK;
 }

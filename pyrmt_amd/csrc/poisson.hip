@@ -683,7 +683,7 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
 }
 
 // one DCT-II pass over nrows rows along axis (0: length nx, 1: length ny; MODE 1 needs 1)
-static int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst,
+int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst,
                      int nrows, int row0) {
     Dct2Plan *P = ctx->dct2;
     const int n = axis == 0 ? P->nx : P->ny;

@@ -426,6 +426,10 @@ void transpose(hipStream_t st, const double *in, int R, int C, double *out);
 int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);
 int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p);
 int dct2_set_lambda(rmt_ctx *ctx, const double *lamx, const double *lamy);
+// one DCT-II pass over nrows rows (mode 0 forward, 1 column solve with row0 = global
+// x-frequency of local row 0, 2 inverse; axis 0: length nx, 1: length ny)
+int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst, int nrows,
+              int row0);
 void dct2_destroy(Dct2Plan *P);
 void per_destroy(PerPlan *P);
 void dct_destroy(DctPlan *);
@@ -440,5 +444,24 @@ size_t extrap_workspace(int ny, int nx, int max_layers);   // bytes of ctx->byte
 // after extrapolate(): the MOM_TX x MOM_TY tiles within `margin` cells of a possible target
 // (device list + count); the momentum of every other cell ignores the extrapolated values
 int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *count);
+
+// --------------------------------------------------------- slab phases (slab.hip) --
+// shared by the cell-centred slabs (rmt_slab) and the MAC slabs (rmt_mac_slab, mac.hip);
+// plane pointers are global-index views (pointer - lo * nx)
+int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, const double *b,
+            const double *xs, const double *ys, int ny, int nx, double dt, double dx, double dy,
+            double x0, double y0, double R, double *X1n, double *X2n, double *phi_pre,
+            int *flags, int jb, int je, int lo, int hi);
+int slab_bits(rmt_ctx *ctx, const double *phi, int nx, int W, unsigned long long *bits, int r0,
+              int r1);
+int slab_rim_pack(rmt_ctx *ctx, const unsigned long long *bits, int ny, int nx, int W, int r0,
+                  int r1, unsigned long long *rimw, int *rowcnt, const double *X1n,
+                  const double *X2n, double *rim, double *count);
+int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *counts, int G,
+                         long long cap, double *X1d, double *X2d, const unsigned long long *bits,
+                         double dx, double dy, int layers, int *exflags, double *X1n,
+                         double *X2n, long c_lo, long c_hi);
+int slab_cols(rmt_ctx *ctx, bool pack, double *Y, int rows, int nx, const int *csplits, int G,
+              double *A);
 
 }  // namespace rmt

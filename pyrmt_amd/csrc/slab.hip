@@ -149,9 +149,9 @@ __global__ void __launch_bounds__(256) k_rim_words(const u64 *__restrict__ bits,
     for (int d = 32; d > 0; d >>= 1) cnt += __shfl_xor(cnt, d);
     if (lane == 0) rowcnt[j - r0] = cnt;
 }
-// exclusive scan of n <= 8192 row counts in place; total -> scal[SC_COUNT]
+// exclusive scan of n <= 8192 row counts in place; total -> *total
 __global__ void __launch_bounds__(1024) k_rim_scan(int *__restrict__ cnt, int n,
-                                                   double *__restrict__ scal) {
+                                                   double *__restrict__ total) {
     __shared__ long long s[1024];
     const int per = (n + 1023) / 1024, t = threadIdx.x, a = t * per, b = min(n, a + per);
     long long loc = 0;
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(1024) k_rim_scan(int *__restrict__ cnt, int n,
     }
     long long run = s[t] - loc;
     for (int k = a; k < b; ++k) { const int c = cnt[k]; cnt[k] = (int)run; run += c; }
-    if (t == 1023) scal[SC_COUNT] = (double)s[1023];
+    if (t == 1023) *total = (double)s[1023];
 }
 // (global index, X1, X2) of every rim cell, raster order
 __global__ void __launch_bounds__(256) k_rim_emit(const u64 *__restrict__ rimw,
@@ -266,6 +266,73 @@ static int check_splits(const int *s, int G, int n, int minsz, bool even) {
         if (s[k + 1] - s[k] < minsz) return RMT_EINVAL;
         if (even && (s[k] & 1)) return RMT_EINVAL;
     }
+    return RMT_OK;
+}
+
+
+// ------------------------------------------- shared with the MAC slabs (mac.hip) --
+int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, const double *b,
+            const double *xs, const double *ys, int ny, int nx, double dt, double dx, double dy,
+            double x0, double y0, double R, double *X1n, double *X2n, double *phi_pre,
+            int *flags, int jb, int je, int lo, int hi) {
+    if (je <= jb) return RMT_OK;
+    k_slab_sl<<<grid1d((long)(je - jb) * nx, 256), 256, 0, ctx->stream>>>(
+        X1, X2, a, b, xs, ys, ny, nx, dt, dx, dy, x0, y0, R, X1n, X2n, phi_pre, flags, jb, je,
+        lo, hi);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int slab_bits(rmt_ctx *ctx, const double *phi, int nx, int W, u64 *bits, int r0, int r1) {
+    k_slab_bits<<<dim3((nx + 255) / 256, r1 - r0), 256, 0, ctx->stream>>>(phi, nx, W, bits, r0);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int slab_rim_pack(rmt_ctx *ctx, const u64 *bits, int ny, int nx, int W, int r0, int r1,
+                  u64 *rimw, int *rowcnt, const double *X1n, const double *X2n, double *rim,
+                  double *count) {
+    const int rows = r1 - r0;
+    k_rim_words<<<(rows + 3) / 4, 256, 0, ctx->stream>>>(bits, ny, nx, W, r0, r1, rimw, rowcnt);
+    k_rim_scan<<<1, 1024, 0, ctx->stream>>>(rowcnt, rows, count);
+    k_rim_emit<<<(rows + 3) / 4, 256, 0, ctx->stream>>>(rimw, rowcnt, W, nx, r0, r1, X1n, X2n,
+                                                        rim);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *counts, int G,
+                         long long cap, double *X1d, double *X2d, const u64 *bits, double dx,
+                         double dy, int layers, int *exflags, double *X1n, double *X2n,
+                         long c_lo, long c_hi) {
+    Counts cn{};
+    for (int k = 0; k < G; ++k) {
+        RMT_CHECK(counts[k] >= 0 && counts[k] <= cap, RMT_EINVAL, "slab: rim count > cap");
+        cn.c[k] = counts[k];
+    }
+    const long tot = (long)G * cap;
+    if (tot > 0) {
+        k_rim_unpack<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, G, cap, X1d, X2d);
+        RMT_LAUNCHED();
+    }
+    RMT_TRY(extrapolate(ctx, X1d, X2d, nullptr, dx, dy, layers, X1d, X2d, exflags, bits));
+    if (tot > 0) {
+        k_rim_writeback<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, G, cap, X1d, X2d,
+                                                                   X1n, X2n, c_lo, c_hi);
+        RMT_LAUNCHED();
+    }
+    return RMT_OK;
+}
+
+int slab_cols(rmt_ctx *ctx, bool pack, double *Y, int rows, int nx, const int *csplits, int G,
+              double *A) {
+    Splits cs{};
+    for (int k = 0; k <= G; ++k) cs.v[k] = csplits[k];
+    const long no = (long)rows * nx;
+    if (no == 0) return RMT_OK;
+    if (pack) k_cols<true><<<grid1d(no, 256), 256, 0, ctx->stream>>>(Y, rows, nx, cs, G, A);
+    else k_cols<false><<<grid1d(no, 256), 256, 0, ctx->stream>>>(Y, rows, nx, cs, G, A);
+    RMT_LAUNCHED();
     return RMT_OK;
 }
 
@@ -397,16 +464,8 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
 
 int rmt_slab_rim_pack(rmt_slab *S) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
-    rmt_ctx *ctx = S->ctx;
-    const int rows = S->r1 - S->r0;
-    k_rim_words<<<(rows + 3) / 4, 256, 0, ctx->stream>>>(S->bits, S->NY, S->NX, S->W, S->r0,
-                                                         S->r1, S->rimw, S->rowcnt);
-    k_rim_scan<<<1, 1024, 0, ctx->stream>>>(S->rowcnt, rows, S->scal);
-    k_rim_emit<<<(rows + 3) / 4, 256, 0, ctx->stream>>>(S->rimw, S->rowcnt, S->W, S->NX, S->r0,
-                                                        S->r1, S->gv(S->X1n), S->gv(S->X2n),
-                                                        S->rim);
-    RMT_LAUNCHED();
-    return RMT_OK;
+    return slab_rim_pack(S->ctx, S->bits, S->NY, S->NX, S->W, S->r0, S->r1, S->rimw, S->rowcnt,
+                         S->gv(S->X1n), S->gv(S->X2n), S->rim, S->scal + SC_COUNT);
 }
 
 int rmt_slab_extrapolate(rmt_slab *S, const double *gathered, const long long *counts,
@@ -414,25 +473,9 @@ int rmt_slab_extrapolate(rmt_slab *S, const double *gathered, const long long *c
     RMT_CHECK(S && counts && (gathered || cap == 0), RMT_EINVAL, "null argument");
     rmt_ctx *ctx = S->ctx;
     const rmt_sim_params &P = S->P;
-    Counts cn{};
-    for (int k = 0; k < S->G; ++k) {
-        RMT_CHECK(counts[k] >= 0 && counts[k] <= cap, RMT_EINVAL, "slab: rim count > cap");
-        cn.c[k] = counts[k];
-    }
-    const long tot = (long)S->G * cap;
-    if (tot > 0) {
-        k_rim_unpack<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, S->G, cap, S->X1d,
-                                                                S->X2d);
-        RMT_LAUNCHED();
-    }
-    RMT_TRY(extrapolate(ctx, S->X1d, S->X2d, nullptr, P.dx, P.dy, P.layers, S->X1d, S->X2d,
-                        S->flags + 4, S->bits));
-    if (tot > 0) {
-        k_rim_writeback<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(
-            gathered, cn, S->G, cap, S->X1d, S->X2d, S->gv(S->X1n), S->gv(S->X2n),
-            (long)S->lo * S->NX, (long)S->hi * S->NX);
-        RMT_LAUNCHED();
-    }
+    RMT_TRY(slab_rim_extrapolate(ctx, gathered, counts, S->G, cap, S->X1d, S->X2d, S->bits, P.dx,
+                                 P.dy, P.layers, S->flags + 4, S->gv(S->X1n), S->gv(S->X2n),
+                                 (long)S->lo * S->NX, (long)S->hi * S->NX));
     const int jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
     k_slab_phi<<<grid1d((long)(je - jb) * S->NX, 256), 256, 0, ctx->stream>>>(
         S->gv(S->X1n), S->gv(S->X2n), P.x0, P.y0, P.R, S->NX, jb, je, S->gv(S->phi),

@@ -66,15 +66,16 @@ class LocalComm:
         with torch.no_grad():
             for k, s in enumerate(slabs):
                 for name in planes:
-                    dst = s.view(name)
+                    dst, e = s.view(name), s.top_extra(name)
                     if k > 0:                      # rows [r0 - n, r0) from slab k - 1
                         o = slabs[k - 1]
                         a = max(s.r0 - nrows, s.lo)
                         dst[a - s.lo:s.r0 - s.lo].copy_(o.view(name)[a - o.lo:s.r0 - o.lo])
-                    if k + 1 < len(slabs):         # rows [r1, r1 + n) from slab k + 1
+                    if k + 1 < len(slabs):         # rows [r1 + e, r1 + e + n) from slab k + 1
                         o = slabs[k + 1]
-                        b = min(s.r1 + nrows, s.hi)
-                        dst[s.r1 - s.lo:b - s.lo].copy_(o.view(name)[s.r1 - o.lo:b - o.lo])
+                        t = s.r1 + e
+                        b = min(t + nrows, s.hi + e)
+                        dst[t - s.lo:b - s.lo].copy_(o.view(name)[t - o.lo:b - o.lo])
 
     def allgather_rows(self, slabs, name):
         for s in slabs:
@@ -135,18 +136,23 @@ class TorchComm:
         dist, k = self.dist, self.rank
         ops, post = [], []
         for name in planes:
-            v = s.view(name)
+            v, e = s.view(name), s.top_extra(name)
+            # a plane with e extra top rows (the MAC v faces: rows lo .. hi) owns rows
+            # [r0, r1 + e); the neighbours' counts match because every slab holds more than
+            # `nrows` rows
             if k > 0:
                 a = max(s.r0 - nrows, s.lo)
-                snd = self._host(v[s.r0 - s.lo:s.r0 - s.lo + (s.r0 - a)].contiguous())
+                o = s.r0 + e - s.lo
+                snd = self._host(v[o:o + (s.r0 - a)].contiguous())
                 rcv = v[a - s.lo:s.r0 - s.lo]
                 rb = rcv.cpu() if self.staged else rcv
                 ops += [(dist.isend, snd, k - 1), (dist.irecv, rb, k - 1)]
                 post.append((rcv, rb))
             if k + 1 < self.G:
-                b = min(s.r1 + nrows, s.hi)
-                snd = self._host(v[s.r1 - s.lo - (b - s.r1):s.r1 - s.lo].contiguous())
-                rcv = v[s.r1 - s.lo:b - s.lo]
+                t = s.r1 + e
+                b = min(t + nrows, s.hi + e)
+                snd = self._host(v[s.r1 - s.lo - (b - t):s.r1 - s.lo].contiguous())
+                rcv = v[t - s.lo:b - s.lo]
                 rb = rcv.cpu() if self.staged else rcv
                 ops += [(dist.isend, snd, k + 1), (dist.irecv, rb, k + 1)]
                 post.append((rcv, rb))
@@ -256,6 +262,9 @@ class Slab:
                 t = t.view(torch.int64)
             self._views[name] = t
         return self._views[name]
+
+    def top_extra(self, name):
+        return 0
 
     def a2a_splits(self):
         """element counts: forward send (to m: rows_me x nc_m), forward recv (from k:
@@ -454,4 +463,203 @@ def soft_disc_in_lid_driven(N, comm):
     X1, X2 = initial_disc_map(N, *kw["disc"], kw["layers"])
     z = np.zeros((N, N))
     sim.set_state(u=z, v=z, p=z, X1=X1, X2=X2)
+    return sim
+
+
+# ------------------------------------------------------------ MAC slabs (config 5) --
+MS_N = 40            # RMT_MAC_SLAB_SCALARS
+MS_FLAGS, MS_JMIN, MS_JMAX, MS_UMAX, MS_CEN, MS_COUNT, MS_ROOT, MS_FIT = 0, 1, 2, 3, 4, 28, 36, 37
+MBUF = {"u": 0, "v": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5, "bits": 6, "rim": 7, "A": 8,
+        "B": 9, "scal": 10}
+
+
+class MacSlab(Slab):
+    """One rmt_mac_slab: cell rows [r0, r1) resident as [lo, hi); u faces like the cells,
+    v faces rows lo .. hi (one extra top row).  Per-disc planes are named "X1:k"."""
+
+    def __init__(self, ctx, params, G, rank, rsplits, csplits):
+        self.lib = L.lib()
+        rs = (ctypes.c_int * (G + 1))(*rsplits)
+        cs = (ctypes.c_int * (G + 1))(*csplits)
+        h = ctypes.c_void_p()
+        L.check(self.lib.rmt_mac_slab_create(ctx.bind(), ctypes.byref(params), G, rank, rs, cs,
+                                             ctypes.byref(h)), "rmt_mac_slab_create")
+        self.h = h
+        info = (ctypes.c_int * 8)()
+        L.check(self.lib.rmt_mac_slab_info(h, info))
+        self.r0, self.r1, self.lo, self.hi, self.c0, self.c1, self.W, _ = list(info)
+        self.G, self.rank, self.splits, self.csplits = G, rank, list(rsplits), list(csplits)
+        self.NY = self.NX = self.N = params.N
+        self._views = {}
+
+    def __del__(self):
+        try:
+            self.lib.rmt_mac_slab_destroy(self.h)
+        except Exception:
+            pass
+
+    def top_extra(self, name):
+        return 1 if name == "v" else 0
+
+    def view(self, name):
+        if name not in self._views:
+            torch = F._torch()
+            base, _, disc = name.partition(":")
+            p = ctypes.c_void_p()
+            L.check(self.lib.rmt_mac_slab_buffer(self.h, MBUF[base], int(disc or 0),
+                                                 ctypes.byref(p)))
+            N, nl, no = self.N, self.hi - self.lo, self.r1 - self.r0
+            nc = self.c1 - self.c0
+            shape = {"u": (nl, N + 1), "v": (nl + 1, N), "bits": (N, self.W),
+                     "rim": (no * N, 3), "A": (no * N,), "B": (N * nc,),
+                     "scal": (MS_N,)}.get(base, (nl, N))
+            t = _wrap_device(torch, p.value, shape)
+            if base == "bits":
+                t = t.view(torch.int64)
+            self._views[name] = t
+        return self._views[name]
+
+
+class MacDistributedSim:
+    """The config-5 MAC step of rmt_mac_sim (mac.hip) decomposed into G row slabs.
+
+    ``comm`` is a LocalComm or a TorchComm, as for DistributedSim.  Fields are bit-identical
+    to ``mac.MacMultiDisc`` when every slab holds 2^m rows at a multiple of 2^m; the centroid
+    diagnostics differ in summation order only.
+    """
+
+    def __init__(self, N, comm, specs, **physics):
+        from .mac import mac_params
+        torch = F._torch()
+        self.torch, self.comm, self.N, self.G = torch, comm, N, comm.G
+        self.specs = list(specs)
+        self.K = len(self.specs)
+        self.params, self.dt = mac_params(N, self.specs, **physics)
+        self.dx = self.params.dx
+        self.rsplits = even_splits(N, self.G, HALO + 1)
+        self.csplits = even_splits(N, self.G, 2)
+        self.ctx = F.ctx_for(N, N)
+        self.slabs = [MacSlab(self.ctx, self.params, self.G, r, self.rsplits, self.csplits)
+                      for r in comm.ranks]
+        self.t = 0.0
+        self.records = []
+        self._counts = (ctypes.c_longlong * self.G)()
+
+    def set_state(self, u=None, v=None, p=None, maps=None):
+        """Full host arrays (u (N, N+1), v (N+1, N), p (N, N), maps [(X1, X2, phi)] per disc)
+        -> every slab's resident rows."""
+        torch = self.torch
+        items = [("u", u), ("v", v), ("p", p)]
+        for k, m in enumerate(maps or ()):
+            items += [(f"X1:{k}", m[0]), (f"X2:{k}", m[1]), (f"phi:{k}", m[2])]
+        for name, arr in items:
+            if arr is None:
+                continue
+            a = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.float64))
+            for s in self.slabs:
+                dst = s.view(name)
+                dst.copy_(a[s.lo:s.hi + s.top_extra(name)].to(dst.device))
+
+    def gather(self, name):
+        """The owned rows of every slab assembled into the full host array (v: N + 1 rows)."""
+        torch = self.torch
+        torch.cuda.synchronize()
+        e = self.slabs[0].top_extra(name)
+        last = self.G - 1
+        def own(s):
+            return s.view(name)[s.r0 - s.lo:s.r1 - s.lo + (e if s.rank == last else 0)]
+        if isinstance(self.comm, LocalComm):
+            return torch.cat([own(s) for s in self.slabs]).cpu().numpy()
+        (s,) = self.slabs
+        mine = own(s).contiguous()
+        mx = max(self.rsplits[k + 1] - self.rsplits[k] for k in range(self.G)) + e
+        pad = torch.zeros((mx, mine.shape[1]), dtype=torch.float64, device=mine.device)
+        pad[:mine.shape[0]].copy_(mine)
+        (g,) = self.comm.allgather([pad])
+        g = g.reshape(self.G, mx, mine.shape[1]).cpu().numpy()
+        return np.concatenate([g[k, :self.rsplits[k + 1] - self.rsplits[k] + (e if k == last else 0)]
+                               for k in range(self.G)])
+
+    def _call(self, fn, *args):
+        for s in self.slabs:
+            L.check(getattr(s.lib, fn)(s.h, *args), fn)
+
+    def _scalars(self):
+        g = self.comm.allgather([s.view("scal") for s in self.slabs])[0]
+        return g.cpu().numpy().reshape(self.G, MS_N)
+
+    def step(self, nsteps=1, t_end=math.inf):
+        self.ctx.bind()
+        comm, S, K = self.comm, self.slabs, self.K
+        halo_planes = ["u", "v"] + [f"X{a}:{k}" for k in range(K) for a in (1, 2)]
+        for _ in range(nsteps):
+            if not (self.t < t_end):
+                break
+            dt = self.dt
+            if self.t + dt > t_end:
+                dt = t_end - self.t
+            comm.halo(S, halo_planes, HALO)
+            self._call("rmt_mac_slab_advect", dt)
+            for k in range(K):
+                comm.allgather_rows(S, f"bits:{k}")
+            self._call("rmt_mac_slab_rim_pack")
+            sc = self._scalars()
+            for k in range(K):
+                counts = [int(c) for c in sc[:, MS_COUNT + k]]
+                gathered, cap = comm.allgather_padded([s.view(f"rim:{k}") for s in S], counts, 3)
+                for r, c in enumerate(counts):
+                    self._counts[r] = c
+                for s, g in zip(S, gathered):
+                    L.check(s.lib.rmt_mac_slab_extrapolate(s.h, k, g.data_ptr(), self._counts,
+                                                           cap), "rmt_mac_slab_extrapolate")
+            self._call("rmt_mac_slab_predict", dt)
+            roots = comm.allgather([s.view("scal")[MS_ROOT:MS_ROOT + 1] for s in S])
+            for s, r in zip(S, roots):
+                L.check(s.lib.rmt_mac_slab_project_rows(s.h, r.data_ptr()),
+                        "rmt_mac_slab_project_rows")
+            sp = [s.a2a_splits() for s in S]
+            comm.all_to_all([s.view("A") for s in S], [s.view("B") for s in S],
+                            [x[0] for x in sp], [x[1] for x in sp])
+            self._call("rmt_mac_slab_project_cols")
+            comm.all_to_all([s.view("B") for s in S], [s.view("A") for s in S],
+                            [x[1] for x in sp], [x[0] for x in sp])
+            self._call("rmt_mac_slab_project_unrows")
+            comm.halo(S, ("p",), 1)
+            self._call("rmt_mac_slab_correct", dt)
+            sc = self._scalars()
+            self.t += dt
+            self._record(sc, dt)
+
+    def _record(self, sc, dt):
+        fl = int(np.bitwise_or.reduce(sc[:, MS_FLAGS].astype(np.int64)))
+        if fl & 1:
+            raise FloatingPointError("advect_reference_map: non-finite velocity (the "
+                                     "simulation diverged)")
+        if fl & 2:
+            raise L.RMTError("MAC slab step: a departure point left the halo rows")
+        if fl & 4:
+            raise L.RMTError("extrapolation sweep aborted (progress wait timed out)")
+        rec = {"t": self.t, "dt": dt, "minJ": float(sc[:, MS_JMIN].min()),
+               "maxJ": float(sc[:, MS_JMAX].max()), "umax": float(sc[:, MS_UMAX].max()),
+               "fitted": int(sc[:, MS_FIT].sum())}
+        cen = sc[:, MS_CEN:MS_CEN + 3 * self.K].sum(axis=0)
+        rec["cx"] = [cen[3 * k] / cen[3 * k + 2] if cen[3 * k + 2] > 0 else math.nan
+                     for k in range(self.K)]
+        rec["cy"] = [cen[3 * k + 1] / cen[3 * k + 2] if cen[3 * k + 2] > 0 else math.nan
+                     for k in range(self.K)]
+        self.records.append(rec)
+
+    def diagnostics(self):
+        keys = self.records[0].keys() if self.records else ()
+        return {k: np.array([r[k] for r in self.records]) for k in keys}
+
+
+def mac_multi_disc_lid(N, comm, n_discs=3, seed=3, specs=None, **physics):
+    """Config 5 (benchmarks/mac_multi_disc_lid.py:36-98) decomposed over comm.G slabs, from
+    the driver's initial condition (same disc placement as mac.MacMultiDisc)."""
+    from .mac import place_discs, initial_maps
+    specs = list(specs) if specs is not None else place_discs(n_discs, seed)
+    sim = MacDistributedSim(N, comm, specs, **physics)
+    z = np.zeros
+    sim.set_state(u=z((N, N + 1)), v=z((N + 1, N)), p=z((N, N)), maps=initial_maps(N, specs))
     return sim

@@ -138,6 +138,38 @@ def place_discs(n, seed, Rrange=(0.07, 0.12), box=(0.18, 0.82)):
     return discs
 
 
+def mac_params(N, specs, U_lid=1.0, mu_s=0.3, mu_f=0.01, rho=1.0, eta=2.0):
+    """rmt_mac_params and the fixed dt of mac_multi_disc_lid.py:36-60."""
+    dx, _ = mac_grid(N, N)
+    specs = list(specs)
+    if not 1 <= len(specs) <= 8:
+        raise ValueError("1..8 discs")
+    cs = np.sqrt(mu_s / rho)
+    dt = min(0.3 * dx / U_lid, 0.2 * dx * dx / (mu_f / rho), 0.3 * dx / (cs + 1e-9))
+    P = L.rmt_mac_params()
+    P.N = N; P.dx = dx; P.n_discs = len(specs)
+    for k, (R, cx, cy) in enumerate(specs):
+        P.R[k], P.cx[k], P.cy[k] = R, cx, cy
+    P.U_lid, P.mu_s, P.mu_f, P.rho, P.eta = U_lid, mu_s, mu_f, rho, eta
+    P.layers = 3
+    P.dt = float(dt)
+    return P, float(dt)
+
+
+def initial_maps(N, specs):
+    """(X1, X2, phi) per disc (mac_multi_disc_lid.py:51-56): xi = x_c * mask, extrapolated."""
+    dx, dy = mac_grid(N, N)
+    xc = (np.arange(N) + 0.5) * dx
+    Xc, Yc = np.meshgrid(xc, xc)
+    out = []
+    for R, cx, cy in specs:
+        phi = np.sqrt((Xc - cx) ** 2 + (Yc - cy) ** 2) - R
+        m = (phi <= 0).astype(float)
+        X1, X2 = extrapolate_reference_map(Xc * m, Yc * m, phi, dx, dy, 3)
+        out.append((X1, X2, np.sqrt((X1 - cx) ** 2 + (X2 - cy) ** 2) - R))
+    return out
+
+
 class MacMultiDisc:
     """benchmarks/mac_multi_disc_lid.py:36-98 on the GPU (rmt_mac_sim_*): state (u, v, p and
     every disc's X1, X2, phi) stays in HBM; one host sync per step reads the diagnostics."""
@@ -155,31 +187,17 @@ class MacMultiDisc:
         self.specs = list(specs) if specs is not None else place_discs(n_discs, seed)
         if not 1 <= len(self.specs) <= 8:
             raise ValueError("1..8 discs")
-        cs = np.sqrt(mu_s / rho)
-        self.dt = min(0.3 * dx / U_lid, 0.2 * dx * dx / (mu_f / rho), 0.3 * dx / (cs + 1e-9))
-        P = L.rmt_mac_params()
-        P.N = N; P.dx = dx; P.n_discs = len(self.specs)
-        for k, (R, cx, cy) in enumerate(self.specs):
-            P.R[k], P.cx[k], P.cy[k] = R, cx, cy
-        P.U_lid, P.mu_s, P.mu_f, P.rho, P.eta = U_lid, mu_s, mu_f, rho, eta
-        P.layers = 3
-        P.dt = float(self.dt)
+        P, self.dt = mac_params(N, self.specs, U_lid, mu_s, mu_f, rho, eta)
         self.ctx = ctx_for(N, N)
         h = ctypes.c_void_p()
         L.check(L.lib().rmt_mac_sim_create(self.ctx.bind(), ctypes.byref(P), ctypes.byref(h)),
                 "rmt_mac_sim_create")
         self.h, self.params = h, P
         self._views = {}
-        # initial maps (mac_multi_disc_lid.py:51-56): xi = x_c * mask, then extrapolated
-        xc = (np.arange(N) + 0.5) * dx
-        Xc, Yc = np.meshgrid(xc, xc)
-        for k, (R, cx, cy) in enumerate(self.specs):
-            phi = np.sqrt((Xc - cx) ** 2 + (Yc - cy) ** 2) - R
-            m = (phi <= 0).astype(float)
-            X1, X2 = extrapolate_reference_map(Xc * m, Yc * m, phi, dx, dy, 3)
+        for k, (X1, X2, phi) in enumerate(initial_maps(N, self.specs)):
             self.field("X1", k).copy_(torch.as_tensor(X1))
             self.field("X2", k).copy_(torch.as_tensor(X2))
-            self.field("phi", k).copy_(torch.as_tensor(np.sqrt((X1 - cx) ** 2 + (X2 - cy) ** 2) - R))
+            self.field("phi", k).copy_(torch.as_tensor(phi))
 
     def __del__(self):
         try:

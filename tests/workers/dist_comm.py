@@ -30,10 +30,18 @@ class FakeSlab:
             "rim": torch.randn(50, 3, generator=g, dtype=torch.float64),
             "A": torch.randn(200, generator=g, dtype=torch.float64),
             "B": torch.zeros(200, dtype=torch.float64),
+            # a MAC v-face plane: rows lo .. hi, owned rows [r0, r1 + 1)
+            "vf": torch.randn(nl + 1, NX, generator=g, dtype=torch.float64),
         }
+        gv = torch.Generator().manual_seed(seed)
+        self.truth = torch.randn(N + 1, NX, generator=gv, dtype=torch.float64)
+        self.v["vf"][self.r0 - self.lo:self.r1 + 1 - self.lo] = self.truth[self.r0:self.r1 + 1]
 
     def view(self, name):
         return self.v[name]
+
+    def top_extra(self, name):
+        return 1 if name == "vf" else 0
 
 
 def main():
@@ -50,6 +58,11 @@ def main():
     tc.halo([mine], ("pc",), 2)
     lc.halo(allr, ("pc",), 2)
     assert torch.equal(mine.view("pc"), allr[rank].view("pc")), "halo 2 rows"
+    # face plane with one extra top row: every resident row equals the global plane
+    tc.halo([mine], ("vf",), HALO)
+    lc.halo(allr, ("vf",), HALO)
+    assert torch.equal(mine.view("vf"), allr[rank].view("vf")), "halo faces"
+    assert torch.equal(mine.view("vf"), mine.truth[mine.lo:mine.hi + 1]), "halo faces truth"
     # known-bit rows
     tc.allgather_rows([mine], "bits")
     lc.allgather_rows(allr, "bits")
