@@ -339,8 +339,11 @@ int rmt_mac_sim_diagnostics(rmt_mac_sim *sim, rmt_mac_diag *out, int max_records
  * (N x W words), 7 rim[disc] (owned cells x 3), 8 A, 9 B (transpose blocks), 10 scalars
  * (RMT_MAC_SLAB_SCALARS doubles: [0] flags 1 non-finite / 2 halo / 4 extrapolation abort,
  * [1] min J, [2] max J, [3] max|u|, [4 + 3k ..] disc k centroid sums (x, y, count),
- * [28 + k] rim count of disc k, [36] row-tree root, [37] cells fitted). */
-#define RMT_MAC_SLAB_SCALARS 40
+ * [28 + k] rim count of disc k, [36] row-tree root, [37] cells fitted, [38 + k] 1 if
+ * an extrapolation target of disc k in the owned rows fits (0 on every slab: the disc's
+ * extrapolation is the identity, rmt_mac_slab_extrapolate_identity replaces the rim
+ * allgather + rmt_mac_slab_extrapolate)). */
+#define RMT_MAC_SLAB_SCALARS 48
 typedef struct rmt_mac_slab rmt_mac_slab;
 int rmt_mac_slab_create(rmt_ctx *ctx, const rmt_mac_params *prm, int G, int rank,
                         const int *row_splits, const int *col_splits, rmt_mac_slab **out);
@@ -351,6 +354,7 @@ int rmt_mac_slab_advect(rmt_mac_slab *slab, double dt);
 int rmt_mac_slab_rim_pack(rmt_mac_slab *slab);
 int rmt_mac_slab_extrapolate(rmt_mac_slab *slab, int disc, const double *gathered_rims,
                              const long long *counts, long long cap);
+int rmt_mac_slab_extrapolate_identity(rmt_mac_slab *slab, int disc);
 int rmt_mac_slab_predict(rmt_mac_slab *slab, double dt);
 int rmt_mac_slab_project_rows(rmt_mac_slab *slab, const double *dev_roots);
 int rmt_mac_slab_project_cols(rmt_mac_slab *slab);

@@ -134,6 +134,7 @@ SIGNATURES = {
     "rmt_mac_slab_rim_pack": (_I, [_P]),
     "rmt_mac_slab_extrapolate": (_I, [_P, _I, _P, ctypes.POINTER(ctypes.c_longlong),
                                       ctypes.c_longlong]),
+    "rmt_mac_slab_extrapolate_identity": (_I, [_P, _I]),
     "rmt_mac_slab_predict": (_I, [_P, _D]),
     "rmt_mac_slab_project_rows": (_I, [_P, _P]),
     "rmt_mac_slab_project_cols": (_I, [_P]),

@@ -116,69 +116,83 @@ __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits
 // the identity -- exactly (functions.py:95-161).  This is the N = 8192 case of config 5,
 // where det(Aw) ~ 1e-14 < 1e-10 for every fit.  One wave per row;
 // the window sums keep the reference's order (raster within the clipped 9x9 window).
+// Rows [jb, je) only (the MAC slabs split the candidates by rows; the known plane is whole).
+// Each lane builds the candidate mask of one word, the wave then walks the candidate words.
 __global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, int ny, int nx,
                                                  int W, double dx, double dy, double r2,
-                                                 int *__restrict__ ctl) {
+                                                 int *__restrict__ ctl, int jb, int je) {
     __shared__ double tb[4][6][96];
     __shared__ u64 tab[256];
     for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int j = blockIdx.x * 4 + wv;
-    if (j < 1 || j > ny - 2) return;
+    const int j = jb + blockIdx.x * 4 + wv;
+    if (j < 1 || j > ny - 2 || j >= je) return;
     double (*t)[96] = tb[wv];
     auto K = [&](int jj, int w) -> u64 {
         return (jj < 0 || jj >= ny || w < 0 || w >= W) ? 0 : kbits[(long)jj * W + w];
     };
-    for (int w0 = 0; w0 < W; ++w0) {
+    for (int wb = 0; wb < W; wb += 64) {
         if (__hip_atomic_load(ctl + EXC_ANY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-        u64 d = 0;
-        for (int jj = j - 1; jj <= j + 1; ++jj) {
-            const u64 a = K(jj, w0 - 1), b = K(jj, w0), e = K(jj, w0 + 1);
-            d |= b | (b << 1) | (a >> 63) | (b >> 1) | (e << 63);
-        }
-        const int i0 = 64 * w0, lo = max(1, i0) - i0, hi = min(nx - 2, i0 + 63) - i0;
-        if (hi < lo) continue;
-        u64 cand = d & ~K(j, w0) & (~0ull >> (63 - hi)) & (~0ull << lo);
-        while (cand) {
-            const int i = i0 + __builtin_ctzll(cand);
-            cand &= cand - 1;
-            const double x0 = dx * i, y0 = dy * j;
-            int inc_n = 0;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
-                bool inc = false;
-                double xi = 0.0, yi = 0.0, w = 0.0;
-                if (q < EX_WIN && jj >= 0 && jj < ny && ii >= 0 && ii < nx &&
-                    ((K(jj, ii >> 6) >> (ii & 63)) & 1)) {
-                    xi = dx * ii; yi = dy * jj;
-                    const double ax = xi - x0, ay = yi - y0, d2 = ax * ax + ay * ay;
-                    if (d2 <= r2) { inc = true; w = exp_glibc_tab(-d2 / r2, tab); }
+        u64 mine = 0;
+        {
+            const int w0 = wb + lane;
+            if (w0 < W) {
+                u64 d = 0;
+                for (int jj = j - 1; jj <= j + 1; ++jj) {
+                    const u64 a = K(jj, w0 - 1), b = K(jj, w0), e = K(jj, w0 + 1);
+                    d |= b | (b << 1) | (a >> 63) | (b >> 1) | (e << 63);
                 }
-                inc_n += __popcll(__ballot(inc));
-                if (q < 96) {
-                    const double wa0 = w * 1.0, wa1 = w * xi, wa2 = w * yi;
-                    t[0][q] = inc ? wa0 * 1.0 : 0.0;  t[1][q] = inc ? wa0 * xi : 0.0;
-                    t[2][q] = inc ? wa0 * yi : 0.0;   t[3][q] = inc ? wa1 * xi : 0.0;
-                    t[4][q] = inc ? wa1 * yi : 0.0;   t[5][q] = inc ? wa2 * yi : 0.0;
-                }
+                const int i0 = 64 * w0, lo = max(1, i0) - i0, hi = min(nx - 2, i0 + 63) - i0;
+                if (hi >= lo) mine = d & ~K(j, w0) & (~0ull >> (63 - hi)) & (~0ull << lo);
             }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            double acc = 0.0;
-            if (lane < 6)
-                for (int q = 0; q < EX_WIN; ++q) acc += t[lane][q];
-            __builtin_amdgcn_wave_barrier();
-            const double A00 = __shfl(acc, 0), A01 = __shfl(acc, 1), A02 = __shfl(acc, 2);
-            const double A11 = __shfl(acc, 3), A12 = __shfl(acc, 4), A22 = __shfl(acc, 5);
-            const double M[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
-            const double det = (M[0] * (M[4] * M[8] - M[5] * M[7])
-                              - M[1] * (M[3] * M[8] - M[5] * M[6])
-                              + M[2] * (M[3] * M[7] - M[4] * M[6]));
-            if (inc_n >= 3 && fabs(det) > 1e-10) {
-                if (lane == 0) atomicOr(ctl + EXC_ANY, 1);
-                return;
+        }
+        u64 words = __ballot(mine != 0);
+        while (words) {
+            const int l = __builtin_ctzll(words);
+            words &= words - 1;
+            u64 cand = __shfl(mine, l);
+            const int i0 = 64 * (wb + l);
+            while (cand) {
+                const int i = i0 + __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const double x0 = dx * i, y0 = dy * j;
+                int inc_n = 0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
+                    bool inc = false;
+                    double xi = 0.0, yi = 0.0, w = 0.0;
+                    if (q < EX_WIN && jj >= 0 && jj < ny && ii >= 0 && ii < nx &&
+                        ((K(jj, ii >> 6) >> (ii & 63)) & 1)) {
+                        xi = dx * ii; yi = dy * jj;
+                        const double ax = xi - x0, ay = yi - y0, d2 = ax * ax + ay * ay;
+                        if (d2 <= r2) { inc = true; w = exp_glibc_tab(-d2 / r2, tab); }
+                    }
+                    inc_n += __popcll(__ballot(inc));
+                    if (q < 96) {
+                        const double wa0 = w * 1.0, wa1 = w * xi, wa2 = w * yi;
+                        t[0][q] = inc ? wa0 * 1.0 : 0.0;  t[1][q] = inc ? wa0 * xi : 0.0;
+                        t[2][q] = inc ? wa0 * yi : 0.0;   t[3][q] = inc ? wa1 * xi : 0.0;
+                        t[4][q] = inc ? wa1 * yi : 0.0;   t[5][q] = inc ? wa2 * yi : 0.0;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                double acc = 0.0;
+                if (lane < 6)
+                    for (int q = 0; q < EX_WIN; ++q) acc += t[lane][q];
+                __builtin_amdgcn_wave_barrier();
+                const double A00 = __shfl(acc, 0), A01 = __shfl(acc, 1), A02 = __shfl(acc, 2);
+                const double A11 = __shfl(acc, 3), A12 = __shfl(acc, 4), A22 = __shfl(acc, 5);
+                const double M[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
+                const double det = (M[0] * (M[4] * M[8] - M[5] * M[7])
+                                  - M[1] * (M[3] * M[8] - M[5] * M[6])
+                                  + M[2] * (M[3] * M[7] - M[4] * M[6]));
+                if (inc_n >= 3 && fabs(det) > 1e-10) {
+                    if (lane == 0) atomicOr(ctl + EXC_ANY, 1);
+                    return;
+                }
             }
         }
     }
@@ -627,6 +641,18 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes) {
     return w;
 }
 
+// k_ex_none over rows [jb, jb + nrows) of a whole known plane: ctl[EXC_ANY] (zeroed by the
+// caller) set iff some first-layer target there is acceptable (MAC slabs, mac.hip)
+int extrap_none_rows(rmt_ctx *ctx, const u64 *kbits, int ny, int nx, double dx, double dy,
+                     int jb, int je, int *ctl) {
+    const double r = 4 * std::sqrt(dx * dx + dy * dy);
+    if (je > jb)
+        k_ex_none<<<grid1d(je - jb, 4), 256, 0, ctx->stream>>>(kbits, ny, nx, (nx + 63) / 64, dx,
+                                                               dy, r * r, ctl, jb, je);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
 size_t extrap_workspace(int ny, int nx, int max_layers) {
     size_t b = 0;
     extrap_layout(nullptr, ny, nx, max_layers, &b);
@@ -668,7 +694,7 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
         // exact shortcut: no target can be accepted -> identity (k_ex_none)
         const double r = 4 * std::sqrt(dx * dx + dy * dy);
         k_ex_none<<<grid1d(ny, 4), 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, dx, dy, r * r,
-                                                           ws.ctl);
+                                                           ws.ctl, 0, ny);
         k_ex_none_fin<<<1, 1, 0, ctx->stream>>>(ws.ctl);
         RMT_LAUNCHED();
         RMT_TRY(extrap_chain_launch(ctx, ws, X1o, X2o, dx, dy, max_layers));

@@ -544,7 +544,7 @@ namespace rmt {
 constexpr int MSL_MAXG = 64;
 enum { MS_FLAGS = 0, MS_JMIN = 1, MS_JMAX = 2, MS_UMAX = 3, MS_CEN = 4,
        MS_COUNT = MS_CEN + 3 * MAC_MAXD, MS_ROOT = MS_COUNT + MAC_MAXD, MS_FIT = MS_ROOT + 1,
-       MS_N = MS_FIT + 3 };
+       MS_ANY = MS_FIT + 1, MS_N = MS_ANY + MAC_MAXD + 2 };
 static_assert(MS_N == RMT_MAC_SLAB_SCALARS, "rmt.h scalar block size");
 
 // J range and diagnostics partials -> the scalar block; flags folded in
@@ -587,6 +587,11 @@ __global__ void __launch_bounds__(256) k_mac_slab_scal(const double *__restrict_
         scal[MS_FIT] = (double)fit;
     }
 }
+// per disc: did the no-op test on the owned rows find an acceptable target?
+__global__ void k_mac_slab_any(const int *__restrict__ nctl, int K, double *__restrict__ scal) {
+    const int k = threadIdx.x;
+    if (k < K) scal[MS_ANY + k] = (double)nctl[k * EXC_WORDS + EXC_ANY];
+}
 }  // namespace rmt
 
 struct rmt_mac_slab {
@@ -607,6 +612,7 @@ struct rmt_mac_slab {
     double *rim[RMT_MAC_MAXD]; // 3 doubles per owned cell
     double *rhs, *A, *Y, *B, *T, *xs, *scal, *part;
     int *flags;                // [0] flags, [4 + 2k, 5 + 2k] disc k {fitted, aborted}
+    int *nctl;                 // K x EXC_WORDS: k_ex_none control words of each disc
     double *gc(double *q) const { return q - (long)lo * N; }         // cells, v faces
     double *gu(double *q) const { return q - (long)lo * (N + 1); }   // u faces
     rmt::DiscSet discs() const {
@@ -651,7 +657,8 @@ int rmt_mac_slab_create(rmt_ctx *ctx, const rmt_mac_params *prm, int G, int rank
     const long nc = S->c1 - S->c0, W = S->W;
     const size_t dbl = 2 * nu + 2 * nv + 6 * nl + 6 * K * nl + 2 * nd + 3 * K * no + 3 * no +
                        2 * nc * N + N + MS_N + (2 + MD_VALS) * MS_BLOCKS + 16;
-    const size_t bytes = dbl * 8 + (size_t)(K * N + rows) * W * 8 + (rows + 64) * 4 + 256;
+    const size_t bytes = dbl * 8 + (size_t)(K * N + rows) * W * 8 + (rows + 64) * 4 +
+                         (size_t)K * EXC_WORDS * 4 + 256;
     RMT_HIP(hipMalloc(&S->block, bytes));
     RMT_HIP(hipMemsetAsync(S->block, 0, bytes, ctx->stream));
     double *q = (double *)S->block;
@@ -680,6 +687,7 @@ int rmt_mac_slab_create(rmt_ctx *ctx, const rmt_mac_params *prm, int G, int rank
     S->rimw = b; b += (long)rows * W;
     S->rowcnt = (int *)b;
     S->flags = S->rowcnt + rows + 32;
+    S->nctl = S->flags + 32;
     std::vector<double> g(N);
     for (int i = 0; i < N; ++i) g[i] = i * prm->dx;   // mac_multi_disc_lid.py:41
     RMT_HIP(hipMemcpyAsync(S->xs, g.data(), N * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -721,7 +729,7 @@ int rmt_mac_slab_advect(rmt_mac_slab *S, double dt) {
     rmt_ctx *ctx = S->ctx;
     const rmt_mac_params &P = S->P;
     const int N = S->N;
-    RMT_HIP(hipMemsetAsync(S->flags, 0, 32 * sizeof(int), ctx->stream));
+    RMT_HIP(hipMemsetAsync(S->flags, 0, (32 + P.n_discs * EXC_WORDS) * sizeof(int), ctx->stream));
     k_mac_centres<<<grid1d((long)(S->hi - S->lo) * N, 256), 256, 0, ctx->stream>>>(
         S->gu(S->u), S->gc(S->v), N, S->gc(S->uc), S->gc(S->vc), S->flags, S->lo, S->hi);
     RMT_LAUNCHED();
@@ -737,10 +745,34 @@ int rmt_mac_slab_advect(rmt_mac_slab *S, double dt) {
 
 int rmt_mac_slab_rim_pack(rmt_mac_slab *S) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
-    for (int k = 0; k < S->P.n_discs; ++k)
+    const int K = S->P.n_discs;
+    for (int k = 0; k < K; ++k) {
         RMT_TRY(slab_rim_pack(S->ctx, S->bits[k], S->N, S->N, S->W, S->r0, S->r1, S->rimw,
                               S->rowcnt, S->gc(S->X1n[k]), S->gc(S->X2n[k]), S->rim[k],
                               S->scal + MS_COUNT + k));
+        // k_ex_none's exact no-op test, candidates split by rows: if no slab finds an
+        // acceptable first-layer target the extrapolation of disc k is the identity
+        RMT_TRY(extrap_none_rows(S->ctx, S->bits[k], S->N, S->N, S->P.dx, S->P.dx, S->r0, S->r1,
+                                 S->nctl + k * EXC_WORDS));
+    }
+    k_mac_slab_any<<<1, 64, 0, S->ctx->stream>>>(S->nctl, K, S->scal);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+// disc k proven a no-op on every slab (scalar MS_ANY + k zero everywhere): keep the
+// advected map, rebuild phi -- what rmt_mac_slab_extrapolate computes then, without the
+// rim allgather and the dense replica
+int rmt_mac_slab_extrapolate_identity(rmt_mac_slab *S, int disc) {
+    RMT_CHECK(S && disc >= 0 && disc < S->P.n_discs, RMT_EINVAL, "bad argument");
+    const rmt_mac_params &P = S->P;
+    const int N = S->N, k = disc;
+    const int jb = std::max(0, S->r0 - 3), je = std::min(N, S->r1 + 3);
+    const long o = (long)jb * N, n = (long)(je - jb) * N;
+    k_mac_phi<<<grid1d(n, 256), 256, 0, S->ctx->stream>>>(
+        S->gc(S->X1n[k]) + o, S->gc(S->X2n[k]) + o, n, P.cx[k], P.cy[k], P.R[k],
+        S->gc(S->X1[k]) + o, S->gc(S->X2[k]) + o, S->gc(S->phi[k]) + o);
+    RMT_LAUNCHED();
     return RMT_OK;
 }
 

@@ -3,6 +3,7 @@
 // 1D over cells with 256-thread workgroups (memory-bound elementwise / small-stencil
 // work: reads coalesce along i, neighbours come from L2).
 #include "rmt_internal.hpp"
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -139,25 +140,29 @@ __global__ void __launch_bounds__(TREE_T) k_rowtree(const double *__restrict__ r
     }
     if (threadIdx.x == 0) *out = s[0];
 }
-// the same aligned tree over G <= 64 slab roots (every thread folds it)
-__device__ __forceinline__ double tree_roots(const double *__restrict__ roots, int G) {
-    double v[64];
-    for (int k = 0; k < G; ++k) v[k] = roots[k];
-    int m = G;
-    while (m > 1) {
-        const int h = (m + 1) / 2;
-        for (int k = 0; k < h; ++k) v[k] = 2 * k + 1 < m ? v[2 * k] + v[2 * k + 1] : v[2 * k];
-        m = h;
+// x -= tree(roots) / count over n cells (numpy mean: sum / count); the same aligned tree
+// over the G <= 64 slab roots, folded once per block in LDS
+constexpr int STM_BLOCKS = 2048;
+__global__ void __launch_bounds__(256) k_sub_tree_mean(double *__restrict__ x, long n,
+                                                       const double *__restrict__ roots, int G,
+                                                       double count) {
+    __shared__ double s[64];
+    __shared__ double mean;
+    if (threadIdx.x < 64) s[threadIdx.x] = threadIdx.x < G ? roots[threadIdx.x] : 0.0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int m = G;
+        while (m > 1) {
+            const int h = (m + 1) / 2;
+            for (int k = 0; k < h; ++k) s[k] = 2 * k + 1 < m ? s[2 * k] + s[2 * k + 1] : s[2 * k];
+            m = h;
+        }
+        mean = s[0] / count;
     }
-    return v[0];
-}
-// x -= tree(roots) / count over n cells (numpy mean: sum / count)
-__global__ void k_sub_tree_mean(double *__restrict__ x, long n, const double *__restrict__ roots,
-                                int G, double count) {
-    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const double m = tree_roots(roots, G) / count;
-    x[k] = x[k] - m;
+    __syncthreads();
+    const double m = mean;
+    for (long k = blockIdx.x * 256L + threadIdx.x; k < n; k += (long)gridDim.x * 256)
+        x[k] = x[k] - m;
 }
 int rowtree_root(rmt_ctx *ctx, const double *x, int nrows, int nx, double *dev_root) {
     RMT_CHECK(nrows >= 1 && nrows <= TREE_MAX && nrows <= ctx->rsum_len, RMT_EINVAL,
@@ -169,7 +174,9 @@ int rowtree_root(rmt_ctx *ctx, const double *x, int nrows, int nx, double *dev_r
 }
 int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int G, double count) {
     RMT_CHECK(G >= 1 && G <= 64, RMT_EINVAL, "sub_tree_mean: 1..64 roots");
-    if (n > 0) k_sub_tree_mean<<<grid1d(n, 256), 256, 0, ctx->stream>>>(x, n, dev_roots, G, count);
+    if (n > 0)
+        k_sub_tree_mean<<<std::min<long>(grid1d(n, 256), STM_BLOCKS), 256, 0, ctx->stream>>>(
+            x, n, dev_roots, G, count);
     RMT_LAUNCHED();
     return RMT_OK;
 }

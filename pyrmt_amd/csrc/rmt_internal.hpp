@@ -441,6 +441,10 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 double dy, int max_layers, double *X1o, double *X2o, int *dev_status = nullptr,
                 const unsigned long long *kin = nullptr);
 size_t extrap_workspace(int ny, int nx, int max_layers);   // bytes of ctx->bytes it uses
+// the exact no-op test of extrapolate() (k_ex_none) on rows [jb, je) of a whole known plane:
+// ctl[EXC_ANY] (extrap.hpp; zeroed by the caller) set iff a first-layer target there fits
+int extrap_none_rows(rmt_ctx *ctx, const unsigned long long *kbits, int ny, int nx, double dx,
+                     double dy, int jb, int je, int *ctl);
 // after extrapolate(): the MOM_TX x MOM_TY tiles within `margin` cells of a possible target
 // (device list + count); the momentum of every other cell ignores the extrapolated values
 int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *count);

@@ -467,8 +467,9 @@ def soft_disc_in_lid_driven(N, comm):
 
 
 # ------------------------------------------------------------ MAC slabs (config 5) --
-MS_N = 40            # RMT_MAC_SLAB_SCALARS
-MS_FLAGS, MS_JMIN, MS_JMAX, MS_UMAX, MS_CEN, MS_COUNT, MS_ROOT, MS_FIT = 0, 1, 2, 3, 4, 28, 36, 37
+MS_N = 48            # RMT_MAC_SLAB_SCALARS
+MS_FLAGS, MS_JMIN, MS_JMAX, MS_UMAX, MS_CEN, MS_COUNT, MS_ROOT, MS_FIT, MS_ANY = \
+    0, 1, 2, 3, 4, 28, 36, 37, 38
 MBUF = {"u": 0, "v": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5, "bits": 6, "rim": 7, "A": 8,
         "B": 9, "scal": 10}
 
@@ -588,6 +589,23 @@ class MacDistributedSim:
         g = self.comm.allgather([s.view("scal") for s in self.slabs])[0]
         return g.cpu().numpy().reshape(self.G, MS_N)
 
+    PHASES = ("halo", "advect", "extrapolate", "predict", "projection", "correct")
+
+    def set_profiling(self, on=True):
+        """HIP events around each phase (summed over the local slabs); phase_times()."""
+        self._prof = bool(on)
+        self._ms = {k: 0.0 for k in self.PHASES}
+        self._nprof = 0
+
+    def phase_times(self):
+        return {k: (v, self._nprof) for k, v in self._ms.items()}
+
+    def _mark(self, ev):
+        if getattr(self, "_prof", False):
+            e = self.torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append(e)
+
     def step(self, nsteps=1, t_end=math.inf):
         self.ctx.bind()
         comm, S, K = self.comm, self.slabs, self.K
@@ -598,13 +616,22 @@ class MacDistributedSim:
             dt = self.dt
             if self.t + dt > t_end:
                 dt = t_end - self.t
+            ev = []
+            self._mark(ev)
             comm.halo(S, halo_planes, HALO)
+            self._mark(ev)
             self._call("rmt_mac_slab_advect", dt)
+            self._mark(ev)
             for k in range(K):
                 comm.allgather_rows(S, f"bits:{k}")
             self._call("rmt_mac_slab_rim_pack")
             sc = self._scalars()
+            ident = 0
             for k in range(K):
+                if not sc[:, MS_ANY + k].any():     # proven identity on every slab
+                    self._call("rmt_mac_slab_extrapolate_identity", k)
+                    ident += 1
+                    continue
                 counts = [int(c) for c in sc[:, MS_COUNT + k]]
                 gathered, cap = comm.allgather_padded([s.view(f"rim:{k}") for s in S], counts, 3)
                 for r, c in enumerate(counts):
@@ -612,7 +639,9 @@ class MacDistributedSim:
                 for s, g in zip(S, gathered):
                     L.check(s.lib.rmt_mac_slab_extrapolate(s.h, k, g.data_ptr(), self._counts,
                                                            cap), "rmt_mac_slab_extrapolate")
+            self._mark(ev)
             self._call("rmt_mac_slab_predict", dt)
+            self._mark(ev)
             roots = comm.allgather([s.view("scal")[MS_ROOT:MS_ROOT + 1] for s in S])
             for s, r in zip(S, roots):
                 L.check(s.lib.rmt_mac_slab_project_rows(s.h, r.data_ptr()),
@@ -624,11 +653,18 @@ class MacDistributedSim:
             comm.all_to_all([s.view("B") for s in S], [s.view("A") for s in S],
                             [x[1] for x in sp], [x[0] for x in sp])
             self._call("rmt_mac_slab_project_unrows")
+            self._mark(ev)
             comm.halo(S, ("p",), 1)
             self._call("rmt_mac_slab_correct", dt)
+            self._mark(ev)
             sc = self._scalars()
             self.t += dt
             self._record(sc, dt)
+            self.records[-1]["identity_discs"] = ident
+            if ev:
+                for k, name in enumerate(self.PHASES):
+                    self._ms[name] += ev[k].elapsed_time(ev[k + 1])
+                self._nprof += 1
 
     def _record(self, sc, dt):
         fl = int(np.bitwise_or.reduce(sc[:, MS_FLAGS].astype(np.int64)))

@@ -61,7 +61,23 @@ def test_mac_slab_extrapolation_fits(gpu):
     from pyrmt_amd import distributed as D
     sim = D.mac_multi_disc_lid(64, D.LocalComm(2))
     sim.step(3)
-    assert sim.diagnostics()["fitted"][-1] > 0
+    d = sim.diagnostics()
+    assert d["fitted"][-1] > 0 and d["identity_discs"][-1] < sim.K
+
+
+def test_mac_slab_identity_path_bitexact(gpu):
+    """N=8192 (config 5): no extrapolation target fits (det(Aw) ~ 1e-12 < 1e-10), the
+    row-split no-op test proves it on every slab and the rim allgather / dense replica are
+    skipped; the fields still match the single-domain step bit for bit"""
+    from pyrmt_amd import distributed as D
+    N, K = 8192, 1
+    ref = _ref(N, K)
+    sim = D.mac_multi_disc_lid(N, D.LocalComm(4))
+    sim.step(K)
+    d = sim.diagnostics()
+    assert d["identity_discs"][-1] == sim.K and d["fitted"][-1] == 0
+    for f in ("u", "v", "p", "X1:0", "X2:1", "phi:2"):
+        np.testing.assert_array_equal(sim.gather(f), _get(ref, f), err_msg=f)
 
 
 def test_mac_slab_two_processes_gloo(gpu):
