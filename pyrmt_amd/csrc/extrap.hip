@@ -32,6 +32,7 @@
 // stores / L2 atomics drained by s_waitcnt vmcnt(0) before the LDS progress word is released,
 // and read only with sc1 (L2) loads; bytes fixed before the launch use plain loads.
 #include "extrap.hpp"
+#include <cstring>
 #include "exp_glibc.h"
 
 namespace rmt {
@@ -632,8 +633,13 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes) {
     w.dmark = (int *)take(maxt * 4);
     w.rej = (int *)take((size_t)ML * EX_MAXREJ * 4);
     w.ctl = (int *)take(EXC_WORDS * 4);
-    // ~2 KB per record on average at the bench sizes; offsets are 25-bit in 64-B units
-    w.arena_bytes = std::min(maxt * 2560LL, (1LL << 31) - 65536);
+    // one fixed slot per fit id (no allocation cursor shared by every wave of k_ex_geom) when
+    // it fits; else a bump allocator (~2 KB per record on average at the bench sizes).
+    // Offsets are stored in 64-B units.
+    static const bool bump = getenv("RMT_EX_ARENA") && !strcmp(getenv("RMT_EX_ARENA"), "bump");
+    const long long cap = (1LL << 31) - 65536;
+    w.slots = !bump && maxt * (long long)CH_MAXREC <= cap;
+    w.arena_bytes = w.slots ? maxt * (long long)CH_MAXREC : std::min(maxt * 2560LL, cap);
     w.arena = take(w.arena_bytes);
     w.maxt = maxt;
     w.plane = plane;

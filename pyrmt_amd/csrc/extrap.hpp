@@ -37,6 +37,7 @@ struct ExWs {
     int *ctl;                                 // EXC_WORDS
     char *arena;
     long long arena_bytes;
+    int slots;                                // 1: record of fit id at id * CH_MAXREC
     long maxt;
     long plane;                               // ny * W
 };

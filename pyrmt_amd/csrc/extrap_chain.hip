@@ -265,11 +265,15 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
         if (lane == 0) { ws.ctl[EXC_FALLBACK] = 1; ws.recoff[id] = -1; }
         return true;
     }
-    if (lane == 0) {
-        off = atomicAdd((unsigned long long *)(ws.ctl + EXC_ARENA), (unsigned long long)bytes);
-        if ((long long)(off + bytes) > ws.arena_bytes) ws.ctl[EXC_FALLBACK] = 1;
+    if (ws.slots) {
+        off = (unsigned long long)id * CH_MAXREC;   // bytes <= CH_MAXREC (nd <= 64)
+    } else {
+        if (lane == 0) {
+            off = atomicAdd((unsigned long long *)(ws.ctl + EXC_ARENA), (unsigned long long)bytes);
+            if ((long long)(off + bytes) > ws.arena_bytes) ws.ctl[EXC_FALLBACK] = 1;
+        }
+        off = rl64(off, 0);
     }
-    off = rl64(off, 0);
     if ((long long)(off + bytes) > ws.arena_bytes) {
         if (lane == 0) ws.recoff[id] = -1;
         return true;   // (fallback sweep recomputes everything)
