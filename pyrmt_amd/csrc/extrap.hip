@@ -73,6 +73,22 @@ __global__ void __launch_bounds__(256) k_ex_bits(const double *__restrict__ phi,
     }
 }
 
+// k_ex_bits when the known plane is given and nothing is copied: one thread per word
+__global__ void __launch_bounds__(256) k_ex_bits_w(const u64 *__restrict__ kin, int ny, int W,
+                                                   int ML, u64 *__restrict__ kbits,
+                                                   u64 *__restrict__ K,
+                                                   unsigned char *__restrict__ rowcand,
+                                                   int *__restrict__ jrange) {
+    const long t = blockIdx.x * 256L + threadIdx.x, plane = (long)ny * W;
+    if (t < plane) {
+        const u64 m = kin[t];
+        kbits[t] = m;
+        for (int L = 0; L < ML; ++L) K[L * plane + t] = m;
+    }
+    if (t < ny) rowcand[t] = 0;
+    if (t == 0) { jrange[0] = 0x7fffffff; jrange[1] = -1; }
+}
+
 // candidate bit plane: Chebyshev dilation of known by L, minus known, interior cells only
 __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits, int ny, int nx,
                                                    int W, int L, u64 *__restrict__ cbits,
@@ -686,9 +702,13 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
     ctx->ex_layers = max_layers;
     ctx->ex_chain = chain;
     const int copy = (X1o != X1) || (X2o != X2);
-    k_ex_bits<<<dim3((nx + 255) / 256, ny), 256, 0, ctx->stream>>>(
-        phi, ny, nx, W, max_layers, ws.kbits, ws.Kold, ws.rowcand, ws.jrange, X1, X2, X1o, X2o,
-        copy, kin);
+    if (kin && !copy)
+        k_ex_bits_w<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(
+            kin, ny, W, max_layers, ws.kbits, ws.Kold, ws.rowcand, ws.jrange);
+    else
+        k_ex_bits<<<dim3((nx + 255) / 256, ny), 256, 0, ctx->stream>>>(
+            phi, ny, nx, W, max_layers, ws.kbits, ws.Kold, ws.rowcand, ws.jrange, X1, X2, X1o,
+            X2o, copy, kin);
     RMT_HIP(hipMemsetAsync(ws.status, 0, 4 * sizeof(int), ctx->stream));
     if (chain) {
         RMT_HIP(hipMemsetAsync(ws.ctl, 0, EXC_WORDS * sizeof(int), ctx->stream));

@@ -349,11 +349,17 @@ __global__ void k_apply_bc(int kind, double lid, double *u, double *v, int ny, i
 // -------------------------------------------------------------------- projection ----
 __global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
                                 const double *__restrict__ p, int ny, int nx, double d_f,
-                                double dx, double dy, double *__restrict__ divU, int jb, int je) {
+                                double dx, double dy, double *__restrict__ divU, int jb, int je,
+                                double rho = 0.0, double dt = 1.0) {
+    // rho > 0: the projection's rhs = (rho * divU) / dt (functions.py:1331, the same two
+    // roundings as the separate scale and divide passes)
     long c = (long)jb * nx + blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (c >= (long)je * nx) return;
     int j = (int)(c / nx), i = (int)(c % nx);
-    if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) { divU[c] = 0.0; return; }
+    if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) {
+        divU[c] = rho > 0 ? (rho * 0.0) / dt : 0.0;
+        return;
+    }
     const double h2x = 2.0 * dx, h2y = 2.0 * dy;
     double gxl = grad2(p + c - 1, 1, i - 1, nx, h2x), gxc = grad2(p + c, 1, i, nx, h2x),
            gxr = grad2(p + c + 1, 1, i + 1, nx, h2x);
@@ -363,7 +369,8 @@ __global__ void k_divergence_rc(const double *__restrict__ a, const double *__re
     double uw = 0.5 * (a[c - 1] + a[c]) - d_f * ((p[c] - p[c - 1]) / dx - 0.5 * (gxl + gxc));
     double vn = 0.5 * (b[c] + b[c + nx]) - d_f * ((p[c + nx] - p[c]) / dy - 0.5 * (gyc + gyu));
     double vs = 0.5 * (b[c - nx] + b[c]) - d_f * ((p[c] - p[c - nx]) / dy - 0.5 * (gyd + gyc));
-    divU[c] = (ue - uw) / dx + (vn - vs) / dy;
+    const double d = (ue - uw) / dx + (vn - vs) / dy;
+    divU[c] = rho > 0 ? (rho * d) / dt : d;
 }
 __global__ void k_divergence_central(const double *__restrict__ a, const double *__restrict__ b,
                                      int ny, int nx, double dx, double dy,
@@ -673,10 +680,16 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
     RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
     double *rhs = ctx->scratch, *pc = rhs + n;
     // functions.py:1292-1295 + :1331: rhs = rho * divU / dt, d_f = dt / mean(rho)
-    if (p_prev) RMT_TRY(rmt_divergence_rc(ctx, a_star, b_star, p_prev, dt / rho, dx, dy, rhs));
-    else RMT_TRY(rmt_divergence_central(ctx, a_star, b_star, dx, dy, rhs));
-    k_scale_copy<<<LAUNCH1D(n)>>>(rhs, n, rho, rhs);
-    k_div_scalar<<<LAUNCH1D(n)>>>(rhs, n, dt, rhs);
+    if (p_prev && rho > 0) {
+        k_divergence_rc<<<LAUNCH1D(n)>>>(a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx,
+                                         dy, rhs, 0, ctx->ny, rho, dt);
+        RMT_LAUNCHED();
+    } else {
+        if (p_prev) RMT_TRY(rmt_divergence_rc(ctx, a_star, b_star, p_prev, dt / rho, dx, dy, rhs));
+        else RMT_TRY(rmt_divergence_central(ctx, a_star, b_star, dx, dy, rhs));
+        k_scale_copy<<<LAUNCH1D(n)>>>(rhs, n, rho, rhs);
+        k_div_scalar<<<LAUNCH1D(n)>>>(rhs, n, dt, rhs);
+    }
     RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc));
     k_project_correct<<<LAUNCH1D(n)>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy,
                                        dt / rho, bc_kind, lid, a, b, p, 0, ctx->ny);

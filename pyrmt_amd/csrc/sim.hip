@@ -29,6 +29,7 @@ struct rmt_sim {
     double *X1n = nullptr, *X2n = nullptr, *us = nullptr, *vs = nullptr;
     double *sxx = nullptr, *sxy = nullptr, *syy = nullptr;
     double *mw = nullptr;            // momentum workspace (8 planes)
+    unsigned long long *kbits = nullptr;   // known plane (phi_pre < 0) from k_sim_sl
     unsigned char *mbytes = nullptr; // solid mask + flag
     double *dscr = nullptr;          // diag partials + scalars
     int *flag = nullptr;             // non-finite flag
@@ -53,19 +54,31 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
                          const double *__restrict__ xs, const double *__restrict__ ys, int ny,
                          int nx, double dt, double dx, double dy, int shape, double x0, double y0,
                          double R, double *__restrict__ X1n, double *__restrict__ X2n,
-                         double *__restrict__ phi_pre, int *bad) {
-    long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)ny * nx) return;
-    int j = (int)(c / nx), i = (int)(c % nx);
-    bool fin = isfinite(a[c]) && isfinite(b[c]);
-    if (__any(!fin) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
-    double ph = disc_phi(X1[c], X2[c], x0, y0, R);
-    phi_pre[c] = ph;
-    double m = ph <= 0 ? 1.0 : 0.0;
-    double xb, yb;
-    sl_backtrace(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, xb, yb);
-    X1n[c] = bilinear(X1, xb, yb, dx, dy, nx, ny) * m;
-    X2n[c] = bilinear(X2, xb, yb, dx, dy, nx, ny) * m;
+                         double *__restrict__ phi_pre, int *bad,
+                         unsigned long long *__restrict__ kbits) {
+    // grid (ceil(nx / 256), ny): a wave covers 64 cells of one row, so the extrapolation's
+    // known plane (phi_pre < 0, 64-cell words) comes out of the same pass (kbits optional)
+    const int j = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const bool in = i < nx;
+    const long c = (long)j * nx + i;
+    bool known = false;
+    if (in) {
+        bool fin = isfinite(a[c]) && isfinite(b[c]);
+        if (!fin) atomicOr(bad, 1);
+        double ph = disc_phi(X1[c], X2[c], x0, y0, R);
+        phi_pre[c] = ph;
+        known = ph < 0;
+        double m = ph <= 0 ? 1.0 : 0.0;
+        double xb, yb;
+        sl_backtrace(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, xb, yb);
+        X1n[c] = bilinear(X1, xb, yb, dx, dy, nx, ny) * m;
+        X2n[c] = bilinear(X2, xb, yb, dx, dy, nx, ny) * m;
+    }
+    if (kbits) {
+        const unsigned long long w = __ballot(known);
+        if ((threadIdx.x & 63) == 0 && (i >> 6) < (nx + 63) / 64)
+            kbits[(long)j * ((nx + 63) / 64) + (i >> 6)] = w;
+    }
 }
 
 // k_sim_sl with the bicubic interpolant (functions.py:228-251, scheme semilagrangian_cubic)
@@ -244,10 +257,9 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
                 double *phi_pre, int *bad) {
-    const long n = (long)ctx->ny * ctx->nx;
-    k_sim_sl<<<grid1d(n, 256), 256, 0, ctx->stream>>>(X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt,
-                                                      dx, dy, RMT_SHAPE_DISC, x0, y0, R, X1n,
-                                                      X2n, phi_pre, bad);
+    k_sim_sl<<<dim3((ctx->nx + 255) / 256, ctx->ny), 256, 0, ctx->stream>>>(
+        X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, dx, dy, RMT_SHAPE_DISC, x0, y0, R, X1n, X2n,
+        phi_pre, bad, nullptr);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -296,7 +308,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     double **planes[] = {&S->u, &S->v, &S->p, &S->X1, &S->X2, &S->phi, &S->phi_pre, &S->J,
                          &S->X1n, &S->X2n, &S->us, &S->vs, &S->sxx, &S->sxy, &S->syy};
     for (auto pp : planes) { *pp = q; q += n; }
-    q += n;  // spare
+    S->kbits = (unsigned long long *)q; q += n;   // ny * ceil(nx / 64) words fit a plane
     S->mw = q; q += MOM_WORK_PLANES * n;
     S->xs = q; q += nx;
     S->ys = q; q += ny;
@@ -394,9 +406,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // 2. advect the reference map with the pre-advection level set and mask
             RMT_HIP(hipMemsetAsync(S->flag, 0, sizeof(int), st));
             if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
-                k_sim_sl<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt,
-                                            P.dx, P.dy, P.shape, P.x0, P.y0, P.R, S->X1n, S->X2n,
-                                            S->phi_pre, S->flag);
+                k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, st>>>(
+                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
+                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN_CUBIC) {
                 k_sim_sl_cubic<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx,
                                                   dt, P.dx, P.dy, P.x0, P.y0, P.R, S->X1n,
@@ -424,8 +436,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // overlap, the speculative phi + momentum start on the second stream once the
             // chip-wide passes are done and the one-workgroup chain kernel is launched
             if (overlap) ctx->ev_chain = S->e_sl;
+            const bool kb = P.scheme == RMT_SCHEME_SEMILAGRANGIAN;   // k_sim_sl wrote kbits
             const int es = extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
-                                       S->X1n, S->X2n, S->flag + 2);
+                                       S->X1n, S->X2n, S->flag + 2, kb ? S->kbits : nullptr);
             ctx->ev_chain = nullptr;
             RMT_TRY(es);
             if (overlap) {
@@ -442,12 +455,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             }
             if (overlap) RMT_TRY(extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount));
             if (S->prof) RMT_HIP(hipEventRecord(S->pev[3], st));
-            int fl[4] = {0, 0, 0, 0};   // non-finite, (momentum), fitted, sweep aborted
-            RMT_HIP(hipMemcpyAsync(fl, S->flag, sizeof(fl), hipMemcpyDeviceToHost, st));
-            RMT_HIP(hipStreamSynchronize(st));
-            RMT_CHECK(!fl[0], RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
-                                              "simulation diverged)");
-            RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
+            // the flags (non-finite velocity, sweep aborted) are read with the diagnostics at
+            // the end of the step: no host round trip between the chain and the projection
         }
         if (S->prof && !solid) {
             RMT_HIP(hipEventRecord(S->pev[2], st));
@@ -477,16 +486,22 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         RMT_TRY(rmt_pressure_projection(ctx, S->us, S->vs, P.dx, P.dy, dt, P.rho_f, P.bc_kind,
                                         P.lid, S->p, S->u, S->v, S->p));
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[5], st));
-        // 7. diagnostics
+        // 7. diagnostics (running them beside the projection on the second stream measured
+        // no gain: both are HBM-bound)
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
                    P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa, 0, ny};
         k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, S->dscr);
         k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, sc + 2);
         RMT_LAUNCHED();
         double dv[DIAG_VALS];
+        int fl[4] = {0, 0, 0, 0};   // non-finite, (momentum), fitted, sweep aborted
         RMT_HIP(hipMemcpyAsync(dv, sc + 2, sizeof(dv), hipMemcpyDeviceToHost, st));
+        if (solid) RMT_HIP(hipMemcpyAsync(fl, S->flag, sizeof(fl), hipMemcpyDeviceToHost, st));
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[6], st));
         RMT_HIP(hipStreamSynchronize(st));
+        RMT_CHECK(!fl[0], RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
+                                          "simulation diverged)");
+        RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
         if (S->prof) {
             float f;
             for (int k = 0; k < 6; ++k) {
