@@ -168,10 +168,30 @@ int rmt_pressure_gradient(rmt_ctx *ctx, const double *p, double dx, double dy, d
  * the DCT-I symbol of functions.py:1091-1104 for this grid (dx, dy). */
 int rmt_solve_poisson_dct(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p);
 /* functions.py:1255-1364 pressure_projection_amg, Neumann branch, constant density rho
- * (the variable-density CG branch returns RMT_ENOTSUP).  p_prev may be NULL. */
+ * (variable density: rmt_pressure_projection_variable).  p_prev may be NULL. */
 int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_star,
                             double dx, double dy, double dt, double rho, int bc_kind,
                             double lid, const double *p_prev, double *a, double *b, double *p);
+/* The variable-density branch (rho a device (ny, nx) array with ptp > 1e-10),
+ * functions.py:1296-1328 + :1350-1364: Rhie-Chow divergence with per-face dt/rho, rhs =
+ * divU/dt - mean, preconditioned CG (scipy.sparse.linalg.cg semantics: x0 = 0, stop when
+ * ||r|| < rtol ||rhs||, at most maxiter iterations; the reference passes tol = 1e-6,
+ * maxiter = 200) on the matrix-free div((1/rho) grad) operator with the DCT-I solve as the
+ * preconditioner, then a = a* - (dt/rho) grad p_c, BC, p = p_prev + p_c - mean.
+ * *iters receives the iteration count (maxiter: not converged, as scipy's info > 0). */
+int rmt_pressure_projection_variable(rmt_ctx *ctx, const double *a_star, const double *b_star,
+                                     double dx, double dy, double dt, const double *rho,
+                                     int bc_kind, double lid, const double *p_prev, double rtol,
+                                     int maxiter, double *a, double *b, double *p, int *iters);
+/* functions.py:1122-1168 _apply_variable_poisson: div((1/rho) grad p), face-averaged 1/rho,
+ * mirror ghosts. */
+int rmt_apply_variable_poisson(rmt_ctx *ctx, const double *p, double dx, double dy,
+                               const double *inv_rho, double *out);
+/* functions.py:1016-1070 _compute_divergence_rc with a variable rho array (per-face
+ * d_f = dt * 0.5 * (1/rho_l + 1/rho_r)). */
+int rmt_divergence_rc_variable(rmt_ctx *ctx, const double *a, const double *b, const double *p,
+                               double dt, const double *rho, double dx, double dy,
+                               double *divU);
 
 /* functions.py:165-192 compute_timestep; host result, blocks. */
 int rmt_compute_timestep(rmt_ctx *ctx, const double *a, const double *b, double dx, double dy,

@@ -269,9 +269,112 @@ def _solve_poisson_dct(rhs, eig):
     return p
 
 
+def _is_variable_rho(rho):
+    return isinstance(rho, np.ndarray) and rho.ndim == 2 and np.ptp(rho) > 1e-10
+
+
+def _compute_divergence_rc_variable(a_star, b_star, p_prev, dt, rho, dx, dy):
+    """functions.py:1016-1070 with a variable rho array (NumPy, the reference's operations
+    in its order): per-face d_f = dt * 0.5 * (1/rho_l + 1/rho_r)."""
+    Ny, Nx = a_star.shape
+    divU = np.zeros((Ny, Nx))
+    dpdx_cc = np.zeros((Ny, Nx)); dpdy_cc = np.zeros((Ny, Nx))
+    dpdx_cc[:, 1:-1] = (p_prev[:, 2:] - p_prev[:, :-2]) / (2.0 * dx)
+    dpdx_cc[:, 0] = (-3.0 * p_prev[:, 0] + 4.0 * p_prev[:, 1] - p_prev[:, 2]) / (2.0 * dx)
+    dpdx_cc[:, -1] = (3.0 * p_prev[:, -1] - 4.0 * p_prev[:, -2] + p_prev[:, -3]) / (2.0 * dx)
+    dpdy_cc[1:-1, :] = (p_prev[2:, :] - p_prev[:-2, :]) / (2.0 * dy)
+    dpdy_cc[0, :] = (-3.0 * p_prev[0, :] + 4.0 * p_prev[1, :] - p_prev[2, :]) / (2.0 * dy)
+    dpdy_cc[-1, :] = (3.0 * p_prev[-1, :] - 4.0 * p_prev[-2, :] + p_prev[-3, :]) / (2.0 * dy)
+    inv_rho = 1.0 / rho
+    u_face = 0.5 * (a_star[:, :-1] + a_star[:, 1:])
+    face_dpdx = (p_prev[:, 1:] - p_prev[:, :-1]) / dx
+    avg_dpdx = 0.5 * (dpdx_cc[:, :-1] + dpdx_cc[:, 1:])
+    d_f_x = dt * 0.5 * (inv_rho[:, :-1] + inv_rho[:, 1:])
+    u_face_rc = u_face - d_f_x * (face_dpdx - avg_dpdx)
+    v_face = 0.5 * (b_star[:-1, :] + b_star[1:, :])
+    face_dpdy = (p_prev[1:, :] - p_prev[:-1, :]) / dy
+    avg_dpdy = 0.5 * (dpdy_cc[:-1, :] + dpdy_cc[1:, :])
+    d_f_y = dt * 0.5 * (inv_rho[:-1, :] + inv_rho[1:, :])
+    v_face_rc = v_face - d_f_y * (face_dpdy - avg_dpdy)
+    divU[1:-1, 1:-1] = ((u_face_rc[1:-1, 1:] - u_face_rc[1:-1, :-1]) / dx +
+                        (v_face_rc[1:, 1:-1] - v_face_rc[:-1, 1:-1]) / dy)
+    return divU
+
+
+def _apply_variable_poisson(p_flat, Nx, Ny, dx, dy, inv_rho):
+    """functions.py:1122-1168 (NumPy, same operations): div((1/rho) grad p), face-averaged
+    1/rho, mirror ghosts."""
+    p = p_flat.reshape((Ny, Nx))
+    result = np.zeros_like(p)
+    cx = 1.0 / dx ** 2
+    cy = 1.0 / dy ** 2
+    px = np.empty((Ny, Nx + 2)); px[:, 1:-1] = p; px[:, 0] = p[:, 1]; px[:, -1] = p[:, -2]
+    py = np.empty((Ny + 2, Nx)); py[1:-1, :] = p; py[0, :] = p[1, :]; py[-1, :] = p[-2, :]
+    rx = np.empty((Ny, Nx + 2)); rx[:, 1:-1] = inv_rho
+    rx[:, 0] = inv_rho[:, 1]; rx[:, -1] = inv_rho[:, -2]
+    be = 0.5 * (rx[:, 1:-1] + rx[:, 2:]); bw = 0.5 * (rx[:, 0:-2] + rx[:, 1:-1])
+    result += cx * (be * (px[:, 2:] - p) - bw * (p - px[:, :-2]))
+    ry = np.empty((Ny + 2, Nx)); ry[1:-1, :] = inv_rho
+    ry[0, :] = inv_rho[1, :]; ry[-1, :] = inv_rho[-2, :]
+    bn = 0.5 * (ry[1:-1, :] + ry[2:, :]); bs = 0.5 * (ry[0:-2, :] + ry[1:-1, :])
+    result += cy * (bn * (py[2:, :] - p) - bs * (p - py[:-2, :]))
+    return result.ravel()
+
+
+def cg(matvec, b, psolve, rtol, maxiter):
+    """scipy.sparse.linalg.cg (scipy 1.15, x0 = 0, atol = 0) restated: the reference calls it
+    with tol=1e-6, maxiter=200 and the DCT solve as M (functions.py:1322-1325).  Returns
+    (x, iterations run)."""
+    r = b.copy()
+    x = np.zeros_like(b)
+    bnrm2 = np.linalg.norm(b)
+    if bnrm2 == 0:
+        return b.copy(), 0
+    atol = rtol * bnrm2
+    rho_prev, p = None, None
+    for it in range(maxiter):
+        if np.linalg.norm(r) < atol:
+            return x, it
+        z = psolve(r)
+        rho_cur = np.dot(r, z)
+        if it > 0:
+            beta = rho_cur / rho_prev
+            p *= beta
+            p += z
+        else:
+            p = np.empty_like(r)
+            p[:] = z[:]
+        q = matvec(p)
+        alpha = rho_cur / np.dot(p, q)
+        x += alpha * p
+        r -= alpha * q
+        rho_prev = rho_cur
+    return x, maxiter
+
+
+def pressure_projection_variable(a_star, b_star, dx, dy, dt, rho, bc_kind, lid, p_prev, eig,
+                                 rtol=1e-6, maxiter=200):
+    """functions.py:1296-1328 + :1347-1364 (variable density): returns (a, b, p, iters)."""
+    Ny, Nx = a_star.shape
+    divU = (_compute_divergence_rc_variable(a_star, b_star, p_prev, dt, rho, dx, dy)
+            if p_prev is not None else _compute_divergence(a_star, b_star, dx, dy))
+    rhs = (divU / dt).ravel()
+    rhs -= np.mean(rhs)
+    inv_rho = 1.0 / rho
+    x, iters = cg(lambda v: _apply_variable_poisson(v, Nx, Ny, dx, dy, inv_rho), rhs,
+                  lambda r: _solve_poisson_dct(r.reshape((Ny, Nx)), eig).ravel(), rtol, maxiter)
+    pc = x.reshape((Ny, Nx))
+    pc -= np.mean(pc)
+    gx, gy = _compute_pressure_gradient(pc, dx, dy)
+    a, b = apply_bc(bc_kind, lid, a_star - (dt / rho) * gx, b_star - (dt / rho) * gy)
+    p = p_prev + pc if p_prev is not None else pc
+    p -= np.mean(p)
+    return a, b, p, iters
+
+
 def _compute_divergence_rc(a, b, p, dt, rho, dx, dy):
-    if isinstance(rho, np.ndarray) and rho.ndim == 2 and np.ptp(rho) > 1e-10:
-        raise NotImplementedError("variable-density Rhie-Chow")
+    if _is_variable_rho(rho):
+        return _compute_divergence_rc_variable(a, b, p, dt, rho, dx, dy)
     d_f = dt / float(np.mean(rho))
     a, b, p = map(_c, (a, b, p)); out = _e(a.shape)
     _lib.rmto_divergence_rc(_p(a), _p(b), _p(p), d_f, a.shape[0], a.shape[1], dx, dy, _p(out))

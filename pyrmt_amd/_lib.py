@@ -92,6 +92,10 @@ SIGNATURES = {
     "rmt_pressure_gradient": (_I, [_P, _P, _D, _D, _P, _P]),
     "rmt_solve_poisson_dct": (_I, [_P, _P, _D, _D, _P]),
     "rmt_pressure_projection": (_I, [_P, _P, _P, _D, _D, _D, _D, _I, _D, _P, _P, _P, _P]),
+    "rmt_pressure_projection_variable": (_I, [_P, _P, _P, _D, _D, _D, _P, _I, _D, _P, _D, _I,
+                                              _P, _P, _P, ctypes.POINTER(_I)]),
+    "rmt_apply_variable_poisson": (_I, [_P, _P, _D, _D, _P, _P]),
+    "rmt_divergence_rc_variable": (_I, [_P, _P, _P, _P, _D, _P, _D, _D, _P]),
     "rmt_compute_timestep": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D,
                                   ctypes.POINTER(_D)]),
     "rmt_sim_create": (_I, [_P, ctypes.POINTER(rmt_sim_params), ctypes.POINTER(_P)]),

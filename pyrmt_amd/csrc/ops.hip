@@ -382,23 +382,6 @@ __global__ void k_divergence_central(const double *__restrict__ a, const double 
                   ? 0.0
                   : (a[c + 1] - a[c - 1]) / (2 * dx) + (b[c + nx] - b[c - nx]) / (2 * dy);
 }
-// functions.py:1073-1089 at one cell.
-__device__ __forceinline__ void pgrad_cell(const double *__restrict__ p, long c, int j, int i,
-                                           int ny, int nx, double dx, double dy, double &gx,
-                                           double &gy) {
-    const double *row = p + (c - i), *col = p + i;
-    gx = 0.0; gy = 0.0;
-    if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1) {
-        gx = (p[c + 1] - p[c - 1]) / (2 * dx);
-        gy = (p[c + nx] - p[c - nx]) / (2 * dy);
-    }
-    if (i == 0) gx = (-3.0 * row[0] + 4.0 * row[1] - row[2]) / (2.0 * dx);
-    if (i == nx - 1) gx = (3.0 * row[nx - 1] - 4.0 * row[nx - 2] + row[nx - 3]) / (2.0 * dx);
-    if (j == 0) gy = (-3.0 * col[0] + 4.0 * col[nx] - col[2L * nx]) / (2.0 * dy);
-    if (j == ny - 1)
-        gy = (3.0 * col[(long)(ny - 1) * nx] - 4.0 * col[(long)(ny - 2) * nx] +
-              col[(long)(ny - 3) * nx]) / (2.0 * dy);
-}
 __global__ void k_pressure_gradient(const double *__restrict__ p, int ny, int nx, double dx,
                                     double dy, double *__restrict__ gx, double *__restrict__ gy) {
     long c = blockIdx.x * (long)blockDim.x + threadIdx.x;

@@ -322,6 +322,23 @@ __device__ __forceinline__ double weno5_diff(const double *f, long s, int k, int
 // benchmarks/common.py:27-50 as data: for boundary kind `kind`, the BC'd value of each
 // velocity component at (j, i) is either a constant or the raw (pre-BC) value of one
 // source cell.  Callers read the raw value themselves (no device lambdas).
+// functions.py:1073-1089 (_compute_pressure_gradient) at one cell
+__device__ __forceinline__ void pgrad_cell(const double *__restrict__ p, long c, int j, int i,
+                                           int ny, int nx, double dx, double dy, double &gx,
+                                           double &gy) {
+    const double *row = p + (c - i), *col = p + i;
+    gx = 0.0; gy = 0.0;
+    if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1) {
+        gx = (p[c + 1] - p[c - 1]) / (2 * dx);
+        gy = (p[c + nx] - p[c - nx]) / (2 * dy);
+    }
+    if (i == 0) gx = (-3.0 * row[0] + 4.0 * row[1] - row[2]) / (2.0 * dx);
+    if (i == nx - 1) gx = (3.0 * row[nx - 1] - 4.0 * row[nx - 2] + row[nx - 3]) / (2.0 * dx);
+    if (j == 0) gy = (-3.0 * col[0] + 4.0 * col[nx] - col[2L * nx]) / (2.0 * dy);
+    if (j == ny - 1)
+        gy = (3.0 * col[(long)(ny - 1) * nx] - 4.0 * col[(long)(ny - 2) * nx] +
+              col[(long)(ny - 3) * nx]) / (2.0 * dy);
+}
 struct BCSrc {
     bool u_const, v_const;
     double u_val, v_val;

@@ -369,7 +369,23 @@ def _rho_scalar(rho):
     return r0
 
 
+def _is_variable_rho(rho):
+    """functions.py:1026 / :1297: a 2D array whose ptp exceeds 1e-10."""
+    if np.isscalar(rho) or not hasattr(rho, "ndim") or rho.ndim != 2:
+        return False
+    r = rho.detach().cpu().numpy() if hasattr(rho, "detach") else np.asarray(rho)
+    return bool(np.ptp(r) > 1e-10)
+
+
 def _compute_divergence_rc(a_star, b_star, p_prev, dt, rho, dx, dy):
+    if _is_variable_rho(rho):
+        io = _IO(a_star, b_star, p_prev, rho)
+        a, b, p, r = map(io.dev, (a_star, b_star, p_prev, rho))
+        out = io.empty(a.shape)
+        c = ctx_for(*a.shape)
+        L.check(L.lib().rmt_divergence_rc_variable(c.bind(), _p(a), _p(b), _p(p), dt, _p(r), dx,
+                                                   dy, _p(out)), "_compute_divergence_rc")
+        return io.out(out)
     r = _rho_scalar(rho)
     io = _IO(a_star, b_star, p_prev); a, b, p = map(io.dev, (a_star, b_star, p_prev))
     out = io.empty(a.shape)
@@ -377,6 +393,18 @@ def _compute_divergence_rc(a_star, b_star, p_prev, dt, rho, dx, dy):
     L.check(L.lib().rmt_divergence_rc(c.bind(), _p(a), _p(b), _p(p), dt / r, dx, dy, _p(out)),
             "_compute_divergence_rc")
     return io.out(out)
+
+
+def _apply_variable_poisson(p_flat, Nx, Ny, dx, dy, inv_rho):
+    """functions.py:1122-1168 (matrix-free div((1/rho) grad p)); flat in, flat out."""
+    io = _IO(p_flat, inv_rho)
+    p = io.dev(p_flat).reshape(Ny, Nx).contiguous()
+    ir = io.dev(inv_rho).reshape(Ny, Nx).contiguous()
+    out = io.empty((Ny, Nx))
+    c = ctx_for(Ny, Nx)
+    L.check(L.lib().rmt_apply_variable_poisson(c.bind(), _p(p), dx, dy, _p(ir), _p(out)),
+            "_apply_variable_poisson")
+    return io.out(out).reshape(-1)
 
 
 def _compute_divergence(a_star, b_star, dx, dy):
@@ -519,6 +547,8 @@ def pressure_projection_amg(a_star, b_star, dx, dy, dt, rho, velocity_bc, A=None
         raise NotImplementedError("the AMG fallback (eigenvalues=None) is outside this build's path")
     _grid_of_eigenvalues(eigenvalues)
     kind, lid = resolve_bc(velocity_bc)
+    if _is_variable_rho(rho):
+        return _projection_variable(a_star, b_star, dx, dy, dt, rho, kind, lid, A, ml, p_prev)
     r = _rho_scalar(rho)
     io = _IO(a_star, b_star, p_prev)
     a_s, b_s, pp = map(io.dev, (a_star, b_star, p_prev))
@@ -526,6 +556,26 @@ def pressure_projection_amg(a_star, b_star, dx, dy, dt, rho, velocity_bc, A=None
     c = ctx_for(*a_s.shape)
     L.check(L.lib().rmt_pressure_projection(c.bind(), _p(a_s), _p(b_s), dx, dy, dt, r, kind, lid,
                                             _p(pp), _p(a), _p(b), _p(p)), "pressure_projection_amg")
+    return io.out(a), io.out(b), io.out(p), A, ml
+
+
+# the reference's scipy.sparse.linalg.cg call (functions.py:1323): tol=1e-6, maxiter=200
+CG_RTOL, CG_MAXITER = 1e-6, 200
+last_cg_iterations = None
+
+
+def _projection_variable(a_star, b_star, dx, dy, dt, rho, kind, lid, A, ml, p_prev):
+    """functions.py:1296-1328 + :1350-1364 (variable density, DCT-preconditioned CG)."""
+    global last_cg_iterations
+    io = _IO(a_star, b_star, p_prev, rho)
+    a_s, b_s, pp, r = map(io.dev, (a_star, b_star, p_prev, rho))
+    a = io.empty(a_s.shape); b = io.empty(a_s.shape); p = io.empty(a_s.shape)
+    c = ctx_for(*a_s.shape)
+    it = ctypes.c_int()
+    L.check(L.lib().rmt_pressure_projection_variable(
+        c.bind(), _p(a_s), _p(b_s), dx, dy, dt, _p(r), kind, lid, _p(pp), CG_RTOL, CG_MAXITER,
+        _p(a), _p(b), _p(p), ctypes.byref(it)), "pressure_projection_amg")
+    last_cg_iterations = it.value
     return io.out(a), io.out(b), io.out(p), A, ml
 
 

@@ -499,6 +499,51 @@ def gen_periodic(N=65):
          null=null, p=p, a=a, b=b, p_prev=p_prev, an=an, bn=bn, pn=pn)
 
 
+def gen_varrho(N=33):
+    """functions.py:1016-1070, 1122-1168, 1296-1328: variable-density Rhie-Chow divergence,
+    the matrix-free operator, and the DCT-preconditioned CG projection.  The reference calls
+    scipy.sparse.linalg.cg(..., tol=1e-6, ...); scipy >= 1.14 (1.15 here) renamed tol to
+    rtol, so the call is routed through a keyword shim (tol -> rtol, nothing else) and the
+    iterations are counted with scipy's own callback.  scipy 1.15's LinearOperator also
+    probes an untyped matvec with an int8 vector, which the reference's operator cannot
+    take (it accumulates into zeros_like(p)); the shim passes dtype=float64, as older scipy
+    inferred."""
+    import scipy.sparse.linalg as sla
+    X, Y, dx, dy = F.create_grid(N, N, 1.0, 1.0)
+    rng = np.random.default_rng(21)
+    phi = np.sqrt((X - 0.5) ** 2 + (Y - 0.45) ** 2) - 0.25
+    H = F.smoothed_heaviside(phi, 2 * dx)
+    rho = (1 - H) * 4.0 + H * 1.0
+    p = rng.standard_normal((N, N))
+    Ap = F._apply_variable_poisson(p.ravel(), N, N, dx, dy, 1.0 / rho)
+    k = 2 * np.pi
+    a = 0.5 * np.sin(k * X) * np.cos(k * Y) + 0.1 * rng.standard_normal((N, N))
+    b = -0.5 * np.cos(k * X) * np.sin(k * Y) + 0.1 * rng.standard_normal((N, N))
+    p_prev = 0.1 * rng.standard_normal((N, N))
+    dt = 1e-3
+    divU = F._compute_divergence_rc(a, b, p_prev, dt, rho, dx, dy)
+    eig = F._precompute_poisson_eigenvalues(N, N, dx, dy)
+    iters = []
+
+    def cg_compat(A, rhs, x0=None, tol=1e-5, maxiter=None, M=None):
+        n = [0]
+        x, info = sla.cg(A, rhs, x0=x0, rtol=tol, maxiter=maxiter, M=M,
+                         callback=lambda xk: n.__setitem__(0, n[0] + 1))
+        iters.append(n[0])
+        return x, info
+    cg_ref, lo_ref = F.cg, F.LinearOperator
+    F.cg = cg_compat
+    F.LinearOperator = lambda shape, matvec: sla.LinearOperator(shape, matvec=matvec,
+                                                                dtype=np.float64)
+    try:
+        an, bn, pn, _, _ = F.pressure_projection_amg(a, b, dx, dy, dt, rho, C.free_slip_box_bc,
+                                                     p_prev=p_prev, eigenvalues=eig)
+    finally:
+        F.cg, F.LinearOperator = cg_ref, lo_ref
+    save("varrho", N=N, dx=dx, dy=dy, rho=rho, p=p, Ap=Ap, a=a, b=b, p_prev=p_prev, dt=dt,
+         divU=divU, eig=eig, an=an, bn=bn, pn=pn, iters=iters[0])
+
+
 def gen_mac_trace(N=64, nsteps=8, n_discs=3, seed=3):
     """Config 5 loop body (benchmarks/mac_multi_disc_lid.py:36-98) with the reference's
     own functions, no I/O: per-step centroids / J range and the final state."""
