@@ -647,6 +647,11 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes) {
     w.rec_by_chain = (long long *)take(maxt * 8);
     w.chain_of = (int *)take(maxt * 4);
     w.dmark = (int *)take(maxt * 4);
+    w.part = (unsigned char *)take(maxt);
+    w.loc = (int *)take(maxt * 4);
+    w.inv = (int *)take(maxt * 4);
+    w.gtag = (int *)take(maxt * 4);
+    w.gval = (double *)take(maxt * 16);
     w.rej = (int *)take((size_t)ML * EX_MAXREJ * 4);
     w.ctl = (int *)take(EXC_WORDS * 4);
     // one fixed slot per fit id (no allocation cursor shared by every wave of k_ex_geom) when

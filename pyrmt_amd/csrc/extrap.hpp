@@ -19,9 +19,12 @@ constexpr int EX_DCAP = 8192;       // fix-up dirty-list capacity
 
 // ctl words (int): fallback flag, abort flag, accepted count, and 64-bit arena cursor
 // EXC_ANY / EXC_NOOP: k_ex_none's proof that no target can be accepted (both paths skip)
+// EXC_CMIN / EXC_CMAX: column range of the targets; EXC_NPART + p: fits in chain part p
 enum { EXC_FALLBACK = 0, EXC_ABORT = 1, EXC_FILLED = 2, EXC_ARENA = 4, EXC_REJ = 8,
        EXC_BASE = 8 + EX_MAXL, EXC_ANY = 8 + 2 * EX_MAXL, EXC_NOOP = EXC_ANY + 1,
-       EXC_WORDS = 8 + 2 * EX_MAXL + 8 };
+       EXC_CMIN = EXC_ANY + 2, EXC_CMAX = EXC_ANY + 3, EXC_NPART = EXC_ANY + 4,
+       EXC_WORDS = 8 + 2 * EX_MAXL + 16 };
+constexpr int CH_MAXP = 4;          // chain parts (workgroups), split by target column
 
 struct ExWs {
     // band detection (both paths) and the fallback sweep
@@ -33,6 +36,13 @@ struct ExWs {
     int *rowcnt, *rowoff, *wordoff, *cbase;   // ML*ny, ML*(ny+1), ML*ny*W, ML*ny
     long long *tcell, *recoff, *rec_by_chain; // MAXT each
     int *chain_of, *dmark;                    // MAXT each
+    // parts: part[x] of chain index x, loc[x] its ordinal within the part, inv[base_p + l]
+    // the chain index of ordinal l of part p (base_p = fits of the parts before p);
+    // cross-part hand-offs go through HBM: gval / gtag by global slot base_p + l (a record's
+    // meta bit 63 marks a fit read by another part)
+    unsigned char *part;                      // MAXT
+    int *loc, *inv, *gtag;                    // MAXT each
+    double *gval;                             // 2 * MAXT
     int *rej;                                 // ML * EX_MAXREJ
     int *ctl;                                 // EXC_WORDS
     char *arena;

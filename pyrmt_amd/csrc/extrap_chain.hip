@@ -30,6 +30,8 @@
 // on the device; extrap.hip then runs the row-ticket sweep instead.
 #include "extrap.hpp"
 #include "exp_glibc.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace rmt {
 
@@ -436,6 +438,37 @@ __global__ void __launch_bounds__(1024) k_ex_order(ExWs ws, int ny, int ML) {
     }
 }
 
+// chain parts: split column = middle of the targets' column range (nparts == 2), so the two
+// workgroups take the two sides of the band; the few fits near the split column hand their
+// values across through HBM
+__global__ void __launch_bounds__(1024) k_ex_split(ExWs ws, int nx, int ML, int nparts) {
+    __shared__ int smin[1024], smax[1024];
+    const int t = threadIdx.x, total = ws.ctl[EXC_BASE + ML];
+    int mn = 0x7fffffff, mx = -1;
+    for (int id = t; id < total; id += 1024) {
+        const int i = (int)(ws.tcell[id] % nx);
+        mn = min(mn, i); mx = max(mx, i);
+    }
+    smin[t] = mn; smax[t] = mx;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if (t < w) { smin[t] = min(smin[t], smin[t + w]); smax[t] = max(smax[t], smax[t + w]); }
+        __syncthreads();
+    }
+    if (t == 0) {
+        ws.ctl[EXC_CMIN] = smin[0];
+        ws.ctl[EXC_CMAX] = smax[0] >= smin[0] ? smax[0] - smin[0] + 1 : 1;   // span
+        ws.ctl[EXC_NPART + CH_MAXP] = nparts;
+    }
+}
+// part of a target column: nparts equal column ranges over the targets' span
+__device__ __forceinline__ int ch_part_of(const int *ctl, int i) {
+    const int np = ctl[EXC_NPART + CH_MAXP];
+    if (np <= 1) return 0;
+    const long q = (long)(i - ctl[EXC_CMIN]) * np / ctl[EXC_CMAX];
+    return (int)min((long)np - 1, max(0L, q));
+}
+
 __global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, int ML,
                                                      int *status) {
     if (ws.ctl[EXC_FALLBACK]) return;
@@ -448,6 +481,7 @@ __global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, in
         const int x = ws.cbase[(long)L * ny + j] +
                       (id - ws.ctl[EXC_BASE + L] - ws.rowoff[(long)L * (ny + 1) + j]);
         ws.chain_of[id] = x;
+        ws.part[x] = (unsigned char)ch_part_of(ws.ctl, (int)(ws.tcell[id] % nx));
         const long long r = ws.recoff[id];
         ws.rec_by_chain[x] = r;
         acc = r >= 0;
@@ -456,8 +490,65 @@ __global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, in
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(status, __popcll(b));
 }
 
-// record sources: fit ids -> chain indices (the ring needs every source < CH_R/2 back);
-// header word 23 <- (chain index, record) of the next accepted fit of the same chain wave
+// ordinals within the parts (chain order kept inside each part), their inverse, the part
+// sizes (ctl[EXC_NPART + p]); resets the cross-part hand-off tags.  One block.
+__global__ void __launch_bounds__(1024) k_ex_local(ExWs ws, int ML) {
+    __shared__ int sc[CH_MAXP][1024];
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int t = threadIdx.x, total = ws.ctl[EXC_BASE + ML], per = (total + 1023) / 1024;
+    const int a = min(total, t * per), b = min(total, a + per);
+    int cnt[CH_MAXP];
+#pragma unroll
+    for (int p = 0; p < CH_MAXP; ++p) cnt[p] = 0;
+    for (int x = a; x < b; ++x) {
+        const int px = ws.part[x];
+#pragma unroll
+        for (int p = 0; p < CH_MAXP; ++p) cnt[p] += px == p;
+    }
+#pragma unroll
+    for (int p = 0; p < CH_MAXP; ++p) sc[p][t] = cnt[p];
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        int v[CH_MAXP];
+#pragma unroll
+        for (int p = 0; p < CH_MAXP; ++p) v[p] = t >= d ? sc[p][t - d] : 0;
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < CH_MAXP; ++p) sc[p][t] += v[p];
+        __syncthreads();
+    }
+    int base[CH_MAXP], run[CH_MAXP];
+    int acc = 0;
+#pragma unroll
+    for (int p = 0; p < CH_MAXP; ++p) {
+        base[p] = acc; acc += sc[p][1023];
+        run[p] = sc[p][t] - cnt[p];
+    }
+    for (int x = a; x < b; ++x) {
+        const int px = ws.part[x];
+        int l = 0, bs = 0;
+#pragma unroll
+        for (int p = 0; p < CH_MAXP; ++p)
+            if (px == p) { l = run[p]++; bs = base[p]; }
+        ws.loc[x] = l;
+        ws.inv[bs + l] = x;
+        ws.gtag[x] = -1;
+    }
+    if (t == 1023) {
+#pragma unroll
+        for (int p = 0; p < CH_MAXP; ++p) { ws.ctl[EXC_NPART + p] = sc[p][1023]; }
+    }
+}
+__device__ __forceinline__ int ch_base(const int *ctl, int p) {
+    int b = 0;
+    for (int q = 0; q < p; ++q) b += ctl[EXC_NPART + q];
+    return b;
+}
+
+// record sources: fit ids -> ring tags within the fit's part (the ring needs every source
+// < CH_R/2 back), or -(global slot + 1) for a source in the other part (marked for the HBM
+// hand-off); header word 23 <- (ordinal, record) of the next accepted fit of the same chain
+// wave of the part
 __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
     if (ws.ctl[EXC_FALLBACK]) return;
     const int id = blockIdx.x * 256 + threadIdx.x, total = ws.ctl[EXC_BASE + ML];
@@ -465,22 +556,32 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
     const long long r = ws.recoff[id];
     if (r < 0) return;
     double *rec = (double *)(ws.arena + ((r & 0xffffffffLL) << 6));
+    // meta bit 63 (set here by the readers in other parts): publish to HBM as well
     const long long meta = __double_as_longlong(rec[1]);
-    const int npad = (int)(meta & 0xffffffff), nd = (int)(meta >> 32);
+    const int nd = (int)((meta >> 32) & 0x7fffffff);
     int2 *dyn = (int2 *)(rec + CH_HDR);   // entry d at int2 index 2d: (k, src)
-    const int x = ws.chain_of[id];
-    (void)npad;
+    const int x = ws.chain_of[id], p = ws.part[x], l = ws.loc[x];
+    const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
     for (int d = 0; d < nd; ++d) {
         const int xs = ws.chain_of[dyn[4 * d].y];
-        dyn[4 * d].y = xs;
         if (xs >= x) { ws.ctl[EXC_ABORT] = 1; atomicExch(ws.status + 1, 1); }   // a bug
-        else if (x - xs >= CH_R / 2) ws.ctl[EXC_FALLBACK] = 1;
+        if (ws.part[xs] == p) {
+            const int ls = ws.loc[xs];
+            dyn[4 * d].y = ls;
+            if (l - ls >= CH_R / 2) ws.ctl[EXC_FALLBACK] = 1;
+        } else {
+            const int g = ch_base(ws.ctl, ws.part[xs]) + ws.loc[xs];
+            dyn[4 * d].y = -(g + 1);
+            const long long rs = ws.rec_by_chain[xs];
+            double *srec = (double *)(ws.arena + ((rs & 0xffffffffLL) << 6));
+            atomicOr((unsigned long long *)&srec[1], 1ull << 63);
+        }
     }
-    int xn = x + CH_W;
-    while (xn < total && ws.rec_by_chain[xn] < 0) xn += CH_W;
-    const long long rn = xn < total ? ws.rec_by_chain[xn] : 0;   // (size64 << 32) | off64
+    int ln = l + CH_W;
+    while (ln < np && ws.rec_by_chain[ws.inv[base + ln]] < 0) ln += CH_W;
+    const long long rn = ln < np ? ws.rec_by_chain[ws.inv[base + ln]] : 0;   // (size64 << 32) | off64
     const unsigned r32 = (unsigned)(rn & 0xffffffffLL) | ((unsigned)(rn >> 32) << 25);
-    rec[23] = __longlong_as_double(((long long)xn << 32) | r32);
+    rec[23] = __longlong_as_double(((long long)ln << 32) | r32);
 }
 
 // ------------------------------------------------------------------ 3. the chain ---
@@ -493,6 +594,29 @@ struct ChainArgs {
     int ML;
     int *status;
 };
+
+// source of a record term: e.y >= 0 -> this part's LDS ring (tag e.y); e.y < 0 -> the other
+// part's HBM hand-off slot -e.y - 1 (tag written after the value, agent-scope release)
+__device__ __forceinline__ bool ch_probe(int ey, const int *tag, const double2 *val,
+                                         const int *gtag, const double *gval, double2 &v) {
+    if (ey >= 0) {
+        const int slot = ey & (CH_R - 1);
+        if (__hip_atomic_load(&tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ey)
+            return false;
+        asm volatile("" ::: "memory");
+        v = val[slot];
+        return true;
+    }
+    const int g = -ey - 1;
+    if (__hip_atomic_load(&gtag[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != g) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const unsigned long long *gv = (const unsigned long long *)gval;
+    v.x = __longlong_as_double((long long)__hip_atomic_load(&gv[2 * g], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT));
+    v.y = __longlong_as_double((long long)__hip_atomic_load(&gv[2 * g + 1], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT));
+    return true;
+}
 
 // record r (packed: 64-B units of offset | size << 25) -> five 16-B pieces per lane; every
 // lane issues the same 5 loads (lanes past the record re-read its last piece, same line).
@@ -568,7 +692,8 @@ __device__ __forceinline__ double dpp_shl(double v, int ctrl) {
 template <bool PROF, int VAR>
 __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                        int *cur, int &wm, double &o_out, long &c_out,
-                                       long long *pr, long long &tl) {
+                                       long long *pr, long long &tl, int *gtag, double *gval,
+                                       int gslot) {
     // ring reuse: every fit < x - CH_R/2 is done (all their readers are < x)
     long spins = 0;
     while (x - CH_R / 2 >= wm) {
@@ -584,7 +709,9 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     CH_STAMP(1);
     const long long meta = __double_as_longlong(B[1]);
     const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
-    const int nd = __builtin_amdgcn_readfirstlane((int)(meta >> 32));
+    const int nd = __builtin_amdgcn_readfirstlane((int)((meta >> 32) & 0x7fffffff));
+    const bool pub = !(VAR & 16) &&
+                     __builtin_amdgcn_readfirstlane((int)((unsigned long long)meta >> 63)) != 0;
     if (npad > CH_TVS || nd > 64 || npad < 0 || nd < 0) return false;   // bug guard
     const double *dyn = B + CH_HDR;
     double *tv = B + CH_HDR + 4 * nd;
@@ -609,12 +736,30 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         e = make_int2((int)(kk & 0xffffffff), (int)(kk >> 32));
         cf[0] = q0.y; cf[1] = q1.x; cf[2] = q1.y;
     }
-    const int slot = e.y & (CH_R - 1);
     bool done = !has;   // product written
+    // VAR bit 4: one part only (no far sources, nothing to publish).  Sources in another
+    // part (e.y < 0; rare: near the part boundaries, and usually published long before) are
+    // awaited first through HBM, so the LDS passes below stay the one-part code.
+    const int slot = e.y & (CH_R - 1);
+    const bool far = !(VAR & 16) && has && e.y < 0;
+    if (!(VAR & 16) && __ballot(far)) {
+        long sp = 0;
+        for (;;) {
+            double2 v;
+            if (far && !done && ch_probe(e.y, tag, val, gtag, gval, v)) {
+#pragma unroll
+                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+                done = true;
+            }
+            if (__ballot(far && !done) == 0) break;
+            if (++sp > CH_SPIN_LIMIT) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
     // pass 1: products of the sources already published; fold up to the first missing one
     {
-        const bool ready = has && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
+        const bool ready = has && !done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
         asm volatile("" ::: "memory");
         if (ready) {
             const double2 v = val[slot];
@@ -666,11 +811,17 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         const double zs = (M0 * (M4 * b2 - b1 * M7) - M1 * (M3 * b2 - b1 * M6) + b0 * C2) * inv_det;
         const double o = xs + ys * x0 + zs * y0;
         ((double *)&val[x & (CH_R - 1)])[lane == 0 ? 0 : 1] = o;
+        if (pub) gval[2 * gslot + (lane == 0 ? 0 : 1)] = o;
         o_out = o;
     }
     asm volatile("" ::: "memory");
     if (lane == 0)
         __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (pub) {   // a fit of the other part reads this one: value, then tag (agent release)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0)
+            __hip_atomic_store(&gtag[gslot], gslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
     c_out = __double_as_longlong(B[0]);
     if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -692,12 +843,14 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
     if (threadIdx.x < CH_W) cur[threadIdx.x] = 0;
     __syncthreads();
     if (ctl[EXC_FALLBACK] || ctl[EXC_ABORT]) return;
-    const int total = ctl[EXC_BASE + C.ML];
+    // this workgroup runs part blockIdx.x; x below is the ordinal within the part
+    const int part = blockIdx.x, base = ch_base(ctl, part);
+    const int total = ctl[EXC_NPART + part];
     double *B = buf[wv];
     // this wave's first accepted fit; every record names the wave's next one (k_ex_relink)
     int x = wv;
     long long r0 = -1;
-    while (x < total && (r0 = C.ws.rec_by_chain[x]) < 0) x += CH_W;
+    while (x < total && (r0 = C.ws.rec_by_chain[C.ws.inv[base + x]]) < 0) x += CH_W;
     unsigned r = (unsigned)(r0 & 0xffffffffLL) | (unsigned)((r0 >> 32) << 25);
     double2 d0, d1, d2, d3, d4;
     if (x < total) CH_LOAD(r);
@@ -723,7 +876,8 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         if (x2 <= x) { ok = false; break; }   // bug guard: the wave's sequence must advance
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
-        if (!ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl)) { ok = false; break; }
+        if (!ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag, C.ws.gval,
+                               base + x)) { ok = false; break; }
         x = x2; r = r2;
     }
     if constexpr (PROF)
@@ -758,9 +912,14 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
         k_ex_fix<<<1, FIXW * 64, 0, st>>>(A);
         RMT_LAUNCHED();
     }
+    // RMT_CH_PARTS: workgroups running the chain, one per column range of the band
+    static const int nparts = getenv("RMT_CH_PARTS") ? std::min(CH_MAXP, std::max(1,
+                                  atoi(getenv("RMT_CH_PARTS")))) : 2;
     k_ex_order<<<1, 1024, 0, st>>>(ws, ny, ML);
+    k_ex_split<<<1, 1024, 0, st>>>(ws, nx, ML, nparts);
     const unsigned idb = grid1d(ws.maxt, 256);
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
+    k_ex_local<<<1, 1024, 0, st>>>(ws, ML);
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
     if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
@@ -769,10 +928,12 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 3;
     if (!prof) {
         switch (var) {
-            case 0: k_ex_chain<false, 0><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 1: k_ex_chain<false, 1><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 2: k_ex_chain<false, 2><<<1, CH_W * 64, 0, st>>>(C, nullptr); break;
-            default: k_ex_chain<false, 3><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+            case 0: k_ex_chain<false, 0><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
+            case 1: k_ex_chain<false, 1><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
+            case 2: k_ex_chain<false, 2><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
+            default:
+                if (nparts == 1) k_ex_chain<false, 19><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+                else k_ex_chain<false, 3><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
         }
         RMT_LAUNCHED();
     } else {
@@ -783,7 +944,7 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
         hipEvent_t e0, e1;
         RMT_HIP(hipEventCreate(&e0)); RMT_HIP(hipEventCreate(&e1));
         RMT_HIP(hipEventRecord(e0, st));
-        k_ex_chain<true, 3><<<1, CH_W * 64, 0, st>>>(C, gp);
+        k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, st));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));
