@@ -5,9 +5,9 @@ O=gpurun_out/s4p2
 mkdir -p $O
 RMT_CH_PARTS=4 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -m gpu > $O/tests2.log 2>&1 || { tail -30 $O/tests2.log; exit 1; }
 tail -2 $O/tests2.log
-for p in 1 2; do
+for p in 3 4; do
   RMT_CH_PARTS=$p timeout -k 10 200 python -u tools/chain_time.py 3 > $O/chain_p$p.log 2>&1 || { tail -5 $O/chain_p$p.log; exit 1; }
   echo parts=$p $(grep variant $O/chain_p$p.log)
 done
-RMT_CH_PARTS=2 timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/bench2.log 2>&1 || exit $?
-tail -1 $O/bench2.log | cut -c1-300
+true
+true
