@@ -441,11 +441,13 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         k_mac_centres<<<grid1d(n, 256), 256, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags, 0,
                                                       N);
         RMT_LAUNCHED();
+        // max |u_c|^2 bounds every velocity sample of the backtraces (the SL block skip)
+        RMT_TRY(reduce_maxsq2_nan(ctx, S->uc, S->vc, n, S->out + 8));
         for (int k = 0; k < K; ++k) {
             // phi from the current map (already S->phi[k]), advect with the pre-advection mask
             RMT_TRY(sl_disc_map(ctx, S->X1[k], S->X2[k], S->uc, S->vc, S->xs, S->ys, dt, dx, dx,
                                 P.cx[k], P.cy[k], P.R[k], S->X1n, S->X2n, S->phi_pre,
-                                S->flags + 1));
+                                S->flags + 1, S->out + 8));
             RMT_TRY(extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, dx, dx, P.layers, S->X1n, S->X2n,
                                 S->flags + 2));
             k_mac_phi<<<grid1d(n, 256), 256, 0, st>>>(S->X1n, S->X2n, n, P.cx[k], P.cy[k], P.R[k],
@@ -734,10 +736,12 @@ int rmt_mac_slab_advect(rmt_mac_slab *S, double dt) {
         S->gu(S->u), S->gc(S->v), N, S->gc(S->uc), S->gc(S->vc), S->flags, S->lo, S->hi);
     RMT_LAUNCHED();
     const int jb = std::max(0, S->r0 - 3), je = std::min(N, S->r1 + 3);
+    RMT_TRY(reduce_maxsq2_nan(ctx, S->uc, S->vc, (long)(S->hi - S->lo) * N, S->scal + MS_N - 1));
     for (int k = 0; k < P.n_discs; ++k) {
         RMT_TRY(slab_sl(ctx, S->gc(S->X1[k]), S->gc(S->X2[k]), S->gc(S->uc), S->gc(S->vc), S->xs,
                         S->xs, N, N, dt, P.dx, P.dx, P.cx[k], P.cy[k], P.R[k], S->gc(S->X1n[k]),
-                        S->gc(S->X2n[k]), S->gc(S->phi_pre[k]), S->flags, jb, je, S->lo, S->hi));
+                        S->gc(S->X2n[k]), S->gc(S->phi_pre[k]), S->flags, jb, je, S->lo, S->hi,
+                        S->scal + MS_N - 1));
         RMT_TRY(slab_bits(ctx, S->gc(S->phi_pre[k]), N, S->W, S->bits[k], S->r0, S->r1));
     }
     return RMT_OK;

@@ -41,8 +41,9 @@ __global__ void __launch_bounds__(RED_T) k_reduce_p1(const double *__restrict__ 
     __shared__ double s[RED_T];
     double acc = OP == 0 ? 0.0 : -INFINITY;
     for (long k = blockIdx.x * (long)RED_T + threadIdx.x; k < n; k += (long)RED_BLOCKS * RED_T) {
-        double x = OP == 2 ? a[k] * a[k] + b[k] * b[k] : a[k];
+        double x = OP >= 2 ? a[k] * a[k] + b[k] * b[k] : a[k];
         if (OP == 0) acc += x;
+        else if (OP == 3) acc = (x > acc || x != x) ? x : acc;   // NaN propagates
         else acc = fmax(acc, x);   // NaN inputs are not on the path (guarded upstream)
     }
     s[threadIdx.x] = acc;
@@ -50,7 +51,10 @@ __global__ void __launch_bounds__(RED_T) k_reduce_p1(const double *__restrict__ 
     for (int w = RED_T / 2; w > 0; w >>= 1) {
         if (threadIdx.x < w)
             s[threadIdx.x] = OP == 0 ? s[threadIdx.x] + s[threadIdx.x + w]
-                                     : fmax(s[threadIdx.x], s[threadIdx.x + w]);
+                             : OP == 3 ? ((s[threadIdx.x + w] > s[threadIdx.x] ||
+                                           s[threadIdx.x + w] != s[threadIdx.x + w])
+                                              ? s[threadIdx.x + w] : s[threadIdx.x])
+                                       : fmax(s[threadIdx.x], s[threadIdx.x + w]);
         __syncthreads();
     }
     if (threadIdx.x == 0) part[blockIdx.x] = s[0];
@@ -61,14 +65,19 @@ __global__ void __launch_bounds__(RED_T) k_reduce_p2(const double *__restrict__ 
                                                      double scale) {
     __shared__ double s[RED_T];
     double acc = OP == 0 ? 0.0 : -INFINITY;
-    for (int k = threadIdx.x; k < RED_BLOCKS; k += RED_T)
-        acc = OP == 0 ? acc + part[k] : fmax(acc, part[k]);
+    for (int k = threadIdx.x; k < RED_BLOCKS; k += RED_T) {
+        const double y = part[k];
+        acc = OP == 0 ? acc + y : OP == 3 ? ((y > acc || y != y) ? y : acc) : fmax(acc, y);
+    }
     s[threadIdx.x] = acc;
     __syncthreads();
     for (int w = RED_T / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w)
-            s[threadIdx.x] = OP == 0 ? s[threadIdx.x] + s[threadIdx.x + w]
-                                     : fmax(s[threadIdx.x], s[threadIdx.x + w]);
+        if (threadIdx.x < w) {
+            const double y = s[threadIdx.x + w];
+            s[threadIdx.x] = OP == 0 ? s[threadIdx.x] + y
+                             : OP == 3 ? ((y > s[threadIdx.x] || y != y) ? y : s[threadIdx.x])
+                                       : fmax(s[threadIdx.x], y);
+        }
         __syncthreads();
     }
     if (threadIdx.x == 0) *out = OP == 0 ? s[0] * scale : s[0];
@@ -82,9 +91,12 @@ static int reduce_impl(rmt_ctx *ctx, int op, const double *a, const double *b, l
     } else if (op == 1) {
         k_reduce_p1<1><<<RED_BLOCKS, RED_T, 0, ctx->stream>>>(a, b, n, ctx->red);
         k_reduce_p2<1><<<1, RED_T, 0, ctx->stream>>>(ctx->red, out, scale);
-    } else {
+    } else if (op == 2) {
         k_reduce_p1<2><<<RED_BLOCKS, RED_T, 0, ctx->stream>>>(a, b, n, ctx->red);
         k_reduce_p2<1><<<1, RED_T, 0, ctx->stream>>>(ctx->red, out, scale);
+    } else {
+        k_reduce_p1<3><<<RED_BLOCKS, RED_T, 0, ctx->stream>>>(a, b, n, ctx->red);
+        k_reduce_p2<3><<<1, RED_T, 0, ctx->stream>>>(ctx->red, out, scale);
     }
     RMT_LAUNCHED();
     return RMT_OK;
@@ -93,6 +105,9 @@ int reduce_sum(rmt_ctx *ctx, const double *x, long n, double *o) { return reduce
 int reduce_max(rmt_ctx *ctx, const double *x, long n, double *o) { return reduce_impl(ctx, 1, x, x, n, o, 1.0); }
 int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double *o) {
     return reduce_impl(ctx, 2, a, b, n, o, 1.0);
+}
+int reduce_maxsq2_nan(rmt_ctx *ctx, const double *a, const double *b, long n, double *o) {
+    return reduce_impl(ctx, 3, a, b, n, o, 1.0);
 }
 int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *o) {
     return reduce_impl(ctx, 0, x, x, n, o, 1.0 / (double)n);

@@ -153,6 +153,37 @@ __device__ __forceinline__ void sl_backtrace(const double *__restrict__ a,
     sl_backtrace_t<false>(a, b, x, y, dt, dx, dy, nx, ny, 0, ny, nullptr, xb, yb);
 }
 
+// Semi-Lagrangian block skip.  With every velocity sample bounded by sqrt(m2) and
+// dt * sqrt(m2) <= 0.9 h, every RK4 stage point and the foot of cell (i, j) lie within 0.9
+// cells of it, so all its bilinear stencils read rows j-1 .. j+2 and columns i-1 .. i+2.  A
+// block of cells [i0, i0 + w) of row j whose map is +0.0 on that whole neighbourhood therefore
+// advects to exactly +0.0 (non-negative weights times +0.0, summed) -- the map is zero away
+// from the solid, so most blocks skip the backtrace.  Rows outside [lo, hi) are not
+// resident: such a block is not certified.  Call with every thread of the block.
+// m2 from reduce_maxsq2_nan: finite only if every velocity is, so a skipped block needs no
+// finiteness check of its own
+__device__ __forceinline__ bool sl_skip_ok(const double *m2, double dt, double h) {
+    return m2 && dt * sqrt(*m2) <= 0.9 * h;
+}
+__device__ __forceinline__ bool sl_zero_block(const double *__restrict__ X1,
+                                              const double *__restrict__ X2, int ny, int nx,
+                                              int j, int i0, int w, int lo, int hi) {
+    const int ja = max(0, j - 1), jb = min(ny - 1, j + 2);
+    const int ia = max(0, i0 - 1), ib = min(nx - 1, i0 + w + 1), cw = ib - ia + 1;
+    const int nq = (jb - ja + 1) * cw;
+    unsigned long long bits = (ja < lo || jb >= hi) ? 1 : 0;
+    if (!bits) {
+        // all loads issued before any test (no early exit: one memory round trip)
+#pragma unroll 4
+        for (int q = threadIdx.x; q < nq; q += blockDim.x) {
+            const long c = (long)(ja + q / cw) * nx + ia + q % cw;
+            bits |= (unsigned long long)__double_as_longlong(X1[c]) |
+                    (unsigned long long)__double_as_longlong(X2[c]);
+        }
+    }
+    return !__syncthreads_or(bits != 0);
+}
+
 // interpolators.py:144-156 cubic_convolution (Catmull-Rom); Numba's x**3 = x * (x * x)
 __device__ __forceinline__ double cubic_conv(double v0, double v1, double v2, double v3, double x) {
     const double a0 = -0.5 * v0 + 1.5 * v1 - 1.5 * v2 + 0.5 * v3;
@@ -371,6 +402,8 @@ constexpr int RED_BLOCKS = 1024, RED_T = 256;   // ctx->red holds RED_BLOCKS + 6
 int reduce_sum(rmt_ctx *ctx, const double *x, long n, double *dev_out);     // device scalar
 int reduce_max(rmt_ctx *ctx, const double *x, long n, double *dev_out);
 int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double *dev_out);
+// the same with NaN propagating (a non-finite velocity makes the bound NaN: no SL block skip)
+int reduce_maxsq2_nan(rmt_ctx *ctx, const double *a, const double *b, long n, double *dev_out);
 int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *dev_out);
 int read_scalar(rmt_ctx *ctx, const double *dev, double *host);
 // row-tree sums (ops.hip): root of rows [0, nrows) of x (row length nx) into *dev_root;
@@ -399,10 +432,11 @@ int diag_rows(rmt_ctx *ctx, const double *phi, const double *J, const double *xs
               const double *X2, const rmt_sim_params &P, int jb, int je, double *part,
               double *out);
 
+// dev_m2 (optional, device): a bound on a^2 + b^2 over the grid (enables the block skip)
 int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
-                double *phi_pre, int *bad);
+                double *phi_pre, int *bad, const double *dev_m2 = nullptr);
 
 // --------------------------------------------------------------------- momentum --
 // every stage keeps its own k and accumulation planes (k1, k2, k3, acc1 = k1 + 2 k2,
@@ -472,7 +506,7 @@ int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *c
 int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, const double *b,
             const double *xs, const double *ys, int ny, int nx, double dt, double dx, double dy,
             double x0, double y0, double R, double *X1n, double *X2n, double *phi_pre,
-            int *flags, int jb, int je, int lo, int hi);
+            int *flags, int jb, int je, int lo, int hi, const double *dev_m2 = nullptr);
 int slab_bits(rmt_ctx *ctx, const double *phi, int nx, int W, unsigned long long *bits, int r0,
               int r1);
 int slab_rim_pack(rmt_ctx *ctx, const unsigned long long *bits, int ny, int nx, int W, int r0,

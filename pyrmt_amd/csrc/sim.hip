@@ -55,24 +55,35 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
                          int nx, double dt, double dx, double dy, int shape, double x0, double y0,
                          double R, double *__restrict__ X1n, double *__restrict__ X2n,
                          double *__restrict__ phi_pre, int *bad,
-                         unsigned long long *__restrict__ kbits) {
+                         unsigned long long *__restrict__ kbits, const double *m2) {
     // grid (ceil(nx / 256), ny): a wave covers 64 cells of one row, so the extrapolation's
     // known plane (phi_pre < 0, 64-cell words) comes out of the same pass (kbits optional)
-    const int j = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const int j = blockIdx.y, i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
     const bool in = i < nx;
     const long c = (long)j * nx + i;
+    const bool zero = sl_skip_ok(m2, dt, fmin(dx, dy)) &&
+                      sl_zero_block(X1, X2, ny, nx, j, i0, 256, 0, ny);
     bool known = false;
-    if (in) {
+    if (in && zero) {
+        // the map is +0.0 here: phi of the origin, advected map +0.0 (no loads); phi_pre
+        // only when no known plane is produced (its only reader is then the extrapolation)
+        const double ph = disc_phi(0.0, 0.0, x0, y0, R);
+        if (!kbits) phi_pre[c] = ph;
+        known = ph < 0;
+        X1n[c] = 0.0; X2n[c] = 0.0;
+    } else if (in) {
         bool fin = isfinite(a[c]) && isfinite(b[c]);
         if (!fin) atomicOr(bad, 1);
         double ph = disc_phi(X1[c], X2[c], x0, y0, R);
-        phi_pre[c] = ph;
+        if (!kbits) phi_pre[c] = ph;
         known = ph < 0;
-        double m = ph <= 0 ? 1.0 : 0.0;
-        double xb, yb;
-        sl_backtrace(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, xb, yb);
-        X1n[c] = bilinear(X1, xb, yb, dx, dy, nx, ny) * m;
-        X2n[c] = bilinear(X2, xb, yb, dx, dy, nx, ny) * m;
+        {
+            double m = ph <= 0 ? 1.0 : 0.0;
+            double xb, yb;
+            sl_backtrace(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, xb, yb);
+            X1n[c] = bilinear(X1, xb, yb, dx, dy, nx, ny) * m;
+            X2n[c] = bilinear(X2, xb, yb, dx, dy, nx, ny) * m;
+        }
     }
     if (kbits) {
         const unsigned long long w = __ballot(known);
@@ -256,10 +267,10 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p2(const double *__restrict__ p
 int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
-                double *phi_pre, int *bad) {
+                double *phi_pre, int *bad, const double *dev_m2) {
     k_sim_sl<<<dim3((ctx->nx + 255) / 256, ctx->ny), 256, 0, ctx->stream>>>(
         X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, dx, dy, RMT_SHAPE_DISC, x0, y0, R, X1n, X2n,
-        phi_pre, bad, nullptr);
+        phi_pre, bad, nullptr, dev_m2);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -381,8 +392,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end)) break;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[0], st));
-        // 1. dt (compute_timestep + the drivers' clip to t_end)
-        RMT_TRY(reduce_maxsq2(ctx, S->u, S->v, n, sc));
+        // 1. dt (compute_timestep + the drivers' clip to t_end); NaN-propagating max so it
+        // also bounds the velocities for the SL block skip
+        RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, n, sc));
         k_dt<<<1, 1, 0, st>>>(sc, S->dt_const, P.cfl, P.dx, sc + 1);
         double hv[2];
         RMT_HIP(hipMemcpyAsync(hv, sc, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -408,7 +420,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
                 k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, st>>>(
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
-                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits);
+                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits, sc);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN_CUBIC) {
                 k_sim_sl_cubic<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx,
                                                   dt, P.dx, P.dy, P.x0, P.y0, P.R, S->X1n,

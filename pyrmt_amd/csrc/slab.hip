@@ -43,7 +43,7 @@ using rmt::u64;
 namespace rmt {
 constexpr int SLAB_MAXG = 64;
 enum { SC_M2 = 0, SC_DIAG = 1, SC_FLAGS = 11, SC_COUNT = 12, SC_ROOT = 13, SC_FIT = 14,
-       SC_N = 16 };
+       SC_M2RES = 15, SC_N = 16 };
 enum { FL_NONFINITE = 1, FL_HALO = 2, FL_EXABORT = 4 };
 struct Splits { int v[SLAB_MAXG + 1]; };
 struct Counts { long long c[SLAB_MAXG]; };
@@ -83,10 +83,19 @@ __global__ void k_slab_sl(const double *__restrict__ X1, const double *__restric
                           int nx, double dt, double dx, double dy, double x0, double y0, double R,
                           double *__restrict__ X1n, double *__restrict__ X2n,
                           double *__restrict__ phi_pre, int *flags, int jb, int je, int lo,
-                          int hi) {
-    const long c = (long)jb * nx + blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)je * nx) return;
-    const int j = (int)(c / nx), i = (int)(c % nx);
+                          int hi, const double *m2) {
+    // grid (ceil(nx / 256), je - jb); the block skip of sl_zero_block (rmt_internal.hpp) with
+    // m2 bounding the velocities of the resident rows
+    const int j = jb + blockIdx.y, i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
+    const bool zero = sl_skip_ok(m2, dt, fmin(dx, dy)) &&
+                      sl_zero_block(X1, X2, ny, nx, j, i0, 256, lo, hi);
+    if (i >= nx) return;
+    const long c = (long)j * nx + i;
+    if (zero) {   // map +0.0 around: no loads (m2 finite: every velocity is)
+        phi_pre[c] = disc_phi(0.0, 0.0, x0, y0, R);
+        X1n[c] = 0.0; X2n[c] = 0.0;
+        return;
+    }
     if (!(isfinite(a[c]) && isfinite(b[c]))) atomicOr(flags, FL_NONFINITE);
     const double ph = disc_phi(X1[c], X2[c], x0, y0, R);
     phi_pre[c] = ph;
@@ -274,11 +283,11 @@ static int check_splits(const int *s, int G, int n, int minsz, bool even) {
 int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, const double *b,
             const double *xs, const double *ys, int ny, int nx, double dt, double dx, double dy,
             double x0, double y0, double R, double *X1n, double *X2n, double *phi_pre,
-            int *flags, int jb, int je, int lo, int hi) {
+            int *flags, int jb, int je, int lo, int hi, const double *dev_m2) {
     if (je <= jb) return RMT_OK;
-    k_slab_sl<<<grid1d((long)(je - jb) * nx, 256), 256, 0, ctx->stream>>>(
+    k_slab_sl<<<dim3((nx + 255) / 256, je - jb), 256, 0, ctx->stream>>>(
         X1, X2, a, b, xs, ys, ny, nx, dt, dx, dy, x0, y0, R, X1n, X2n, phi_pre, flags, jb, je,
-        lo, hi);
+        lo, hi, dev_m2);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -451,10 +460,12 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
     const rmt_sim_params &P = S->P;
     const int NX = S->NX, jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
     RMT_HIP(hipMemsetAsync(S->flags, 0, 8 * sizeof(int), ctx->stream));
-    k_slab_sl<<<grid1d((long)(je - jb) * NX, 256), 256, 0, ctx->stream>>>(
+    // max |u|^2 over the resident rows: bounds every velocity sample of the backtraces
+    RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, (long)(S->hi - S->lo) * NX, S->scal + SC_M2RES));
+    k_slab_sl<<<dim3((NX + 255) / 256, je - jb), 256, 0, ctx->stream>>>(
         S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt, P.dx,
         P.dy, P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre), S->flags, jb, je,
-        S->lo, S->hi);
+        S->lo, S->hi, S->scal + SC_M2RES);
     RMT_LAUNCHED();
     k_slab_bits<<<dim3((NX + 255) / 256, S->r1 - S->r0), 256, 0, ctx->stream>>>(
         S->gv(S->phi_pre), NX, S->W, S->bits, S->r0);
