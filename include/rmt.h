@@ -232,7 +232,8 @@ typedef struct {
 
 int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out);
 int rmt_sim_destroy(rmt_sim *sim);
-/* field ids: 0 u (a), 1 v (b), 2 p, 3 X1, 4 X2, 5 phi (last rebuilt), 6 J */
+/* field ids: 0 u (a), 1 v (b), 2 p, 3 X1, 4 X2, 5 phi (last rebuilt), 6 J, 7 sigma_xx,
+ * 8 sigma_xy, 9 sigma_yy (the solid stress of the last momentum step) */
 int rmt_sim_field(rmt_sim *sim, int field, double **dev_ptr);
 /* Enqueue nsteps loop bodies.  dt comes from compute_timestep on device and is clipped to
  * t_end - t as the drivers do; steps after t >= t_end are no-ops.  No host sync. */

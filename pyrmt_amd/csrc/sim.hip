@@ -374,8 +374,8 @@ int rmt_sim_destroy(rmt_sim *S) {
 
 int rmt_sim_field(rmt_sim *S, int field, double **ptr) {
     RMT_CHECK(S && ptr, RMT_EINVAL, "null argument");
-    double *f[] = {S->u, S->v, S->p, S->X1, S->X2, S->phi, S->J};
-    RMT_CHECK(field >= 0 && field < 7, RMT_EINVAL, "unknown field id");
+    double *f[] = {S->u, S->v, S->p, S->X1, S->X2, S->phi, S->J, S->sxx, S->sxy, S->syy};
+    RMT_CHECK(field >= 0 && field < 10, RMT_EINVAL, "unknown field id");
     *ptr = f[field];
     return RMT_OK;
 }

@@ -17,7 +17,8 @@ from . import _lib as L
 from . import functions as F
 from .bc import NOSLIP_LID, FREESLIP_BOX
 
-FIELDS = {"u": 0, "a": 0, "v": 1, "b": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5, "J": 6}
+FIELDS = {"u": 0, "a": 0, "v": 1, "b": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5, "J": 6,
+          "sigma_xx": 7, "sigma_xy": 8, "sigma_yy": 9}
 SCHEMES = {"semilagrangian": 0, "weno5": 1, "central2": 2, "conservative": 3,
            "semilagrangian_cubic": 4}
 
