@@ -204,17 +204,33 @@ struct DiagArgs {
 __global__ void __launch_bounds__(DIAG_T) k_diag_p1(DiagArgs A, double *__restrict__ part) {
     __shared__ double s[DIAG_VALS][DIAG_T];
     double v[DIAG_VALS] = {0, 0, 0, INFINITY, -INFINITY, 0, 0, 0, INFINITY, -INFINITY};
-    const long n = (long)A.je * A.nx;
-    for (long c = (long)A.jb * A.nx + blockIdx.x * (long)DIAG_T + threadIdx.x; c < n;
-         c += (long)DIAG_BLOCKS * DIAG_T) {
-        int j = (int)(c / A.nx), i = (int)(c % A.nx);
-        double ph = A.phi[c];
-        bool solid = ph <= 0.0;
+    // Each thread visits c0, c0 + S, c0 + 2S, ... (S = grid size) in that order; the loads
+    // of DIAG_U consecutive visits are issued together and (j, i) advance by (S / nx, S % nx)
+    // without a 64-bit division per cell.  Same cells, same accumulation order as one visit
+    // per iteration.
+    constexpr int DIAG_U = 4;
+    const long n = (long)A.je * A.nx, S = (long)DIAG_BLOCKS * DIAG_T;
+    const int dj = (int)(S / A.nx), di = (int)(S % A.nx);
+    long c = (long)A.jb * A.nx + blockIdx.x * (long)DIAG_T + threadIdx.x;
+    int j = (int)(c / A.nx), i = (int)(c % A.nx);
+    while (c < n) {
+        double phq[DIAG_U], Jq[DIAG_U];
+#pragma unroll
+        for (int k = 0; k < DIAG_U; ++k) {
+            const long ck = c + k * S;
+            phq[k] = ck < n ? A.phi[ck] : 0.0;
+            Jq[k] = ck < n ? A.J[ck] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < DIAG_U; ++k) {
+        if (c >= n) break;
+        const double ph = phq[k];
+        const bool solid = ph <= 0.0;
         if (solid) {
             v[0] += A.xs[i]; v[1] += A.ys[j]; v[2] += 1.0;
             v[8] = fmin(v[8], A.ys[j]); v[9] = fmax(v[9], A.ys[j]);
         }
-        double Jc = A.J[c];
+        const double Jc = Jq[k];
         v[3] = fmin(v[3], Jc); v[4] = fmax(v[4], Jc);
         if (A.energies) {
             double H = heaviside(ph, A.w_t);
@@ -227,6 +243,9 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p1(DiagArgs A, double *__restri
             double dxy = 0.5 * (grad2(A.u + c, A.nx, j, A.ny, h2y) + grad2(A.v + c, 1, i, A.nx, h2x));
             double mu = H * A.mu_f + (1 - H) * A.eta_s;
             v[7] += 2.0 * mu * (dudx * dudx + dvdy * dvdy + 2.0 * (dxy * dxy));
+        }
+        c += S; j += dj; i += di;
+        if (i >= A.nx) { i -= A.nx; ++j; }
         }
     }
     for (int k = 0; k < DIAG_VALS; ++k) s[k][threadIdx.x] = v[k];

@@ -2,7 +2,7 @@
 # session 5: full GPU suite, default bench line (with CPU baseline), kernel stats of the bench,
 # MAC line -- on the tree after the SL block skip and the output writers
 set -o pipefail
-O=gpurun_out/s5f
+O=gpurun_out/${1:-s5f}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
