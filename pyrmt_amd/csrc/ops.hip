@@ -362,15 +362,18 @@ __global__ void k_apply_bc(int kind, double lid, double *u, double *v, int ny, i
 }
 
 // -------------------------------------------------------------------- projection ----
+// rows [jb, je) of an nx-wide plane: blockIdx.y = row - jb, 256 columns per block
+static inline dim3 rows_grid(int nx, int jb, int je) { return dim3((nx + 255) / 256, je - jb); }
 __global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
                                 const double *__restrict__ p, int ny, int nx, double d_f,
                                 double dx, double dy, double *__restrict__ divU, int jb, int je,
                                 double rho = 0.0, double dt = 1.0) {
     // rho > 0: the projection's rhs = (rho * divU) / dt (functions.py:1331, the same two
-    // roundings as the separate scale and divide passes)
-    long c = (long)jb * nx + blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)je * nx) return;
-    int j = (int)(c / nx), i = (int)(c % nx);
+    // roundings as the separate scale and divide passes).  Grid: rows_grid (one block row
+    // per grid row, no per-cell division).
+    const int j = jb + (int)blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nx || j >= je) return;
+    const long c = (long)j * nx + i;
     if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) {
         divU[c] = rho > 0 ? (rho * 0.0) / dt : 0.0;
         return;
@@ -422,9 +425,9 @@ __global__ void k_project_correct(const double *__restrict__ a_s, const double *
                                   int ny, int nx, double dx, double dy, double dt_rho, int bc,
                                   double lid, double *__restrict__ a, double *__restrict__ b,
                                   double *__restrict__ p, int jb, int je) {
-    long c = (long)jb * nx + blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= (long)je * nx) return;
-    int j = (int)(c / nx), i = (int)(c % nx);
+    const int j = jb + (int)blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nx || j >= je) return;
+    const long c = (long)j * nx + i;
     BCSrc s = bc_source(bc, lid, j, i, ny, nx);
     a[c] = s.u_const ? s.u_val : corrected(a_s, pc, s.u_src, ny, nx, dx, dy, dt_rho, 0);
     b[c] = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, dx, dy, dt_rho, 1);
@@ -444,7 +447,7 @@ __global__ void k_div_scalar(const double *__restrict__ x, long n, double s,
 int divergence_rc_rows(rmt_ctx *ctx, const double *a, const double *b, const double *p,
                        double d_f, double dx, double dy, double *divU, int jb, int je) {
     if (je > jb)
-        k_divergence_rc<<<grid1d((long)(je - jb) * ctx->nx, 256), 256, 0, ctx->stream>>>(
+        k_divergence_rc<<<rows_grid(ctx->nx, jb, je), 256, 0, ctx->stream>>>(
             a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU, jb, je);
     RMT_LAUNCHED();
     return RMT_OK;
@@ -453,7 +456,7 @@ int project_correct_rows(rmt_ctx *ctx, const double *a_s, const double *b_s, con
                          const double *p_prev, double dx, double dy, double dt_rho, int bc,
                          double lid, double *a, double *b, double *p, int jb, int je) {
     if (je > jb)
-        k_project_correct<<<grid1d((long)(je - jb) * ctx->nx, 256), 256, 0, ctx->stream>>>(
+        k_project_correct<<<rows_grid(ctx->nx, jb, je), 256, 0, ctx->stream>>>(
             a_s, b_s, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt_rho, bc, lid, a, b, p, jb, je);
     RMT_LAUNCHED();
     return RMT_OK;
@@ -651,7 +654,7 @@ int rmt_apply_velocity_bc(rmt_ctx *ctx, int bc_kind, double lid, double *u, doub
 }
 int rmt_divergence_rc(rmt_ctx *ctx, const double *a, const double *b, const double *p,
                       double d_f, double dx, double dy, double *divU) {
-    k_divergence_rc<<<LAUNCH1D(N_CELLS)>>>(a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU, 0, ctx->ny);
+    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU, 0, ctx->ny);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -679,7 +682,7 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
     double *rhs = ctx->scratch, *pc = rhs + n;
     // functions.py:1292-1295 + :1331: rhs = rho * divU / dt, d_f = dt / mean(rho)
     if (p_prev && rho > 0) {
-        k_divergence_rc<<<LAUNCH1D(n)>>>(a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx,
+        k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx,
                                          dy, rhs, 0, ctx->ny, rho, dt);
         RMT_LAUNCHED();
     } else {
@@ -689,7 +692,7 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
         k_div_scalar<<<LAUNCH1D(n)>>>(rhs, n, dt, rhs);
     }
     RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc));
-    k_project_correct<<<LAUNCH1D(n)>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy,
+    k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy,
                                        dt / rho, bc_kind, lid, a, b, p, 0, ctx->ny);
     RMT_LAUNCHED();
     RMT_TRY(sub_mean_rows(ctx, p, ctx->ny, ctx->nx));
