@@ -112,13 +112,16 @@ int rmt_advect_sl_cubic_rk4(rmt_ctx *ctx, const double *q, const double *a, cons
 int rmt_all_finite2(rmt_ctx *ctx, const double *a, const double *b, int *finite);
 
 /* functions.py:48-163 extrapolate_reference_map: exact raster-order (Gauss-Seidel)
- * semantics of the reference; outputs may alias the inputs. */
+ * semantics of the reference; outputs may alias the inputs.  Blocks until the result is
+ * complete and returns RMT_EDEVICE if the extrapolation aborted (bug guard / spin timeout),
+ * so a caller never sees a partly extrapolated map with RMT_OK. */
 int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, const double *X2,
                                   const double *phi, double dx, double dy, int max_layers,
                                   double *X1_out, double *X2_out);
 /* librmt diagnostics for the extrapolation (no reference counterpart).  mode 0 (default):
  * geometry-first chain path, row-ticket sweep when its capacity limits are exceeded;
- * 1: sweep only; 2: chain path's pre-passes, then the sweep forced.  rmt_extrap_last_path
+ * 1: sweep only; 2: chain path's pre-passes, then the sweep forced; 3: mode 0, then the
+ * abort status is raised (exercises the callers' error paths).  rmt_extrap_last_path
  * (blocks) reports what the last call on ctx ran: 0 chain, 1 sweep. */
 int rmt_extrap_set_mode(int mode);
 int rmt_extrap_last_path(rmt_ctx *ctx, int *path);
@@ -198,6 +201,28 @@ int rmt_compute_timestep(rmt_ctx *ctx, const double *a, const double *b, double 
                          double CFL, double dt_min_cap, double mu_s, double rho_s, double gamma,
                          double rho_f, double mu_f, double eta_s, double kappa, double *dt);
 
+/* ---- standalone diagnostics and the blended RHS (pyRMT/__init__.py:16, :28-31) --------
+ * Energies return a host scalar and block; the sum runs in np.sum's own order (pairwise over
+ * 8192-element chunks), so a bit-exact density gives a bit-exact energy. */
+/* output.py:6-39: sum(0.5 rho (a^2 + b^2)) dx dy, rho = (1-H) rho_s + H rho_f */
+int rmt_compute_kinetic_energy(rmt_ctx *ctx, const double *a, const double *b, double rho_f,
+                               double rho_s, const double *phi, double w_t, double dx, double dy,
+                               double *ke);
+/* output.py:41-134: neo-Hookean + volumetric strain energy over phi <= 0 (edge-padded grads) */
+int rmt_compute_strain_energy(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi,
+                              double mu_s, double dx, double dy, double kappa, double *se);
+/* output.py:136-193: viscous dissipation rate, mu = H mu_f + (1-H) eta_s */
+int rmt_compute_viscous_dissipation(rmt_ctx *ctx, const double *a, const double *b, double mu_f,
+                                    const double *phi, double w_t, double dx, double dy,
+                                    double eta_s, double *diss);
+/* functions.py:897-944 velocity_rhs_blended_optimized: H, rho_local device arrays; the
+ * surface-tension force fx, fy device arrays or both NULL (the scalar 0.0 of the gamma = 0
+ * path).  (phi, dH_dx, dH_dy of the reference signature are unused by its body.) */
+int rmt_velocity_rhs_blended(rmt_ctx *ctx, const double *u, const double *v, const double *p,
+                             const double *sxx, const double *sxy, const double *syy, double dx,
+                             double dy, double mu_f, const double *H, const double *rho,
+                             const double *fx, const double *fy, double *rhs_u, double *rhs_v);
+
 /* ---- fused, device-resident time step (the loop body of the benchmark drivers) ----- */
 typedef enum {
     RMT_SHAPE_NONE = 0,   /* pure fluid (lid_driven_cavity.py): phi = 1, no solid       */
@@ -235,8 +260,11 @@ int rmt_sim_destroy(rmt_sim *sim);
 /* field ids: 0 u (a), 1 v (b), 2 p, 3 X1, 4 X2, 5 phi (last rebuilt), 6 J, 7 sigma_xx,
  * 8 sigma_xy, 9 sigma_yy (the solid stress of the last momentum step) */
 int rmt_sim_field(rmt_sim *sim, int field, double **dev_ptr);
-/* Enqueue nsteps loop bodies.  dt comes from compute_timestep on device and is clipped to
- * t_end - t as the drivers do; steps after t >= t_end are no-ops.  No host sync. */
+/* Run nsteps loop bodies.  dt comes from compute_timestep on device and is clipped to
+ * t_end - t as the drivers do; steps after t >= t_end are no-ops.  Blocks: the diagnostics
+ * and flags of the enqueued steps are read back (see rmt_sim_set_sync_every) and errors
+ * (non-finite velocity, extrapolation abort) are returned synchronously; the call returns once
+ * the last step has finished on the stream. */
 int rmt_sim_step(rmt_sim *sim, int nsteps, double t_end);
 /* Phase timers (HIP events on the context stream, accumulated over steps while on):
  * ms[0] dt reduction, [1] advection, [2] extrapolation, [3] momentum (prep + 4 stages +
@@ -340,8 +368,13 @@ typedef struct {
     double t, dt, minJ, maxJ, umax;
     int n_discs;
     double cx[RMT_MAC_MAXD], cy[RMT_MAC_MAXD];   /* centroid of phi_k <= 0 (:104)        */
+    int diverged;   /* mac_multi_disc_lid.py:100-103: u non-finite, min J < 0, max J > 20 or a
+                       disc with no phi <= 0 cell after this step; the sim stops stepping     */
 } rmt_mac_diag;
 typedef struct rmt_mac_sim rmt_mac_sim;
+/* rmt_mac_sim_step stops after a step whose record has diverged set (the reference driver
+ * breaks out of its loop there); later calls are no-ops.  RMT_EDEVICE on an extrapolation
+ * abort, RMT_ENONFINITE on a non-finite velocity fed to the advection. */
 int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **out);
 int rmt_mac_sim_destroy(rmt_mac_sim *sim);
 int rmt_mac_sim_field(rmt_mac_sim *sim, int field, int disc, double **dev_ptr);

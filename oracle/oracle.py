@@ -39,6 +39,7 @@ def _load():
     D, I, L, P = ctypes.c_double, ctypes.c_int, ctypes.c_long, ctypes.c_void_p
     sig = {
         "rmto_set_threads": (None, [I]),
+        "rmto_set_all_cores": (None, [I]),
         "rmto_grad_x_2nd": (None, [P, I, I, D, P]),
         "rmto_grad_y_2nd": (None, [P, I, I, D, P]),
         "rmto_diff_upwind_3rd": (None, [P, P, I, I, D, I, P]),
@@ -54,6 +55,7 @@ def _load():
         "rmto_momentum_rk4": (None, [P, P, P, P, P, I, D, D, D, D, D, D, D, D, D, P, D, D, I, D,
                                      I, I, P, P, P, P, P, P]),
         "rmto_divergence_rc": (None, [P, P, P, D, I, I, D, D, P]),
+        "rmto_velocity_rhs_blended": (None, [P, P, P, P, P, P, P, P, P, P, I, I, D, D, D, P, P]),
         "rmto_divergence_central": (None, [P, P, I, I, D, D, P]),
         "rmto_pressure_gradient": (None, [P, I, I, D, D, P, P]),
         "rmto_pairwise_sum": (D, [P, L]),
@@ -75,6 +77,12 @@ _lib = _load()
 def set_threads(n):
     """OpenMP threads for the kernels the reference runs with Numba parallel=True."""
     _lib.rmto_set_threads(int(n))
+
+
+def set_all_cores(on):
+    """All-cores mode: OpenMP also on the per-cell loops the reference runs serially (same
+    results bit for bit; the extrapolation sweep stays serial).  Off = faithful threading."""
+    _lib.rmto_set_all_cores(int(bool(on)))
 
 
 def _c(a):
@@ -248,6 +256,24 @@ def momentum_step_rk4(u, v, p, X1, X2, bc_kind, lid, mu_s, kappa, eta_s, dx, dy,
                            int(bool(stress_band)), detg_clamp, u.shape[0], u.shape[1],
                            *map(_p, outs))
     return tuple(outs)
+
+
+def velocity_rhs_blended_optimized(u, v, p, sxx, sxy, syy, dx, dy, phi, mu_f, H, dH_dx, dH_dy,
+                                   rho_local, st_force_x, st_force_y):
+    """functions.py:897-944 (phi, dH_dx, dH_dy unused, as in the reference)."""
+    shp = np.shape(u)
+    u, v, p, sxx, sxy, syy = map(_c, (u, v, p, sxx, sxy, syy))
+    H = _c(np.broadcast_to(H, shp)); rho = _c(np.broadcast_to(rho_local, shp))
+    scalar0 = np.ndim(st_force_x) == 0 and np.ndim(st_force_y) == 0 and \
+        float(st_force_x) == 0.0 and float(st_force_y) == 0.0
+    fx = None if scalar0 else _c(np.broadcast_to(st_force_x, shp))
+    fy = None if scalar0 else _c(np.broadcast_to(st_force_y, shp))
+    ru = _e(shp); rv = _e(shp)
+    _lib.rmto_velocity_rhs_blended(_p(u), _p(v), _p(p), _p(sxx), _p(sxy), _p(syy), _p(H),
+                                   _p(rho), fx.ctypes.data if fx is not None else None,
+                                   fy.ctypes.data if fy is not None else None, shp[0], shp[1],
+                                   dx, dy, mu_f, _p(ru), _p(rv))
+    return ru, rv
 
 
 # ── projection (functions.py:1005-1364) ──────────────────────────────────────────

@@ -53,7 +53,8 @@ class rmt_mac_params(ctypes.Structure):
 class rmt_mac_diag(ctypes.Structure):
     _fields_ = [("t", ctypes.c_double), ("dt", ctypes.c_double), ("minJ", ctypes.c_double),
                 ("maxJ", ctypes.c_double), ("umax", ctypes.c_double), ("n_discs", ctypes.c_int),
-                ("cx", ctypes.c_double * 8), ("cy", ctypes.c_double * 8)]
+                ("cx", ctypes.c_double * 8), ("cy", ctypes.c_double * 8),
+                ("diverged", ctypes.c_int)]
 
 
 _P, _D, _I, _L = ctypes.c_void_p, ctypes.c_double, ctypes.c_int, ctypes.c_long
@@ -98,6 +99,12 @@ SIGNATURES = {
     "rmt_divergence_rc_variable": (_I, [_P, _P, _P, _P, _D, _P, _D, _D, _P]),
     "rmt_compute_timestep": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D,
                                   ctypes.POINTER(_D)]),
+    "rmt_compute_kinetic_energy": (_I, [_P, _P, _P, _D, _D, _P, _D, _D, _D, ctypes.POINTER(_D)]),
+    "rmt_compute_strain_energy": (_I, [_P, _P, _P, _P, _D, _D, _D, _D, ctypes.POINTER(_D)]),
+    "rmt_compute_viscous_dissipation": (_I, [_P, _P, _P, _D, _P, _D, _D, _D, _D,
+                                             ctypes.POINTER(_D)]),
+    "rmt_velocity_rhs_blended": (_I, [_P, _P, _P, _P, _P, _P, _P, _D, _D, _D, _P, _P, _P, _P,
+                                      _P, _P]),
     "rmt_sim_create": (_I, [_P, ctypes.POINTER(rmt_sim_params), ctypes.POINTER(_P)]),
     "rmt_sim_destroy": (_I, [_P]),
     "rmt_sim_field": (_I, [_P, _I, ctypes.POINTER(_P)]),

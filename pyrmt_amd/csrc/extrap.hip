@@ -764,6 +764,12 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
         hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
     }
     if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
+    if (force == 3) {   // diagnostic: report an abort (tests of the callers' error paths)
+        const int one = 1;
+        RMT_HIP(hipMemcpyAsync(ws.status + 1, &one, sizeof(int), hipMemcpyHostToDevice,
+                               ctx->stream));
+        RMT_HIP(hipStreamSynchronize(ctx->stream));
+    }
     if (dev_status)
         RMT_HIP(hipMemcpyAsync(dev_status, ws.status, 2 * sizeof(int), hipMemcpyDeviceToDevice,
                                ctx->stream));
@@ -777,11 +783,20 @@ extern "C" int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, con
                                              const double *phi, double dx, double dy,
                                              int max_layers, double *X1_out, double *X2_out) {
     RMT_CHECK(ctx, RMT_EINVAL, "null ctx");
-    return rmt::extrapolate(ctx, X1, X2, phi, dx, dy, max_layers, X1_out, X2_out, nullptr);
+    // the status words (fitted count, abort) land in the shared scratch; read them back so an
+    // aborted chain / sweep is an error, not a partly extrapolated map returned with RMT_OK
+    RMT_TRY(rmt::ensure_scratch(ctx, 2 * sizeof(int)));
+    int *dst = (int *)ctx->scratch;
+    RMT_TRY(rmt::extrapolate(ctx, X1, X2, phi, dx, dy, max_layers, X1_out, X2_out, dst));
+    int hs[2] = {0, 0};
+    RMT_HIP(hipMemcpyAsync(hs, dst, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
+    RMT_HIP(hipStreamSynchronize(ctx->stream));
+    RMT_CHECK(!hs[1], RMT_EDEVICE, "extrapolation aborted (progress wait timed out)");
+    return RMT_OK;
 }
 
 extern "C" int rmt_extrap_set_mode(int mode) {
-    RMT_CHECK(mode >= 0 && mode <= 2, RMT_EINVAL, "extrapolation mode must be 0, 1 or 2");
+    RMT_CHECK(mode >= 0 && mode <= 3, RMT_EINVAL, "extrapolation mode must be 0 .. 3");
     rmt::g_ex_mode = mode;
     return RMT_OK;
 }

@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
     for (int k = 0; k < MD_VALS; ++k) acc[k] = 0.0;
     const long n = (long)(je - jb) * N, nf = (long)(je - jb) * (N + 1);
     for (long t = blockIdx.x * (long)MS_TPB + threadIdx.x; t < nf; t += (long)MS_BLOCKS * MS_TPB) {
-        acc[3 * MAC_MAXD] = fmax(acc[3 * MAC_MAXD], fabs(u[(long)jb * (N + 1) + t]));
+        acc[3 * MAC_MAXD] = nanmax(acc[3 * MAC_MAXD], fabs(u[(long)jb * (N + 1) + t]));
         if (t < n) {
             const long c = (long)jb * N + t;
             const int j = (int)(c / N), i = (int)(c % N);
@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
         __syncthreads();
         for (int w = MS_TPB / 2; w > 0; w >>= 1) {
             if (threadIdx.x < w)
-                s[threadIdx.x] = k == 3 * MAC_MAXD ? fmax(s[threadIdx.x], s[threadIdx.x + w])
+                s[threadIdx.x] = k == 3 * MAC_MAXD ? nanmax(s[threadIdx.x], s[threadIdx.x + w])
                                                    : s[threadIdx.x] + s[threadIdx.x + w];
             __syncthreads();
         }
@@ -293,6 +293,7 @@ struct rmt_mac_sim {
     double *xs, *ys, *part, *out;
     int *flags;
     double t = 0;
+    bool diverged = false;
     std::vector<rmt_mac_diag> diag;
 };
 
@@ -434,7 +435,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
     const double dx = P.dx, w_t = 2.0 * dx, eps = 3.0 * dx, nu = P.mu_f / P.rho;
     const double dx2 = std::pow(dx, 2.0);
     for (int it = 0; it < nsteps; ++it) {
-        if (!(S->t < t_end)) break;
+        if (!(S->t < t_end) || S->diverged) break;
         double dt = P.dt;
         if (S->t + dt > t_end) dt = t_end - S->t;
         RMT_HIP(hipMemsetAsync(S->flags, 0, 4 * sizeof(int), st));
@@ -476,6 +477,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         RMT_HIP(hipStreamSynchronize(st));
         RMT_CHECK(!fl[0] && !fl[1], RMT_ENONFINITE,
                   "advect_reference_map: non-finite velocity (the simulation diverged)");
+        RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
         S->t += dt;
         rmt_mac_diag r{};
         r.t = S->t; r.dt = dt; r.n_discs = K;
@@ -487,14 +489,20 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         for (int b = 0; b < MS_BLOCKS; ++b)
             for (int k = 0; k < MD_VALS; ++k) {
                 const double x = dp[(size_t)b * MD_VALS + k];
-                acc[k] = k == 3 * MAC_MAXD ? std::fmax(acc[k], x) : acc[k] + x;
+                acc[k] = k == 3 * MAC_MAXD ? nanmax(acc[k], x) : acc[k] + x;
             }
         for (int k = 0; k < K; ++k) {
             r.cx[k] = acc[3 * k + 2] > 0 ? acc[3 * k] / acc[3 * k + 2] : NAN;
             r.cy[k] = acc[3 * k + 2] > 0 ? acc[3 * k + 1] / acc[3 * k + 2] : NAN;
         }
         r.umax = acc[3 * MAC_MAXD];
+        // mac_multi_disc_lid.py:100-103: the driver stops on a non-finite u, a folded (J < 0)
+        // or over-stretched (J > 20) map, or a disc with no phi <= 0 cell left
+        bool lost = false;
+        for (int k = 0; k < K; ++k) lost |= !(acc[3 * k + 2] > 0);
+        r.diverged = !std::isfinite(r.umax) || r.minJ < 0.0 || r.maxJ > 20.0 || lost;
         S->diag.push_back(r);
+        if (r.diverged) { S->diverged = true; break; }
     }
     return RMT_OK;
 }
@@ -564,14 +572,15 @@ __global__ void __launch_bounds__(256) k_mac_slab_scal(const double *__restrict_
             const double x = v == 0 ? part[2 * b] : v == 1 ? part[2 * b + 1]
                            : v == 2 + 3 * K ? dp[(long)b * MD_VALS + 3 * MAC_MAXD]
                                             : dp[(long)b * MD_VALS + (v - 2)];
-            a = kind == 0 ? fmin(a, x) : kind == 1 ? fmax(a, x) : a + x;
+            a = kind == 0 ? fmin(a, x) : kind == 1 ? (v == 1 ? fmax(a, x) : nanmax(a, x)) : a + x;
         }
         s[t] = a;
         __syncthreads();
         for (int w = 128; w > 0; w >>= 1) {
             if (t < w) {
                 const double x = s[t + w];
-                s[t] = kind == 0 ? fmin(s[t], x) : kind == 1 ? fmax(s[t], x) : s[t] + x;
+                s[t] = kind == 0 ? fmin(s[t], x)
+                     : kind == 1 ? (v == 1 ? fmax(s[t], x) : nanmax(s[t], x)) : s[t] + x;
             }
             __syncthreads();
         }

@@ -177,23 +177,6 @@ __global__ void k_dt(const double *m2, double dt_const, double cfl, double dx, d
     *out = fmin(dt_const, cfl * dx / (sqrt(*m2) + 1e-6));
 }
 
-// output.py:41-134 strain-energy density at one cell (4-cell edge-padded central grads).
-__device__ __forceinline__ double se_density(const double *__restrict__ X1,
-                                             const double *__restrict__ X2, long c, int j, int i,
-                                             int ny, int nx, double dx, double dy, double mu_s,
-                                             double kappa) {
-    long cl = i > 0 ? c - 1 : c, cr = i < nx - 1 ? c + 1 : c;
-    long cd = j > 0 ? c - nx : c, cu = j < ny - 1 ? c + nx : c;
-    double G11 = (X1[cr] - X1[cl]) / (2 * dx), G12 = (X1[cu] - X1[cd]) / (2 * dy);
-    double G21 = (X2[cr] - X2[cl]) / (2 * dx), G22 = (X2[cu] - X2[cd]) / (2 * dy);
-    double detG = G11 * G22 - G12 * G21;
-    if (!(fabs(detG) > 1e-10)) return 0.0;
-    double F11 = G22 / detG, F12 = -G12 / detG, F21 = -G21 / detG, F22 = G11 / detG;
-    double I1 = (F11 * F11 + F21 * F21) + (F12 * F12 + F22 * F22);
-    double Jv = 1.0 / detG, jm = Jv - 1.0;
-    return 0.5 * mu_s * (I1 - 2.0) + 0.5 * kappa * (jm * jm);
-}
-
 struct DiagArgs {
     const double *phi, *J, *xs, *ys, *u, *v, *X1, *X2;
     int ny, nx, energies;

@@ -544,6 +544,7 @@ class MacDistributedSim:
                       for r in comm.ranks]
         self.t = 0.0
         self.records = []
+        self.diverged = False
         self._counts = (ctypes.c_longlong * self.G)()
 
     def set_state(self, u=None, v=None, p=None, maps=None):
@@ -611,7 +612,7 @@ class MacDistributedSim:
         comm, S, K = self.comm, self.slabs, self.K
         halo_planes = ["u", "v"] + [f"X{a}:{k}" for k in range(K) for a in (1, 2)]
         for _ in range(nsteps):
-            if not (self.t < t_end):
+            if not (self.t < t_end) or self.diverged:
                 break
             dt = self.dt
             if self.t + dt > t_end:
@@ -683,6 +684,11 @@ class MacDistributedSim:
                      for k in range(self.K)]
         rec["cy"] = [cen[3 * k + 1] / cen[3 * k + 2] if cen[3 * k + 2] > 0 else math.nan
                      for k in range(self.K)]
+        # mac_multi_disc_lid.py:100-103: stop on non-finite u, J < 0, J > 20 or a lost disc
+        lost = any(not cen[3 * k + 2] > 0 for k in range(self.K))
+        rec["diverged"] = int(not math.isfinite(rec["umax"]) or rec["minJ"] < 0.0
+                              or rec["maxJ"] > 20.0 or lost)
+        self.diverged = bool(rec["diverged"])
         self.records.append(rec)
 
     def diagnostics(self):

@@ -163,7 +163,8 @@ def extrapolate_reference_map(X1, X2, phi, dx, dy, max_layers):
 
 def extrapolation_mode(mode):
     """librmt diagnostic: 0 chain path (default, sweep on capacity fallback), 1 sweep only,
-    2 chain pre-passes then the sweep forced."""
+    2 chain pre-passes then the sweep forced, 3 mode 0 then an abort is reported (error-path
+    tests)."""
     L.check(L.lib().rmt_extrap_set_mode(int(mode)), "rmt_extrap_set_mode")
 
 
@@ -351,6 +352,69 @@ def momentum_step_rk4(u, v, p, X1, X2, velocity_bc, mu_s, kappa, eta_s, dx, dy, 
     L.check(L.lib().rmt_momentum_step_rk4(c.bind(), ctypes.byref(prm), _p(u), _p(v), _p(p), _p(X1),
                                           _p(X2), _p(phi), *map(_p, outs)), "momentum_step_rk4")
     return tuple(io.out(o) for o in outs)
+
+
+def velocity_rhs_blended_optimized(u, v, p, sigma_sxx_s_elastic, sigma_sxy_s_elastic,
+                                   sigma_syy_s_elastic, dx, dy, phi, mu_f, H, dH_dx, dH_dy,
+                                   rho_local, st_force_x, st_force_y):
+    """functions.py:897-944: blended-stress divergence + 3rd-order upwind advection - grad p,
+    over (rho_local + 1e-12).  H, rho_local and the surface-tension force may be arrays or
+    scalars (broadcast as NumPy would); phi, dH_dx, dH_dy are unused, as in the reference."""
+    shape = np.shape(u) if not hasattr(u, "shape") else tuple(u.shape)
+    torch = _torch()
+
+    def full(a):
+        if isinstance(a, torch.Tensor):
+            return a.expand(shape) if a.dim() < 2 else a
+        return np.broadcast_to(np.asarray(a, dtype=np.float64), shape)
+
+    zero_f = all(np.ndim(f) == 0 and float(f) == 0.0 and not isinstance(f, torch.Tensor)
+                 for f in (st_force_x, st_force_y))
+    arrays = (u, v, p, sigma_sxx_s_elastic, sigma_sxy_s_elastic, sigma_syy_s_elastic,
+              full(H), full(rho_local))
+    io = _IO(*arrays)
+    d = [io.dev(a) for a in arrays]
+    fx = fy = None
+    if not zero_f:   # a non-zero scalar force, or arrays
+        fx = io.dev(full(st_force_x)); fy = io.dev(full(st_force_y))
+    ru = io.empty(shape); rv = io.empty(shape)
+    c = ctx_for(*shape)
+    L.check(L.lib().rmt_velocity_rhs_blended(c.bind(), *map(_p, d[:6]), dx, dy, mu_f, _p(d[6]),
+                                             _p(d[7]), _p(fx), _p(fy), _p(ru), _p(rv)),
+            "velocity_rhs_blended_optimized")
+    return io.out(ru), io.out(rv)
+
+
+# ── diagnostics (output.py:6-193) ─────────────────────────────────────────────────
+def compute_kinetic_energy(a, b, rho_f, rho_s, phi, w_t, dx, dy):
+    """output.py:6-39: sum(0.5 rho (a^2 + b^2)) dx dy with rho = (1-H) rho_s + H rho_f."""
+    io = _IO(a, b, phi); a, b, phi = map(io.dev, (a, b, phi))
+    out = ctypes.c_double()
+    c = ctx_for(*a.shape)
+    L.check(L.lib().rmt_compute_kinetic_energy(c.bind(), _p(a), _p(b), rho_f, rho_s, _p(phi), w_t,
+                                               dx, dy, ctypes.byref(out)), "compute_kinetic_energy")
+    return out.value
+
+
+def compute_strain_energy(X1, X2, phi, mu_s, dx, dy, kappa=0.0):
+    """output.py:41-134: (mu_s/2)(I1 - 2) + (kappa/2)(J - 1)^2 over the solid cells."""
+    io = _IO(X1, X2, phi); X1, X2, phi = map(io.dev, (X1, X2, phi))
+    out = ctypes.c_double()
+    c = ctx_for(*X1.shape)
+    L.check(L.lib().rmt_compute_strain_energy(c.bind(), _p(X1), _p(X2), _p(phi), mu_s, dx, dy,
+                                              kappa, ctypes.byref(out)), "compute_strain_energy")
+    return out.value
+
+
+def compute_viscous_dissipation(a, b, mu_f, phi, w_t, dx, dy, eta_s=0.0):
+    """output.py:136-193: sum(2 mu (D_xx^2 + D_yy^2 + 2 D_xy^2)) dx dy."""
+    io = _IO(a, b, phi); a, b, phi = map(io.dev, (a, b, phi))
+    out = ctypes.c_double()
+    c = ctx_for(*a.shape)
+    L.check(L.lib().rmt_compute_viscous_dissipation(c.bind(), _p(a), _p(b), mu_f, _p(phi), w_t,
+                                                    dx, dy, eta_s, ctypes.byref(out)),
+            "compute_viscous_dissipation")
+    return out.value
 
 
 # ── projection (functions.py:1005-1364) ──────────────────────────────────────────

@@ -231,6 +231,7 @@ class MacMultiDisc:
         K = len(self.specs)
         out = {k: np.array([getattr(buf[i], k) for i in range(n.value)])
                for k in ("t", "dt", "minJ", "maxJ", "umax")}
+        out["diverged"] = np.array([buf[i].diverged for i in range(n.value)], dtype=np.int32)
         out["cx"] = np.array([[buf[i].cx[k] for k in range(K)] for i in range(n.value)])
         out["cy"] = np.array([[buf[i].cy[k] for k in range(K)] for i in range(n.value)])
         return out

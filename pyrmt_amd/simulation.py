@@ -151,9 +151,11 @@ def soft_disc_in_lid_driven(N=128, scheme="semilagrangian", stress_band=False, d
     return sim
 
 
-def disc_in_taylor_green(N=128, scheme="weno5", stress_band=False):
+def disc_in_taylor_green(N=128, scheme="semilagrangian", stress_band=False):
     """Config 3: disc (0.5, 0.5, 0.2) in a Taylor-Green vortex, free-slip box, with the
-    per-step energies (disc_in_taylor_green.py:161-190 parameters)."""
+    per-step energies (disc_in_taylor_green.py:161-190 parameters).  The default scheme is the
+    reference driver's ('semilagrangian', disc_in_taylor_green.py:39, :150); config 3 passes
+    'weno5'."""
     sim0 = F.create_grid(N, N, 1.0, 1.0)
     w_t = 2.0 * sim0[2]
     layers = max(3, int(np.ceil(w_t / sim0[2])) + 1)

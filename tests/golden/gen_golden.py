@@ -257,6 +257,33 @@ def gen_operator_cases():
          dts=dts, ke=ke, se=se, ed=ed)
 
 
+# ── 3b. velocity_rhs_blended_optimized standalone (pyRMT/__init__.py:16 export) ────
+def gen_vrhs():
+    """functions.py:897-944 on the operator-case inputs: blended stress with a non-trivial
+    density (rho_s = 2), surface-tension force as the scalar 0.0 (the momentum path) and as
+    arrays."""
+    rng = np.random.default_rng(7)
+    N = 49
+    X, Y, dx, dy = F.create_grid(N, N, 1.0, 1.0)
+    phi = np.sqrt((X - 0.5) ** 2 + (Y - 0.5) ** 2) - 0.25
+    X1 = X + 0.05 * np.sin(2 * np.pi * Y) * np.cos(np.pi * X)
+    X2 = Y - 0.04 * np.sin(np.pi * X) * np.sin(2 * np.pi * Y)
+    sxx, sxy, syy, _ = F.solid_cauchy_stress(X1, X2, dx, dy, 0.7, 0.3, phi)
+    u = 0.3 * np.sin(2 * np.pi * X) * np.cos(np.pi * Y) + 0.01 * rng.standard_normal((N, N))
+    v = -0.2 * np.cos(np.pi * X) * np.sin(2 * np.pi * Y) + 0.01 * rng.standard_normal((N, N))
+    p = 0.1 * np.cos(np.pi * X) * np.cos(np.pi * Y)
+    H = F.smoothed_heaviside(phi, 2 * dx)
+    rho = (1 - H) * 2.0 + H * 1.0
+    dHx = np.gradient(H, dx, axis=1); dHy = np.gradient(H, dy, axis=0)
+    fx = 0.05 * rng.standard_normal((N, N)); fy = 0.05 * rng.standard_normal((N, N))
+    r0 = F.velocity_rhs_blended_optimized(u, v, p, sxx, sxy, syy, dx, dy, phi, 0.01, H, dHx, dHy,
+                                          rho, 0.0, 0.0)
+    r1 = F.velocity_rhs_blended_optimized(u, v, p, sxx, sxy, syy, dx, dy, phi, 0.01, H, dHx, dHy,
+                                          rho, fx, fy)
+    save("vrhs", N=N, dx=dx, dy=dy, phi=phi, u=u, v=v, p=p, sxx=sxx, sxy=sxy, syy=syy, H=H,
+         rho=rho, fx=fx, fy=fy, ru0=r0[0], rv0=r0[1], ru1=r1[0], rv1=r1[1])
+
+
 # ── 4. WENO5 (config 3) ─────────────────────────────────────────────────────────
 def gen_weno():
     rng = np.random.default_rng(7)
@@ -615,6 +642,7 @@ if __name__ == "__main__":
     t0 = time.time()
     gen_primitives()
     gen_operator_cases()
+    gen_vrhs()
     gen_weno()
     gen_mac()
     gen_soft_disc_driver_check()

@@ -1,0 +1,159 @@
+"""GPU parity at the BASELINE configs' own sizes (BASELINE.json `configs`).
+
+The fused device step (rmt_sim_step / rmt_mac_sim_step through the C ABI) against the oracle
+(oracle/, pinned bit-exact to the reference's fixtures) on the same inputs:
+  config 4  soft_disc_in_lid_driven N=4096, 2 fused steps (the bench workload) vs the live
+            oracle: X1, X2 after step 1 bit-exact, everything after step 2 at stated bars;
+  config 2  soft_disc_in_lid_driven N=256, 1000 steps: centroid / J trajectory;
+  config 3  disc_in_taylor_green N=1024 WENO5 + SSP-RK3, 20 steps: KE, SE, dissipation,
+            its running integral and the total energy (disc_in_taylor_green.py:226-243);
+  config 5  mac_multi_disc_lid N=8192 (3 discs, seed 3), 2 steps vs the oracle's fixture
+            (tests/golden/gen_oracle_large.py: ~90 s per oracle step at this size).
+Bars: bit-exact where the arithmetic has no transcendental function and no FFT on the path
+to the compared value; otherwise the stated tolerance.  The only sources of difference are
+the device `sin` of the smoothed Heaviside (ocml vs glibc, <= 1 ulp) and the DCT (the LDS
+Stockham FFT vs pocketfft), both ~1e-16 relative per step.
+The oracle runs in all-cores mode here (same results bit for bit, OpenMP on every per-cell
+loop) so each test stays well inside the GPU box's per-test time limit.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fast_oracle(oracle):
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    oracle.set_all_cores(True)
+    yield oracle
+    oracle.set_all_cores(False)
+
+
+def _maxdiff(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b))))
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float64).tobytes()).hexdigest()
+
+
+def test_config4_fused_step_N4096_vs_oracle(gpu, fast_oracle):
+    """The bench workload: 2 fused steps at N=4096 against the oracle's loop body."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    N = 4096
+    ref = fast_oracle.SoftDisc(N, "lid")
+    sim = soft_disc_in_lid_driven(N)
+    # the initial narrow-band extrapolation (GPU chain vs the serial oracle sweep)
+    assert _sha(sim.get("X1")) == _sha(ref.X1) and _sha(sim.get("X2")) == _sha(ref.X2)
+    r1 = ref.step()
+    sim.step(1)
+    # step 1 starts from rest: advection and extrapolation are exact (no transcendental
+    # function before the map update), so the advected + extrapolated map is bit-exact
+    np.testing.assert_array_equal(sim.get("X1"), ref.X1)
+    np.testing.assert_array_equal(sim.get("X2"), ref.X2)
+    u1, v1, p1 = (sim.get(k) for k in ("u", "v", "p"))
+    for got, want in ((u1, ref.a), (v1, ref.b), (p1, ref.p)):
+        assert _maxdiff(got, want) <= 1e-12 * max(1.0, np.abs(want).max())
+    r2 = ref.step()
+    sim.step(1)
+    d = sim.diagnostics()
+    for k, r in enumerate((r1, r2)):
+        np.testing.assert_allclose(d["dt"][k], r["dt"], rtol=1e-13)
+        np.testing.assert_allclose([d["cx"][k], d["cy"][k]], [r["cx"], r["cy"]], rtol=1e-6)  # north star
+        np.testing.assert_allclose([d["cx"][k], d["cy"][k]], [r["cx"], r["cy"]], rtol=1e-13)  # achieved
+        np.testing.assert_allclose([d["minJ"][k], d["maxJ"][k]], [r["minJ"], r["maxJ"]], rtol=1e-11)
+    ex1, ex2 = _maxdiff(sim.get("X1"), ref.X1), _maxdiff(sim.get("X2"), ref.X2)
+    eu = _maxdiff(sim.get("u"), ref.a) / max(1.0, np.abs(ref.a).max())
+    ev = _maxdiff(sim.get("v"), ref.b) / max(1.0, np.abs(ref.a).max())
+    ep = _maxdiff(sim.get("p"), ref.p) / max(1.0, np.abs(ref.p).max())
+    print(f"\n[config4 N=4096] step 2: |dX1| {ex1:.3g} |dX2| {ex2:.3g} |du| {eu:.3g} "
+          f"|dv| {ev:.3g} |dp| {ep:.3g}")
+    assert max(ex1, ex2) <= 1e-11
+    assert max(eu, ev, ep) <= 1e-10
+
+
+def test_config2_N256_1000_steps(gpu, fast_oracle):
+    """soft_disc_in_lid_driven N=256 (semi-Lagrangian): the per-step centroid / J trajectory
+    (soft_disc_in_lid_driven.py:233) over 1000 steps."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    N, S = 256, 1000
+    ref = fast_oracle.SoftDisc(N, "lid")
+    rec = [ref.step() for _ in range(S)]
+    sim = soft_disc_in_lid_driven(N)
+    sim.step(S)
+    d = sim.diagnostics()
+    want = np.array([[r[k] for k in ("t", "cx", "cy", "minJ", "maxJ")] for r in rec])
+    got = np.stack([d[k] for k in ("t", "cx", "cy", "minJ", "maxJ")], axis=1)
+    rel = np.abs(got - want) / np.abs(want)
+    print(f"\n[config2 N=256 x{S}] max rel: t {rel[:, 0].max():.3g} cx {rel[:, 1].max():.3g} "
+          f"cy {rel[:, 2].max():.3g} minJ {rel[:, 3].max():.3g} maxJ {rel[:, 4].max():.3g}; "
+          f"|dX1| {_maxdiff(sim.get('X1'), ref.X1):.3g} |du| {_maxdiff(sim.get('u'), ref.a):.3g}")
+    np.testing.assert_allclose(got[:, 1:3], want[:, 1:3], rtol=1e-6)     # north star
+    np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=1e-12)
+    np.testing.assert_allclose(got[:, 1:3], want[:, 1:3], rtol=1e-12)    # achieved
+    np.testing.assert_allclose(got[:, 3:], want[:, 3:], rtol=1e-9)
+
+
+def test_config3_N1024_weno5_energies(gpu, fast_oracle):
+    """disc_in_taylor_green N=1024, WENO5 + SSP-RK3: per-step KE, SE, dissipation, its
+    integral, total energy E (the drift check of disc_in_taylor_green.py:249-250), r_y, J."""
+    from pyrmt_amd.simulation import disc_in_taylor_green
+    N, S = 1024, 20
+    ref = fast_oracle.SoftDisc(N, "tg", "weno5")
+    rec = [ref.step(energies=True) for _ in range(S)]
+    sim = disc_in_taylor_green(N, "weno5")
+    sim.step(S)
+    d = sim.diagnostics()
+    keys = ("t", "ke", "se", "diss", "integ", "ry", "minJ")
+    want = np.array([[r[k] for k in keys] + [r["E"]] for r in rec])
+    got = np.stack([d[k] for k in keys] + [d["ke"] + d["se"] + d["integ"]], axis=1)
+    rel = np.abs(got - want) / np.abs(want)
+    print(f"\n[config3 N=1024 x{S}] max rel per column {dict(zip(keys + ('E',), rel.max(0)))}")
+    drift = (got[-1, 7] - got[0, 7]) / got[0, 7]
+    drift_ref = (want[-1, 7] - want[0, 7]) / want[0, 7]
+    print(f"  energy drift over {S} steps: gpu {drift:.6e} oracle {drift_ref:.6e}")
+    np.testing.assert_allclose(got, want, rtol=1e-6)       # north star
+    np.testing.assert_allclose(got, want, rtol=1e-11)      # achieved
+
+
+def test_config5_mac_N8192_vs_oracle_fixture(gpu):
+    """mac_multi_disc_lid N=8192, 3 discs (seed 3): 2 steps against the oracle fixture."""
+    from pyrmt_amd.mac import MacMultiDisc
+    g = golden("mac8192_oracle")
+    N, st = int(g["N"]), int(g["stride"])
+    sim = MacMultiDisc(N, n_discs=3, seed=3)
+    np.testing.assert_array_equal(np.array(sim.specs), g["specs"])
+    assert sim.dt == float(g["dt"])
+    worst = {}
+    for s in (1, 2):
+        sim.step(1)
+        for k in range(3):
+            jc, ic = g[f"rowcol_d{k}"]
+            for name in ("X1", "X2", "phi"):
+                f = sim.get(name, k)
+                key = f"{name}_d{k}_s{s}"
+                if s == 1:   # from rest: the maps are exact (no sin / DCT upstream)
+                    assert _sha(f) == str(g[key + "_sha"]), key
+                e = max(_maxdiff(f[jc], g[key + "_row"]), _maxdiff(f[:, ic], g[key + "_col"]),
+                        _maxdiff(f[::st, ::st], g[key + "_sub"]))
+                worst[key] = e
+                assert e <= 1e-12, (key, e)
+        for name in ("u", "v", "p"):
+            want = g[f"{name}_s{s}"]
+            got = sim.get(name)[::st, ::st]
+            e = _maxdiff(got, want) / max(1.0, np.abs(want).max())
+            worst[f"{name}_s{s}"] = e
+            assert e <= 1e-10, (name, s, e)
+    d = sim.diagnostics()
+    gd = g["diag"]
+    got = np.concatenate([np.stack([d["t"], d["dt"], d["minJ"], d["maxJ"]], 1), d["cx"], d["cy"]], 1)
+    print(f"\n[config5 N=8192] worst field diffs {max(worst.values()):.3g}; diag max rel "
+          f"{np.max(np.abs(got - gd) / np.abs(gd)):.3g}")
+    np.testing.assert_allclose(got, gd, rtol=1e-6)      # north star
+    np.testing.assert_allclose(got, gd, rtol=1e-12)     # achieved

@@ -94,3 +94,44 @@ def test_mac_multi_disc_trace(M):
     for k in range(3):
         np.testing.assert_allclose(sim.get("X1", k), g[f"X1_{k}_end"], rtol=0, atol=1e-9)
         np.testing.assert_allclose(sim.get("X2", k), g[f"X2_{k}_end"], rtol=0, atol=1e-9)
+
+
+def test_mac_sim_stops_on_divergence(M):
+    """mac_multi_disc_lid.py:100-103: the loop stops after a step with J < 0 (a folded map);
+    the record of that step is kept and flagged, later steps are not run."""
+    sim = M.MacMultiDisc(64, n_discs=3, seed=3)
+    R, cx, cy = sim.specs[0]
+    X1 = sim.get("X1", 0)
+    sim.field("X1", 0).copy_(sim.torch.as_tensor(2 * cx - X1))   # mirrored map: det G < 0
+    sim.step(5)
+    d = sim.diagnostics()
+    assert len(d["t"]) == 1 and d["diverged"][0] == 1 and d["minJ"][0] < 0
+    sim.step(3)
+    assert len(sim.diagnostics()["t"]) == 1
+
+
+def test_mac_sim_raises_on_extrapolation_abort(M, gpu):
+    """An aborted extrapolation is an error (RMTError), not a silently unfinished band."""
+    from pyrmt_amd import _lib as L
+    sim = M.MacMultiDisc(64, n_discs=3, seed=3)
+    gpu.functions.extrapolation_mode(3)
+    try:
+        with pytest.raises(L.RMTError):
+            sim.step(1)
+    finally:
+        gpu.functions.extrapolation_mode(0)
+
+
+def test_extrapolate_reference_map_raises_on_abort(gpu):
+    from pyrmt_amd import _lib as L
+    N = 65
+    X, Y, dx, dy = gpu.create_grid(N, N, 1.0, 1.0)
+    phi = np.sqrt((X - 0.5) ** 2 + (Y - 0.5) ** 2) - 0.2
+    m = (phi <= 0).astype(float)
+    gpu.functions.extrapolation_mode(3)
+    try:
+        with pytest.raises(L.RMTError):
+            gpu.extrapolate_reference_map(X * m, Y * m, phi, dx, dy, 3)
+    finally:
+        gpu.functions.extrapolation_mode(0)
+    gpu.extrapolate_reference_map(X * m, Y * m, phi, dx, dy, 3)   # mode 0 again: no error

@@ -347,3 +347,45 @@ def test_ghia_rms_full_run(gpu, Re, key):
     assert steps == int(pin[f"{key}_steps"])
     rms = ghia_rms(sim, gd["y"], gd["u"])
     assert abs(rms - float(pin[f"{key}_rms"])) < 1e-10, (rms, float(pin[f"{key}_rms"]))
+
+
+# ── standalone exports of the reference's per-step diagnostics / blended RHS ────────
+def test_velocity_rhs_blended_bitwise(gpu):
+    """functions.py:897-944 (pyRMT/__init__.py:16): H and rho_local are inputs, so no
+    transcendental function is involved: bit-exact against the reference's fixture."""
+    g = golden("vrhs")
+    dx, dy = float(g["dx"]), float(g["dy"])
+    args = (g["u"], g["v"], g["p"], g["sxx"], g["sxy"], g["syy"], dx, dy, g["phi"], 0.01, g["H"],
+            None, None, g["rho"])
+    ru, rv = gpu.velocity_rhs_blended_optimized(*args, 0.0, 0.0)
+    _eq(ru, g["ru0"]); _eq(rv, g["rv0"])
+    ru, rv = gpu.velocity_rhs_blended_optimized(*args, g["fx"], g["fy"])
+    _eq(ru, g["ru1"]); _eq(rv, g["rv1"])
+
+
+def test_energy_exports(gpu, oracle):
+    """output.py:6-193 (pyRMT/__init__.py:28-31) against the reference's fixture values: the
+    strain energy has no transcendental function and is summed in np.sum's order, so it is
+    bit-exact; KE and dissipation go through the smoothed Heaviside (device sin vs glibc)."""
+    o = golden("operators")
+    dx, dy = float(o["dx"]), float(o["dy"])
+    se = gpu.compute_strain_energy(o["X1"], o["X2"], o["phi"], 0.7, dx, dy, kappa=0.3)
+    assert se == float(o["se"]), (se, float(o["se"]))
+    ke = gpu.compute_kinetic_energy(o["a"], o["b"], 1.0, 1.0, o["phi"], 2 * dx, dx, dy)
+    ed = gpu.compute_viscous_dissipation(o["a"], o["b"], 0.01, o["phi"], 2 * dx, dx, dy, eta_s=0.02)
+    np.testing.assert_allclose(ke, float(o["ke"]), rtol=1e-14)
+    np.testing.assert_allclose(ed, float(o["ed"]), rtol=1e-14)
+    # larger grids: several full 8192-cell chunks plus a partial one, against the oracle
+    N = 333
+    X, Y, dx, dy = gpu.create_grid(N, N, 1.0, 1.0)
+    phi = np.sqrt((X - 0.45) ** 2 + (Y - 0.55) ** 2) - 0.3
+    X1 = X + 0.03 * np.sin(3 * Y); X2 = Y - 0.02 * np.cos(2 * X)
+    a = np.sin(2 * np.pi * X) * np.cos(np.pi * Y); b = -np.cos(np.pi * X) * np.sin(2 * np.pi * Y)
+    assert gpu.compute_strain_energy(X1, X2, phi, 0.3, dx, dy, 0.1) == \
+        oracle.compute_strain_energy(X1, X2, phi, 0.3, dx, dy, kappa=0.1)
+    np.testing.assert_allclose(gpu.compute_kinetic_energy(a, b, 1.0, 2.0, phi, 2 * dx, dx, dy),
+                               oracle.compute_kinetic_energy(a, b, 1.0, 2.0, phi, 2 * dx, dx, dy),
+                               rtol=1e-14)
+    np.testing.assert_allclose(gpu.compute_viscous_dissipation(a, b, 0.01, phi, 2 * dx, dx, dy, 0.05),
+                               oracle.compute_viscous_dissipation(a, b, 0.01, phi, 2 * dx, dx, dy, 0.05),
+                               rtol=1e-14)
