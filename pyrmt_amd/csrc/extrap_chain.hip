@@ -651,25 +651,20 @@ __device__ __forceinline__ bool ch_probe(int ey, const int *tag, const double2 *
         const long long t_ = __builtin_amdgcn_s_memtime();             \
         pr[k] += t_ - tl; tl = t_;                                     \
     }
-// fold row[p0, p1) into acc in order, 8 terms per step with the next 8 in flight; reads
-// past p1 give +0.0 (exact: every Bw term is >= 0, so acc is never -0.0)
-__device__ __forceinline__ double ch_fold_range(double acc, const double *row, int p0, int p1) {
-    if (p0 >= p1) return acc;
-    double a[8], b[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a[q] = p0 + q < p1 ? row[p0 + q] : 0.0;
-    for (int q0 = p0; q0 < p1; q0 += 8) {
-        const bool more = q0 + 8 < p1;
+// fold row[8*c0 .. 8*c1) into acc in order; two 8-term chunks of reads in flight
+__device__ __forceinline__ double ch_fold(double acc, const double *row, int c0, int c1) {
+    if (c0 >= c1) return acc;
+    const double2 *r2 = (const double2 *)row;
+    double2 a0 = r2[4 * c0], a1 = r2[4 * c0 + 1], a2 = r2[4 * c0 + 2], a3 = r2[4 * c0 + 3];
+    for (int c = c0; c < c1; ++c) {
+        double2 b0, b1, b2, b3;
+        const bool more = c + 1 < c1;
         if (more) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) b[q] = q0 + 8 + q < p1 ? row[q0 + 8 + q] : 0.0;
+            b0 = r2[4 * c + 4]; b1 = r2[4 * c + 5]; b2 = r2[4 * c + 6]; b3 = r2[4 * c + 7];
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc += a[q];
-        if (more) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) a[q] = b[q];
-        }
+        acc += a0.x; acc += a0.y; acc += a1.x; acc += a1.y;
+        acc += a2.x; acc += a2.y; acc += a3.x; acc += a3.y;
+        if (more) { a0 = b0; a1 = b1; a2 = b2; a3 = b3; }
     }
     return acc;
 }
@@ -761,78 +756,50 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    // pass 1: products of the sources already published (tag and value read back to back:
-    // one wave's LDS operations are performed in order, so a matching tag means the value read
-    // after it is the published one)
-    if (has && !done) {
-        const int t = __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // pass 1: products of the sources already published; fold up to the first missing one
+    {
+        const bool ready = has && !done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
         asm volatile("" ::: "memory");
-        const unsigned long long *vw = (const unsigned long long *)&val[slot];
-        const double vx = __longlong_as_double((long long)__hip_atomic_load(
-            &vw[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        const double vy = __longlong_as_double((long long)__hip_atomic_load(
-            &vw[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (t == e.y) {
+        if (ready) {
+            const double2 v = val[slot];
 #pragma unroll
-            for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? vx : vy);
+            for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
             done = true;
         }
     }
+    // first window term whose source is still missing: sources are listed in window order
+    const u64 pend = __ballot(!done);
+    const int kmiss = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : npad;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // the sources still missing, in window order: fold up to each one before waiting for it,
-    // with the 16 terms after it already in registers, so that only its product, those adds
-    // and the solve follow its arrival
-    const double *row = tv + min(lane, 5) * npad;
-    u64 pend = __ballot(!done);
-    int pos = 0;
+    const int c1 = kmiss >> 3, nch = npad >> 3;
+    if (lane < 6) acc = ch_fold(acc, tv + lane * npad, 0, c1);
+    CH_STAMP(3);
+    // pass 2: wait for the missing sources, then the rest of the fold
     if (pend) {
-        CH_STAMP(3);
         long sp = 0;
         if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-        while (pend) {
-            const int d = __builtin_ctzll(pend);
-            pend &= pend - 1;
-            const int kp = __builtin_amdgcn_readlane(e.x, d), src = __builtin_amdgcn_readlane(e.y, d);
-            const int kend = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : npad;
-            const double c0 = rlf(cf[0], d), c1 = rlf(cf[1], d), c2 = rlf(cf[2], d);
-            const int m3 = lane % 3;
-            const double cs = m3 == 0 ? c0 : (m3 == 1 ? c1 : c2);
-            if (lane < 6) acc = ch_fold_range(acc, row, pos, kp);
-            double ra[8], rb[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                ra[q] = kp + 1 + q < kend ? row[kp + 1 + q] : 0.0;
-                rb[q] = kp + 9 + q < kend ? row[kp + 9 + q] : 0.0;
-            }
-            const int ps = src & (CH_R - 1);
-            const unsigned long long *vw = (const unsigned long long *)&val[ps] + (lane >= 3 ? 1 : 0);
-            double v;
-            for (;;) {
-                const int t = __hip_atomic_load(&tag[ps], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (;;) {
+            if (!done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
                 asm volatile("" ::: "memory");
-                v = __longlong_as_double((long long)__hip_atomic_load(
-                    vw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                if (__builtin_amdgcn_readfirstlane(t) == src) break;
-                if (++sp > CH_SPIN_LIMIT) return false;
-                if constexpr (PROF) pr[7] += 1;
-                if constexpr (!(VAR & 2)) __builtin_amdgcn_s_sleep(0);
-            }
-            if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(3);
-            CH_STAMP(2);
-            acc = acc + cs * v;
+                const double2 v = val[slot];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc += ra[q];
-            if (kp + 9 < kend) {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) acc += rb[q];
+                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+                done = true;
             }
-            if (lane < 6 && kp + 17 < kend) acc = ch_fold_range(acc, row, kp + 17, kend);
-            pos = kend;
-            if constexpr (VAR & 1) if (pend) __builtin_amdgcn_s_setprio(0);
+            if (__ballot(!done) == 0) break;
+            if (++sp > CH_SPIN_LIMIT) return false;
+            if constexpr (PROF) pr[7] += 1;
+            if constexpr (!(VAR & 2)) __builtin_amdgcn_s_sleep(0);
         }
+        if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(3);
+        CH_STAMP(2);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    if (lane < 6) acc = ch_fold_range(acc, row, pos, npad);
+    if (lane < 6) acc = ch_fold(acc, tv + lane * npad, c1, nch);
     if constexpr (PROF) asm volatile("" : "+v"(acc));
     CH_STAMP(4);
     // utils.py:134-166 on lanes 0 (X1) and 3 (X2) with the precomputed cofactors
