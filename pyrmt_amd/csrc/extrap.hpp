@@ -10,7 +10,7 @@ typedef unsigned long long u64;
 
 constexpr int EX_MAXL = 8;          // layers the chain path handles (more -> fallback sweep)
 constexpr int CH_R = 2048;          // chain value ring (slots, chain order); deps < CH_R/2 back
-constexpr int CH_W = 12;            // chain workgroup waves (3 per SIMD: 168 VGPRs)
+constexpr int CH_W = 12;            // chain workgroup waves (3 per SIMD)
 constexpr int CH_HDR = 24;          // record header, doubles
 constexpr int CH_TVS = 88;          // padded fold terms per sum (81 rounded up to 8)
 constexpr int CH_MAXREC = 8 * (CH_HDR + 6 * CH_TVS + 4 * 64);   // 6464 B (<= 64 sources)

@@ -31,7 +31,9 @@
 #include "extrap.hpp"
 #include "exp_glibc.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 namespace rmt {
 
@@ -593,6 +595,8 @@ struct ChainArgs {
     double *X1e, *X2e;
     int ML;
     int *status;
+    long long *trace;   // PROF diagnostic: per fit {start, ready, published, critical source,
+                        // wave, cell} (s_memrealtime), indexed by global chain slot
 };
 
 // source of a record term: e.y >= 0 -> this part's LDS ring (tag e.y); e.y < 0 -> the other
@@ -693,7 +697,9 @@ template <bool PROF, int VAR>
 __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                        int *cur, int &wm, double &o_out, long &c_out,
                                        long long *pr, long long &tl, int *gtag, double *gval,
-                                       int gslot) {
+                                       int gslot, long long *trace = nullptr, int base = 0) {
+    long long tr_start = 0, tr_ready = 0;
+    int tr_crit = -1;
     // ring reuse: every fit < x - CH_R/2 is done (all their readers are < x)
     long spins = 0;
     while (x - CH_R / 2 >= wm) {
@@ -707,6 +713,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         }
     }
     CH_STAMP(1);
+    if constexpr (PROF) tr_start = __builtin_amdgcn_s_memrealtime();
     const long long meta = __double_as_longlong(B[1]);
     const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
     const int nd = __builtin_amdgcn_readfirstlane((int)((meta >> 32) & 0x7fffffff));
@@ -781,6 +788,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         long sp = 0;
         if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
         for (;;) {
+            bool now = false;
             if (!done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
                 asm volatile("" ::: "memory");
@@ -788,6 +796,11 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
 #pragma unroll
                 for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
                 done = true;
+                now = true;
+            }
+            if constexpr (PROF) {
+                const u64 fl = __ballot(now);
+                if (fl) tr_crit = __builtin_amdgcn_readlane(e.y, __builtin_ctzll(fl));
             }
             if (__ballot(!done) == 0) break;
             if (++sp > CH_SPIN_LIMIT) return false;
@@ -796,6 +809,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         }
         if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(3);
         CH_STAMP(2);
+        if constexpr (PROF) tr_ready = __builtin_amdgcn_s_memrealtime();
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
@@ -826,6 +840,15 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     c_out = __double_as_longlong(B[0]);
     if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     CH_STAMP(5);
+    if constexpr (PROF) {
+        if (trace && lane == 0) {
+            const long long tp = __builtin_amdgcn_s_memrealtime();
+            long long *t = trace + 6L * gslot;
+            t[0] = tr_start; t[1] = tr_ready ? tr_ready : tr_start; t[2] = tp;
+            t[3] = tr_crit >= 0 ? base + tr_crit : (tr_crit < -1 ? -tr_crit - 1 : -1);
+            t[4] = threadIdx.x >> 6; t[5] = c_out;
+        }
+    }
     return true;
 }
 
@@ -877,7 +900,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
         if (!ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag, C.ws.gval,
-                               base + x)) { ok = false; break; }
+                               base + x, C.trace, base)) { ok = false; break; }
         x = x2; r = r2;
     }
     if constexpr (PROF)
@@ -923,7 +946,7 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
     if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
-    ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status};
+    ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status, nullptr};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
     static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 3;
     if (!prof) {
@@ -943,6 +966,16 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
         RMT_HIP(hipMemsetAsync(gp, 0, sizeof(hp), st));
         hipEvent_t e0, e1;
         RMT_HIP(hipEventCreate(&e0)); RMT_HIP(hipEventCreate(&e1));
+        // RMT_EX_TRACE=<path>: per-fit timestamps of the first profiled call, raw int64
+        // (tools/chain_trace.py reconstructs the critical path)
+        static const char *tpath = getenv("RMT_EX_TRACE");
+        static bool traced = false;
+        long long *dtr = nullptr;
+        if (tpath && !traced) {
+            RMT_HIP(hipMalloc(&dtr, 6 * sizeof(long long) * ws.maxt));
+            RMT_HIP(hipMemsetAsync(dtr, 0, 6 * sizeof(long long) * ws.maxt, st));
+            C.trace = dtr;
+        }
         RMT_HIP(hipEventRecord(e0, st));
         k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
@@ -957,6 +990,16 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
                 "products %.3g fold %.3g solve+publish %.3g store+prefetch %.3g (Mclk, all "
                 "waves) polls %lld\n", ms, hs[0], hp[0] / 1e6, hp[1] / 1e6, hp[2] / 1e6,
                 hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6, hp[6] / 1e6, hp[7]);
+        if (dtr) {
+            std::vector<long long> h(6 * ws.maxt);
+            int tot = 0;
+            RMT_HIP(hipMemcpy(&tot, ws.ctl + EXC_BASE + ML, sizeof(int), hipMemcpyDeviceToHost));
+            RMT_HIP(hipMemcpy(h.data(), dtr, 6 * sizeof(long long) * tot, hipMemcpyDeviceToHost));
+            FILE *f = fopen(tpath, "wb");
+            if (f) { fwrite(h.data(), sizeof(long long), 6 * (size_t)tot, f); fclose(f); }
+            hipFree(dtr);
+            traced = true;
+        }
         hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
     }
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], st));
