@@ -27,12 +27,35 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # (reads u, v, p, X1, X2; writes u*, v*) = 7 planes x 8 B per cell for one RK4 pass.
 RK4_ALG_BYTES_PER_CELL = 7 * 8
 STEP_ALG_BYTES_PER_CELL = 208  # the whole step
-# HBM bytes per k_mom_stage launch at N=4096 from the PMC passes (FETCH_SIZE + WRITE_SIZE,
-# calibrated; profiles/r01/), None where not measured for this N
-TRAFFIC_PER_LAUNCH = 2134390187   # 15.9 planes: 12.9 read + 3.0 written (profiles/r01/hbm_traffic_n4096.md)
-# longest dependency chain of the bench-state extrapolation at N=4096 in fits, scheduled
-# row by row on 8 waves (tools/extrap_depth.py)
-CHAIN_DEPTH_4096 = 4493
+# HBM bytes per launch and per step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
+# bench (scripts/gpu.sh pmc -> tools/pmc_traffic.py; FETCH x2 per the gfx950 calibration)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_n4096.json")
+# dependent fits on the critical path of the bench-state extrapolation at N=4096 (per-fit
+# trace of the chain kernel, tools/chain_trace.py; profiles/r02/chain_trace/)
+CHAIN_DEPTH_4096 = 3257
+# the reference's only published timing: the collocated soft-disc step at N=128 on "CPU
+# (8 threads)", ~31 ms/step (docs/PERFORMANCE.md:3-5) = 0.53 M cell-updates/s
+REF_PUBLISHED = {"value": 128 * 128 / 0.031, "unit": "cell-updates/s", "grid": 128,
+                 "ms_per_step": 31.0, "source": "reference docs/PERFORMANCE.md:3-5 (CPU, 8 threads)"}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def _pmc(n, ws):
+    """(bytes per k_mom_stage launch, bytes per step, git rev) from the committed PMC passes."""
+    if n != 4096 or ws != 1 or not os.path.exists(PMC_TRAFFIC):
+        return None, None, None
+    d = json.load(open(PMC_TRAFFIC))
+    k = d["kernels"].get("k_mom_stage")
+    return (k["bytes_per_launch"] if k else None), d["per_step"].get("total"), d.get("git_rev")
 
 
 def _dist():
@@ -44,23 +67,36 @@ def _dist():
 
 def cpu_baseline(n, steps):
     """The oracle (C restatement of the reference's Numba kernels + the same NumPy/SciPy
-    calls) timed on this host: faithful threading (OpenMP only in the kernels that Numba
-    runs parallel=True)."""
+    calls) timed on this host, two ways: faithful threading (OpenMP only in the kernels the
+    reference runs Numba parallel=True; everything else serial, as the reference) and
+    all-cores (OpenMP on every per-cell loop; the extrapolation sweep stays serial).  Both
+    give the same results bit for bit.  Threads: the box's CPU share (16), os.cpu_count()
+    reports the whole machine there."""
     import sys
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
-    cores = min(16, os.cpu_count() or 1)
+    cores = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 16)
     O.set_threads(cores)
-    sim = O.SoftDisc(n, "lid")
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        sim.step()
-    dt = time.perf_counter() - t0
-    return {"value": n * n * steps / dt, "unit": "cell-updates/s", "cores": cores,
-            "kind": "port",
-            "sample": f"{steps} full steps of the N={n} soft-disc loop body (oracle, "
-                      f"OpenMP only where the reference uses Numba parallel=True), "
-                      f"{dt:.1f} s on {platform.processor() or platform.machine()}"}
+    out = {}
+    for mode, allc in (("faithful", False), ("all_cores", True)):
+        O.set_all_cores(allc)
+        sim = O.SoftDisc(n, "lid")
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sim.step()
+        dt = time.perf_counter() - t0
+        out[mode] = {"value": n * n * steps / dt, "s_per_step": dt / steps}
+    O.set_all_cores(False)
+    f = out["faithful"]
+    return {"value": f["value"], "unit": "cell-updates/s", "cores": cores, "kind": "port",
+            "all_cores": {"value": out["all_cores"]["value"],
+                          "s_per_step": out["all_cores"]["s_per_step"], "cores": cores},
+            "cpu": _cpu_model(), "nproc": os.cpu_count(),
+            "reference_published": REF_PUBLISHED,
+            "sample": f"{steps} full step(s) of the N={n} soft-disc loop body per variant "
+                      f"(oracle: faithful {f['s_per_step']:.1f} s/step with OpenMP only where "
+                      f"the reference uses Numba parallel=True; all-cores "
+                      f"{out['all_cores']['s_per_step']:.1f} s/step) on {_cpu_model()}"}
 
 
 def main():
@@ -69,7 +105,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grid", "--n", dest="n", type=int, default=4096)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -97,27 +133,38 @@ def main():
         sim = soft_disc_in_lid_driven(N)
     sim.step(args.warmup)
     torch.cuda.synchronize()
+
+    def timed(k):
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sim.step(k)
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if ws > 1:
+            t = torch.tensor([el], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    # `value`: the K steps with no profiling events; then the same K steps again with HIP
+    # events around each phase and around the dominant kernel's launches (the roofline and
+    # the phase breakdown come from this second timed region)
+    elapsed = timed(args.steps)
     sim.set_profiling(True)
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    sim.step(args.steps)
-    torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed_prof = timed(args.steps)
     ph = sim.phase_times()
+    sim.set_profiling(False)
     d = sim.diagnostics()
     assert np.all(np.isfinite(d["cx"])) and np.all(np.isfinite(d["umax"])), "non-finite state"
 
     if rank == 0:
         cells = N * N * args.steps          # one problem (strong scaling when ws > 1)
         value = cells / elapsed
+        traffic, step_traffic, pmc_rev = _pmc(N, ws)
         rk_ms, rk_intervals = ph["rk4_stage_kernels"]
         rk_launches = rk_intervals if ws == 1 else 4 * rk_intervals
         per_launch_s = rk_ms / 1e3 / rk_launches
@@ -142,7 +189,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_mom_stage (fused RK4 stage, 4 launches/step)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": TRAFFIC_PER_LAUNCH if N == 4096 and ws == 1 else None,
+                         "traffic": traffic, "traffic_rev": pmc_rev,
                          "launch_ms": per_launch_s * 1e3,
                          "alg_bytes_per_launch": alg_per_launch},
             # the dominant kernel by time is not HBM-bound: the exact raster-order extrapolation
@@ -153,7 +200,11 @@ def main():
             "step_roofline": {"alg_bytes_per_cell": STEP_ALG_BYTES_PER_CELL,
                               "per_gpu": True,
                               "achieved_GBs": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9,
-                              "frac": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9 / HBM_PEAK_GBS},
+                              "frac": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9 / HBM_PEAK_GBS,
+                              "traffic_per_step": step_traffic,
+                              "measured_GBs": (step_traffic / (elapsed / args.steps) / 1e9
+                                               if step_traffic else None)},
+            "ms_per_step_profiled": elapsed_prof / args.steps * 1e3,
             "phase_ms_per_step": {k: v[0] / max(1, args.steps) for k, v in ph.items()},
         }
         if not args.no_cpu_baseline and ws == 1:

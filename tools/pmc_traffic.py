@@ -1,0 +1,67 @@
+"""HBM traffic per kernel launch and per step from two rocprofv3 PMC passes of a short bench
+(scripts/gpu.sh pmc: `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE`, each with --kernel-trace).
+
+FETCH_SIZE is doubled (gfx950 counts 128-B requests at 64 B: MI355X_MICROARCH.md section HBM;
+calibrated on librmt's own 8-B/lane pattern in round 1, profiles/r01/hbm_traffic_n4096.md),
+WRITE_SIZE is taken as is.  Per step: the dispatches from the second k_dt launch (the first
+kernel of a step after its max|u| reduction) to the end, divided by the steps they cover.
+
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [git-rev]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(d, counter):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not f:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    rows = list(csv.DictReader(open(f[0])))
+    per = {}
+    for r in rows:
+        if r.get("Counter_Name") != counter:
+            continue
+        did = int(r["Dispatch_Id"])
+        name = r["Kernel_Name"].split("(")[0].split("<")[0].strip()
+        per[did] = (name, per.get(did, (name, 0.0))[1] + float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    rev = sys.argv[4] if len(sys.argv) > 4 else ""
+    fe = load(fdir, "FETCH_SIZE")
+    wr = load(wdir, "WRITE_SIZE")
+    kern = defaultdict(lambda: [0, 0.0, 0.0])
+    for did, (name, v) in fe.items():
+        k = kern[name]; k[0] += 1; k[1] += 2.0 * v * 1024.0   # FETCH_SIZE is in KiB
+    for did, (name, v) in wr.items():
+        kern[name][2] += v * 1024.0
+    # per step, from the fetch pass's dispatch order
+    order = sorted(fe)
+    starts = [d for d in order if fe[d][0] == "k_dt"]
+    step = {}
+    for label, per, scale in (("fetch", fe, 2.0), ("write", wr, 1.0)):
+        if len(starts) >= 2:
+            tot = sum(v for d, (n, v) in per.items() if d >= starts[1]) * scale * 1024.0
+            step[label] = tot / (len(starts) - 1)
+    res = {"git_rev": rev, "units": "bytes", "fetch_correction": 2.0,
+           "kernels": {n: {"launches": c, "fetch_per_launch": f / max(c, 1),
+                           "write_per_launch": w / max(c, 1),
+                           "bytes_per_launch": (f + w) / max(c, 1)}
+                       for n, (c, f, w) in sorted(kern.items(), key=lambda kv: -(kv[1][1] + kv[1][2]))},
+           "per_step": {"fetch": step.get("fetch"), "write": step.get("write"),
+                        "total": (step["fetch"] + step["write"]) if step else None,
+                        "steps": len(starts) - 1}}
+    json.dump(res, open(out, "w"), indent=1)
+    print(f"per step: {res['per_step']}")
+    for n, k in list(res["kernels"].items())[:12]:
+        print(f"{n:40s} x{k['launches']:4d}  {k['bytes_per_launch'] / 1e9:.3f} GB/launch")
+
+
+if __name__ == "__main__":
+    main()
