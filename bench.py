@@ -54,8 +54,8 @@ def _pmc(n, ws):
     if n != 4096 or ws != 1 or not os.path.exists(PMC_TRAFFIC):
         return None, None, None
     d = json.load(open(PMC_TRAFFIC))
-    k = d["kernels"].get("k_mom_stage")
-    return (k["bytes_per_launch"] if k else None), d["per_step"].get("total"), d.get("git_rev")
+    k = d["kernels"].get("k_mom_stage")     # the full-grid stage launches the events time
+    return (k["bytes_per_full_launch"] if k else None), d["per_step"].get("total"), d.get("git_rev")
 
 
 def _dist():
@@ -105,7 +105,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--grid", "--n", dest="n", type=int, default=4096)
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

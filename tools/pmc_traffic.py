@@ -31,16 +31,33 @@ def load(d, counter):
     return per
 
 
+def full(b):
+    if not b:
+        return {}
+    big = [x for x in b if x >= 0.25 * max(b)]
+    return {"launches_full": len(big), "bytes_per_full_launch": sum(big) / len(big)}
+
+
 def main():
     fdir, wdir, out = sys.argv[1:4]
     rev = sys.argv[4] if len(sys.argv) > 4 else ""
     fe = load(fdir, "FETCH_SIZE")
     wr = load(wdir, "WRITE_SIZE")
     kern = defaultdict(lambda: [0, 0.0, 0.0])
+    per_launch = defaultdict(list)      # bytes of each dispatch (fetch pass + write pass)
     for did, (name, v) in fe.items():
         k = kern[name]; k[0] += 1; k[1] += 2.0 * v * 1024.0   # FETCH_SIZE is in KiB
     for did, (name, v) in wr.items():
         kern[name][2] += v * 1024.0
+    # the two passes are separate runs of the same command: pair the n-th dispatch of a
+    # kernel in one with the n-th in the other
+    fseq, wseq = defaultdict(list), defaultdict(list)
+    for did in sorted(fe):
+        fseq[fe[did][0]].append(2.0 * fe[did][1] * 1024.0)
+    for did in sorted(wr):
+        wseq[wr[did][0]].append(wr[did][1] * 1024.0)
+    for n in fseq:
+        per_launch[n] = [a + b for a, b in zip(fseq[n], wseq.get(n, []))]
     # per step, from the fetch pass's dispatch order
     order = sorted(fe)
     starts = [d for d in order if fe[d][0] == "k_dt"]
@@ -52,7 +69,11 @@ def main():
     res = {"git_rev": rev, "units": "bytes", "fetch_correction": 2.0,
            "kernels": {n: {"launches": c, "fetch_per_launch": f / max(c, 1),
                            "write_per_launch": w / max(c, 1),
-                           "bytes_per_launch": (f + w) / max(c, 1)}
+                           "bytes_per_launch": (f + w) / max(c, 1),
+                           # launches over the whole grid (a kernel also launched on a tile
+                           # list, e.g. k_mom_stage's re-run on the extrapolated tiles, moves
+                           # a fraction of that): those above a quarter of the largest
+                           **full(per_launch[n])}
                        for n, (c, f, w) in sorted(kern.items(), key=lambda kv: -(kv[1][1] + kv[1][2]))},
            "per_step": {"fetch": step.get("fetch"), "write": step.get("write"),
                         "total": (step["fetch"] + step["write"]) if step else None,
@@ -60,7 +81,8 @@ def main():
     json.dump(res, open(out, "w"), indent=1)
     print(f"per step: {res['per_step']}")
     for n, k in list(res["kernels"].items())[:12]:
-        print(f"{n:40s} x{k['launches']:4d}  {k['bytes_per_launch'] / 1e9:.3f} GB/launch")
+        print(f"{n:40s} x{k['launches']:4d}  {k['bytes_per_launch'] / 1e9:.3f} GB/launch  "
+              f"full x{k.get('launches_full', 0)} {k.get('bytes_per_full_launch', 0) / 1e9:.3f}")
 
 
 if __name__ == "__main__":
