@@ -780,7 +780,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     const int kmiss = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : npad;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int c1 = kmiss >> 3, nch = npad >> 3;
+    int c1 = kmiss >> 3;
+    const int nch = npad >> 3;
     if (lane < 6) acc = ch_fold(acc, tv + lane * npad, 0, c1);
     CH_STAMP(3);
     // pass 2: wait for the missing sources, then the rest of the fold
@@ -802,7 +803,21 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
                 const u64 fl = __ballot(now);
                 if (fl) tr_crit = __builtin_amdgcn_readlane(e.y, __builtin_ctzll(fl));
             }
-            if (__ballot(!done) == 0) break;
+            const u64 left = __ballot(!done);
+            if (left == 0) break;
+            if constexpr ((VAR & 32) != 0) {
+                // one source left: fold every chunk before its term now, so that only the
+                // chunks from its own to the end remain after it arrives
+                if (__popcll(left) == 1) {
+                    const int c2 = __builtin_amdgcn_readlane(e.x, __builtin_ctzll(left)) >> 3;
+                    if (c2 > c1) {
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        if (lane < 6) acc = ch_fold(acc, tv + lane * npad, c1, c2);
+                        c1 = c2;
+                    }
+                }
+            }
             if (++sp > CH_SPIN_LIMIT) return false;
             if constexpr (PROF) pr[7] += 1;
             if constexpr (!(VAR & 2)) __builtin_amdgcn_s_sleep(0);
@@ -954,6 +969,10 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
             case 0: k_ex_chain<false, 0><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 1: k_ex_chain<false, 1><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 2: k_ex_chain<false, 2><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
+            case 35:
+                if (nparts == 1) k_ex_chain<false, 51><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+                else k_ex_chain<false, 35><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
+                break;
             default:
                 if (nparts == 1) k_ex_chain<false, 19><<<1, CH_W * 64, 0, st>>>(C, nullptr);
                 else k_ex_chain<false, 3><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
@@ -977,7 +996,8 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
             C.trace = dtr;
         }
         RMT_HIP(hipEventRecord(e0, st));
-        k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
+        if (var == 35) k_ex_chain<true, 35><<<nparts, CH_W * 64, 0, st>>>(C, gp);
+        else k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, st));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));

@@ -172,8 +172,13 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     int tiles_x, int ntiles, double *__restrict__ ku, double *__restrict__ kv,
     const double *__restrict__ ainu, const double *__restrict__ ainv, double *__restrict__ accu,
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
-    const int *__restrict__ tlist, const int *__restrict__ tcount) {
+    const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp) {
     __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
+    if (dtp) {   // the same roundings as mom_stage's host constants
+        const double dt = *dtp;
+        coef = stage == 0 ? 0.0 : stage == 3 ? dt : 0.5 * dt;
+        dt6 = dt / 6.0;
+    }
     __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
     // tlist: the listed tiles only (momentum_fixup); otherwise every tile of rows [jb, je)
     if (tlist && (int)blockIdx.x >= *tcount) return;
@@ -328,7 +333,7 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
         u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid,
         P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx,
         tiles_x, ntiles, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, ainu, ainv, aou, aov,
-        u_new, v_new, ws, tlist, tcount);
+        u_new, v_new, ws, tlist, tcount, W.dtp);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -385,7 +390,8 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
                           nullptr, nullptr));
     }
-    RMT_CHECK(!unfused || !win, RMT_ENOTSUP, "RMT_MOM_UNFUSED: single-domain only");
+    RMT_CHECK(!unfused || (!win && !W.dtp), RMT_ENOTSUP,
+              "RMT_MOM_UNFUSED: single-domain, host-dt only");
     for (int s = 0; s < 4 && unfused; ++s) {
         // stage 0 reads only u, v; kp* still point at valid planes
         const double *kpu = s ? kbu[(s - 1) & 1] : u, *kpv = s ? kbv[(s - 1) & 1] : v;

@@ -187,6 +187,13 @@ int rowtree_root(rmt_ctx *ctx, const double *x, int nrows, int nx, double *dev_r
     RMT_LAUNCHED();
     return RMT_OK;
 }
+int rowtree_sums(rmt_ctx *ctx, int nrows, double *dev_root) {
+    RMT_CHECK(nrows >= 1 && nrows <= TREE_MAX && nrows <= ctx->rsum_len, RMT_EINVAL,
+              "rowtree_sums: rows out of range");
+    k_rowtree<<<1, TREE_T, 0, ctx->stream>>>(ctx->rsum, nrows, dev_root);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
 int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int G, double count) {
     RMT_CHECK(G >= 1 && G <= 64, RMT_EINVAL, "sub_tree_mean: 1..64 roots");
     if (n > 0)
@@ -367,7 +374,9 @@ static inline dim3 rows_grid(int nx, int jb, int je) { return dim3((nx + 255) / 
 __global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
                                 const double *__restrict__ p, int ny, int nx, double d_f,
                                 double dx, double dy, double *__restrict__ divU, int jb, int je,
-                                double rho = 0.0, double dt = 1.0) {
+                                double rho = 0.0, double dt = 1.0,
+                                const double *__restrict__ dtp = nullptr) {
+    if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
     // rho > 0: the projection's rhs = (rho * divU) / dt (functions.py:1331, the same two
     // roundings as the separate scale and divide passes).  Grid: rows_grid (one block row
     // per grid row, no per-cell division).
@@ -412,26 +421,52 @@ __global__ void k_pressure_gradient(const double *__restrict__ p, int ny, int nx
 // with pc = p_raw - mean(p_raw) (mean on device).  Writes p before its own mean removal.
 // functions.py:1350-1358 after the solve: a = a* - (dt/rho) dpc/dx, BC, p = p_prev + pc.
 // Writes p before its mean removal.
+// pc - m is the mean-free correction (m: the solve's mean, subtracted here as pc is read)
 __device__ __forceinline__ double corrected(const double *__restrict__ s,
                                             const double *__restrict__ pc, long c, int ny, int nx,
-                                            double dx, double dy, double dt_rho, int comp) {
+                                            double dx, double dy, double dt_rho, int comp, double m) {
     int j = (int)(c / nx), i = (int)(c % nx);
     double gx, gy;
-    pgrad_cell(pc, c, j, i, ny, nx, dx, dy, gx, gy);
+    pgrad_cell(pc, c, j, i, ny, nx, dx, dy, gx, gy, m);
     return s[c] - dt_rho * (comp == 0 ? gx : gy);
 }
+// root (nullable): the row-tree sum of pc (dct_solve's dev_root), mean = root / count
 __global__ void k_project_correct(const double *__restrict__ a_s, const double *__restrict__ b_s,
                                   const double *__restrict__ pc, const double *__restrict__ p_prev,
                                   int ny, int nx, double dx, double dy, double dt_rho, int bc,
                                   double lid, double *__restrict__ a, double *__restrict__ b,
-                                  double *__restrict__ p, int jb, int je) {
+                                  double *__restrict__ p, int jb, int je,
+                                  const double *__restrict__ root, double count,
+                                  const double *__restrict__ dtp = nullptr, double rho = 1.0,
+                                  double *__restrict__ m2part = nullptr) {
     const int j = jb + (int)blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nx || j >= je) return;
-    const long c = (long)j * nx + i;
-    BCSrc s = bc_source(bc, lid, j, i, ny, nx);
-    a[c] = s.u_const ? s.u_val : corrected(a_s, pc, s.u_src, ny, nx, dx, dy, dt_rho, 0);
-    b[c] = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, dx, dy, dt_rho, 1);
-    p[c] = p_prev ? p_prev[c] + pc[c] : pc[c];
+    double q = -INFINITY;
+    if (i < nx && j < je) {
+        if (dtp) dt_rho = *dtp / rho;   // the host's dt / rho
+        const double m = root ? *root / count : 0.0;
+        const long c = (long)j * nx + i;
+        BCSrc s = bc_source(bc, lid, j, i, ny, nx);
+        const double ua = s.u_const ? s.u_val : corrected(a_s, pc, s.u_src, ny, nx, dx, dy, dt_rho, 0, m);
+        const double vb = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, dx, dy, dt_rho, 1, m);
+        a[c] = ua; b[c] = vb;
+        p[c] = p_prev ? p_prev[c] + (pc[c] - m) : (pc[c] - m);
+        q = ua * ua + vb * vb;
+    }
+    if (m2part) {
+        // max of u^2 + v^2 over the block, NaN-propagating (k_reduce_p1<3>'s rule; a max is
+        // exact in any order)
+        __shared__ double s[256];
+        s[threadIdx.x] = q;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) {
+                const double y = s[threadIdx.x + w];
+                if (y > s[threadIdx.x] || y != y) s[threadIdx.x] = y;
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) m2part[(long)blockIdx.y * gridDim.x + blockIdx.x] = s[0];
+    }
 }
 __global__ void k_scale_copy(const double *__restrict__ x, long n, double s,
                              double *__restrict__ y) {
@@ -457,7 +492,8 @@ int project_correct_rows(rmt_ctx *ctx, const double *a_s, const double *b_s, con
                          double lid, double *a, double *b, double *p, int jb, int je) {
     if (je > jb)
         k_project_correct<<<rows_grid(ctx->nx, jb, je), 256, 0, ctx->stream>>>(
-            a_s, b_s, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt_rho, bc, lid, a, b, p, jb, je);
+            a_s, b_s, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt_rho, bc, lid, a, b, p, jb, je,
+            nullptr, 1.0);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -691,9 +727,11 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
         k_scale_copy<<<LAUNCH1D(n)>>>(rhs, n, rho, rhs);
         k_div_scalar<<<LAUNCH1D(n)>>>(rhs, n, dt, rhs);
     }
-    RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc));
+    // pc = the raw solve; its mean (functions.py:1119) is subtracted inside the correction
+    double *root = ctx->red + RED_BLOCKS + 17;
+    RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc, root));
     k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy,
-                                       dt / rho, bc_kind, lid, a, b, p, 0, ctx->ny);
+                                       dt / rho, bc_kind, lid, a, b, p, 0, ctx->ny, root, (double)n);
     RMT_LAUNCHED();
     RMT_TRY(sub_mean_rows(ctx, p, ctx->ny, ctx->nx));
     return RMT_OK;
@@ -722,3 +760,25 @@ int rmt_compute_timestep(rmt_ctx *ctx, const double *a, const double *b, double 
     return RMT_OK;
 }
 }  // extern "C"
+
+namespace rmt {
+int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
+                   double dy, const double *dtp, double rho, int bc_kind, double lid,
+                   const double *p_prev, double *a, double *b, double *p, double *m2part) {
+    RMT_CHECK(bc_kind >= 0 && bc_kind <= 3 && p_prev && rho > 0, RMT_EINVAL,
+              "projection_dev: bad arguments");
+    const long n = (long)ctx->ny * ctx->nx;
+    RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
+    double *rhs = ctx->scratch, *pc = rhs + n;
+    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
+        a_star, b_star, p_prev, ctx->ny, ctx->nx, 0.0, dx, dy, rhs, 0, ctx->ny, rho, 1.0, dtp);
+    RMT_LAUNCHED();
+    double *root = ctx->red + RED_BLOCKS + 17;
+    RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc, root));
+    k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
+        a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy, 0.0, bc_kind, lid, a, b, p, 0,
+        ctx->ny, root, (double)n, dtp, rho, m2part);
+    RMT_LAUNCHED();
+    return sub_mean_rows(ctx, p, ctx->ny, ctx->nx);
+}
+}  // namespace rmt

@@ -14,6 +14,7 @@
 //   ->  rows (x, inverse).
 // HBM traffic: 10 planes per solve.  Other sizes: rocFFT R2C rounds (the previous path).
 #include "rmt_internal.hpp"
+#include "dft_consts.hpp"
 #include <vector>
 
 namespace rmt {
@@ -32,7 +33,7 @@ struct DctPlan {
     // LDS FFT path
     bool lds = false;
     int big = 0;                            // a radix above 13 present
-    double2 *Wx = nullptr, *Wy = nullptr;   // e^{-2 pi i t / M} tables
+    double2 *Wx = nullptr, *Wy = nullptr;   // per-pass twiddle tables (twiddles())
     int radx[16] = {0}, rady[16] = {0}, npx = 0, npy = 0;
 };
 
@@ -80,41 +81,60 @@ static void host_lambda(int n, double h, std::vector<double> &lam) {
     for (int k = 0; k < n; ++k) lam[k] = -2.0 * (1.0 - std::cos(M_PI * k / (n - 1))) / h2;
 }
 
-constexpr int DCT_T = 512;        // threads per row pair
 constexpr int DCT_MAXM = 8192;    // complex LDS entries (128 KB)
-constexpr int DCT_RCS = 98;       // 3 + 5 + 7 + 11 + 13 + 17 + 19 + 23 radix constants
 
-// radices of M for the LDS FFT (4 for pairs of 2); false if a prime factor > 31 remains
+// Radix plan of a length-M FFT: prime factors (2 .. 23), then 2s grouped into 8 / 4, 3s into
+// 9, a leftover 2 with a 5 (10) or a 3 (6): M = 8190 = 2 3^2 5 7 13 runs as 9, 10, 7, 13 --
+// four LDS passes instead of six.  false if a prime factor > 23 remains.
 static bool factor(int M, int *rad, int *np) {
-    int n = 0, m = M;
-    while (m % 4 == 0) { rad[n++] = 4; m /= 4; }
-    for (int r : {2, 3, 5, 7, 11, 13, 17, 19, 23})
-        while (m % r == 0) { if (n >= 16) return false; rad[n++] = r; m /= r; }
+    if (M < 2 || M > DCT_MAXM) return false;
+    int cnt[24] = {0}, m = M;
+    for (int q : {2, 3, 5, 7, 11, 13, 17, 19, 23})
+        while (m % q == 0) { ++cnt[q]; m /= q; }
+    if (m != 1) return false;
+    int n = 0;
+    auto put = [&](int r) { if (n < 16) rad[n++] = r; };
+    while (cnt[2] >= 3) { put(8); cnt[2] -= 3; }
+    if (cnt[2] == 2) { put(4); cnt[2] = 0; }
+    while (cnt[3] >= 2) { put(9); cnt[3] -= 2; }
+    if (cnt[2] && cnt[5]) { put(10); --cnt[2]; --cnt[5]; }
+    if (cnt[2] && cnt[3]) { put(6); --cnt[2]; --cnt[3]; }
+    for (int q : {2, 3, 5, 7, 11, 13, 17, 19, 23})
+        while (cnt[q]) { put(q); --cnt[q]; }
     *np = n;
-    return m == 1 && M >= 2 && M <= DCT_MAXM;
+    return n < 16;
 }
 
-// radix constants e^{-2 pi i t/R} for every supported odd radix, at these offsets
-static const int kRcR[8] = {3, 5, 7, 11, 13, 17, 19, 23};
-static int rc_offset(int R) {
-    int o = 0;
-    for (int r : kRcR) { if (r == R) return o; o += r; }
-    return 0;
+static bool big_radix(const int *rad, int np) {
+    for (int k = 0; k < np; ++k) if (rad[k] > 13) return true;
+    return false;
 }
 
-static int twiddles(int M, double2 **W) {
+// Per-pass twiddle table of the Stockham passes, in pass order: pass (R, Ns) holds
+// e^{-2 pi i k r / (Ns R)} at [(r - 1) Ns + k], r = 1 .. R-1, k < Ns (M - 1 entries in all);
+// angles from long double, exact where k r / (Ns R) is a multiple of 1/4
+static int twiddles(int M, const int *rad, int np, double2 **W) {
     const long double PI = 3.141592653589793238462643383279502884L;
-    std::vector<double2> h(M + DCT_RCS);
-    for (int t = 0; t < M; ++t) {
-        long double a = 2.0L * PI * t / M;
-        h[t] = make_double2((double)cosl(a), (double)-sinl(a));
+    std::vector<double2> h;
+    h.reserve(M);
+    int Ns = 1;
+    for (int q = 0; q < np; ++q) {
+        const int R = rad[q], L = Ns * R;
+        for (int r = 1; r < R; ++r)
+            for (int k = 0; k < Ns; ++k) {
+                const long t = (long)k * r % L;
+                if ((4 * t) % L == 0) {
+                    const int e = (int)(4 * t / L);
+                    const double c[4] = {1.0, 0.0, -1.0, 0.0}, sn[4] = {0.0, 1.0, 0.0, -1.0};
+                    h.push_back(make_double2(c[e], -sn[e]));
+                } else {
+                    const long double a = 2.0L * PI * t / L;
+                    h.push_back(make_double2((double)cosl(a), (double)-sinl(a)));
+                }
+            }
+        Ns = L;
     }
-    int o = M;
-    for (int R : kRcR)
-        for (int t = 0; t < R; ++t, ++o) {
-            long double a = 2.0L * PI * t / R;
-            h[o] = make_double2((double)cosl(a), (double)-sinl(a));
-        }
+    h.push_back(make_double2(1.0, 0.0));
     RMT_HIP(hipMalloc(W, h.size() * sizeof(double2)));
     RMT_HIP(hipMemcpy(*W, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice));
     return RMT_OK;
@@ -129,14 +149,13 @@ int dct_plan(rmt_ctx *ctx, double dx, double dy) {
         const int Mx = 2 * (P->nx - 1), My = 2 * (P->ny - 1);
         static const bool force_rocfft = getenv("RMT_DCT_ROCFFT") && atoi(getenv("RMT_DCT_ROCFFT"));
         P->lds = !force_rocfft && factor(Mx, P->radx, &P->npx) && factor(My, P->rady, &P->npy);
-        for (int k = 0; k < P->npx; ++k) P->big |= P->radx[k] > 13;
-        for (int k = 0; k < P->npy; ++k) P->big |= P->rady[k] > 13;
+        P->big = big_radix(P->radx, P->npx) || big_radix(P->rady, P->npy);
     }
     if (!P->lds && !g_rocfft_ready) { RMT_TRY(rf(rocfft_setup(), "setup")); g_rocfft_ready = true; }
     if (P->lds && !P->Wx) {
         const size_t n = (size_t)P->ny * P->nx;
-        RMT_TRY(twiddles(2 * (P->nx - 1), &P->Wx));
-        RMT_TRY(twiddles(2 * (P->ny - 1), &P->Wy));
+        RMT_TRY(twiddles(2 * (P->nx - 1), P->radx, P->npx, &P->Wx));
+        RMT_TRY(twiddles(2 * (P->ny - 1), P->rady, P->npy, &P->Wy));
         RMT_HIP(hipMalloc(&P->T, n * sizeof(double)));
         RMT_HIP(hipMalloc(&P->lamx, P->nx * sizeof(double)));
         RMT_HIP(hipMalloc(&P->lamy, P->ny * sizeof(double)));
@@ -226,15 +245,38 @@ static int round_rows(rmt_ctx *ctx, DctPlan *P, rocfft_plan plan, const double *
 }
 
 // ---------------------------------------------------------------- LDS FFT path --
+// Threads per workgroup: 1024 (16 waves, 128 VGPRs) for radices up to 13; 512 when a radix
+// 17 / 19 / 23 pass is in the plan (its butterfly alone holds ~45 complex values).
+template <int BIG> struct FftT { static constexpr int T = BIG ? 512 : 1024; };
+
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(__builtin_fma(a.x, b.x, -a.y * b.y), __builtin_fma(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 
-// in-register DFT of length R (forward, e^{-2 pi i jm/R}); constants from the W table
+// a * e^{-2 pi i t / R}, t a constant after unrolling (exact for multiples of R / 4)
 template <int R>
-__device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *rc) {
+__device__ __forceinline__ double2 wmul(double2 a, int t) {
+    t %= R;
+    if (t == 0) return a;
+    if (4 * t == R) return make_double2(a.y, -a.x);
+    if (2 * t == R) return make_double2(-a.x, -a.y);
+    if (4 * t == 3 * R) return make_double2(-a.y, a.x);
+    const double c = Rc<R>::c[t], sn = Rc<R>::s[t];
+    return make_double2(__builtin_fma(a.x, c, a.y * sn), __builtin_fma(a.y, c, -(a.x * sn)));
+}
+
+constexpr bool is_prime(int R) {
+    for (int d = 2; d * d <= R; ++d) if (R % d == 0) return false;
+    return R >= 2;
+}
+// first factor of a composite radix: 8 = 2 x 4, 9 = 3 x 3, 10 = 2 x 5, 6 = 2 x 3, 4 = 2 x 2
+constexpr int split(int R) { return R % 2 == 0 ? 2 : 3; }
+
+// forward DFT of length R in registers (e^{-2 pi i n k / R}), constants from dft_consts.hpp
+template <int R>
+__device__ __forceinline__ void dft(double2 *v) {
     if constexpr (R == 2) {
         const double2 a = v[0], b = v[1];
         v[0] = cadd(a, b); v[1] = csub(a, b);
@@ -244,7 +286,8 @@ __device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *rc) {
         v[0] = cadd(t0, t2); v[2] = csub(t0, t2);
         v[1] = make_double2(t1.x + t3.y, t1.y - t3.x);   // t1 - i t3
         v[3] = make_double2(t1.x - t3.y, t1.y + t3.x);   // t1 + i t3
-    } else {
+    } else if constexpr (is_prime(R)) {
+        // odd prime: X_m = A_m -/+ i S_m from the symmetric / antisymmetric input pairs
         constexpr int K = (R - 1) / 2;
         double2 a[K], b[K];
         double2 x0 = v[0];
@@ -259,82 +302,110 @@ __device__ __forceinline__ void small_dft(double2 (&v)[R], const double2 *rc) {
             double2 A = v[0], S = make_double2(0.0, 0.0);
 #pragma unroll
             for (int j = 1; j <= K; ++j) {
-                const double2 w = rc[(j * m) % R];   // (cos, -sin) of 2 pi jm / R
-                A.x = __builtin_fma(a[j - 1].x, w.x, A.x);
-                A.y = __builtin_fma(a[j - 1].y, w.x, A.y);
-                S.x = __builtin_fma(b[j - 1].x, -w.y, S.x);
-                S.y = __builtin_fma(b[j - 1].y, -w.y, S.y);
+                const double c = Rc<R>::c[(j * m) % R], sn = Rc<R>::s[(j * m) % R];
+                A.x = __builtin_fma(a[j - 1].x, c, A.x);
+                A.y = __builtin_fma(a[j - 1].y, c, A.y);
+                S.x = __builtin_fma(b[j - 1].x, sn, S.x);
+                S.y = __builtin_fma(b[j - 1].y, sn, S.y);
             }
             v[m] = make_double2(A.x + S.y, A.y - S.x);        // A - i S
             v[R - m] = make_double2(A.x - S.y, A.y + S.x);    // A + i S
         }
         v[0] = x0;
+    } else {
+        // R = A B: n = B n1 + n2, k = k1 + A k2; DFT_A over n1, twiddle w_R^{n2 k1}, DFT_B
+        constexpr int A = split(R), B = R / A;
+        double2 y[R];
+#pragma unroll
+        for (int n2 = 0; n2 < B; ++n2) {
+            double2 t[A];
+#pragma unroll
+            for (int n1 = 0; n1 < A; ++n1) t[n1] = v[B * n1 + n2];
+            dft<A>(t);
+#pragma unroll
+            for (int k1 = 0; k1 < A; ++k1) y[n2 * A + k1] = wmul<R>(t[k1], n2 * k1);
+        }
+#pragma unroll
+        for (int k1 = 0; k1 < A; ++k1) {
+            double2 t[B];
+#pragma unroll
+            for (int n2 = 0; n2 < B; ++n2) t[n2] = y[n2 * A + k1];
+            dft<B>(t);
+#pragma unroll
+            for (int k2 = 0; k2 < B; ++k2) v[k1 + A * k2] = t[k2];
+        }
     }
 }
 
-// Twiddles e^{-2 pi i t/M} as Wh[t >> 7] * Wl[t & 127] (both tables in LDS, <= 2 ulp)
-struct Tw { const double2 *hi, *lo; };
-__device__ __forceinline__ double2 tw(const Tw &T, int t) { return cmul(T.hi[t >> 7], T.lo[t & 127]); }
-
-// Per pass: radix, Ns (product of the earlier radices), and 1/Ns for divide-free index math
-struct Pass { int R, Ns; float inv; int rc; };   // rc: offset of this radix's constants
+// Per pass: radix, Ns (product of the earlier radices), 1/Ns for divide-free index math, and
+// the offset of the pass's twiddles in the table
+struct Pass { int R, Ns; float inv; int tw; };
 struct Radices { Pass p[16]; int n; };
 
-// one Stockham pass of radix R over z[0..M)
-template <int R>
-__device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps, const Tw &T,
-                                         const double2 *rcs) {
-    constexpr int BPT = (DCT_MAXM / DCT_T + R - 1) / R;   // butterflies per thread (max)
+// one Stockham pass of radix R over z[0..M): read every butterfly's inputs and twiddles ->
+// barrier -> twiddle + DFT_R -> write -> barrier
+template <int R, int NT>
+__device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps,
+                                         const double2 *__restrict__ tw) {
+    constexpr int BPT = (DCT_MAXM / NT + R - 1) / R;   // butterflies per thread (max)
     const int nb = M / R, tid = threadIdx.x, Ns = ps.Ns;
-    const double2 *rc = rcs + ps.rc;
-    double2 v[BPT][R];
+    double2 v[BPT][R], w[BPT][R - 1];
+    int o[BPT];
 #pragma unroll
     for (int b = 0; b < BPT; ++b) {
-        const int j = tid + b * DCT_T;
-        if (j < nb)
-#pragma unroll
-            for (int r = 0; r < R; ++r) v[b][r] = z[j + r * nb];
-    }
-    __syncthreads();
-    const int tstep = M / (Ns * R);
-#pragma unroll
-    for (int b = 0; b < BPT; ++b) {
-        const int j = tid + b * DCT_T;
+        const int j = tid + b * NT;
         if (j < nb) {
             int g = (int)((float)j * ps.inv), k = j - g * Ns;   // j = g Ns + k
             if (k < 0) { --g; k += Ns; } else if (k >= Ns) { ++g; k -= Ns; }
+            o[b] = g * Ns * R + k;
+            if (Ns > 1) {
+                const double2 *t = tw + ps.tw + k;
+#pragma unroll
+                for (int r = 1; r < R; ++r) w[b][r - 1] = t[(r - 1) * Ns];
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[b][r] = z[j + r * nb];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+        const int j = tid + b * NT;
+        if (j < nb) {
             if (Ns > 1)
 #pragma unroll
-                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], tw(T, k * r * tstep));
-            small_dft<R>(v[b], rc);
-            const int o = g * Ns * R + k;
+                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], w[b][r - 1]);
+            dft<R>(v[b]);
 #pragma unroll
-            for (int r = 0; r < R; ++r) z[o + r * Ns] = v[b][r];
+            for (int r = 0; r < R; ++r) z[o[b] + r * Ns] = v[b][r];
         }
     }
     __syncthreads();
 }
 
-// BIG = 0: radices 2..13; BIG = 1: up to 23 (one kernel holding every radix up to 31 spills,
-// so 29 and 31 go to rocFFT)
 template <int BIG>
-__device__ void fft_lds(double2 *z, int M, const Radices &rd, const Tw &T, const double2 *rcs) {
+__device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__restrict__ tw) {
+    constexpr int NT = FftT<BIG>::T;
     for (int q = 0; q < rd.n; ++q) {
         const Pass &ps = rd.p[q];
         switch (ps.R) {
-            case 2: fft_pass<2>(z, M, ps, T, rcs); break;
-            case 3: fft_pass<3>(z, M, ps, T, rcs); break;
-            case 4: fft_pass<4>(z, M, ps, T, rcs); break;
-            case 5: fft_pass<5>(z, M, ps, T, rcs); break;
-            case 7: fft_pass<7>(z, M, ps, T, rcs); break;
-            case 11: fft_pass<11>(z, M, ps, T, rcs); break;
-            case 13: fft_pass<13>(z, M, ps, T, rcs); break;
+            case 2: fft_pass<2, NT>(z, M, ps, tw); break;
+            case 3: fft_pass<3, NT>(z, M, ps, tw); break;
+            case 4: fft_pass<4, NT>(z, M, ps, tw); break;
+            case 5: fft_pass<5, NT>(z, M, ps, tw); break;
+            case 6: fft_pass<6, NT>(z, M, ps, tw); break;
+            case 7: fft_pass<7, NT>(z, M, ps, tw); break;
+            case 8: fft_pass<8, NT>(z, M, ps, tw); break;
+            case 9: fft_pass<9, NT>(z, M, ps, tw); break;
+            case 10: fft_pass<10, NT>(z, M, ps, tw); break;
+            case 11: fft_pass<11, NT>(z, M, ps, tw); break;
+            case 13: fft_pass<13, NT>(z, M, ps, tw); break;
             default:
                 if constexpr (BIG) {
                     switch (ps.R) {
-                        case 17: fft_pass<17>(z, M, ps, T, rcs); break;
-                        case 19: fft_pass<19>(z, M, ps, T, rcs); break;
-                        case 23: fft_pass<23>(z, M, ps, T, rcs); break;
+                        case 17: fft_pass<17, NT>(z, M, ps, tw); break;
+                        case 19: fft_pass<19, NT>(z, M, ps, tw); break;
+                        case 23: fft_pass<23, NT>(z, M, ps, tw); break;
                     }
                 }
         }
@@ -351,30 +422,27 @@ __device__ __forceinline__ void put_even(double2 *z, int n, int M, int j, double
 // x-frequencies kx (transposed plane), and the column transform is forward DCT, / eig,
 // inverse DCT (the eig of functions.py:1091-1104: lam_x[kx] + lam_y[ky], (0,0) -> 1).
 template <bool SOLVE, int BIG>
-__global__ void __launch_bounds__(DCT_T) k_dct1(const double *__restrict__ src,
-                                                double *__restrict__ dst, int rows, int n,
-                                                const double2 *__restrict__ W, Radices rd,
-                                                double scale, const double *__restrict__ lamr,
-                                                const double *__restrict__ lamk, int row0) {
+__global__ void __launch_bounds__(FftT<BIG>::T) k_dct1(const double *__restrict__ src,
+                                                       double *__restrict__ dst, int rows, int n,
+                                                       const double2 *__restrict__ W, Radices rd,
+                                                       double scale, const double *__restrict__ lamr,
+                                                       const double *__restrict__ lamk, int row0,
+                                                       double *__restrict__ rs) {
+    constexpr int NT = FftT<BIG>::T;
     extern __shared__ double2 z[];
-    __shared__ double2 twh[DCT_MAXM / 128], twl[128], rcs[DCT_RCS];
+    __shared__ double red[512];
     const int M = 2 * (n - 1), rA = 2 * blockIdx.x, rB = rA + 1, tid = threadIdx.x;
-    // tables: W has M + 192 entries: [0, M) e^{-2 pi i t/M}, then at M the small-radix constants
-    if (tid < DCT_MAXM / 128) twh[tid] = (tid << 7) < M ? W[tid << 7] : make_double2(1.0, 0.0);
-    if (tid < 128) twl[tid] = tid < M ? W[tid] : make_double2(1.0, 0.0);
-    if (tid < DCT_RCS) rcs[tid] = W[M + tid];
-    const Tw T{twh, twl};
     const bool hasB = rB < rows;
     const double *sa = src + (long)rA * n, *sb = src + (long)rB * n;
-    for (int j = tid; j < n; j += DCT_T) put_even(z, n, M, j, sa[j], hasB ? sb[j] : 0.0);
+    for (int j = tid; j < n; j += NT) put_even(z, n, M, j, sa[j], hasB ? sb[j] : 0.0);
     __syncthreads();
-    fft_lds<BIG>(z, M, rd, T, rcs);
+    fft_lds<BIG>(z, M, rd, W);
     if constexpr (SOLVE) {
-        constexpr int PER = (4096 + DCT_T) / DCT_T;
+        constexpr int PER = (4096 + NT) / NT;
         double2 q[PER];
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
-            const int k = tid + t * DCT_T;
+            const int k = tid + t * NT;
             if (k < n) {
                 const double2 Z = z[k];
                 // row0: global frequency of local row 0 (slab-decomposed solves)
@@ -386,17 +454,35 @@ __global__ void __launch_bounds__(DCT_T) k_dct1(const double *__restrict__ src,
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
-            const int k = tid + t * DCT_T;
+            const int k = tid + t * NT;
             if (k < n) put_even(z, n, M, k, q[t].x, q[t].y);
         }
         __syncthreads();
-        fft_lds<BIG>(z, M, rd, T, rcs);
+        fft_lds<BIG>(z, M, rd, W);
     }
     double *da = dst + (long)rA * n, *db = dst + (long)rB * n;
-    for (int k = tid; k < n; k += DCT_T) {
+    for (int k = tid; k < n; k += NT) {
         const double2 Z = z[k];
         da[k] = Z.x * scale;
         if (hasB) db[k] = Z.y * scale;
+    }
+    if (rs) {
+        // the sums k_rowsum would take of the two rows written: 256 strided partials per
+        // row, then the halving tree (ops.hip)
+        if (tid < 512) {
+            const int t = tid & 255;
+            double acc = 0.0;
+            if (tid < 256) for (int k = t; k < n; k += 256) acc += z[k].x * scale;
+            else for (int k = t; k < n; k += 256) acc += z[k].y * scale;
+            red[tid] = acc;
+        }
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (tid < 512 && (tid & 255) < w) red[tid] = red[tid] + red[tid + w];
+            __syncthreads();
+        }
+        if (tid == 0) rs[rA] = red[0];
+        if (tid == 256 && hasB) rs[rB] = red[256];
     }
 }
 
@@ -418,9 +504,10 @@ __global__ void __launch_bounds__(256) k_transpose(const double *__restrict__ in
 
 static Radices radices(const int *rad, int np) {
     Radices rd{};
-    int Ns = 1;
+    int Ns = 1, off = 0;
     for (int k = 0; k < np; ++k) {
-        rd.p[k] = Pass{rad[k], Ns, (float)(1.0 / Ns), rc_offset(rad[k])};
+        rd.p[k] = Pass{rad[k], Ns, (float)(1.0 / Ns), off};
+        off += (rad[k] - 1) * Ns;
         Ns *= rad[k];
     }
     rd.n = np;
@@ -430,10 +517,11 @@ static Radices radices(const int *rad, int np) {
 // One LDS DCT-I pass over nrows rows of length n (axis 0: n = nx, axis 1: n = ny).  SOLVE
 // (axis 1 only): forward, / eig, inverse, with rows = x-frequencies row0 .. row0 + nrows.
 int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
-             int row0, double scale) {
+             int row0, double scale, double *rs) {
     DctPlan *P = ctx->dct;
     RMT_CHECK(P && P->lds, RMT_ENOTSUP, "dct_pass: no LDS DCT plan for this grid");
     RMT_CHECK(!solve || axis == 1, RMT_EINVAL, "dct_pass: the solve pass runs along y");
+    RMT_CHECK(!rs || (!solve && nrows <= ctx->rsum_len), RMT_EINVAL, "dct_pass: row sums");
     static bool attr = false;
     if (!attr) {
         const void *fs[4] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
@@ -444,6 +532,7 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
         attr = true;
     }
     if (nrows <= 0) return RMT_OK;
+    const int NT = P->big ? FftT<1>::T : FftT<0>::T;
     const int n = axis == 0 ? P->nx : P->ny;
     const Radices rd = axis == 0 ? radices(P->radx, P->npx) : radices(P->rady, P->npy);
     const double2 *W = axis == 0 ? P->Wx : P->Wy;
@@ -451,11 +540,11 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     const unsigned g = (nrows + 1) / 2;
     hipStream_t st = ctx->stream;
     if (solve) {
-        if (P->big) k_dct1<true, 1><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0);
-        else k_dct1<true, 0><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0);
+        if (P->big) k_dct1<true, 1><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
+        else k_dct1<true, 0><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
     } else {
-        if (P->big) k_dct1<false, 1><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0);
-        else k_dct1<false, 0><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0);
+        if (P->big) k_dct1<false, 1><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
+        else k_dct1<false, 0><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
     }
     RMT_LAUNCHED();
     return RMT_OK;
@@ -467,7 +556,7 @@ void transpose(hipStream_t st, const double *in, int R, int C, double *out) {
     k_transpose<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out);
 }
 
-static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p) {
+static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p, double *rs) {
     const int ny = P->ny, nx = P->nx;
     hipStream_t st = ctx->stream;
     // forward along x: p <- DCT_x(rhs) (p doubles as scratch), then T <- p^T (nx x ny)
@@ -476,20 +565,21 @@ static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p)
     // columns: DCT_y, / eig, inverse DCT_y (scaled), in place on T
     RMT_TRY(dct_pass(ctx, true, 1, P->T, P->T, nx, 0, 1.0 / (2.0 * (ny - 1))));
     transpose(st, P->T, nx, ny, p);
-    // inverse along x, in place
-    RMT_TRY(dct_pass(ctx, false, 0, p, p, ny, 0, 1.0 / (2.0 * (nx - 1))));
+    // inverse along x, in place (+ the row sums of the result)
+    RMT_TRY(dct_pass(ctx, false, 0, p, p, ny, 0, 1.0 / (2.0 * (nx - 1)), rs));
     RMT_LAUNCHED();
     return RMT_OK;
 }
 
 int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
-              const double *dev_mean_sub) {
-    (void)dev_mean_sub;
+              double *dev_root) {
     RMT_TRY(dct_plan(ctx, dx, dy));
     DctPlan *P = ctx->dct;
     const int ny = P->ny, nx = P->nx;
     if (P->lds) {
-        RMT_TRY(dct_lds_solve(ctx, P, rhs, p));
+        const bool fuse = dev_root && ny <= ctx->rsum_len;
+        RMT_TRY(dct_lds_solve(ctx, P, rhs, p, fuse ? ctx->rsum : nullptr));
+        if (fuse) return rowtree_sums(ctx, ny, dev_root);
     } else {
         rocfft_plan px = P->px, py = P->py ? P->py : P->px;
         // forward: along x (rows of rhs) -> T[ki][j]; along y -> p[kj][ki] / eig
@@ -500,6 +590,7 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
         RMT_TRY(round_rows(ctx, P, py, P->T, nx, ny, 1.0 / (2.0 * (ny - 1)), nullptr, nullptr, p));
     }
     RMT_TRY(sub_mean_rows(ctx, p, ny, nx));
+    if (dev_root) RMT_HIP(hipMemsetAsync(dev_root, 0, sizeof(double), ctx->stream));
     return RMT_OK;
 }
 
@@ -518,21 +609,17 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
 __device__ __forceinline__ int mk_src(int m, int n) { return m < n / 2 ? 2 * m : 2 * (n - 1 - m) + 1; }
 
 template <int MODE, int BIG>
-__global__ void __launch_bounds__(DCT_T) k_dct2(const double *__restrict__ src,
-                                                double *__restrict__ dst, int rows, int n,
-                                                const double2 *__restrict__ W,
-                                                const double2 *__restrict__ Wq, Radices rd,
-                                                const double *__restrict__ lamr,
-                                                const double *__restrict__ lamk, int row0,
-                                                double scale) {
+__global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict__ src,
+                                                       double *__restrict__ dst, int rows, int n,
+                                                       const double2 *__restrict__ W,
+                                                       const double2 *__restrict__ Wq, Radices rd,
+                                                       const double *__restrict__ lamr,
+                                                       const double *__restrict__ lamk, int row0,
+                                                       double scale) {
+    constexpr int DCT_T = FftT<BIG>::T;
     extern __shared__ double2 z[];
-    __shared__ double2 twh[DCT_MAXM / 128], twl[128], rcs[DCT_RCS];
     constexpr int PER = DCT_MAXM / DCT_T;
     const int rA = 2 * blockIdx.x, rB = rA + 1, tid = threadIdx.x;
-    if (tid < DCT_MAXM / 128) twh[tid] = (tid << 7) < n ? W[tid << 7] : make_double2(1.0, 0.0);
-    if (tid < 128) twl[tid] = tid < n ? W[tid] : make_double2(1.0, 0.0);
-    if (tid < DCT_RCS) rcs[tid] = W[n + tid];
-    const Tw T{twh, twl};
     const bool hasB = rB < rows;
     const double *sa = src + (long)rA * n, *sb = src + (long)rB * n;
     double *da = dst + (long)rA * n, *db = dst + (long)rB * n;
@@ -542,7 +629,7 @@ __global__ void __launch_bounds__(DCT_T) k_dct2(const double *__restrict__ src,
             z[m] = make_double2(sa[q], hasB ? sb[q] : 0.0);
         }
         __syncthreads();
-        fft_lds<BIG>(z, n, rd, T, rcs);
+        fft_lds<BIG>(z, n, rd, W);
         double2 y[PER];
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
@@ -598,7 +685,7 @@ __global__ void __launch_bounds__(DCT_T) k_dct2(const double *__restrict__ src,
         }
     }
     __syncthreads();
-    fft_lds<BIG>(z, n, rd, T, rcs);
+    fft_lds<BIG>(z, n, rd, W);
     const double s = scale / n;
     for (int m = tid; m < n; m += DCT_T) {
         const double2 R = z[m];
@@ -654,11 +741,10 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
         set_error("DCT-II solve: N must be even, <= 8192, and factor into radices <= 23");
         return RMT_ENOTSUP;
     }
-    for (int k = 0; k < P->npx; ++k) P->big |= P->radx[k] > 13;
-    for (int k = 0; k < P->npy; ++k) P->big |= P->rady[k] > 13;
+    P->big = big_radix(P->radx, P->npx) || big_radix(P->rady, P->npy);
     ctx->dct2 = P;
-    RMT_TRY(twiddles(nx, &P->Wx));
-    RMT_TRY(twiddles(ny, &P->Wy));
+    RMT_TRY(twiddles(nx, P->radx, P->npx, &P->Wx));
+    RMT_TRY(twiddles(ny, P->rady, P->npy, &P->Wy));
     RMT_TRY(quarter_twiddles(nx, &P->Qx));
     RMT_TRY(quarter_twiddles(ny, &P->Qy));
     std::vector<double> lx, ly;
@@ -692,7 +778,7 @@ int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst,
     const size_t lds = (size_t)n * sizeof(double2);
     const unsigned g = (nrows + 1) / 2;
     hipStream_t st = ctx->stream;
-#define DCT2_L(M, B) k_dct2<M, B><<<g, DCT_T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0)
+#define DCT2_L(M, B) k_dct2<M, B><<<g, FftT<B>::T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0)
     if (P->big) {
         if (mode == 0) DCT2_L(0, 1); else if (mode == 1) DCT2_L(1, 1); else DCT2_L(2, 1);
     } else {

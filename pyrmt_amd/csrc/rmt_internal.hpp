@@ -377,21 +377,23 @@ __device__ __forceinline__ double weno5_diff(const double *f, long s, int k, int
 // velocity component at (j, i) is either a constant or the raw (pre-BC) value of one
 // source cell.  Callers read the raw value themselves (no device lambdas).
 // functions.py:1073-1089 (_compute_pressure_gradient) at one cell
+// of p - m (m: a mean not yet subtracted from p; x - 0.0 == x, so m = 0 is the plain field)
 __device__ __forceinline__ void pgrad_cell(const double *__restrict__ p, long c, int j, int i,
                                            int ny, int nx, double dx, double dy, double &gx,
-                                           double &gy) {
+                                           double &gy, double m = 0.0) {
     const double *row = p + (c - i), *col = p + i;
     gx = 0.0; gy = 0.0;
     if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1) {
-        gx = (p[c + 1] - p[c - 1]) / (2 * dx);
-        gy = (p[c + nx] - p[c - nx]) / (2 * dy);
+        gx = ((p[c + 1] - m) - (p[c - 1] - m)) / (2 * dx);
+        gy = ((p[c + nx] - m) - (p[c - nx] - m)) / (2 * dy);
     }
-    if (i == 0) gx = (-3.0 * row[0] + 4.0 * row[1] - row[2]) / (2.0 * dx);
-    if (i == nx - 1) gx = (3.0 * row[nx - 1] - 4.0 * row[nx - 2] + row[nx - 3]) / (2.0 * dx);
-    if (j == 0) gy = (-3.0 * col[0] + 4.0 * col[nx] - col[2L * nx]) / (2.0 * dy);
+    if (i == 0) gx = (-3.0 * (row[0] - m) + 4.0 * (row[1] - m) - (row[2] - m)) / (2.0 * dx);
+    if (i == nx - 1)
+        gx = (3.0 * (row[nx - 1] - m) - 4.0 * (row[nx - 2] - m) + (row[nx - 3] - m)) / (2.0 * dx);
+    if (j == 0) gy = (-3.0 * (col[0] - m) + 4.0 * (col[nx] - m) - (col[2L * nx] - m)) / (2.0 * dy);
     if (j == ny - 1)
-        gy = (3.0 * col[(long)(ny - 1) * nx] - 4.0 * col[(long)(ny - 2) * nx] +
-              col[(long)(ny - 3) * nx]) / (2.0 * dy);
+        gy = (3.0 * (col[(long)(ny - 1) * nx] - m) - 4.0 * (col[(long)(ny - 2) * nx] - m) +
+              (col[(long)(ny - 3) * nx] - m)) / (2.0 * dy);
 }
 struct BCSrc {
     bool u_const, v_const;
@@ -432,7 +434,15 @@ int read_scalar(rmt_ctx *ctx, const double *dev, double *host);
 // row-tree sums (ops.hip): root of rows [0, nrows) of x (row length nx) into *dev_root;
 // x -= tree(G roots) / count; and both for a whole (ny, nx) plane
 int rowtree_root(rmt_ctx *ctx, const double *x, int nrows, int nx, double *dev_root);
+// the tree over row sums already in ctx->rsum (dct_pass's rs)
+int rowtree_sums(rmt_ctx *ctx, int nrows, double *dev_root);
 int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int G, double count);
+// functions.py:1255-1364 (constant density, Neumann DCT-I) for the fused step: dt read from
+// the device (dtp), and the max of u^2 + v^2 over the corrected velocity per 256-cell block
+// into m2part (the next step's compute_timestep input), ceil(nx / 256) * ny entries
+int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
+                   double dy, const double *dtp, double rho, int bc_kind, double lid,
+                   const double *p_prev, double *a, double *b, double *p, double *m2part);
 int sub_mean_rows(rmt_ctx *ctx, double *x, int ny, int nx);
 
 // Row window of a slab-decomposed call (slab.hip): planes are addressed with GLOBAL cell
@@ -470,11 +480,13 @@ struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + 
     double *k3u, *k3v, *acc2u, *acc2v;
     unsigned char *solid;
     int *any_solid;
+    const double *dtp;           // device dt (the fused step's k_dt output), or null: P->dt
 };
 inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
     return MomWork{w,          w + n,      w + 2 * n,  w + 3 * n,  w + 4 * n,  w + 5 * n,
                    w + 6 * n,  w + 7 * n,  w + 8 * n,  w + 9 * n,  w + 10 * n, w + 11 * n,
-                   w + 12 * n, w + 13 * n, w + 14 * n, w + 15 * n, w + 16 * n, solid, flag};
+                   w + 12 * n, w + 13 * n, w + 14 * n, w + 15 * n, w + 16 * n, solid, flag,
+                   nullptr};
 }
 int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                  const double *p, const double *X1, const double *X2, const double *phi,
@@ -489,12 +501,16 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
                    const MomWork &W, const int *tiles, const int *count, int max_tiles);
 
 // ---------------------------------------------------------------------- poisson --
+// dev_root: nullptr -> p = solve - mean (functions.py:1119); else p = the raw solve and
+// *dev_root = its row-tree sum (mean = *dev_root / (ny nx), the caller subtracts it as it
+// reads p), or 0 when the mean was subtracted already (rocFFT path)
 int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
-              const double *dev_mean_sub = nullptr);
+              double *dev_root = nullptr);
 int dct_plan(rmt_ctx *ctx, double dx, double dy);
 bool dct_lds_ready(rmt_ctx *ctx);
+// rs (nullable): per-row sums of the output, in k_rowsum's order (rowtree_sums finishes them)
 int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
-             int row0, double scale);
+             int row0, double scale, double *rs = nullptr);
 void transpose(hipStream_t st, const double *in, int R, int C, double *out);
 // MAC grid (mac.py:104-123): DCT-II Neumann solve on a (ny, nx) cell grid, (0,0) -> 0
 int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);

@@ -16,6 +16,8 @@ namespace rmt {
 
 
 constexpr int DIAG_VALS = 10, DIAG_BLOCKS = 512, DIAG_T = 256;
+// ring record: [0, DIAG_VALS) the diagnostics, then max |u|^2, dt, the 4 step flags
+constexpr int RING_N = 64, RING_VALS = DIAG_VALS + 6;
 
 }  // namespace rmt
 
@@ -40,6 +42,11 @@ struct rmt_sim {
     hipStream_t st2 = nullptr;
     hipEvent_t e_sl = nullptr, e_mom = nullptr;
     int *tiles = nullptr, *tcount = nullptr, max_tiles = 0;
+    // device-resident dt and diagnostics (rmt_sim_step's asynchronous path): per-block
+    // max |u|^2 partials from the projection, and a ring of per-step records read back once
+    // per RING_N steps
+    double *m2part = nullptr, *ring = nullptr;
+    int m2n = 0;
     bool prof = false;
     hipEvent_t pev[7] = {};
     double ms[8] = {};
@@ -52,10 +59,12 @@ namespace rmt {
 __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict__ X2,
                          const double *__restrict__ a, const double *__restrict__ b,
                          const double *__restrict__ xs, const double *__restrict__ ys, int ny,
-                         int nx, double dt, double dx, double dy, int shape, double x0, double y0,
-                         double R, double *__restrict__ X1n, double *__restrict__ X2n,
+                         int nx, double dt_arg, double dx, double dy, int shape, double x0,
+                         double y0, double R, double *__restrict__ X1n, double *__restrict__ X2n,
                          double *__restrict__ phi_pre, int *bad,
-                         unsigned long long *__restrict__ kbits, const double *m2) {
+                         unsigned long long *__restrict__ kbits, const double *m2,
+                         const double *__restrict__ dtp = nullptr) {
+    const double dt = dtp ? *dtp : dt_arg;
     // grid (ceil(nx / 256), ny): a wave covers 64 cells of one row, so the extrapolation's
     // known plane (phi_pre < 0, 64-cell words) comes out of the same pass (kbits optional)
     const int j = blockIdx.y, i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
@@ -175,6 +184,41 @@ __global__ void __launch_bounds__(256) k_phi_tiles(const double *__restrict__ X1
 // dt on device-ready scalars: returned to the host (one sync per step).
 __global__ void k_dt(const double *m2, double dt_const, double cfl, double dx, double *out) {
     *out = fmin(dt_const, cfl * dx / (sqrt(*m2) + 1e-6));
+}
+// the same dt with max |u|^2 folded from the projection's per-block partials (NaN-propagating
+// max, exact in any order): sc[0] = max |u|^2, sc[1] = dt; both stay on the device
+__global__ void __launch_bounds__(1024) k_dt_part(const double *__restrict__ part, int np,
+                                                  double dt_const, double cfl, double dx,
+                                                  double *__restrict__ sc) {
+    __shared__ double s[1024];
+    double acc = -INFINITY;
+    for (int k = threadIdx.x; k < np; k += 1024) {
+        const double y = part[k];
+        if (y > acc || y != y) acc = y;
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            const double y = s[threadIdx.x + w];
+            if (y > s[threadIdx.x] || y != y) s[threadIdx.x] = y;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double m2 = s[0];
+        sc[0] = m2;
+        sc[1] = fmin(dt_const, cfl * dx / (sqrt(m2) + 1e-6));
+    }
+}
+// completes a ring record after k_diag_p2 wrote its diagnostics: max |u|^2, dt, flags
+__global__ void k_ring_put(const double *__restrict__ sc, const int *__restrict__ flag,
+                           double *__restrict__ e) {
+    if (threadIdx.x == 0) {
+        e[DIAG_VALS] = sc[0];
+        e[DIAG_VALS + 1] = sc[1];
+        for (int k = 0; k < 4; ++k) e[DIAG_VALS + 2 + k] = flag ? (double)flag[k] : 0.0;
+    }
 }
 
 struct DiagArgs {
@@ -356,6 +400,9 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
         RMT_HIP(hipMalloc(&S->tiles, (S->max_tiles + 64) * sizeof(int)));
         S->tcount = S->tiles + S->max_tiles;
     }
+    S->m2n = ((nx + 255) / 256) * ny;
+    RMT_HIP(hipMalloc(&S->m2part, ((size_t)S->m2n + (size_t)RING_N * RING_VALS) * sizeof(double)));
+    S->ring = S->m2part + S->m2n;
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
     return RMT_OK;
@@ -364,6 +411,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
 int rmt_sim_destroy(rmt_sim *S) {
     if (!S) return RMT_OK;
     hipFree(S->block);
+    if (S->m2part) hipFree(S->m2part);
     if (S->tiles) hipFree(S->tiles);
     if (S->e_sl) hipEventDestroy(S->e_sl);
     if (S->e_mom) hipEventDestroy(S->e_mom);
@@ -382,6 +430,30 @@ int rmt_sim_field(rmt_sim *S, int field, double **ptr) {
     return RMT_OK;
 }
 
+// One step's host bookkeeping from its diagnostics record: error flags, t, the diag entry.
+static int sim_record(rmt_sim *S, const double *dv, double m2, double dt, const int *fl) {
+    const rmt_sim_params &P = S->P;
+    RMT_CHECK(!fl[0], RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
+                                      "simulation diverged)");
+    RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
+    S->t += dt;
+    rmt_diag r{};
+    r.t = S->t; r.dt = dt;
+    r.cx = dv[2] > 0 ? dv[0] / dv[2] : NAN;
+    r.cy = dv[2] > 0 ? dv[1] / dv[2] : NAN;
+    r.minJ = dv[3]; r.maxJ = dv[4]; r.umax = std::sqrt(m2);
+    if (P.energies) {
+        r.ke = dv[5] * P.dx * P.dy;
+        r.se = dv[6] * P.dx * P.dy;
+        r.diss = dv[7] * P.dx * P.dy;
+        S->integ += r.diss * dt;
+        r.integ = S->integ;
+        r.ry = dv[2] > 0 ? 0.5 * (dv[9] - dv[8]) : NAN;
+    }
+    S->diag.push_back(r);
+    return RMT_OK;
+}
+
 int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     RMT_CHECK(S, RMT_EINVAL, "null sim");
     rmt_ctx *ctx = S->ctx;
@@ -391,18 +463,51 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     const unsigned g = grid1d(n, 256);
     hipStream_t st = ctx->stream;
     double *sc = S->dscr + DIAG_BLOCKS * DIAG_VALS;   // [0] maxsq, [1] dt, [2..11] diag
+    // Asynchronous path (no t_end: nothing to clip): dt is computed and consumed on the
+    // device, max |u|^2 comes out of the projection, and the per-step diagnostics go to a
+    // device ring read back every RING_N steps -- no host round trip inside the loop.  The
+    // synchronous path (t_end clip, profiling, the Eulerian schemes) reads dt back each step.
+    static const bool force_sync = getenv("RMT_SIM_SYNC") && atoi(getenv("RMT_SIM_SYNC"));
+    const bool async = !force_sync && !S->prof && std::isinf(t_end) && t_end > 0 &&
+                       P.scheme == RMT_SCHEME_SEMILAGRANGIAN;
+    int slot = 0;
+    auto flush = [&]() -> int {
+        if (!slot) return RMT_OK;
+        std::vector<double> h((size_t)slot * RING_VALS);
+        RMT_HIP(hipMemcpyAsync(h.data(), S->ring, h.size() * sizeof(double),
+                               hipMemcpyDeviceToHost, st));
+        RMT_HIP(hipStreamSynchronize(st));
+        const int cnt = slot;
+        slot = 0;
+        for (int k = 0; k < cnt; ++k) {
+            const double *e = h.data() + (size_t)k * RING_VALS;
+            int fl[4];
+            for (int q = 0; q < 4; ++q) fl[q] = (int)e[DIAG_VALS + 2 + q];
+            RMT_TRY(sim_record(S, e, e[DIAG_VALS], e[DIAG_VALS + 1], fl));
+        }
+        return RMT_OK;
+    };
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end)) break;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[0], st));
         // 1. dt (compute_timestep + the drivers' clip to t_end); NaN-propagating max so it
         // also bounds the velocities for the SL block skip
-        RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, n, sc));
-        k_dt<<<1, 1, 0, st>>>(sc, S->dt_const, P.cfl, P.dx, sc + 1);
-        double hv[2];
-        RMT_HIP(hipMemcpyAsync(hv, sc, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
-        RMT_HIP(hipStreamSynchronize(st));
-        double dt = hv[1];
-        if (S->t + dt > t_end) dt = t_end - S->t;
+        double hv[2] = {0.0, 0.0}, dt = NAN;
+        if (async && it > 0) {
+            k_dt_part<<<1, 1024, 0, st>>>(S->m2part, S->m2n, S->dt_const, P.cfl, P.dx, sc);
+            RMT_LAUNCHED();
+        } else {
+            RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, n, sc));
+            k_dt<<<1, 1, 0, st>>>(sc, S->dt_const, P.cfl, P.dx, sc + 1);
+            RMT_LAUNCHED();
+        }
+        if (!async) {
+            RMT_HIP(hipMemcpyAsync(hv, sc, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+            RMT_HIP(hipStreamSynchronize(st));
+            dt = hv[1];
+            if (S->t + dt > t_end) dt = t_end - S->t;
+        }
+        const double *dtp = async ? sc + 1 : nullptr;
         const bool solid = P.shape != RMT_SHAPE_NONE;
         rmt_momentum_params M{};
         M.bc_kind = P.bc_kind; M.lid = P.lid; M.mu_s = P.mu_s; M.kappa = P.kappa;
@@ -410,6 +515,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         M.dx = P.dx; M.dy = P.dy; M.dt = dt; M.stress_band = P.stress_band;
         M.detg_clamp = P.detg_clamp;
         MomWork W = mom_work(S->mw, n, S->mbytes, S->flag + 1);
+        W.dtp = dtp;
         // the extrapolation chain occupies one CU for milliseconds; everything it does not
         // feed runs beside it: the momentum of every cell, from the pre-extrapolation map, on
         // a second stream, re-run afterwards on the tiles within reach of a target
@@ -422,7 +528,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
                 k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, st>>>(
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
-                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits, sc);
+                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits, sc, dtp);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN_CUBIC) {
                 k_sim_sl_cubic<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx,
                                                   dt, P.dx, P.dy, P.x0, P.y0, P.R, S->X1n,
@@ -497,14 +603,26 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         }
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[4], st));
         // 6. projection (constant density rho_f; Neumann DCT-I)
-        RMT_TRY(rmt_pressure_projection(ctx, S->us, S->vs, P.dx, P.dy, dt, P.rho_f, P.bc_kind,
-                                        P.lid, S->p, S->u, S->v, S->p));
+        if (async)
+            RMT_TRY(projection_dev(ctx, S->us, S->vs, P.dx, P.dy, dtp, P.rho_f, P.bc_kind, P.lid,
+                                   S->p, S->u, S->v, S->p, S->m2part));
+        else
+            RMT_TRY(rmt_pressure_projection(ctx, S->us, S->vs, P.dx, P.dy, dt, P.rho_f,
+                                            P.bc_kind, P.lid, S->p, S->u, S->v, S->p));
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[5], st));
         // 7. diagnostics (running them beside the projection on the second stream measured
         // no gain: both are HBM-bound)
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
                    P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa, 0, ny};
         k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, S->dscr);
+        if (async) {
+            double *e = S->ring + (size_t)slot * RING_VALS;
+            k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, e);
+            k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
+            RMT_LAUNCHED();
+            if (++slot == RING_N) RMT_TRY(flush());
+            continue;
+        }
         k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, sc + 2);
         RMT_LAUNCHED();
         double dv[DIAG_VALS];
@@ -513,9 +631,6 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (solid) RMT_HIP(hipMemcpyAsync(fl, S->flag, sizeof(fl), hipMemcpyDeviceToHost, st));
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[6], st));
         RMT_HIP(hipStreamSynchronize(st));
-        RMT_CHECK(!fl[0], RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
-                                          "simulation diverged)");
-        RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
         if (S->prof) {
             float f;
             for (int k = 0; k < 6; ++k) {
@@ -529,23 +644,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 S->ms[7] += f; S->calls[7] += 1;
             }
         }
-        S->t += dt;
-        rmt_diag r{};
-        r.t = S->t; r.dt = dt;
-        r.cx = dv[2] > 0 ? dv[0] / dv[2] : NAN;
-        r.cy = dv[2] > 0 ? dv[1] / dv[2] : NAN;
-        r.minJ = dv[3]; r.maxJ = dv[4]; r.umax = std::sqrt(hv[0]);
-        if (P.energies) {
-            r.ke = dv[5] * P.dx * P.dy;
-            r.se = dv[6] * P.dx * P.dy;
-            r.diss = dv[7] * P.dx * P.dy;
-            S->integ += r.diss * dt;
-            r.integ = S->integ;
-            r.ry = dv[2] > 0 ? 0.5 * (dv[9] - dv[8]) : NAN;
-        }
-        S->diag.push_back(r);
+        RMT_TRY(sim_record(S, dv, hv[0], dt, fl));
     }
-    return RMT_OK;
+    return flush();
 }
 
 int rmt_sim_set_profiling(rmt_sim *S, int on) {

@@ -548,8 +548,13 @@ int rmt_slab_project_unrows(rmt_slab *S) {
     double *pc = S->gv(S->pc) + (long)S->r0 * S->NX;
     k_cols<false><<<grid1d(no, 256), 256, 0, ctx->stream>>>(S->Y, rows, S->NX, S->cs, S->G, S->A);
     RMT_LAUNCHED();
-    RMT_TRY(dct_pass(ctx, false, 0, S->Y, pc, rows, 0, 1.0 / (2.0 * (S->NX - 1))));
-    return rowtree_root(ctx, pc, rows, S->NX, S->scal + SC_ROOT);
+    if (rows > ctx->rsum_len) {
+        RMT_TRY(dct_pass(ctx, false, 0, S->Y, pc, rows, 0, 1.0 / (2.0 * (S->NX - 1))));
+        return rowtree_root(ctx, pc, rows, S->NX, S->scal + SC_ROOT);
+    }
+    // the row sums come out of the inverse pass itself (k_rowsum's order)
+    RMT_TRY(dct_pass(ctx, false, 0, S->Y, pc, rows, 0, 1.0 / (2.0 * (S->NX - 1)), ctx->rsum));
+    return rowtree_sums(ctx, rows, S->scal + SC_ROOT);
 }
 
 int rmt_slab_sub_mean(rmt_slab *S, int which, const double *roots) {
