@@ -15,6 +15,7 @@
 // HBM traffic: 10 planes per solve.  Other sizes: rocFFT R2C rounds (the previous path).
 #include "rmt_internal.hpp"
 #include "dft_consts.hpp"
+#include <algorithm>
 #include <vector>
 
 namespace rmt {
@@ -82,6 +83,7 @@ static void host_lambda(int n, double h, std::vector<double> &lam) {
 }
 
 constexpr int DCT_MAXM = 8192;    // complex LDS entries (128 KB)
+constexpr int K1_MAXN = DCT_MAXM / 2;   // k_dct1's complex FFT length (n <= 4097)
 
 // Radix plan of a length-M FFT: prime factors (2 .. 23), then 2s grouped into 8 / 4, 3s into
 // 9, a leftover 2 with a 5 (10) or a 3 (6): M = 8190 = 2 3^2 5 7 13 runs as 9, 10, 7, 13 --
@@ -101,6 +103,8 @@ static bool factor(int M, int *rad, int *np) {
     if (cnt[2] && cnt[3]) { put(6); --cnt[2]; --cnt[3]; }
     for (int q : {2, 3, 5, 7, 11, 13, 17, 19, 23})
         while (cnt[q]) { put(q); --cnt[q]; }
+    // ascending: the largest radix runs last, where Ns (the base-twiddle count) is M / R
+    std::sort(rad, rad + n);
     *np = n;
     return n < 16;
 }
@@ -110,35 +114,42 @@ static bool big_radix(const int *rad, int np) {
     return false;
 }
 
-// Per-pass twiddle table of the Stockham passes, in pass order: pass (R, Ns) holds
-// e^{-2 pi i k r / (Ns R)} at [(r - 1) Ns + k], r = 1 .. R-1, k < Ns (M - 1 entries in all);
-// angles from long double, exact where k r / (Ns R) is a multiple of 1/4
-static int twiddles(int M, const int *rad, int np, double2 **W) {
+// Twiddles of the Stockham passes, in pass order: pass (R, Ns) holds e^{-2 pi i k r / (Ns R)}
+// at [(r - 1) Ns + k], r = 1 .. R-1, k < Ns (M - 1 entries in all, L2-resident: every
+// workgroup reads the same table), from long double, exact where k r / (Ns R) is a multiple
+// of 1/4.  post: then k_dct1's packed-real split factors e^{-2 pi i k / (2M)}, k = 0 .. M.
+static double2 unit_root(long t, long L) {
     const long double PI = 3.141592653589793238462643383279502884L;
+    t %= L;
+    if ((4 * t) % L == 0) {
+        const int e = (int)(4 * t / L);
+        const double c[4] = {1.0, 0.0, -1.0, 0.0}, sn[4] = {0.0, 1.0, 0.0, -1.0};
+        return make_double2(c[e], -sn[e]);
+    }
+    const long double a = 2.0L * PI * t / L;
+    return make_double2((double)cosl(a), (double)-sinl(a));
+}
+static int twiddles(int M, const int *rad, int np, double2 **W, bool post = false) {
     std::vector<double2> h;
-    h.reserve(M);
+    h.reserve(2 * (size_t)M + 2);
     int Ns = 1;
     for (int q = 0; q < np; ++q) {
         const int R = rad[q], L = Ns * R;
         for (int r = 1; r < R; ++r)
-            for (int k = 0; k < Ns; ++k) {
-                const long t = (long)k * r % L;
-                if ((4 * t) % L == 0) {
-                    const int e = (int)(4 * t / L);
-                    const double c[4] = {1.0, 0.0, -1.0, 0.0}, sn[4] = {0.0, 1.0, 0.0, -1.0};
-                    h.push_back(make_double2(c[e], -sn[e]));
-                } else {
-                    const long double a = 2.0L * PI * t / L;
-                    h.push_back(make_double2((double)cosl(a), (double)-sinl(a)));
-                }
-            }
+            for (int k = 0; k < Ns; ++k) h.push_back(unit_root((long)k * r, L));
         Ns = L;
     }
+    if (post)
+        for (long k = 0; k <= M; ++k) h.push_back(unit_root(k, 2L * M));
     h.push_back(make_double2(1.0, 0.0));
     RMT_HIP(hipMalloc(W, h.size() * sizeof(double2)));
     RMT_HIP(hipMemcpy(*W, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice));
     return RMT_OK;
 }
+
+// LDS budget of one FFT workgroup: the length-M sequence + 4 KB static
+constexpr size_t FFT_LDS_MAX = 160 * 1024 - 4096;
+static bool lds_fits(int M) { return (size_t)M * sizeof(double2) <= FFT_LDS_MAX; }
 
 int dct_plan(rmt_ctx *ctx, double dx, double dy) {
     DctPlan *P = ctx->dct;
@@ -146,16 +157,19 @@ int dct_plan(rmt_ctx *ctx, double dx, double dy) {
     if (!P) {
         P = ctx->dct = new DctPlan;
         P->ny = ctx->ny; P->nx = ctx->nx;
-        const int Mx = 2 * (P->nx - 1), My = 2 * (P->ny - 1);
+        // k_dct1's complex FFT length: N = n - 1 (half the even extension)
+        const int Nx = P->nx - 1, Ny = P->ny - 1;
         static const bool force_rocfft = getenv("RMT_DCT_ROCFFT") && atoi(getenv("RMT_DCT_ROCFFT"));
-        P->lds = !force_rocfft && factor(Mx, P->radx, &P->npx) && factor(My, P->rady, &P->npy);
+        P->lds = !force_rocfft && Nx >= 2 && Ny >= 2 && Nx < K1_MAXN && Ny < K1_MAXN &&
+                 factor(Nx, P->radx, &P->npx) && factor(Ny, P->rady, &P->npy) &&
+                 lds_fits(Nx) && lds_fits(Ny);
         P->big = big_radix(P->radx, P->npx) || big_radix(P->rady, P->npy);
     }
     if (!P->lds && !g_rocfft_ready) { RMT_TRY(rf(rocfft_setup(), "setup")); g_rocfft_ready = true; }
     if (P->lds && !P->Wx) {
         const size_t n = (size_t)P->ny * P->nx;
-        RMT_TRY(twiddles(2 * (P->nx - 1), P->radx, P->npx, &P->Wx));
-        RMT_TRY(twiddles(2 * (P->ny - 1), P->rady, P->npy, &P->Wy));
+        RMT_TRY(twiddles(P->nx - 1, P->radx, P->npx, &P->Wx, true));
+        RMT_TRY(twiddles(P->ny - 1, P->rady, P->npy, &P->Wy, true));
         RMT_HIP(hipMalloc(&P->T, n * sizeof(double)));
         RMT_HIP(hipMalloc(&P->lamx, P->nx * sizeof(double)));
         RMT_HIP(hipMalloc(&P->lamy, P->ny * sizeof(double)));
@@ -342,14 +356,18 @@ __device__ __forceinline__ void dft(double2 *v) {
 struct Pass { int R, Ns; float inv; int tw; };
 struct Radices { Pass p[16]; int n; };
 
-// one Stockham pass of radix R over z[0..M): read every butterfly's inputs and twiddles ->
-// barrier -> twiddle + DFT_R -> write -> barrier
-template <int R, int NT>
+// one Stockham pass of radix R over z[0..M): load every butterfly's twiddles (global table,
+// issued first) and inputs, twiddle them -> barrier -> DFT_R -> write -> barrier
+template <int R, int NT, int MAXN>
 __device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps,
                                          const double2 *__restrict__ tw) {
-    constexpr int BPT = (DCT_MAXM / NT + R - 1) / R;   // butterflies per thread (max)
-    const int nb = M / R, tid = threadIdx.x, Ns = ps.Ns;
-    double2 v[BPT][R], w[BPT][R - 1];
+    constexpr int BPT = (MAXN / R + NT - 1) / NT;      // butterflies per thread (max)
+    const int nb = M / R, Ns = ps.Ns;
+    // opaque per pass: the per-thread addresses below are not hoisted out of a caller's loop
+    // (k_dct1's two transforms), where they would hold registers across every pass
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    double2 v[BPT][R];
     int o[BPT];
 #pragma unroll
     for (int b = 0; b < BPT; ++b) {
@@ -358,13 +376,17 @@ __device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps,
             int g = (int)((float)j * ps.inv), k = j - g * Ns;   // j = g Ns + k
             if (k < 0) { --g; k += Ns; } else if (k >= Ns) { ++g; k -= Ns; }
             o[b] = g * Ns * R + k;
+            double2 w[R - 1];
             if (Ns > 1) {
                 const double2 *t = tw + ps.tw + k;
 #pragma unroll
-                for (int r = 1; r < R; ++r) w[b][r - 1] = t[(r - 1) * Ns];
+                for (int r = 1; r < R; ++r) w[r - 1] = t[(r - 1) * Ns];
             }
 #pragma unroll
             for (int r = 0; r < R; ++r) v[b][r] = z[j + r * nb];
+            if (Ns > 1)
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], w[r - 1]);
         }
     }
     __syncthreads();
@@ -372,9 +394,6 @@ __device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps,
     for (int b = 0; b < BPT; ++b) {
         const int j = tid + b * NT;
         if (j < nb) {
-            if (Ns > 1)
-#pragma unroll
-                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], w[b][r - 1]);
             dft<R>(v[b]);
 #pragma unroll
             for (int r = 0; r < R; ++r) z[o[b] + r * Ns] = v[b][r];
@@ -383,106 +402,151 @@ __device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps,
     __syncthreads();
 }
 
-template <int BIG>
+// the radix passes of rd over z[0..M), M <= MAXN, NT threads
+template <int BIG, int NT, int MAXN>
 __device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__restrict__ tw) {
-    constexpr int NT = FftT<BIG>::T;
     for (int q = 0; q < rd.n; ++q) {
         const Pass &ps = rd.p[q];
         switch (ps.R) {
-            case 2: fft_pass<2, NT>(z, M, ps, tw); break;
-            case 3: fft_pass<3, NT>(z, M, ps, tw); break;
-            case 4: fft_pass<4, NT>(z, M, ps, tw); break;
-            case 5: fft_pass<5, NT>(z, M, ps, tw); break;
-            case 6: fft_pass<6, NT>(z, M, ps, tw); break;
-            case 7: fft_pass<7, NT>(z, M, ps, tw); break;
-            case 8: fft_pass<8, NT>(z, M, ps, tw); break;
-            case 9: fft_pass<9, NT>(z, M, ps, tw); break;
-            case 10: fft_pass<10, NT>(z, M, ps, tw); break;
-            case 11: fft_pass<11, NT>(z, M, ps, tw); break;
-            case 13: fft_pass<13, NT>(z, M, ps, tw); break;
+            case 2: fft_pass<2, NT, MAXN>(z, M, ps, tw); break;
+            case 3: fft_pass<3, NT, MAXN>(z, M, ps, tw); break;
+            case 4: fft_pass<4, NT, MAXN>(z, M, ps, tw); break;
+            case 5: fft_pass<5, NT, MAXN>(z, M, ps, tw); break;
+            case 6: fft_pass<6, NT, MAXN>(z, M, ps, tw); break;
+            case 7: fft_pass<7, NT, MAXN>(z, M, ps, tw); break;
+            case 8: fft_pass<8, NT, MAXN>(z, M, ps, tw); break;
+            case 9: fft_pass<9, NT, MAXN>(z, M, ps, tw); break;
+            case 10: fft_pass<10, NT, MAXN>(z, M, ps, tw); break;
+            case 11: fft_pass<11, NT, MAXN>(z, M, ps, tw); break;
+            case 13: fft_pass<13, NT, MAXN>(z, M, ps, tw); break;
             default:
                 if constexpr (BIG) {
                     switch (ps.R) {
-                        case 17: fft_pass<17, NT>(z, M, ps, tw); break;
-                        case 19: fft_pass<19, NT>(z, M, ps, tw); break;
-                        case 23: fft_pass<23, NT>(z, M, ps, tw); break;
+                        case 17: fft_pass<17, NT, MAXN>(z, M, ps, tw); break;
+                        case 19: fft_pass<19, NT, MAXN>(z, M, ps, tw); break;
+                        case 23: fft_pass<23, NT, MAXN>(z, M, ps, tw); break;
                     }
                 }
         }
     }
 }
 
-// even extension of the row pair (a, b) into z: z[j] = z[M - j] = (a_j, b_j)
-__device__ __forceinline__ void put_even(double2 *z, int n, int M, int j, double a, double b) {
-    z[j] = make_double2(a, b);
-    if (j >= 1 && j <= n - 2) z[M - j] = make_double2(a, b);
+// DCT-I of one real row per workgroup.  The even extension e (length M = 2N, N = n - 1) is
+// real, so its length-M DFT -- the unnormalised DCT-I -- comes from ONE length-N complex FFT
+// of z_m = e_{2m} + i e_{2m+1} (the packed-real FFT): with Z = FFT_N(z), Z_N = Z_0 and
+// W^k = e^{-2 pi i k / M} = c_k - i s_k,
+//   X_k     = (S + c_k T - s_k D) / 2,   X_{N-k} = (S - c_k T + s_k D) / 2,
+//   S = Re Z_k + Re Z_{N-k},  D = Re Z_k - Re Z_{N-k},  T = Im Z_k + Im Z_{N-k}.
+// Read as doubles, z IS e (d[j] = e_j), so packing is the even extension itself.  N complex
+// entries = 64 KB for n = 4096: two workgroups share a CU, one's HBM traffic hiding behind
+// the other's LDS passes.  SOLVE: rows are x-frequencies kx of the transposed plane; forward
+// DCT, / eig (functions.py:1091-1104: lam_x[kx] + lam_y[ky], (0,0) -> 1), inverse DCT.
+// (launch bounds: two workgroups per CU -- 4 waves per SIMD at 512 threads, 128 VGPRs)
+template <int BIG> struct K1T { static constexpr int T = BIG ? 256 : 512; };
+
+template <int NT>
+__device__ __forceinline__ void put_row_even(double *d, int N, const double *__restrict__ x) {
+    for (int j = threadIdx.x; j <= N; j += NT) {
+        const double v = x[j];
+        d[j] = v;
+        if (j >= 1 && j < N) d[2 * N - j] = v;
+    }
 }
 
-// DCT-I along the rows of src (rows x n) -> dst, row pairs per workgroup.  SOLVE: rows are
-// x-frequencies kx (transposed plane), and the column transform is forward DCT, / eig,
-// inverse DCT (the eig of functions.py:1091-1104: lam_x[kx] + lam_y[ky], (0,0) -> 1).
 template <bool SOLVE, int BIG>
-__global__ void __launch_bounds__(FftT<BIG>::T) k_dct1(const double *__restrict__ src,
-                                                       double *__restrict__ dst, int rows, int n,
-                                                       const double2 *__restrict__ W, Radices rd,
-                                                       double scale, const double *__restrict__ lamr,
-                                                       const double *__restrict__ lamk, int row0,
-                                                       double *__restrict__ rs) {
-    constexpr int NT = FftT<BIG>::T;
+__global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double *__restrict__ src,
+                                                      double *__restrict__ dst, int rows, int n,
+                                                      const double2 *__restrict__ W,
+                                                      Radices rd, double scale,
+                                                      const double *__restrict__ lamr,
+                                                      const double *__restrict__ lamk, int row0,
+                                                      double *__restrict__ rs) {
+    constexpr int NT = K1T<BIG>::T;
+    constexpr int PP = (K1_MAXN / 2 + NT - 1) / NT;   // (k, N - k) pairs per thread, N < K1_MAXN
     extern __shared__ double2 z[];
-    __shared__ double red[512];
-    const int M = 2 * (n - 1), rA = 2 * blockIdx.x, rB = rA + 1, tid = threadIdx.x;
-    const bool hasB = rB < rows;
-    const double *sa = src + (long)rA * n, *sb = src + (long)rB * n;
-    for (int j = tid; j < n; j += NT) put_even(z, n, M, j, sa[j], hasB ? sb[j] : 0.0);
-    __syncthreads();
-    fft_lds<BIG>(z, M, rd, W);
-    if constexpr (SOLVE) {
-        constexpr int PER = (4096 + NT) / NT;
-        double2 q[PER];
+    __shared__ double red[256];
+    const int N = n - 1, r = blockIdx.x, tid = threadIdx.x;
+    double *d = (double *)z;
+    const double2 *Wq0 = W + (N - 1);   // after the N - 1 pass twiddles: W^k, k = 0 .. N
+    put_row_even<NT>(d, N, src + (long)r * n);
+    // SOLVE runs the transform twice (forward, then inverse on the divided spectrum): one
+    // loop, so that the FFT is inlined once
+#pragma unroll 1
+    for (int it = 0; it < (SOLVE ? 2 : 1); ++it) {
+        __syncthreads();
+        fft_lds<BIG, NT, K1_MAXN>(z, N, rd, W);
+        // opaque per iteration: keeps the twiddle / eigenvalue loads below from being hoisted
+        // above the FFT (they would hold ~40 registers across it)
+        const double2 *Wq = Wq0;
+        const double *lr = lamr, *lk = lamk;
+        int tid = threadIdx.x;
+        asm volatile("" : "+s"(Wq), "+s"(lr), "+s"(lk), "+v"(tid));
+        double xa[PP], xb[PP];   // X_k, X_{N-k} for k = tid + t NT <= N / 2
 #pragma unroll
-        for (int t = 0; t < PER; ++t) {
+        for (int t = 0; t < PP; ++t) {
             const int k = tid + t * NT;
-            if (k < n) {
-                const double2 Z = z[k];
-                // row0: global frequency of local row 0 (slab-decomposed solves)
-                const double eA = (row0 + rA == 0 && k == 0) ? 1.0 : lamr[row0 + rA] + lamk[k];
-                const double eB = hasB ? lamr[row0 + rB] + lamk[k] : 1.0;
-                q[t] = make_double2(Z.x / eA, hasB ? Z.y / eB : 0.0);
+            if (k <= N / 2) {
+                const double2 A = z[k], B = z[k ? N - k : 0], w = Wq[k];
+                const double S = A.x + B.x, D = A.x - B.x, T = A.y + B.y;
+                const double c = w.x, sn = -w.y;
+                xa[t] = 0.5 * (S + c * T - sn * D);
+                xb[t] = 0.5 * (S - c * T + sn * D);
             }
         }
-        __syncthreads();
+        if (SOLVE && it == 0) {
+            const int kx = row0 + r;
+            __syncthreads();   // every Z read
 #pragma unroll
-        for (int t = 0; t < PER; ++t) {
+            for (int t = 0; t < PP; ++t) {
+                const int k = tid + t * NT;
+                if (k <= N / 2) {
+                    const double ea = (kx == 0 && k == 0) ? 1.0 : lr[kx] + lk[k];
+                    const double ya = xa[t] / ea;
+                    d[k] = ya;
+                    if (k >= 1) d[2 * N - k] = ya;
+                    const int kb = N - k;
+                    if (kb != k) {
+                        const double yb = xb[t] / (lr[kx] + lk[kb]);
+                        d[kb] = yb;
+                        if (kb >= 1 && kb < N) d[2 * N - kb] = yb;
+                    }
+                }
+                // one pair's divisions at a time: interleaved, their expansions spill
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            continue;
+        }
+        double *o = dst + (long)r * n;
+#pragma unroll
+        for (int t = 0; t < PP; ++t) {
             const int k = tid + t * NT;
-            if (k < n) put_even(z, n, M, k, q[t].x, q[t].y);
+            if (k <= N / 2) {
+                o[k] = xa[t] * scale;
+                if (N - k != k) o[N - k] = xb[t] * scale;
+            }
         }
-        __syncthreads();
-        fft_lds<BIG>(z, M, rd, W);
-    }
-    double *da = dst + (long)rA * n, *db = dst + (long)rB * n;
-    for (int k = tid; k < n; k += NT) {
-        const double2 Z = z[k];
-        da[k] = Z.x * scale;
-        if (hasB) db[k] = Z.y * scale;
-    }
-    if (rs) {
-        // the sums k_rowsum would take of the two rows written: 256 strided partials per
-        // row, then the halving tree (ops.hip)
-        if (tid < 512) {
-            const int t = tid & 255;
-            double acc = 0.0;
-            if (tid < 256) for (int k = t; k < n; k += 256) acc += z[k].x * scale;
-            else for (int k = t; k < n; k += 256) acc += z[k].y * scale;
-            red[tid] = acc;
-        }
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if (tid < 512 && (tid & 255) < w) red[tid] = red[tid] + red[tid + w];
+        if (rs) {
+            // the sum k_rowsum would take of the row written: 256 strided partials, then the
+            // halving tree (ops.hip)
             __syncthreads();
+#pragma unroll
+            for (int t = 0; t < PP; ++t) {
+                const int k = tid + t * NT;
+                if (k <= N / 2) { d[k] = xa[t] * scale; d[N - k] = xb[t] * scale; }
+            }
+            __syncthreads();
+            if (tid < 256) {
+                double acc = 0.0;
+                for (int k = tid; k < n; k += 256) acc += d[k];
+                red[tid] = acc;
+            }
+            __syncthreads();
+            for (int w = 128; w > 0; w >>= 1) {
+                if (tid < w) red[tid] = red[tid] + red[tid + w];
+                __syncthreads();
+            }
+            if (tid == 0) rs[r] = red[0];
         }
-        if (tid == 0) rs[rA] = red[0];
-        if (tid == 256 && hasB) rs[rB] = red[256];
     }
 }
 
@@ -528,23 +592,23 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
                              (const void *)k_dct1<false, 1>, (const void *)k_dct1<true, 1>};
         for (auto f : fs)
             RMT_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        DCT_MAXM * 16));
+                                        (int)FFT_LDS_MAX));
         attr = true;
     }
     if (nrows <= 0) return RMT_OK;
-    const int NT = P->big ? FftT<1>::T : FftT<0>::T;
     const int n = axis == 0 ? P->nx : P->ny;
-    const Radices rd = axis == 0 ? radices(P->radx, P->npx) : radices(P->rady, P->npy);
+    const int *rad = axis == 0 ? P->radx : P->rady, np = axis == 0 ? P->npx : P->npy;
+    const Radices rd = radices(rad, np);
     const double2 *W = axis == 0 ? P->Wx : P->Wy;
-    const size_t lds = 2 * (size_t)(n - 1) * sizeof(double2);
-    const unsigned g = (nrows + 1) / 2;
+    const size_t lds = (size_t)(n - 1) * sizeof(double2);
+    const unsigned g = (unsigned)nrows;   // one row per workgroup
     hipStream_t st = ctx->stream;
     if (solve) {
-        if (P->big) k_dct1<true, 1><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
-        else k_dct1<true, 0><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
+        if (P->big) k_dct1<true, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
+        else k_dct1<true, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
     } else {
-        if (P->big) k_dct1<false, 1><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
-        else k_dct1<false, 0><<<g, NT, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
+        if (P->big) k_dct1<false, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
+        else k_dct1<false, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
     }
     RMT_LAUNCHED();
     return RMT_OK;
@@ -629,7 +693,7 @@ __global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict_
             z[m] = make_double2(sa[q], hasB ? sb[q] : 0.0);
         }
         __syncthreads();
-        fft_lds<BIG>(z, n, rd, W);
+        fft_lds<BIG, FftT<BIG>::T, DCT_MAXM>(z, n, rd, W);
         double2 y[PER];
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
@@ -685,7 +749,7 @@ __global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict_
         }
     }
     __syncthreads();
-    fft_lds<BIG>(z, n, rd, W);
+    fft_lds<BIG, FftT<BIG>::T, DCT_MAXM>(z, n, rd, W);
     const double s = scale / n;
     for (int m = tid; m < n; m += DCT_T) {
         const double2 R = z[m];
@@ -736,7 +800,8 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
     if (P) { dct2_destroy(P); ctx->dct2 = nullptr; }
     P = new Dct2Plan;
     P->ny = ny; P->nx = nx; P->dx = dx; P->dy = dy;
-    if ((nx & 1) || (ny & 1) || !factor(nx, P->radx, &P->npx) || !factor(ny, P->rady, &P->npy)) {
+    if ((nx & 1) || (ny & 1) || !factor(nx, P->radx, &P->npx) || !factor(ny, P->rady, &P->npy) ||
+        !lds_fits(nx) || !lds_fits(ny)) {
         delete P;
         set_error("DCT-II solve: N must be even, <= 8192, and factor into radices <= 23");
         return RMT_ENOTSUP;
@@ -762,7 +827,7 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
                              (const void *)k_dct2<1, 1>, (const void *)k_dct2<2, 1>};
         for (auto f : fs)
             RMT_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        DCT_MAXM * 16));
+                                        (int)FFT_LDS_MAX));
         attr = true;
     }
     return RMT_OK;
