@@ -780,8 +780,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     const int kmiss = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : npad;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    int c1 = kmiss >> 3;
-    const int nch = npad >> 3;
+    const int c1 = kmiss >> 3, nch = npad >> 3;
     if (lane < 6) acc = ch_fold(acc, tv + lane * npad, 0, c1);
     CH_STAMP(3);
     // pass 2: wait for the missing sources, then the rest of the fold
@@ -805,19 +804,6 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             }
             const u64 left = __ballot(!done);
             if (left == 0) break;
-            if constexpr ((VAR & 32) != 0) {
-                // one source left: fold every chunk before its term now, so that only the
-                // chunks from its own to the end remain after it arrives
-                if (__popcll(left) == 1) {
-                    const int c2 = __builtin_amdgcn_readlane(e.x, __builtin_ctzll(left)) >> 3;
-                    if (c2 > c1) {
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                        if (lane < 6) acc = ch_fold(acc, tv + lane * npad, c1, c2);
-                        c1 = c2;
-                    }
-                }
-            }
             if (++sp > CH_SPIN_LIMIT) return false;
             if constexpr (PROF) pr[7] += 1;
             if constexpr (!(VAR & 2)) __builtin_amdgcn_s_sleep(0);
@@ -832,13 +818,17 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     if constexpr (PROF) asm volatile("" : "+v"(acc));
     CH_STAMP(4);
     // utils.py:134-166 on lanes 0 (X1) and 3 (X2) with the precomputed cofactors
-    const double bb1 = dpp_shl(acc, 1), bb2 = dpp_shl(acc, 2);
+    double bb1 = dpp_shl(acc, 1), bb2 = dpp_shl(acc, 2);
+    if constexpr (PROF) asm volatile("" : "+v"(bb1), "+v"(bb2));
+    CH_STAMP(8);
     if (lane == 0 || lane == 3) {
         const double b0 = acc, b1 = bb1, b2 = bb2;
         const double xs = (b0 * C0 - M1 * (b1 * M8 - M5 * b2) + M2 * (b1 * M7 - M4 * b2)) * inv_det;
         const double ys = (M0 * (b1 * M8 - M5 * b2) - b0 * C1 + M2 * (M3 * b2 - b1 * M6)) * inv_det;
         const double zs = (M0 * (M4 * b2 - b1 * M7) - M1 * (M3 * b2 - b1 * M6) + b0 * C2) * inv_det;
-        const double o = xs + ys * x0 + zs * y0;
+        double o = xs + ys * x0 + zs * y0;
+        if constexpr (PROF) asm volatile("" : "+v"(o));
+        CH_STAMP(9);
         ((double *)&val[x & (CH_R - 1)])[lane == 0 ? 0 : 1] = o;
         if (pub) gval[2 * gslot + (lane == 0 ? 0 : 1)] = o;
         o_out = o;
@@ -851,6 +841,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         if (lane == 0)
             __hip_atomic_store(&gtag[gslot], gslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    CH_STAMP(10);
     if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
     c_out = __double_as_longlong(B[0]);
     if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -894,7 +886,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
     if (x < total) CH_LOAD(r);
     int wm = 0;
     bool ok = true;
-    long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tl = 0;
+    long long pr[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tl = 0;
     if constexpr (PROF) tl = __builtin_amdgcn_s_memtime();
     double o = 0.0;      // previous fit's value (lane 0: X1, lane 3: X2) and cell
     long c = -1;
@@ -920,7 +912,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
     }
     if constexpr (PROF)
         if (lane == 0)
-            for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&gprof[k], pr[k]);
+            for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long *)&gprof[k], pr[k]);
     if (ok && c >= 0 && (lane == 0 || lane == 3)) (lane == 0 ? X1e : X2e)[c] = o;
     __hip_atomic_store(&cur[wv], 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (!ok && lane == 0) {
@@ -969,10 +961,6 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
             case 0: k_ex_chain<false, 0><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 1: k_ex_chain<false, 1><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 2: k_ex_chain<false, 2><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 35:
-                if (nparts == 1) k_ex_chain<false, 51><<<1, CH_W * 64, 0, st>>>(C, nullptr);
-                else k_ex_chain<false, 35><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
-                break;
             default:
                 if (nparts == 1) k_ex_chain<false, 19><<<1, CH_W * 64, 0, st>>>(C, nullptr);
                 else k_ex_chain<false, 3><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
@@ -980,7 +968,7 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
         RMT_LAUNCHED();
     } else {
         // diagnostic: per-phase shader clocks summed over the chain waves
-        long long *gp = nullptr, hp[8];
+        long long *gp = nullptr, hp[12];
         RMT_HIP(hipMalloc(&gp, sizeof(hp)));
         RMT_HIP(hipMemsetAsync(gp, 0, sizeof(hp), st));
         hipEvent_t e0, e1;
@@ -996,8 +984,7 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
             C.trace = dtr;
         }
         RMT_HIP(hipEventRecord(e0, st));
-        if (var == 35) k_ex_chain<true, 35><<<nparts, CH_W * 64, 0, st>>>(C, gp);
-        else k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
+        k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, st));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));
@@ -1008,8 +995,11 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
         RMT_HIP(hipEventElapsedTime(&ms, e0, e1));
         fprintf(stderr, "[chain-prof] %.3f ms fits=%d | stage %.3g throttle %.3g wait %.3g "
                 "products %.3g fold %.3g solve+publish %.3g store+prefetch %.3g (Mclk, all "
-                "waves) polls %lld\n", ms, hs[0], hp[0] / 1e6, hp[1] / 1e6, hp[2] / 1e6,
-                hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6, hp[6] / 1e6, hp[7]);
+                "waves) polls %lld | post split (clk/fit): fold %.0f dpp %.0f solve %.0f "
+                "publish %.0f\n", ms, hs[0], hp[0] / 1e6, hp[1] / 1e6, hp[2] / 1e6,
+                hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6, hp[6] / 1e6, hp[7],
+                (double)hp[4] / std::max(1, hs[0]), (double)hp[8] / std::max(1, hs[0]),
+                (double)hp[9] / std::max(1, hs[0]), (double)hp[10] / std::max(1, hs[0]));
         if (dtr) {
             std::vector<long long> h(6 * ws.maxt);
             int tot = 0;
