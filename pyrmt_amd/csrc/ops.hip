@@ -375,7 +375,9 @@ __global__ void k_divergence_rc(const double *__restrict__ a, const double *__re
                                 const double *__restrict__ p, int ny, int nx, double d_f,
                                 double dx, double dy, double *__restrict__ divU, int jb, int je,
                                 double rho = 0.0, double dt = 1.0,
-                                const double *__restrict__ dtp = nullptr) {
+                                const double *__restrict__ dtp = nullptr,
+                                const unsigned char *__restrict__ rowmark = nullptr) {
+    if (rowmark && !rowmark[jb + blockIdx.y]) return;   // only the listed rows
     if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
     // rho > 0: the projection's rhs = (rho * divU) / dt (functions.py:1331, the same two
     // roundings as the separate scale and divide passes).  Grid: rows_grid (one block row
@@ -762,6 +764,35 @@ int rmt_compute_timestep(rmt_ctx *ctx, const double *a, const double *b, double 
 }  // extern "C"
 
 namespace rmt {
+// The projection in two parts around the extrapolation chain (sim.hip): the Rhie-Chow rhs and
+// the row DCT-I of every row (or of the marked rows only) into scratch, then the rest.
+int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
+                    double dy, const double *dtp, double dt, double rho, const double *p_prev,
+                    const unsigned char *rowmark) {
+    RMT_CHECK(p_prev && rho > 0, RMT_EINVAL, "projection_rows: bad arguments");
+    const long n = (long)ctx->ny * ctx->nx;
+    RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
+    double *rhs = ctx->scratch, *pc = rhs + n;
+    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
+        a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx, dy, rhs, 0, ctx->ny, rho, dt, dtp,
+        rowmark);
+    RMT_LAUNCHED();
+    RMT_TRY(dct_plan(ctx, dx, dy));
+    return dct_pass(ctx, false, 0, rhs, pc, ctx->ny, 0, 1.0, nullptr, rowmark);
+}
+int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
+                      double dy, const double *dtp, double dt, double rho, int bc_kind,
+                      double lid, const double *p_prev, double *a, double *b, double *p,
+                      double *m2part) {
+    const long n = (long)ctx->ny * ctx->nx;
+    double *pc = ctx->scratch + n, *root = ctx->red + RED_BLOCKS + 17;
+    RMT_TRY(dct_solve_after_rows(ctx, pc, root));
+    k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
+        a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt / rho, bc_kind, lid, a, b, p, 0,
+        ctx->ny, root, (double)n, dtp, rho, m2part);
+    RMT_LAUNCHED();
+    return sub_mean_rows(ctx, p, ctx->ny, ctx->nx);
+}
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                    double dy, const double *dtp, double rho, int bc_kind, double lid,
                    const double *p_prev, double *a, double *b, double *p, double *m2part) {

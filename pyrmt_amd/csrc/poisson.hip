@@ -460,7 +460,9 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
                                                       Radices rd, double scale,
                                                       const double *__restrict__ lamr,
                                                       const double *__restrict__ lamk, int row0,
-                                                      double *__restrict__ rs) {
+                                                      double *__restrict__ rs,
+                                                      const unsigned char *__restrict__ rowmark) {
+    if (rowmark && !rowmark[blockIdx.x]) return;   // only the listed rows
     constexpr int NT = K1T<BIG>::T;
     constexpr int PP = (K1_MAXN / 2 + NT - 1) / NT;   // (k, N - k) pairs per thread, N < K1_MAXN
     extern __shared__ double2 z[];
@@ -581,11 +583,12 @@ static Radices radices(const int *rad, int np) {
 // One LDS DCT-I pass over nrows rows of length n (axis 0: n = nx, axis 1: n = ny).  SOLVE
 // (axis 1 only): forward, / eig, inverse, with rows = x-frequencies row0 .. row0 + nrows.
 int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
-             int row0, double scale, double *rs) {
+             int row0, double scale, double *rs, const unsigned char *rowmark) {
     DctPlan *P = ctx->dct;
     RMT_CHECK(P && P->lds, RMT_ENOTSUP, "dct_pass: no LDS DCT plan for this grid");
     RMT_CHECK(!solve || axis == 1, RMT_EINVAL, "dct_pass: the solve pass runs along y");
     RMT_CHECK(!rs || (!solve && nrows <= ctx->rsum_len), RMT_EINVAL, "dct_pass: row sums");
+    RMT_CHECK(!rowmark || (!solve && !rs), RMT_EINVAL, "dct_pass: row marks on a plain row pass");
     static bool attr = false;
     if (!attr) {
         const void *fs[4] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
@@ -604,11 +607,11 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     const unsigned g = (unsigned)nrows;   // one row per workgroup
     hipStream_t st = ctx->stream;
     if (solve) {
-        if (P->big) k_dct1<true, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
-        else k_dct1<true, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr);
+        if (P->big) k_dct1<true, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
+        else k_dct1<true, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
     } else {
-        if (P->big) k_dct1<false, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
-        else k_dct1<false, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs);
+        if (P->big) k_dct1<false, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark);
+        else k_dct1<false, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark);
     }
     RMT_LAUNCHED();
     return RMT_OK;
@@ -633,6 +636,18 @@ static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p,
     RMT_TRY(dct_pass(ctx, false, 0, p, p, ny, 0, 1.0 / (2.0 * (nx - 1)), rs));
     RMT_LAUNCHED();
     return RMT_OK;
+}
+
+int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root) {
+    DctPlan *P = ctx->dct;
+    RMT_CHECK(P && P->lds && P->ny <= ctx->rsum_len, RMT_ENOTSUP,
+              "dct_solve_after_rows: LDS DCT plan needed");
+    const int ny = P->ny, nx = P->nx;
+    transpose(ctx->stream, pc, ny, nx, P->T);
+    RMT_TRY(dct_pass(ctx, true, 1, P->T, P->T, nx, 0, 1.0 / (2.0 * (ny - 1))));
+    transpose(ctx->stream, P->T, nx, ny, pc);
+    RMT_TRY(dct_pass(ctx, false, 0, pc, pc, ny, 0, 1.0 / (2.0 * (nx - 1)), ctx->rsum));
+    return rowtree_sums(ctx, ny, dev_root);
 }
 
 int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,

@@ -440,6 +440,16 @@ int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int 
 // functions.py:1255-1364 (constant density, Neumann DCT-I) for the fused step: dt read from
 // the device (dtp), and the max of u^2 + v^2 over the corrected velocity per 256-cell block
 // into m2part (the next step's compute_timestep input), ceil(nx / 256) * ny entries
+// the same projection split around the extrapolation chain: rows part (Rhie-Chow rhs + row
+// DCT-I into ctx->scratch; rowmark: only the marked rows, else all), then the rest (dtp null:
+// the scalar dt)
+int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
+                    double dy, const double *dtp, double dt, double rho, const double *p_prev,
+                    const unsigned char *rowmark);
+int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
+                      double dy, const double *dtp, double dt, double rho, int bc_kind,
+                      double lid, const double *p_prev, double *a, double *b, double *p,
+                      double *m2part);
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                    double dy, const double *dtp, double rho, int bc_kind, double lid,
                    const double *p_prev, double *a, double *b, double *p, double *m2part);
@@ -508,9 +518,14 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
               double *dev_root = nullptr);
 int dct_plan(rmt_ctx *ctx, double dx, double dy);
 bool dct_lds_ready(rmt_ctx *ctx);
-// rs (nullable): per-row sums of the output, in k_rowsum's order (rowtree_sums finishes them)
+// rs (nullable): per-row sums of the output, in k_rowsum's order (rowtree_sums finishes them);
+// rowmark (nullable): transform only the rows r with rowmark[r] != 0
 int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
-             int row0, double scale, double *rs = nullptr);
+             int row0, double scale, double *rs = nullptr,
+             const unsigned char *rowmark = nullptr);
+// the LDS solve after its forward row pass (pc holds DCT_x of the rhs): columns, inverse rows,
+// the row-tree sum of the result into *dev_root (mean not subtracted)
+int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root);
 void transpose(hipStream_t st, const double *in, int R, int C, double *out);
 // MAC grid (mac.py:104-123): DCT-II Neumann solve on a (ny, nx) cell grid, (0,0) -> 0
 int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);
@@ -548,6 +563,10 @@ int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, c
             int *flags, int jb, int je, int lo, int hi, const double *dev_m2 = nullptr);
 int slab_bits(rmt_ctx *ctx, const double *phi, int nx, int W, unsigned long long *bits, int r0,
               int r1);
+// cells whose 15x15 box holds a known and an unknown cell (the values the extrapolation can
+// read or write), as bit words of the whole grid; rowcnt: ny + 1 ints of scratch
+int rim_words(rmt_ctx *ctx, const unsigned long long *bits, int ny, int nx, int W,
+              unsigned long long *rimw, int *rowcnt);
 int slab_rim_pack(rmt_ctx *ctx, const unsigned long long *bits, int ny, int nx, int W, int r0,
                   int r1, unsigned long long *rimw, int *rowcnt, const double *X1n,
                   const double *X2n, double *rim, double *count);

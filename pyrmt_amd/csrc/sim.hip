@@ -40,13 +40,22 @@ struct rmt_sim {
     void *block = nullptr;
     // overlap of the (one-CU) extrapolation chain with a speculative momentum pass
     hipStream_t st2 = nullptr;
-    hipEvent_t e_sl = nullptr, e_mom = nullptr;
+    hipEvent_t e_sl = nullptr, e_mom = nullptr, e_rows = nullptr;
     int *tiles = nullptr, *tcount = nullptr, max_tiles = 0;
     // device-resident dt and diagnostics (rmt_sim_step's asynchronous path): per-block
     // max |u|^2 partials from the projection, and a ring of per-step records read back once
     // per RING_N steps
     double *m2part = nullptr, *ring = nullptr;
     int m2n = 0;
+    // the projection's row pass runs beside the chain; only the rows of the fix-up tiles
+    // (+-1 for the Rhie-Chow stencil) are redone after it
+    unsigned char *rowmark = nullptr;
+    bool split_proj = false;
+    // the advection split: the rim cells (within 7 of the known/unknown interface, all the
+    // extrapolation reads) before the chain, the rest beside it on the second stream
+    unsigned long long *rimw = nullptr;
+    int *rimcnt = nullptr;
+    hipEvent_t e_bits = nullptr;
     bool prof = false;
     hipEvent_t pev[7] = {};
     double ms[8] = {};
@@ -63,13 +72,24 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
                          double y0, double R, double *__restrict__ X1n, double *__restrict__ X2n,
                          double *__restrict__ phi_pre, int *bad,
                          unsigned long long *__restrict__ kbits, const double *m2,
-                         const double *__restrict__ dtp = nullptr) {
+                         const double *__restrict__ dtp = nullptr, int mode = 0,
+                         const unsigned long long *__restrict__ rimw = nullptr,
+                         const int *__restrict__ rimcnt = nullptr) {
     const double dt = dtp ? *dtp : dt_arg;
     // grid (ceil(nx / 256), ny): a wave covers 64 cells of one row, so the extrapolation's
-    // known plane (phi_pre < 0, 64-cell words) comes out of the same pass (kbits optional)
+    // known plane (phi_pre < 0, 64-cell words) comes out of the same pass (kbits optional).
+    // mode 1: only the rim cells (rimw), mode 2: every other cell -- the same per-cell result,
+    // split so that the extrapolation can start after the (small) rim part
     const int j = blockIdx.y, i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
     const bool in = i < nx;
     const long c = (long)j * nx + i;
+    bool mine = true;
+    if (mode == 1 && rimcnt[j] == 0) return;   // no rim cell in this row
+    if (mode) {
+        const bool rim = in && ((rimw[(long)j * ((nx + 63) / 64) + (i >> 6)] >> (i & 63)) & 1);
+        if (mode == 1 && !__syncthreads_or(rim)) return;   // whole block outside the rim
+        mine = (mode == 1) == rim;
+    }
     const bool zero = sl_skip_ok(m2, dt, fmin(dx, dy)) &&
                       sl_zero_block(X1, X2, ny, nx, j, i0, 256, 0, ny);
     bool known = false;
@@ -77,14 +97,14 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
         // the map is +0.0 here: phi of the origin, advected map +0.0 (no loads); phi_pre
         // only when no known plane is produced (its only reader is then the extrapolation)
         const double ph = disc_phi(0.0, 0.0, x0, y0, R);
-        if (!kbits) phi_pre[c] = ph;
+        if (!kbits && !mode) phi_pre[c] = ph;
         known = ph < 0;
-        X1n[c] = 0.0; X2n[c] = 0.0;
-    } else if (in) {
+        if (mine) { X1n[c] = 0.0; X2n[c] = 0.0; }
+    } else if (in && mine) {
         bool fin = isfinite(a[c]) && isfinite(b[c]);
         if (!fin) atomicOr(bad, 1);
         double ph = disc_phi(X1[c], X2[c], x0, y0, R);
-        if (!kbits) phi_pre[c] = ph;
+        if (!kbits && !mode) phi_pre[c] = ph;
         known = ph < 0;
         {
             double m = ph <= 0 ? 1.0 : 0.0;
@@ -99,6 +119,19 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
         if ((threadIdx.x & 63) == 0 && (i >> 6) < (nx + 63) / 64)
             kbits[(long)j * ((nx + 63) / 64) + (i >> 6)] = w;
     }
+}
+
+// the known plane alone (phi of the pre-advection map < 0: k_sim_sl's `known`), 64-cell words
+__global__ void __launch_bounds__(256) k_sim_bits(const double *__restrict__ X1,
+                                                  const double *__restrict__ X2, int nx,
+                                                  double x0, double y0, double R,
+                                                  unsigned long long *__restrict__ kbits) {
+    const int j = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    const long c = (long)j * nx + i;
+    const bool known = i < nx && disc_phi(X1[c], X2[c], x0, y0, R) < 0;
+    const unsigned long long w = __ballot(known);
+    if ((threadIdx.x & 63) == 0 && (i >> 6) < (nx + 63) / 64)
+        kbits[(long)j * ((nx + 63) / 64) + (i >> 6)] = w;
 }
 
 // k_sim_sl with the bicubic interpolant (functions.py:228-251, scheme semilagrangian_cubic)
@@ -210,6 +243,15 @@ __global__ void __launch_bounds__(1024) k_dt_part(const double *__restrict__ par
         sc[0] = m2;
         sc[1] = fmin(dt_const, cfl * dx / (sqrt(m2) + 1e-6));
     }
+}
+// rows [16 ty - 1, 16 ty + 17) of every listed fix-up tile: the rows whose Rhie-Chow rhs
+// (u*, v* at j-1 .. j+1) the tile re-run can change
+__global__ void k_mark_rows(const int *__restrict__ tiles, const int *__restrict__ count,
+                            int tiles_x, int ny, unsigned char *__restrict__ rowmark) {
+    if ((int)blockIdx.x >= *count) return;
+    const int j0 = (tiles[blockIdx.x] / tiles_x) * MOM_TY - 1;
+    const int j = j0 + (int)threadIdx.x;
+    if (threadIdx.x < MOM_TY + 2 && j >= 0 && j < ny) rowmark[j] = 1;
 }
 // completes a ring record after k_diag_p2 wrote its diagnostics: max |u|^2, dt, flags
 __global__ void k_ring_put(const double *__restrict__ sc, const int *__restrict__ flag,
@@ -396,13 +438,24 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
         RMT_HIP(hipStreamCreateWithPriority(&S->st2, hipStreamNonBlocking, least));
         RMT_HIP(hipEventCreateWithFlags(&S->e_sl, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_mom, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_rows, hipEventDisableTiming));
         S->max_tiles = ((nx + MOM_TX - 1) / MOM_TX) * ((ny + MOM_TY - 1) / MOM_TY);
         RMT_HIP(hipMalloc(&S->tiles, (S->max_tiles + 64) * sizeof(int)));
         S->tcount = S->tiles + S->max_tiles;
     }
     S->m2n = ((nx + 255) / 256) * ny;
-    RMT_HIP(hipMalloc(&S->m2part, ((size_t)S->m2n + (size_t)RING_N * RING_VALS) * sizeof(double)));
+    const size_t Wn = (size_t)(nx + 63) / 64;
+    RMT_HIP(hipMalloc(&S->m2part, ((size_t)S->m2n + (size_t)RING_N * RING_VALS + ny / 8 + 8 +
+                                   (size_t)ny * Wn + ny / 2 + 8) * sizeof(double)));
     S->ring = S->m2part + S->m2n;
+    S->rowmark = (unsigned char *)(S->ring + (size_t)RING_N * RING_VALS);
+    S->rimw = (unsigned long long *)(S->ring + (size_t)RING_N * RING_VALS + ny / 8 + 8);
+    S->rimcnt = (int *)(S->rimw + (size_t)ny * Wn);
+    if (S->st2) RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
+    if (S->st2 && prm->rho_f > 0) {
+        RMT_TRY(dct_plan(ctx, prm->dx, prm->dy));
+        S->split_proj = dct_lds_ready(ctx) && ny <= ctx->rsum_len;
+    }
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
     return RMT_OK;
@@ -415,6 +468,8 @@ int rmt_sim_destroy(rmt_sim *S) {
     if (S->tiles) hipFree(S->tiles);
     if (S->e_sl) hipEventDestroy(S->e_sl);
     if (S->e_mom) hipEventDestroy(S->e_mom);
+    if (S->e_rows) hipEventDestroy(S->e_rows);
+    if (S->e_bits) hipEventDestroy(S->e_bits);
     if (S->st2) hipStreamDestroy(S->st2);
     for (auto e : S->pev) if (e) hipEventDestroy(e);
     S->ctx->prof = false;
@@ -525,7 +580,19 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (solid) {
             // 2. advect the reference map with the pre-advection level set and mask
             RMT_HIP(hipMemsetAsync(S->flag, 0, sizeof(int), st));
-            if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
+            if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && overlap && S->e_bits) {
+                // known plane -> rim words -> the rim's advection here; the rest on the second
+                // stream, beside the extrapolation (which reads rim cells only)
+                const dim3 gsl((nx + 255) / 256, ny);
+                k_sim_bits<<<gsl, 256, 0, st>>>(S->X1, S->X2, nx, P.x0, P.y0, P.R, S->kbits);
+                RMT_LAUNCHED();
+                RMT_TRY(rim_words(ctx, S->kbits, ny, nx, (nx + 63) / 64, S->rimw, S->rimcnt));
+                RMT_HIP(hipEventRecord(S->e_bits, st));
+                k_sim_sl<<<gsl, 256, 0, st>>>(
+                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
+                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, nullptr, sc, dtp, 1,
+                    S->rimw, S->rimcnt);
+            } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
                 k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, st>>>(
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
                     P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits, sc, dtp);
@@ -563,15 +630,30 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_TRY(es);
             if (overlap) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
+                if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits) {
+                    // the advection of every non-rim cell, once the chain has started (earlier
+                    // its blocks would crowd out the one-workgroup band passes)
+                    k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, S->st2>>>(
+                        S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
+                        P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, nullptr, sc, dtp, 2,
+                        S->rimw, S->rimcnt);
+                    RMT_LAUNCHED();
+                }
                 k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R,
                                                       S->phi, S->X1, S->X2);
                 RMT_LAUNCHED();
                 ctx->stream = S->st2;
-                const int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi,
-                                            S->us, S->vs, S->sxx, S->sxy, S->syy, S->J, W);
+                int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi,
+                                      S->us, S->vs, S->sxx, S->sxy, S->syy, S->J, W);
+                if (ms == RMT_OK) ms = hipEventRecord(S->e_mom, S->st2) ? RMT_EDEVICE : RMT_OK;
+                // and the projection's rows from the speculative u*, v* (the fix-up tiles the
+                // main stream re-runs meanwhile only feed rows it redoes afterwards)
+                if (ms == RMT_OK && S->split_proj)
+                    ms = projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
+                                         nullptr);
                 ctx->stream = st;
                 RMT_TRY(ms);
-                RMT_HIP(hipEventRecord(S->e_mom, S->st2));
+                RMT_HIP(hipEventRecord(S->e_rows, S->st2));
             }
             if (overlap) RMT_TRY(extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount));
             if (S->prof) RMT_HIP(hipEventRecord(S->pev[3], st));
@@ -603,7 +685,19 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         }
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[4], st));
         // 6. projection (constant density rho_f; Neumann DCT-I)
-        if (async)
+        if (overlap && S->split_proj) {
+            // redo the rows the fix-up tiles reach, then the column pass and the rest
+            const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
+            RMT_HIP(hipMemsetAsync(S->rowmark, 0, ny, st));
+            k_mark_rows<<<S->max_tiles, 64, 0, st>>>(S->tiles, S->tcount, tiles_x, ny, S->rowmark);
+            RMT_LAUNCHED();
+            RMT_HIP(hipStreamWaitEvent(st, S->e_rows, 0));
+            RMT_TRY(projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
+                                    S->rowmark));
+            RMT_TRY(projection_finish(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, P.bc_kind,
+                                      P.lid, S->p, S->u, S->v, S->p,
+                                      async ? S->m2part : nullptr));
+        } else if (async)
             RMT_TRY(projection_dev(ctx, S->us, S->vs, P.dx, P.dy, dtp, P.rho_f, P.bc_kind, P.lid,
                                    S->p, S->u, S->v, S->p, S->m2part));
         else

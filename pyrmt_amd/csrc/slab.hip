@@ -310,6 +310,13 @@ int slab_rim_pack(rmt_ctx *ctx, const u64 *bits, int ny, int nx, int W, int r0, 
     return RMT_OK;
 }
 
+// rim words of the whole grid (the fused step's split advection, sim.hip)
+int rim_words(rmt_ctx *ctx, const u64 *bits, int ny, int nx, int W, u64 *rimw, int *rowcnt) {
+    k_rim_words<<<(ny + 3) / 4, 256, 0, ctx->stream>>>(bits, ny, nx, W, 0, ny, rimw, rowcnt);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
 int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *counts, int G,
                          long long cap, double *X1d, double *X2d, const u64 *bits, double dx,
                          double dy, int layers, int *exflags, double *X1n, double *X2n,
