@@ -225,7 +225,7 @@ __global__ void k_grad_y(const double *__restrict__ f, int ny, int nx, double h2
                          double *__restrict__ out) {
     long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (c >= (long)ny * nx) return;
-    int j = (int)(c / nx), i = (int)(c % nx);
+    int j = (int)(c / nx);
     out[c] = grad2(f + c, nx, j, ny, h2);
 }
 __global__ void k_upwind(const double *__restrict__ f, const double *__restrict__ vel, int ny,

@@ -6,13 +6,16 @@
 // the real and imaginary parts of one complex sequence come back separated in Re and Im.
 // scipy's inverse DCT-I is the forward one scaled by 1/(2(n-1)) per axis.
 //
-// Main path (M <= 8192 and M = product of radices 2..31): k_dct1 -- one workgroup per row
-// pair, the whole length-M complex sequence resident in LDS (<= 128 KB), a mixed-radix
-// Stockham FFT with register-staged passes (read every butterfly input -> barrier ->
-// twiddle + small DFT -> write -> barrier).  A 2D solve is five launches:
+// Main path (n - 1 < 4096, a product of radices 2..23): k_dct1 -- one workgroup per row,
+// the row's even extension packed as a length-(n-1) complex sequence resident in LDS
+// (<= 64 KB, two workgroups per CU), a mixed-radix Stockham FFT (radices grouped into
+// in-register composite butterflies of up to 10; twiddles from a global per-pass table),
+// then the packed-real split into the DCT-I.  A 2D solve is five launches:
 //   rows (x)  ->  transpose  ->  columns: DCT, / eig, inverse DCT, fused  ->  transpose
-//   ->  rows (x, inverse).
-// HBM traffic: 10 planes per solve.  Other sizes: rocFFT R2C rounds (the previous path).
+//   ->  rows (x, inverse, + the row sums of the mean).
+// HBM traffic: 10 planes per solve.  Reading the columns in place instead of transposing
+// (strided, XCD-grouped workgroups) measured slower: 380 us for the fused column pass
+// against 63 + 234 + 43 us with the transposes.  Other sizes: rocFFT R2C rounds.
 #include "rmt_internal.hpp"
 #include "dft_consts.hpp"
 #include <algorithm>
@@ -467,7 +470,7 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
     constexpr int PP = (K1_MAXN / 2 + NT - 1) / NT;   // (k, N - k) pairs per thread, N < K1_MAXN
     extern __shared__ double2 z[];
     __shared__ double red[256];
-    const int N = n - 1, r = blockIdx.x, tid = threadIdx.x;
+    const int N = n - 1, r = blockIdx.x;
     double *d = (double *)z;
     const double2 *Wq0 = W + (N - 1);   // after the N - 1 pass twiddles: W^k, k = 0 .. N
     put_row_even<NT>(d, N, src + (long)r * n);
