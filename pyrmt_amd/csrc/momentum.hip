@@ -6,6 +6,7 @@
 // s2 -> k3, acc += 2 k3; s3 -> u* = u + dt/6 (acc + k4) (pre-BC), i.e. exactly the
 // reference's left-to-right (((k1 + 2 k2) + 2 k3) + k4).
 #include "rmt_internal.hpp"
+#include <utility>
 #include <algorithm>
 
 namespace rmt {
@@ -38,13 +39,13 @@ __global__ void __launch_bounds__(256) k_mom_prep_tiles(
     double w_t, double rho_s, double rho_f, double *__restrict__ sxx, double *__restrict__ sxy,
     double *__restrict__ syy, double *__restrict__ J, double *__restrict__ H,
     double *__restrict__ rho, unsigned char *__restrict__ solid, const int *__restrict__ tiles,
-    const int *__restrict__ count, int tiles_x) {
+    const int *__restrict__ count, int tiles_x, int jlo, int jhi) {
     if ((int)blockIdx.x >= *count) return;
     const int t = tiles[blockIdx.x];
     const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
     for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
         const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
-        if (j >= ny || i >= nx) continue;
+        if (j >= ny || i >= nx || j < jlo || j >= jhi) continue;   // rows [jlo, jhi) only
         const long c = (long)j * nx + i;
         Stress s{0.0, 0.0, 0.0, 1.0};
         if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1)
@@ -172,7 +173,8 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     int tiles_x, int ntiles, double *__restrict__ ku, double *__restrict__ kv,
     const double *__restrict__ ainu, const double *__restrict__ ainv, double *__restrict__ accu,
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
-    const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp) {
+    const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
+    int olo, int ohi) {
     __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
     if (dtp) {   // the same roundings as mom_stage's host constants
         const double dt = *dtp;
@@ -259,7 +261,7 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
         for (int it = 0; it < MS_NO; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
             const int j = j0 + ry, i = i0 + rx;
-            ok[it] = q < MS_TX * MS_TY && j < rw.je && i < nx;
+            ok[it] = q < MS_TX * MS_TY && j >= olo && j < ohi && i < nx;   // output rows
             const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
             // grad2(p) operands (functions.py:941): centred inside, one-sided at the edges
             // (inside: c+1 / c-1; i == 0: c+1; i == nx-1: c-1 as the "+s" operand; the "-s"
@@ -319,10 +321,13 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
 }
 
 // One fused stage launch: k_{s+1} -> (k1 | k2 | k3)[s], acc1 / acc2 / u* (see MomWork)
+// tlist: tiles of the whole grid (ws.jb = 0), outputs on rows [olo, ohi); else the tiles of
+// rows [ws.jb, ws.je)
 static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const double *u,
                      const double *v, const double *p, const double *sxx, const double *sxy,
                      const double *syy, const MomWork &W, double *u_new, double *v_new,
-                     RowWin ws, int ntiles, const int *tlist, const int *tcount) {
+                     RowWin ws, int ntiles, const int *tlist, const int *tcount, int olo,
+                     int ohi) {
     const int nx = ctx->nx, ny = ctx->ny, tiles_x = (nx + MS_TX - 1) / MS_TX;
     const double coef[4] = {0.0, 0.5 * P->dt, 0.5 * P->dt, P->dt}, dt6 = P->dt / 6.0;
     double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
@@ -333,7 +338,7 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
         u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid,
         P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx,
         tiles_x, ntiles, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, ainu, ainv, aou, aov,
-        u_new, v_new, ws, tlist, tcount, W.dtp);
+        u_new, v_new, ws, tlist, tcount, W.dtp, olo, ohi);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -388,7 +393,7 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
-                          nullptr, nullptr));
+                          nullptr, nullptr, ws.jb, ws.je));
     }
     RMT_CHECK(!unfused || (!win && !W.dtp), RMT_ENOTSUP,
               "RMT_MOM_UNFUSED: single-domain, host-dt only");
@@ -418,21 +423,26 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
 int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                    const double *p, const double *X1, const double *X2, const double *phi,
                    double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
-                   const MomWork &W, const int *tiles, const int *count, int max_tiles) {
+                   const MomWork &W, const int *tiles, const int *count, int max_tiles,
+                   const RowWin *win) {
     const int ny = ctx->ny, nx = ctx->nx;
     static_assert(MOM_TX == MS_TX && MOM_TY == MS_TY, "fixup tiles are the stage tiles");
     const double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
     const int tiles_x = (nx + MS_TX - 1) / MS_TX;
+    // the rows momentum_rk4 computes for this window: prep on w0 +- 7, stage s on w0 +- 2(3-s)
+    const RowWin w0 = win ? *win : RowWin{0, ny, 0, ny};
+    auto grow = [&](int m) { return std::pair<int, int>{std::max(w0.jb - m, 0), std::min(w0.je + m, ny)}; };
     k_mom_prep_tiles<<<max_tiles, 256, 0, ctx->stream>>>(
         X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
-        P->rho_f, sxx, sxy, syy, J, W.H, W.rho, W.solid, tiles, count, tiles_x);
+        P->rho_f, sxx, sxy, syy, J, W.H, W.rho, W.solid, tiles, count, tiles_x, grow(7).first,
+        grow(7).second);
     RMT_LAUNCHED();
-    const RowWin all{0, ny, 0, ny};
+    const RowWin all{0, ny, w0.lo, w0.hi};
     for (int s = 0; s < 4; ++s)
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, all, max_tiles,
-                          tiles, count));
+                          tiles, count, grow(2 * (3 - s)).first, grow(2 * (3 - s)).second));
     k_bc_edges<<<grid1d(2 * (nx + ny), 256), 256, 0, ctx->stream>>>(P->bc_kind, P->lid, u_new,
-                                                                     v_new, ny, nx, 0, ny);
+                                                                     v_new, ny, nx, w0.jb, w0.je);
     RMT_LAUNCHED();
     return RMT_OK;
 }

@@ -508,7 +508,8 @@ constexpr int MOM_TX = 64, MOM_TY = 16;
 int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                    const double *p, const double *X1, const double *X2, const double *phi,
                    double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
-                   const MomWork &W, const int *tiles, const int *count, int max_tiles);
+                   const MomWork &W, const int *tiles, const int *count, int max_tiles,
+                   const RowWin *win = nullptr);
 
 // ---------------------------------------------------------------------- poisson --
 // dev_root: nullptr -> p = solve - mean (functions.py:1119); else p = the raw solve and

@@ -70,6 +70,13 @@ struct rmt_slab {
     double *xs, *ys;
     double *scal, *part;
     int *flags;            // [0] flags, [4..5] extrapolation {fitted, aborted}
+    // the momentum beside the (replicated) chain, as rmt_sim_step: a speculative pass on a
+    // second stream from the pre-extrapolation map, re-run on the tiles a target can reach
+    hipStream_t st2 = nullptr;
+    hipEvent_t e_chain = nullptr, e_mom = nullptr;
+    int *tiles = nullptr, *tcount = nullptr, max_tiles = 0;
+    double dt_cur = 0;
+    bool spec = false;     // a speculative momentum is in flight for this step
     double *gv(double *q) const { return q - (long)lo * NX; }   // global-index view
 };
 
@@ -244,6 +251,29 @@ __global__ void k_slab_phi(const double *__restrict__ X1n, const double *__restr
     phi[c] = disc_phi(a, b, x0, y0, R);
 }
 
+// k_slab_phi on the listed fix-up tiles, rows [jb, je) only
+__global__ void __launch_bounds__(256) k_slab_phi_tiles(const double *__restrict__ X1n,
+                                                        const double *__restrict__ X2n,
+                                                        double x0, double y0, double R, int nx,
+                                                        int jb, int je, double *__restrict__ phi,
+                                                        double *__restrict__ X1,
+                                                        double *__restrict__ X2,
+                                                        const int *__restrict__ tiles,
+                                                        const int *__restrict__ count,
+                                                        int tiles_x) {
+    if ((int)blockIdx.x >= *count) return;
+    const int t = tiles[blockIdx.x];
+    const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
+    for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
+        const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
+        if (j < jb || j >= je || i >= nx) continue;
+        const long c = (long)j * nx + i;
+        const double a = X1n[c], b = X2n[c];
+        X1[c] = a; X2[c] = b;
+        phi[c] = disc_phi(a, b, x0, y0, R);
+    }
+}
+
 // ------------------------------------------------------------------ projection --
 // rhs = rho * divU / dt (k_scale_copy then k_div_scalar in ops.hip: the same two roundings)
 __global__ void k_slab_rhs(double *__restrict__ x, long n, double rho, double dt) {
@@ -357,6 +387,7 @@ int slab_cols(rmt_ctx *ctx, bool pack, double *Y, int rows, int nx, const int *c
 using namespace rmt;
 
 #define SLAB_RW(S) RowWin{0, 0, (S)->lo, (S)->hi}
+static int slab_momentum_pass(rmt_slab *S, double dt, bool fixup);
 
 extern "C" {
 
@@ -426,6 +457,16 @@ int rmt_slab_create(rmt_ctx *ctx, const rmt_sim_params *prm, int G, int rank,
         d = std::fmin(d, CFL * rho_min * std::pow(dx, 2.0) / (4.0 * mu_max));
     S->dt_const = std::fmin(d, prm->dt_cap);
     RMT_TRY(ensure_bytes(ctx, extrap_workspace(S->NY, S->NX, prm->layers)));
+    if (prm->layers >= 1 && prm->layers <= 12) {
+        int least = 0, greatest = 0;
+        RMT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        RMT_HIP(hipStreamCreateWithPriority(&S->st2, hipStreamNonBlocking, least));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_chain, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_mom, hipEventDisableTiming));
+        S->max_tiles = ((S->NX + MOM_TX - 1) / MOM_TX) * ((S->NY + MOM_TY - 1) / MOM_TY);
+        RMT_HIP(hipMalloc(&S->tiles, (S->max_tiles + 64) * sizeof(int)));
+        S->tcount = S->tiles + S->max_tiles;
+    }
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
     return RMT_OK;
@@ -433,7 +474,12 @@ int rmt_slab_create(rmt_ctx *ctx, const rmt_sim_params *prm, int G, int rank,
 
 int rmt_slab_destroy(rmt_slab *S) {
     if (!S) return RMT_OK;
+    if (S->st2) hipStreamSynchronize(S->st2);
     hipFree(S->block);
+    if (S->tiles) hipFree(S->tiles);
+    if (S->e_chain) hipEventDestroy(S->e_chain);
+    if (S->e_mom) hipEventDestroy(S->e_mom);
+    if (S->st2) hipStreamDestroy(S->st2);
     delete S;
     return RMT_OK;
 }
@@ -466,6 +512,7 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
     rmt_ctx *ctx = S->ctx;
     const rmt_sim_params &P = S->P;
     const int NX = S->NX, jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
+    S->dt_cur = dt;
     RMT_HIP(hipMemsetAsync(S->flags, 0, 8 * sizeof(int), ctx->stream));
     // max |u|^2 over the resident rows: bounds every velocity sample of the backtraces
     RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, (long)(S->hi - S->lo) * NX, S->scal + SC_M2RES));
@@ -491,19 +538,59 @@ int rmt_slab_extrapolate(rmt_slab *S, const double *gathered, const long long *c
     RMT_CHECK(S && counts && (gathered || cap == 0), RMT_EINVAL, "null argument");
     rmt_ctx *ctx = S->ctx;
     const rmt_sim_params &P = S->P;
-    RMT_TRY(slab_rim_extrapolate(ctx, gathered, counts, S->G, cap, S->X1d, S->X2d, S->bits, P.dx,
-                                 P.dy, P.layers, S->flags + 4, S->gv(S->X1n), S->gv(S->X2n),
-                                 (long)S->lo * S->NX, (long)S->hi * S->NX));
+    static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
+    S->spec = S->st2 && !no_overlap;
     const int jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
-    k_slab_phi<<<grid1d((long)(je - jb) * S->NX, 256), 256, 0, ctx->stream>>>(
+    if (S->spec) ctx->ev_chain = S->e_chain;
+    const int es = slab_rim_extrapolate(ctx, gathered, counts, S->G, cap, S->X1d, S->X2d, S->bits,
+                                        P.dx, P.dy, P.layers, S->flags + 4, S->gv(S->X1n),
+                                        S->gv(S->X2n), (long)S->lo * S->NX, (long)S->hi * S->NX);
+    ctx->ev_chain = nullptr;
+    RMT_TRY(es);
+    if (!S->spec) {
+        k_slab_phi<<<grid1d((long)(je - jb) * S->NX, 256), 256, 0, ctx->stream>>>(
+            S->gv(S->X1n), S->gv(S->X2n), P.x0, P.y0, P.R, S->NX, jb, je, S->gv(S->phi),
+            S->gv(S->X1), S->gv(S->X2));
+        RMT_LAUNCHED();
+        return RMT_OK;
+    }
+    // beside the chain (second stream, from the advected map before the rim write-back): phi
+    // and the slab's momentum; the main stream lists the tiles a target can reach
+    RMT_HIP(hipStreamWaitEvent(S->st2, S->e_chain, 0));
+    k_slab_phi<<<grid1d((long)(je - jb) * S->NX, 256), 256, 0, S->st2>>>(
         S->gv(S->X1n), S->gv(S->X2n), P.x0, P.y0, P.R, S->NX, jb, je, S->gv(S->phi),
         S->gv(S->X1), S->gv(S->X2));
     RMT_LAUNCHED();
-    return RMT_OK;
+    hipStream_t st = ctx->stream;
+    ctx->stream = S->st2;
+    const int ms = slab_momentum_pass(S, S->dt_cur, false);
+    ctx->stream = st;
+    RMT_TRY(ms);
+    RMT_HIP(hipEventRecord(S->e_mom, S->st2));
+    return extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount);
 }
 
 int rmt_slab_momentum(rmt_slab *S, double dt) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
+    if (S->spec) {
+        RMT_CHECK(dt == S->dt_cur, RMT_EINVAL, "slab momentum: dt differs from the advection's");
+        S->spec = false;
+        rmt_ctx *ctx = S->ctx;
+        const rmt_sim_params &P = S->P;
+        const int jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
+        RMT_HIP(hipStreamWaitEvent(ctx->stream, S->e_mom, 0));
+        k_slab_phi_tiles<<<S->max_tiles, 256, 0, ctx->stream>>>(
+            S->gv(S->X1n), S->gv(S->X2n), P.x0, P.y0, P.R, S->NX, jb, je, S->gv(S->phi),
+            S->gv(S->X1), S->gv(S->X2), S->tiles, S->tcount, (S->NX + MOM_TX - 1) / MOM_TX);
+        RMT_LAUNCHED();
+        return slab_momentum_pass(S, dt, true);
+    }
+    return slab_momentum_pass(S, dt, false);
+}
+}  // extern "C"
+
+// the slab's RK4 momentum on its window (fixup: only the listed tiles, after the chain)
+static int slab_momentum_pass(rmt_slab *S, double dt, bool fixup) {
     const rmt_sim_params &P = S->P;
     rmt_momentum_params M{};
     M.bc_kind = P.bc_kind; M.lid = P.lid; M.mu_s = P.mu_s; M.kappa = P.kappa;
@@ -513,10 +600,17 @@ int rmt_slab_momentum(rmt_slab *S, double dt) {
     const long nl = (long)(S->hi - S->lo) * S->NX, off = (long)S->lo * S->NX;
     MomWork W = mom_work(S->mw - off, nl, S->solid - off, S->flags + 1);
     const RowWin win{std::max(0, S->r0 - 1), std::min(S->NY, S->r1 + 1), S->lo, S->hi};
+    if (fixup)
+        return momentum_fixup(S->ctx, &M, S->gv(S->u), S->gv(S->v), S->gv(S->p), S->gv(S->X1),
+                              S->gv(S->X2), S->gv(S->phi), S->gv(S->us), S->gv(S->vs),
+                              S->gv(S->sxx), S->gv(S->sxy), S->gv(S->syy), S->gv(S->J), W,
+                              S->tiles, S->tcount, S->max_tiles, &win);
     return momentum_rk4(S->ctx, &M, S->gv(S->u), S->gv(S->v), S->gv(S->p), S->gv(S->X1),
                         S->gv(S->X2), S->gv(S->phi), S->gv(S->us), S->gv(S->vs), S->gv(S->sxx),
                         S->gv(S->sxy), S->gv(S->syy), S->gv(S->J), W, &win);
 }
+
+extern "C" {
 
 int rmt_slab_project_rows(rmt_slab *S, double dt) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
