@@ -317,6 +317,9 @@ int rmt_slab_destroy(rmt_slab *slab);
 int rmt_slab_info(rmt_slab *slab, int *ints8, double *dt_const);
 int rmt_slab_buffer(rmt_slab *slab, int id, void **dev_ptr);
 int rmt_slab_begin(rmt_slab *slab);                      /* scal[0] of the initial state  */
+/* optional, while the halo exchange is in flight: the advection of the rows that read no
+ * halo row; rmt_slab_advect (after the halo) then does the remaining rows */
+int rmt_slab_advect_interior(rmt_slab *slab, double dt);
 int rmt_slab_advect(rmt_slab *slab, double dt);          /* then: allgather known bit rows */
 int rmt_slab_rim_pack(rmt_slab *slab);                   /* then: allgather rim entries    */
 int rmt_slab_extrapolate(rmt_slab *slab, const double *gathered, const long long *counts,

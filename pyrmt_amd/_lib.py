@@ -125,6 +125,7 @@ SIGNATURES = {
     "rmt_slab_info": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "rmt_slab_buffer": (_I, [_P, _I, ctypes.POINTER(_P)]),
     "rmt_slab_begin": (_I, [_P]),
+    "rmt_slab_advect_interior": (_I, [_P, _D]),
     "rmt_slab_advect": (_I, [_P, _D]),
     "rmt_slab_rim_pack": (_I, [_P]),
     "rmt_slab_extrapolate": (_I, [_P, _P, ctypes.POINTER(ctypes.c_longlong), ctypes.c_longlong]),

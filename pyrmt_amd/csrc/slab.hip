@@ -43,7 +43,7 @@ using rmt::u64;
 namespace rmt {
 constexpr int SLAB_MAXG = 64;
 enum { SC_M2 = 0, SC_DIAG = 1, SC_FLAGS = 11, SC_COUNT = 12, SC_ROOT = 13, SC_FIT = 14,
-       SC_M2RES = 15, SC_N = 16 };
+       SC_M2RES = 15, SC_N = 16, SC_M2OWN = 16 /* device-only, past the exported block */ };
 enum { FL_NONFINITE = 1, FL_HALO = 2, FL_EXABORT = 4 };
 struct Splits { int v[SLAB_MAXG + 1]; };
 struct Counts { long long c[SLAB_MAXG]; };
@@ -77,6 +77,7 @@ struct rmt_slab {
     int *tiles = nullptr, *tcount = nullptr, max_tiles = 0;
     double dt_cur = 0;
     bool spec = false;     // a speculative momentum is in flight for this step
+    bool interior = false; // rmt_slab_advect_interior ran for this step
     double *gv(double *q) const { return q - (long)lo * NX; }   // global-index view
 };
 
@@ -507,20 +508,59 @@ int rmt_slab_begin(rmt_slab *S) {
     return reduce_maxsq2(S->ctx, S->u + o, S->v + o, n, S->scal + SC_M2);
 }
 
+// rows [r0 + 10, r1 - 10): every sample of their backtraces lies in owned rows (the step
+// moves a departure point by far less than a cell), so they need no halo row and can run
+// while the halo exchange is in flight; a NaN-propagating max |u|^2 over the owned rows
+// bounds their velocities (bilinear rows checked against [r0, r1))
+static void slab_interior_rows(const rmt_slab *S, int *ib, int *ie) {
+    *ib = S->r0 + 10; *ie = std::max(*ib, S->r1 - 10);
+}
+int rmt_slab_advect_interior(rmt_slab *S, double dt) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    rmt_ctx *ctx = S->ctx;
+    const rmt_sim_params &P = S->P;
+    const int NX = S->NX;
+    int ib, ie;
+    slab_interior_rows(S, &ib, &ie);
+    S->dt_cur = dt;
+    S->interior = true;
+    RMT_HIP(hipMemsetAsync(S->flags, 0, 8 * sizeof(int), ctx->stream));
+    if (ie > ib) {
+        const long o = (long)(S->r0 - S->lo) * NX, no = (long)(S->r1 - S->r0) * NX;
+        RMT_TRY(reduce_maxsq2_nan(ctx, S->u + o, S->v + o, no, S->scal + SC_M2OWN));
+        k_slab_sl<<<dim3((NX + 255) / 256, ie - ib), 256, 0, ctx->stream>>>(
+            S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt,
+            P.dx, P.dy, P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
+            S->flags, ib, ie, S->r0, S->r1, S->scal + SC_M2OWN);
+        RMT_LAUNCHED();
+    }
+    return RMT_OK;
+}
+
 int rmt_slab_advect(rmt_slab *S, double dt) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
     rmt_ctx *ctx = S->ctx;
     const rmt_sim_params &P = S->P;
     const int NX = S->NX, jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
+    RMT_CHECK(!S->interior || dt == S->dt_cur, RMT_EINVAL, "slab advect: dt differs");
+    const bool in = S->interior;
+    S->interior = false;
     S->dt_cur = dt;
-    RMT_HIP(hipMemsetAsync(S->flags, 0, 8 * sizeof(int), ctx->stream));
+    if (!in) RMT_HIP(hipMemsetAsync(S->flags, 0, 8 * sizeof(int), ctx->stream));
     // max |u|^2 over the resident rows: bounds every velocity sample of the backtraces
     RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, (long)(S->hi - S->lo) * NX, S->scal + SC_M2RES));
-    k_slab_sl<<<dim3((NX + 255) / 256, je - jb), 256, 0, ctx->stream>>>(
-        S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt, P.dx,
-        P.dy, P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre), S->flags, jb, je,
-        S->lo, S->hi, S->scal + SC_M2RES);
-    RMT_LAUNCHED();
+    int ib = je, ie = je;   // rows done by rmt_slab_advect_interior
+    if (in) slab_interior_rows(S, &ib, &ie);
+    const int segs[2][2] = {{jb, std::min(ib, je)}, {std::max(ie, jb), je}};
+    for (int k = 0; k < (in ? 2 : 1); ++k) {
+        const int a = in ? segs[k][0] : jb, b = in ? segs[k][1] : je;
+        if (b <= a) continue;
+        k_slab_sl<<<dim3((NX + 255) / 256, b - a), 256, 0, ctx->stream>>>(
+            S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt,
+            P.dx, P.dy, P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
+            S->flags, a, b, S->lo, S->hi, S->scal + SC_M2RES);
+        RMT_LAUNCHED();
+    }
     k_slab_bits<<<dim3((NX + 255) / 256, S->r1 - S->r0), 256, 0, ctx->stream>>>(
         S->gv(S->phi_pre), NX, S->W, S->bits, S->r0);
     RMT_LAUNCHED();

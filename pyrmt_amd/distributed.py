@@ -77,6 +77,12 @@ class LocalComm:
                         b = min(t + nrows, s.hi + e)
                         dst[t - s.lo:b - s.lo].copy_(o.view(name)[t - o.lo:b - o.lo])
 
+    def halo_start(self, slabs, planes, nrows):
+        self.halo(slabs, planes, nrows)
+
+    def halo_finish(self, handle):
+        pass
+
     def allgather_rows(self, slabs, name):
         for s in slabs:
             dst = s.view(name)
@@ -132,6 +138,12 @@ class TorchComm:
             dst.copy_(src)
 
     def halo(self, slabs, planes, nrows):
+        self.halo_finish(self.halo_start(slabs, planes, nrows))
+
+    def halo_start(self, slabs, planes, nrows):
+        """Post the halo sends / receives; the interior work runs before halo_finish.  With
+        RCCL the receives land on RCCL's stream and halo_finish only orders the compute
+        stream after them (no host wait)."""
         (s,) = slabs
         dist, k = self.dist, self.rank
         ops, post = [], []
@@ -157,15 +169,20 @@ class TorchComm:
                 ops += [(dist.isend, snd, k + 1), (dist.irecv, rb, k + 1)]
                 post.append((rcv, rb))
         if not ops:
-            return
+            return None
         if self.staged:
             reqs = [f(t, peer, group=self.group) for f, t, peer in ops]
-            for r in reqs:
-                r.wait()
         else:
             p2p = [dist.P2POp(f, t, peer, group=self.group) for f, t, peer in ops]
-            for r in dist.batch_isend_irecv(p2p):
-                r.wait()
+            reqs = dist.batch_isend_irecv(p2p)
+        return reqs, post
+
+    def halo_finish(self, handle):
+        if handle is None:
+            return
+        reqs, post = handle
+        for r in reqs:
+            r.wait()
         for rcv, rb in post:
             self._back(rcv, rb)
 
@@ -377,11 +394,14 @@ class DistributedSim:
                 break
             ev = []
             self._mark(ev)
-            comm.halo(S, ("u", "v", "p", "X1", "X2"), HALO)
             m2 = self.m2
             dt = min(self.dt_const, self.cfl * self.dx / (math.sqrt(m2) + 1e-6))
             if self.t + dt > t_end:
                 dt = t_end - self.t
+            # halo in flight while the rows that need none are advected
+            h = comm.halo_start(S, ("u", "v", "p", "X1", "X2"), HALO)
+            self._call("rmt_slab_advect_interior", dt)
+            comm.halo_finish(h)
             self._mark(ev)
             # advection + exact extrapolation (band replicated on every slab)
             self._call("rmt_slab_advect", dt)
