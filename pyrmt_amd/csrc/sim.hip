@@ -10,6 +10,7 @@
 //   diagnostics: centroid of phi <= 0, J min/max (+ KE, SE, dissipation)
 // State (u, v, p, X1, X2) stays in HBM; one host sync per step reads dt.
 #include "rmt_internal.hpp"
+#include <utility>
 #include <vector>
 
 namespace rmt {
@@ -56,6 +57,10 @@ struct rmt_sim {
     unsigned long long *rimw = nullptr;
     int *rimcnt = nullptr;
     hipEvent_t e_bits = nullptr;
+    // the next step's known plane, written by the phi kernels of this step (nx % 64 == 0):
+    // double-buffered with kbits, valid from the second step of a call on
+    unsigned long long *kbits_next = nullptr;
+    bool bits_ready = false;
     bool prof = false;
     hipEvent_t pev[7] = {};
     double ms[8] = {};
@@ -177,18 +182,28 @@ __global__ void k_mask_mul(double *__restrict__ X1, double *__restrict__ X2,
 
 // phi = rebuild(X1n, X2n) (functions.py:1366) fused with the copy of the extrapolated
 // map back into the state planes (keeps rmt_sim_field pointers stable).
+// nbits (nullable; nx % 64 == 0): the known plane of the NEXT step's advection, phi < 0 of
+// this map (k_sim_bits' bits), one 64-cell word per wave
 __global__ void k_phi_rebuild(const double *__restrict__ X1n, const double *__restrict__ X2n,
                               long n, int shape, double x0, double y0, double R,
                               double *__restrict__ phi, double *__restrict__ X1,
-                              double *__restrict__ X2) {
+                              double *__restrict__ X2, unsigned long long *__restrict__ nbits) {
     long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (c >= n) return;
-    if (shape == RMT_SHAPE_DISC) {
-        double a = X1n[c], b = X2n[c];
-        X1[c] = a; X2[c] = b;
-        phi[c] = disc_phi(a, b, x0, y0, R);
-    } else {
-        phi[c] = 1.0;
+    bool known = false;
+    if (c < n) {
+        if (shape == RMT_SHAPE_DISC) {
+            double a = X1n[c], b = X2n[c];
+            X1[c] = a; X2[c] = b;
+            const double ph = disc_phi(a, b, x0, y0, R);
+            phi[c] = ph;
+            known = ph < 0;
+        } else {
+            phi[c] = 1.0;
+        }
+    }
+    if (nbits) {
+        const unsigned long long w = __ballot(known);
+        if ((threadIdx.x & 63) == 0 && c < n) nbits[c >> 6] = w;
     }
 }
 
@@ -200,17 +215,26 @@ __global__ void __launch_bounds__(256) k_phi_tiles(const double *__restrict__ X1
                                                    double *__restrict__ X1,
                                                    double *__restrict__ X2,
                                                    const int *__restrict__ tiles,
-                                                   const int *__restrict__ count, int tiles_x) {
+                                                   const int *__restrict__ count, int tiles_x,
+                                                   unsigned long long *__restrict__ nbits) {
     if ((int)blockIdx.x >= *count) return;
     const int t = tiles[blockIdx.x];
     const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
     for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
         const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
-        if (j >= ny || i >= nx) continue;
-        const long c = (long)j * nx + i;
-        const double a = X1n[c], b = X2n[c];
-        X1[c] = a; X2[c] = b;
-        phi[c] = disc_phi(a, b, x0, y0, R);
+        bool known = false;
+        if (j < ny && i < nx) {
+            const long c = (long)j * nx + i;
+            const double a = X1n[c], b = X2n[c];
+            X1[c] = a; X2[c] = b;
+            const double ph = disc_phi(a, b, x0, y0, R);
+            phi[c] = ph;
+            known = ph < 0;
+        }
+        if (nbits) {   // a wave is one 64-cell word of row j (tile columns are word-aligned)
+            const unsigned long long w = __ballot(known);
+            if ((threadIdx.x & 63) == 0 && j < ny) nbits[(long)j * (nx >> 6) + (i0 >> 6)] = w;
+        }
     }
 }
 
@@ -446,11 +470,13 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     S->m2n = ((nx + 255) / 256) * ny;
     const size_t Wn = (size_t)(nx + 63) / 64;
     RMT_HIP(hipMalloc(&S->m2part, ((size_t)S->m2n + (size_t)RING_N * RING_VALS + ny / 8 + 8 +
-                                   (size_t)ny * Wn + ny / 2 + 8) * sizeof(double)));
+                                   (size_t)ny * Wn + ny / 2 + 8 + (size_t)ny * Wn) *
+                                      sizeof(double)));
     S->ring = S->m2part + S->m2n;
     S->rowmark = (unsigned char *)(S->ring + (size_t)RING_N * RING_VALS);
     S->rimw = (unsigned long long *)(S->ring + (size_t)RING_N * RING_VALS + ny / 8 + 8);
     S->rimcnt = (int *)(S->rimw + (size_t)ny * Wn);
+    S->kbits_next = (unsigned long long *)((double *)S->rimcnt + ny / 2 + 8);
     if (S->st2) RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
     if (S->st2 && prm->rho_f > 0) {
         RMT_TRY(dct_plan(ctx, prm->dx, prm->dy));
@@ -542,6 +568,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         }
         return RMT_OK;
     };
+    S->bits_ready = false;   // the caller may have changed the map between calls
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end)) break;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[0], st));
@@ -564,6 +591,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         }
         const double *dtp = async ? sc + 1 : nullptr;
         const bool solid = P.shape != RMT_SHAPE_NONE;
+        // this step's phi kernels also write the next step's known plane (split advection)
+        unsigned long long *nb = (solid && P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits &&
+                                  nx % 64 == 0) ? S->kbits_next : nullptr;
         rmt_momentum_params M{};
         M.bc_kind = P.bc_kind; M.lid = P.lid; M.mu_s = P.mu_s; M.kappa = P.kappa;
         M.eta_s = P.eta_s; M.rho_s = P.rho_s; M.rho_f = P.rho_f; M.mu_f = P.mu_f; M.w_t = P.w_t;
@@ -584,8 +614,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 // known plane -> rim words -> the rim's advection here; the rest on the second
                 // stream, beside the extrapolation (which reads rim cells only)
                 const dim3 gsl((nx + 255) / 256, ny);
-                k_sim_bits<<<gsl, 256, 0, st>>>(S->X1, S->X2, nx, P.x0, P.y0, P.R, S->kbits);
-                RMT_LAUNCHED();
+                if (!S->bits_ready) {
+                    k_sim_bits<<<gsl, 256, 0, st>>>(S->X1, S->X2, nx, P.x0, P.y0, P.R, S->kbits);
+                    RMT_LAUNCHED();
+                }
                 RMT_TRY(rim_words(ctx, S->kbits, ny, nx, (nx + 63) / 64, S->rimw, S->rimcnt));
                 RMT_HIP(hipEventRecord(S->e_bits, st));
                 k_sim_sl<<<gsl, 256, 0, st>>>(
@@ -640,7 +672,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     RMT_LAUNCHED();
                 }
                 k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R,
-                                                      S->phi, S->X1, S->X2);
+                                                      S->phi, S->X1, S->X2, nb);
                 RMT_LAUNCHED();
                 ctx->stream = S->st2;
                 int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi,
@@ -670,7 +702,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
             k_phi_tiles<<<S->max_tiles, 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
                                                        S->phi, S->X1, S->X2, S->tiles, S->tcount,
-                                                       tiles_x);
+                                                       tiles_x, nb);
             RMT_LAUNCHED();
             RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
                                    S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,
@@ -678,7 +710,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         } else {
             // 4. phi from the advected + extrapolated map
             k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R, S->phi,
-                                              S->X1, S->X2);
+                                              S->X1, S->X2, nb);
             // 5. momentum (RK4)
             RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
                                  S->sxx, S->sxy, S->syy, S->J, W));
@@ -714,6 +746,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, e);
             k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
             RMT_LAUNCHED();
+            if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
             if (++slot == RING_N) RMT_TRY(flush());
             continue;
         }
@@ -738,6 +771,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 S->ms[7] += f; S->calls[7] += 1;
             }
         }
+        if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
         RMT_TRY(sim_record(S, dv, hv[0], dt, fl));
     }
     return flush();
