@@ -728,7 +728,7 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                                                            ws.ctl, 0, ny);
         k_ex_none_fin<<<1, 1, 0, ctx->stream>>>(ws.ctl);
         RMT_LAUNCHED();
-        RMT_TRY(extrap_chain_launch(ctx, ws, X1o, X2o, dx, dy, max_layers));
+        RMT_TRY(extrap_chain_prep(ctx, ws, X1o, X2o, dx, dy, max_layers));
     }
     const int *ctl = chain ? ws.ctl : nullptr;
     k_ex_dilate<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(
@@ -764,6 +764,8 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
         hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
     }
     if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
+    // the chain after the sweep: both read the fallback flag the chain prep settled
+    if (chain) RMT_TRY(extrap_chain_run(ctx, ws, X1o, X2o, max_layers));
     if (force == 3) {   // diagnostic: report an abort (tests of the callers' error paths)
         const int one = 1;
         RMT_HIP(hipMemcpyAsync(ws.status + 1, &one, sizeof(int), hipMemcpyHostToDevice,

@@ -925,8 +925,11 @@ bool extrap_chain_supported(int ny, int nx, int ML) {
     return ML >= 1 && ML <= EX_MAXL && ny >= 3 && nx >= 3;
 }
 
-int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
-                        double dx, double dy, int ML) {
+// the chip-wide passes that turn the band into chain records (the chain kernel itself is
+// extrap_chain_run, launched after the fallback sweep's launch so that the sweep -- an
+// early exit unless a capacity limit tripped -- does not wait behind the chain)
+int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
+                      double dx, double dy, int ML) {
     const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
     hipStream_t st = ctx->stream;
     const unsigned rows = grid1d(ny, 4);
@@ -951,6 +954,15 @@ int extrap_chain_launch(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
     k_ex_local<<<1, 1024, 0, st>>>(ws, ML);
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
+                     int ML) {
+    hipStream_t st = ctx->stream;
+    static const int nparts = getenv("RMT_CH_PARTS") ? std::min(CH_MAXP, std::max(1,
+                                  atoi(getenv("RMT_CH_PARTS")))) : 2;
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
     if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status, nullptr};
