@@ -61,6 +61,7 @@ struct rmt_sim {
     // double-buffered with kbits, valid from the second step of a call on
     unsigned long long *kbits_next = nullptr;
     bool bits_ready = false;
+    int *segs = nullptr;     // rim row segments (k_rim_segments): ny * ceil(nx / 256) + count
     bool prof = false;
     hipEvent_t pev[7] = {};
     double ms[8] = {};
@@ -70,29 +71,25 @@ struct rmt_sim {
 namespace rmt {
 
 // SL advection of (X1, X2) with the pre-advection level set and mask (one pass).
-__global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict__ X2,
-                         const double *__restrict__ a, const double *__restrict__ b,
-                         const double *__restrict__ xs, const double *__restrict__ ys, int ny,
-                         int nx, double dt_arg, double dx, double dy, int shape, double x0,
-                         double y0, double R, double *__restrict__ X1n, double *__restrict__ X2n,
-                         double *__restrict__ phi_pre, int *bad,
-                         unsigned long long *__restrict__ kbits, const double *m2,
-                         const double *__restrict__ dtp = nullptr, int mode = 0,
-                         const unsigned long long *__restrict__ rimw = nullptr,
-                         const int *__restrict__ rimcnt = nullptr) {
-    const double dt = dtp ? *dtp : dt_arg;
-    // grid (ceil(nx / 256), ny): a wave covers 64 cells of one row, so the extrapolation's
-    // known plane (phi_pre < 0, 64-cell words) comes out of the same pass (kbits optional).
-    // mode 1: only the rim cells (rimw), mode 2: every other cell -- the same per-cell result,
-    // split so that the extrapolation can start after the (small) rim part
-    const int j = blockIdx.y, i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
+// One 256-cell row segment (j, i0) of the SL advection of (X1, X2) with the pre-advection
+// level set and mask.  A wave covers 64 cells of one row, so the extrapolation's known plane
+// (phi_pre < 0, 64-cell words) comes out of the same pass (kbits optional).  mode 1: only the
+// rim cells (rimw), mode 2: every other cell -- the same per-cell result, split so that the
+// extrapolation can start after the (small) rim part.  Block-uniform control flow (the zero
+// test is a block reduction).
+__device__ __forceinline__ void sl_segment(
+    const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ a,
+    const double *__restrict__ b, const double *__restrict__ xs, const double *__restrict__ ys,
+    int ny, int nx, double dt, double dx, double dy, double x0, double y0, double R,
+    double *__restrict__ X1n, double *__restrict__ X2n, double *__restrict__ phi_pre, int *bad,
+    unsigned long long *__restrict__ kbits, const double *m2, int mode,
+    const unsigned long long *__restrict__ rimw, int j, int i0) {
+    const int i = i0 + threadIdx.x;
     const bool in = i < nx;
     const long c = (long)j * nx + i;
     bool mine = true;
-    if (mode == 1 && rimcnt[j] == 0) return;   // no rim cell in this row
     if (mode) {
         const bool rim = in && ((rimw[(long)j * ((nx + 63) / 64) + (i >> 6)] >> (i & 63)) & 1);
-        if (mode == 1 && !__syncthreads_or(rim)) return;   // whole block outside the rim
         mine = (mode == 1) == rim;
     }
     const bool zero = sl_skip_ok(m2, dt, fmin(dx, dy)) &&
@@ -123,6 +120,54 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
         const unsigned long long w = __ballot(known);
         if ((threadIdx.x & 63) == 0 && (i >> 6) < (nx + 63) / 64)
             kbits[(long)j * ((nx + 63) / 64) + (i >> 6)] = w;
+    }
+}
+
+// grid (ceil(nx / 256), ny)
+__global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict__ X2,
+                         const double *__restrict__ a, const double *__restrict__ b,
+                         const double *__restrict__ xs, const double *__restrict__ ys, int ny,
+                         int nx, double dt_arg, double dx, double dy, int shape, double x0,
+                         double y0, double R, double *__restrict__ X1n, double *__restrict__ X2n,
+                         double *__restrict__ phi_pre, int *bad,
+                         unsigned long long *__restrict__ kbits, const double *m2,
+                         const double *__restrict__ dtp = nullptr, int mode = 0,
+                         const unsigned long long *__restrict__ rimw = nullptr) {
+    (void)shape;
+    const double dt = dtp ? *dtp : dt_arg;
+    sl_segment(X1, X2, a, b, xs, ys, ny, nx, dt, dx, dy, x0, y0, R, X1n, X2n, phi_pre, bad, kbits,
+               m2, mode, rimw, blockIdx.y, blockIdx.x * 256);
+}
+
+// the row segments holding a rim cell, listed (any order)
+__global__ void __launch_bounds__(256) k_rim_segments(const unsigned long long *__restrict__ rimw,
+                                                      int ny, int nx, int *__restrict__ list,
+                                                      int *__restrict__ count) {
+    const int nbx = (nx + 255) / 256, W = (nx + 63) / 64;
+    const long id = blockIdx.x * 256L + threadIdx.x;
+    if (id >= (long)ny * nbx) return;
+    const int j = (int)(id / nbx), bx = (int)(id % nbx);
+    unsigned long long any = 0;
+    for (int w = 4 * bx; w < min(4 * bx + 4, W); ++w) any |= rimw[(long)j * W + w];
+    if (any) list[atomicAdd(count, 1)] = (int)id;
+}
+// mode 1 over the listed segments: a fixed grid walking the list (its length is on the
+// device only)
+__global__ void k_sim_sl_rim(const double *__restrict__ X1, const double *__restrict__ X2,
+                             const double *__restrict__ a, const double *__restrict__ b,
+                             const double *__restrict__ xs, const double *__restrict__ ys,
+                             int ny, int nx, double dt_arg, double dx, double dy, double x0,
+                             double y0, double R, double *__restrict__ X1n,
+                             double *__restrict__ X2n, int *bad, const double *m2,
+                             const double *__restrict__ dtp,
+                             const unsigned long long *__restrict__ rimw,
+                             const int *__restrict__ list, const int *__restrict__ count) {
+    const double dt = dtp ? *dtp : dt_arg;
+    const int nbx = (nx + 255) / 256, cnt = *count;
+    for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
+        const int id = list[k];
+        sl_segment(X1, X2, a, b, xs, ys, ny, nx, dt, dx, dy, x0, y0, R, X1n, X2n, nullptr, bad,
+                   nullptr, m2, 1, rimw, id / nbx, (id % nbx) * 256);
     }
 }
 
@@ -470,13 +515,14 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     S->m2n = ((nx + 255) / 256) * ny;
     const size_t Wn = (size_t)(nx + 63) / 64;
     RMT_HIP(hipMalloc(&S->m2part, ((size_t)S->m2n + (size_t)RING_N * RING_VALS + ny / 8 + 8 +
-                                   (size_t)ny * Wn + ny / 2 + 8 + (size_t)ny * Wn) *
-                                      sizeof(double)));
+                                   (size_t)ny * Wn + ny / 2 + 8 + (size_t)ny * Wn +
+                                   (size_t)ny * ((nx + 255) / 256) / 2 + 8) * sizeof(double)));
     S->ring = S->m2part + S->m2n;
     S->rowmark = (unsigned char *)(S->ring + (size_t)RING_N * RING_VALS);
     S->rimw = (unsigned long long *)(S->ring + (size_t)RING_N * RING_VALS + ny / 8 + 8);
     S->rimcnt = (int *)(S->rimw + (size_t)ny * Wn);
     S->kbits_next = (unsigned long long *)((double *)S->rimcnt + ny / 2 + 8);
+    S->segs = (int *)(S->kbits_next + (size_t)ny * Wn);
     if (S->st2) RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
     if (S->st2 && prm->rho_f > 0) {
         RMT_TRY(dct_plan(ctx, prm->dx, prm->dy));
@@ -620,10 +666,13 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 }
                 RMT_TRY(rim_words(ctx, S->kbits, ny, nx, (nx + 63) / 64, S->rimw, S->rimcnt));
                 RMT_HIP(hipEventRecord(S->e_bits, st));
-                k_sim_sl<<<gsl, 256, 0, st>>>(
-                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
-                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, nullptr, sc, dtp, 1,
-                    S->rimw, S->rimcnt);
+                const long nseg = (long)ny * ((nx + 255) / 256);
+                int *scount = S->segs + nseg;
+                RMT_HIP(hipMemsetAsync(scount, 0, sizeof(int), st));
+                k_rim_segments<<<grid1d(nseg, 256), 256, 0, st>>>(S->rimw, ny, nx, S->segs, scount);
+                k_sim_sl_rim<<<1024, 256, 0, st>>>(
+                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.x0, P.y0,
+                    P.R, S->X1n, S->X2n, S->flag, sc, dtp, S->rimw, S->segs, scount);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
                 k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, st>>>(
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
@@ -668,7 +717,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, S->st2>>>(
                         S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
                         P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, nullptr, sc, dtp, 2,
-                        S->rimw, S->rimcnt);
+                        S->rimw);
                     RMT_LAUNCHED();
                 }
                 k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R,
