@@ -371,19 +371,14 @@ __global__ void k_apply_bc(int kind, double lid, double *u, double *v, int ny, i
 // -------------------------------------------------------------------- projection ----
 // rows [jb, je) of an nx-wide plane: blockIdx.y = row - jb, 256 columns per block
 static inline dim3 rows_grid(int nx, int jb, int je) { return dim3((nx + 255) / 256, je - jb); }
-__global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
-                                const double *__restrict__ p, int ny, int nx, double d_f,
-                                double dx, double dy, double *__restrict__ divU, int jb, int je,
-                                double rho = 0.0, double dt = 1.0,
-                                const double *__restrict__ dtp = nullptr,
-                                const unsigned char *__restrict__ rowmark = nullptr) {
-    if (rowmark && !rowmark[jb + blockIdx.y]) return;   // only the listed rows
-    if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
-    // rho > 0: the projection's rhs = (rho * divU) / dt (functions.py:1331, the same two
-    // roundings as the separate scale and divide passes).  Grid: rows_grid (one block row
-    // per grid row, no per-cell division).
-    const int j = jb + (int)blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nx || j >= je) return;
+// rho > 0: the projection's rhs = (rho * divU) / dt (functions.py:1331, the same two
+// roundings as the separate scale and divide passes)
+__device__ __forceinline__ void div_rc_cell(const double *__restrict__ a,
+                                            const double *__restrict__ b,
+                                            const double *__restrict__ p, int ny, int nx,
+                                            double d_f, double dx, double dy,
+                                            double *__restrict__ divU, double rho, double dt,
+                                            int j, int i) {
     const long c = (long)j * nx + i;
     if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) {
         divU[c] = rho > 0 ? (rho * 0.0) / dt : 0.0;
@@ -400,6 +395,39 @@ __global__ void k_divergence_rc(const double *__restrict__ a, const double *__re
     double vs = 0.5 * (b[c - nx] + b[c]) - d_f * ((p[c] - p[c - nx]) / dy - 0.5 * (gyd + gyc));
     const double d = (ue - uw) / dx + (vn - vs) / dy;
     divU[c] = rho > 0 ? (rho * d) / dt : d;
+}
+__global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
+                                const double *__restrict__ p, int ny, int nx, double d_f,
+                                double dx, double dy, double *__restrict__ divU, int jb, int je,
+                                double rho = 0.0, double dt = 1.0,
+                                const double *__restrict__ dtp = nullptr,
+                                const unsigned char *__restrict__ rowmark = nullptr) {
+    if (rowmark && !rowmark[jb + blockIdx.y]) return;   // only the listed rows
+    if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
+    // Grid: rows_grid (one block row per grid row, no per-cell division).
+    const int j = jb + (int)blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nx || j >= je) return;
+    div_rc_cell(a, b, p, ny, nx, d_f, dx, dy, divU, rho, dt, j, i);
+}
+// The rhs on the listed MOM_TX x MOM_TY tiles grown by one cell (the cells whose stencil
+// reads a u*, v* the momentum fix-up rewrote); one block per tile.  Overlapping grown tiles
+// write the same value twice.
+__global__ void __launch_bounds__(256) k_divergence_tiles(
+    const double *__restrict__ a, const double *__restrict__ b, const double *__restrict__ p,
+    int ny, int nx, double dx, double dy, double *__restrict__ divU, double rho, double dt,
+    const double *__restrict__ dtp, const int *__restrict__ tiles,
+    const int *__restrict__ count, int tiles_x) {
+    if ((int)blockIdx.x >= *count) return;
+    if (dtp) dt = *dtp;
+    const double d_f = dt / rho;   // as the host's dt / rho
+    const int t = tiles[blockIdx.x];
+    const int i0 = (t % tiles_x) * MOM_TX - 1, j0 = (t / tiles_x) * MOM_TY - 1;
+    constexpr int TW = MOM_TX + 2, TH = MOM_TY + 2;
+    for (int e = threadIdx.x; e < TW * TH; e += blockDim.x) {
+        const int j = j0 + e / TW, i = i0 + e % TW;
+        if (j >= 0 && j < ny && i >= 0 && i < nx)
+            div_rc_cell(a, b, p, ny, nx, d_f, dx, dy, divU, rho, dt, j, i);
+    }
 }
 __global__ void k_divergence_central(const double *__restrict__ a, const double *__restrict__ b,
                                      int ny, int nx, double dx, double dy,
@@ -768,14 +796,21 @@ namespace rmt {
 // the row DCT-I of every row (or of the marked rows only) into scratch, then the rest.
 int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                     double dy, const double *dtp, double dt, double rho, const double *p_prev,
-                    const unsigned char *rowmark) {
-    RMT_CHECK(p_prev && rho > 0, RMT_EINVAL, "projection_rows: bad arguments");
+                    const unsigned char *rowmark, const int *tiles, const int *tcount,
+                    int max_tiles) {
+    RMT_CHECK(p_prev && rho > 0 && (!tiles || rowmark), RMT_EINVAL,
+              "projection_rows: bad arguments");
     const long n = (long)ctx->ny * ctx->nx;
     RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
     double *rhs = ctx->scratch, *pc = rhs + n;
-    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
-        a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx, dy, rhs, 0, ctx->ny, rho, dt, dtp,
-        rowmark);
+    if (tiles)   // the rhs of the other cells of the marked rows is still in scratch
+        k_divergence_tiles<<<max_tiles, 256, 0, ctx->stream>>>(
+            a_star, b_star, p_prev, ctx->ny, ctx->nx, dx, dy, rhs, rho, dt, dtp, tiles, tcount,
+            (ctx->nx + MOM_TX - 1) / MOM_TX);
+    else
+        k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
+            a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx, dy, rhs, 0, ctx->ny, rho, dt,
+            dtp, rowmark);
     RMT_LAUNCHED();
     RMT_TRY(dct_plan(ctx, dx, dy));
     return dct_pass(ctx, false, 0, rhs, pc, ctx->ny, 0, 1.0, nullptr, rowmark);

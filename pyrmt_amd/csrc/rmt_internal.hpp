@@ -445,7 +445,8 @@ int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int 
 // the scalar dt)
 int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                     double dy, const double *dtp, double dt, double rho, const double *p_prev,
-                    const unsigned char *rowmark);
+                    const unsigned char *rowmark, const int *tiles = nullptr,
+                    const int *tcount = nullptr, int max_tiles = 0);
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,

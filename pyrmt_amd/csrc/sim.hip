@@ -767,14 +767,15 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[4], st));
         // 6. projection (constant density rho_f; Neumann DCT-I)
         if (overlap && S->split_proj) {
-            // redo the rows the fix-up tiles reach, then the column pass and the rest
+            // redo the rhs on the fix-up tiles (+1 cell) and the row DCT of the rows they
+            // reach, then the column pass and the rest
             const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
             RMT_HIP(hipMemsetAsync(S->rowmark, 0, ny, st));
             k_mark_rows<<<S->max_tiles, 64, 0, st>>>(S->tiles, S->tcount, tiles_x, ny, S->rowmark);
             RMT_LAUNCHED();
             RMT_HIP(hipStreamWaitEvent(st, S->e_rows, 0));
             RMT_TRY(projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
-                                    S->rowmark));
+                                    S->rowmark, S->tiles, S->tcount, S->max_tiles));
             RMT_TRY(projection_finish(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, P.bc_kind,
                                       P.lid, S->p, S->u, S->v, S->p,
                                       async ? S->m2part : nullptr));
