@@ -157,6 +157,11 @@ int rmt_momentum_step_rk4(rmt_ctx *ctx, const rmt_momentum_params *prm, const do
                           const double *phi, double *u_new, double *v_new, double *sxx,
                           double *sxy, double *syy, double *J);
 
+/* librmt diagnostic (no reference counterpart): 0 (default) one LDS-tiled kernel per RK4
+ * stage, 1 the four stages of a tile in one temporally blocked kernel (per-stage kernels for
+ * periodic BCs), 2 unfused per-cell passes.  Bit-identical results in every mode. */
+int rmt_momentum_set_mode(int mode);
+
 /* ---- projection (functions.py:1005-1364) ------------------------------------------- */
 /* functions.py:1016-1071 _compute_divergence_rc, constant density: d_f = dt / mean(rho) */
 int rmt_divergence_rc(rmt_ctx *ctx, const double *a, const double *b, const double *p,

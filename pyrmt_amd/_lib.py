@@ -81,6 +81,7 @@ SIGNATURES = {
     "rmt_advect_sl_cubic_rk4": (_I, [_P, _P, _P, _P, _P, _P, _D, _D, _D, _P]),
     "rmt_extrapolate_reference_map": (_I, [_P, _P, _P, _P, _D, _D, _I, _P, _P]),
     "rmt_extrap_set_mode": (_I, [_I]),
+    "rmt_momentum_set_mode": (_I, [_I]),
     "rmt_extrap_last_path": (_I, [_P, ctypes.POINTER(_I)]),
     "rmt_rebuild_phi_disc": (_I, [_P, _P, _P, _D, _D, _D, _P]),
     "rmt_solid_cauchy_stress": (_I, [_P, _P, _P, _D, _D, _D, _D, _P, _D, _D, _I, _P, _P, _P, _P]),

@@ -761,7 +761,7 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 "window %.3g wait %.3g load %.3g sum %.3g solve+store %.3g (Mclk, all waves)\n",
                 ms, hs[0], hp[7], hp[0] / 1e6, hp[6] / 1e6, hp[1] / 1e6, hp[2] / 1e6,
                 hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6);
-        hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
+        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipFree(gp);
     }
     if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
     // the chain after the sweep: both read the fallback flag the chain prep settled

@@ -1019,10 +1019,10 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
             RMT_HIP(hipMemcpy(h.data(), dtr, 6 * sizeof(long long) * tot, hipMemcpyDeviceToHost));
             FILE *f = fopen(tpath, "wb");
             if (f) { fwrite(h.data(), sizeof(long long), 6 * (size_t)tot, f); fclose(f); }
-            hipFree(dtr);
+            (void)hipFree(dtr);
             traced = true;
         }
-        hipEventDestroy(e0); hipEventDestroy(e1); hipFree(gp);
+        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipFree(gp);
     }
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], st));
     return RMT_OK;

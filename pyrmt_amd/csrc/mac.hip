@@ -405,7 +405,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
 
 int rmt_mac_sim_destroy(rmt_mac_sim *S) {
     if (!S) return RMT_OK;
-    hipFree(S->block);
+    (void)hipFree(S->block);
     delete S;
     return RMT_OK;
 }
@@ -710,7 +710,7 @@ int rmt_mac_slab_create(rmt_ctx *ctx, const rmt_mac_params *prm, int G, int rank
 
 int rmt_mac_slab_destroy(rmt_mac_slab *S) {
     if (!S) return RMT_OK;
-    hipFree(S->block);
+    (void)hipFree(S->block);
     delete S;
     return RMT_OK;
 }

@@ -343,6 +343,216 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
     return RMT_OK;
 }
 
+// ------------------------------------------------------------ temporally blocked RK4 --
+// The four stages of one TX x TY output tile in one workgroup.  Stage s needs stage s-1 two
+// cells out (upwind3 / grad2 of the blended stress), so on the tile plus an 8-cell halo the
+// stage velocity lives in LDS on halo 2(3-s)+2, the blended stress on 2(3-s)+1 and k is formed
+// on 2(3-s); the per-cell inputs (u, v, elastic stress, H, grad p) and the RK4 accumulators
+// stay in registers.  HBM sees u, v, p, sxx, sxy, syy, H, solid once and u*, v* once (the
+// per-stage kernel moves ~16 planes per stage).  The per-cell arithmetic and its order are
+// k_mom_stage's (bit-identical).  Not for periodic BCs, whose sources lie across the domain.
+struct Rk4Args {
+    const double *u, *v, *p, *sxx, *sxy, *syy, *H;
+    const unsigned char *solid;
+    double *outu, *outv;
+    const int *tlist, *tcount;   // listed tiles (fix-up), else every tile of rows [rw.jb, rw.je)
+    const double *dtp;           // device dt, or null: dt
+    double dt, lid, mu_f, eta_s, rho_s, rho_f, dx, dy;
+    int bc, visc, ny, nx, tiles_x, ntiles, olo, ohi;   // outputs on rows [olo, ohi)
+    RowWin rw;
+};
+constexpr int RK_HL = 8;
+template <int TX, int TY>
+constexpr int rk4_lds() { return 5 * (TX + 2 * RK_HL) * (TY + 2 * RK_HL) * (int)sizeof(double); }
+
+template <int TX, int TY, int NT>
+__global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
+    constexpr int HL = RK_HL, RX = TX + 2 * HL, RY = TY + 2 * HL, NR = RX * RY;
+    constexpr int NQ = (NR + NT - 1) / NT;
+    extern __shared__ double rk_lds[];
+    double *U = rk_lds, *V = U + NR, *GX = V + NR, *GM = GX + NR, *GY = GM + NR;
+    if (A.tlist && (int)blockIdx.x >= *A.tcount) return;
+    const int tile = A.tlist ? A.tlist[blockIdx.x] : xcd_tile(blockIdx.x, A.ntiles);
+    const int ri = (tile % A.tiles_x) * TX - HL, rj = A.rw.jb + (tile / A.tiles_x) * TY - HL;
+    const int nx = A.nx, ny = A.ny;
+    const double dx = A.dx, dy = A.dy, h2x = 2 * dx, h2y = 2 * dy;
+    const double dt = A.dtp ? *A.dtp : A.dt;
+    // mom_stage's constants: coef {0, dt/2, dt/2, dt}, dt / 6
+    const double chalf = 0.5 * dt, dt6 = dt / 6.0;
+    const bool edge_fix = A.bc == RMT_BC_FREESLIP_BOX &&
+                          (ri <= 0 || rj <= 0 || ri + RX >= nx || rj + RY >= ny);
+    double u0[NQ], v0[NQ], ex[NQ], ey[NQ], exy[NQ], hh[NQ], dpx[NQ], dpy[NQ], au[NQ], av[NQ];
+    unsigned okm = 0, solm = 0, ucm = 0, vcm = 0;
+    // inputs: the region's u, v (BC'd into LDS), elastic stress, H, solid; grad p on the
+    // stage-0 k region (all loads before the LDS stores)
+    {
+        double su[NQ], sv[NQ];
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) {
+            const int q = threadIdx.x + m * NT, ly = q / RX, lx = q % RX;
+            const int j = rj + ly, i = ri + lx;
+            const bool ok = q < NR && j >= A.rw.lo && j < A.rw.hi && i >= 0 && i < nx;
+            const long c = ok ? (long)j * nx + i : (long)A.rw.lo * nx;
+            const BCSrc s = bc_source(A.bc, A.lid, ok ? j : 1, ok ? i : 1, ny, nx);
+            okm |= (unsigned)ok << m;
+            ucm |= (unsigned)s.u_const << m;
+            vcm |= (unsigned)s.v_const << m;
+            const double a = A.u[ok ? s.u_src : c], b = A.v[ok ? s.v_src : c];
+            su[m] = !ok ? 0.0 : s.u_const ? s.u_val : a;
+            sv[m] = !ok ? 0.0 : s.v_const ? 0.0 : b;
+            u0[m] = A.u[c]; v0[m] = A.v[c];
+            ex[m] = A.sxx[c]; ey[m] = A.syy[c]; exy[m] = A.sxy[c]; hh[m] = A.H[c];
+            solm |= (unsigned)(A.solid[c] != 0) << m;
+            const bool k0 = ok && ly >= HL - 6 && ly < HL + TY + 6 && lx >= HL - 6 && lx < HL + TX + 6;
+            dpx[m] = k0 ? grad2(A.p + c, 1, i, nx, h2x) : 0.0;
+            dpy[m] = k0 ? grad2(A.p + c, nx, j, ny, h2y) : 0.0;
+            au[m] = 0.0; av[m] = 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) {
+            const int q = threadIdx.x + m * NT;
+            if (q < NR) { U[q] = su[m]; V[q] = sv[m]; }
+        }
+    }
+    __syncthreads();
+    for (int st = 0; st < 4; ++st) {
+        const int hk = 2 * (3 - st), hg = hk + 1;
+        // per-slot indices recomputed every stage (kept from being hoisted: registers)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        // blended stress on halo hg (functions.py:717-735, 906-921)
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) {
+            const int q = tid + m * NT, ly = q / RX, lx = q % RX;
+            if (q >= NR || ly < HL - hg || ly >= HL + TY + hg || lx < HL - hg || lx >= HL + TX + hg)
+                continue;
+            const int j = rj + ly, i = ri + lx;
+            double oxx = 0.0, oxy = 0.0, oyy = 0.0;
+            if ((okm >> m) & 1) {
+                const double *pu = U + q, *pv = V + q;
+                const double dudx = grad2(pu, 1, i, nx, h2x), dvdy = grad2(pv, RX, j, ny, h2y);
+                const double dudy = grad2(pu, RX, j, ny, h2y), dvdx = grad2(pv, 1, i, nx, h2x);
+                double e1 = ex[m], e2 = ey[m], e3 = exy[m];
+                if (A.visc && ((solm >> m) & 1)) {
+                    e1 = e1 + A.eta_s * dudx;
+                    e2 = e2 + A.eta_s * dvdy;
+                    e3 = e3 + A.eta_s * 0.5 * (dudy + dvdx);
+                }
+                const double h = hh[m], omh = 1 - h;
+                oxx = h * (2 * A.mu_f * dudx) + omh * e1;
+                oyy = h * (2 * A.mu_f * dvdy) + omh * e2;
+                oxy = h * (A.mu_f * (dudy + dvdx)) + omh * e3;
+            }
+            GX[q] = oxx; GM[q] = oxy; GY[q] = oyy;
+        }
+        __syncthreads();
+        // RHS on halo hk, RK4 accumulation (functions.py:923-944, 743-758)
+        double ru[NQ], rv[NQ];
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) {
+            ru[m] = 0.0; rv[m] = 0.0;
+            const int q = tid + m * NT, ly = q / RX, lx = q % RX;
+            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + TY + hk ||
+                lx < HL - hk || lx >= HL + TX + hk)
+                continue;
+            const int j = rj + ly, i = ri + lx;
+            if (st == 3 && (j < A.olo || j >= A.ohi)) continue;
+            const double divx = grad2(GX + q, 1, i, nx, h2x) + grad2(GM + q, RX, j, ny, h2y);
+            const double divy = grad2(GM + q, 1, i, nx, h2x) + grad2(GY + q, RX, j, ny, h2y);
+            const double *pu = U + q, *pv = V + q;
+            const double uc = *pu, vc = *pv;
+            const double uadv = -uc * upwind3(pu, 1, i, nx, uc, dx) - vc * upwind3(pu, RX, j, ny, vc, dy);
+            const double vadv = -uc * upwind3(pv, 1, i, nx, uc, dx) - vc * upwind3(pv, RX, j, ny, vc, dy);
+            const double h = hh[m];
+            const double den = ((1 - h) * A.rho_s + h * A.rho_f) + 1e-12;
+            const double k1 = uadv + (divx + 0.0 - dpx[m]) / den;
+            const double k2 = vadv + (divy + 0.0 - dpy[m]) / den;
+            if (st == 0) {
+                au[m] = k1; av[m] = k2;
+            } else if (st < 3) {
+                au[m] = au[m] + 2 * k1; av[m] = av[m] + 2 * k2;
+            }
+            if (st < 3) {   // the next stage's raw velocity u + coef k
+                const double cf = st == 2 ? dt : chalf;
+                ru[m] = u0[m] + cf * k1; rv[m] = v0[m] + cf * k2;
+            } else {
+                const long c = (long)j * nx + i;
+                if (ly >= HL && ly < HL + TY && lx >= HL && lx < HL + TX) {
+                    A.outu[c] = u0[m] + dt6 * (au[m] + k1);
+                    A.outv[c] = v0[m] + dt6 * (av[m] + k2);
+                }
+            }
+        }
+        if (st == 3) break;
+        __syncthreads();
+        // the next stage's velocity on halo hk: raw values, BC constants kept, BC copies after
+#pragma unroll
+        for (int m = 0; m < NQ; ++m) {
+            const int q = tid + m * NT, ly = q / RX, lx = q % RX;
+            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + TY + hk ||
+                lx < HL - hk || lx >= HL + TX + hk)
+                continue;
+            const int j = rj + ly, i = ri + lx;
+            const bool edge = i == 0 || i == nx - 1 || j == 0 || j == ny - 1;
+            if (!((ucm >> m) & 1) && !(edge_fix && edge)) U[q] = ru[m];
+            if (!((vcm >> m) & 1) && !(edge_fix && edge)) V[q] = rv[m];
+        }
+        if (edge_fix) {
+            __syncthreads();
+#pragma unroll
+            for (int m = 0; m < NQ; ++m) {
+                const int q = tid + m * NT, ly = q / RX, lx = q % RX;
+                if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + TY + hk ||
+                    lx < HL - hk || lx >= HL + TX + hk)
+                    continue;
+                const int j = rj + ly, i = ri + lx;
+                if (!(i == 0 || i == nx - 1 || j == 0 || j == ny - 1)) continue;
+                const BCSrc s = bc_source(A.bc, A.lid, j, i, ny, nx);
+                const long c = (long)j * nx + i;
+                auto loc = [&](long src) {
+                    const long d = src - c;
+                    return q + (d == nx ? RX : d == -(long)nx ? -RX : (int)d);
+                };
+                if (!s.u_const) U[q] = U[loc(s.u_src)];
+                if (!s.v_const) V[q] = V[loc(s.v_src)];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int TX, int TY, int NT>
+static int launch_rk4(rmt_ctx *ctx, const Rk4Args &A, int nblocks) {
+    static bool attr = false;
+    if (!attr) {
+        RMT_HIP(hipFuncSetAttribute((const void *)k_mom_rk4<TX, TY, NT>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, rk4_lds<TX, TY>()));
+        attr = true;
+    }
+    if (nblocks <= 0) return RMT_OK;
+    k_mom_rk4<TX, TY, NT><<<nblocks, NT, rk4_lds<TX, TY>(), ctx->stream>>>(A);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+static Rk4Args rk4_args(const rmt_momentum_params *P, const double *u, const double *v,
+                        const double *p, const double *sxx, const double *sxy,
+                        const double *syy, const MomWork &W, double *u_new, double *v_new,
+                        int ny, int nx) {
+    Rk4Args A{};
+    A.u = u; A.v = v; A.p = p; A.sxx = sxx; A.sxy = sxy; A.syy = syy; A.H = W.H;
+    A.solid = W.solid; A.outu = u_new; A.outv = v_new; A.dtp = W.dtp;
+    A.dt = P->dt; A.lid = P->lid; A.mu_f = P->mu_f; A.eta_s = P->eta_s; A.rho_s = P->rho_s;
+    A.rho_f = P->rho_f; A.dx = P->dx; A.dy = P->dy; A.bc = P->bc_kind;
+    A.visc = P->eta_s > 0.0; A.ny = ny; A.nx = nx;
+    return A;
+}
+// 0: per-stage kernels (k_mom_stage), 1: temporally blocked RK4 (k_mom_rk4) where the BC
+// allows, 2: unfused per-cell passes (single domain).  Mode 1 moves ~9 planes per RK4 pass
+// instead of ~64 but measured slower at N = 4096 (2.50 vs 2.12 ms full pass, 0.36 vs 0.13 ms
+// fix-up): the fp64 divisions of ~1.7x halo recompute at 3 waves per SIMD are latency-bound.
+static int g_mom_mode = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED")) ? 2 : 0;
+constexpr int RK_TX = 48, RK_TY = 32, RK_T = 768;   // full pass: region 64 x 48 (one row a wave)
+
 // Final BC (functions.py:760) on the boundary cells of rows [jb, je) only: the bottom / top
 // rows when the window holds them, then the side columns.
 __global__ void k_bc_edges(int kind, double lid, double *u, double *v, int ny, int nx, int jb,
@@ -387,9 +597,17 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     const double coef[4] = {0.0, 0.5 * P->dt, 0.5 * P->dt, P->dt}, dt6 = P->dt / 6.0;
     double *kbu[2] = {W.k1u, W.k2u}, *kbv[2] = {W.k1v, W.k2v};
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-    static const bool unfused = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED"));
+    const bool unfused = g_mom_mode == 2;
+    const bool blocked = g_mom_mode == 1 && P->bc_kind != RMT_BC_PERIODIC;
     const int tiles_x = (nx + MS_TX - 1) / MS_TX;
-    for (int s = 0; s < 4 && !unfused; ++s) {
+    if (blocked) {
+        Rk4Args A = rk4_args(P, u, v, p, sxx, sxy, syy, W, u_new, v_new, ny, nx);
+        A.tiles_x = (nx + RK_TX - 1) / RK_TX;
+        A.ntiles = A.tiles_x * ((w0.je - w0.jb + RK_TY - 1) / RK_TY);
+        A.olo = w0.jb; A.ohi = w0.je; A.rw = w0;
+        RMT_TRY((launch_rk4<RK_TX, RK_TY, RK_T>(ctx, A, A.ntiles)));
+    }
+    for (int s = 0; s < 4 && !unfused && !blocked; ++s) {
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
@@ -438,6 +656,12 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
         grow(7).second);
     RMT_LAUNCHED();
     const RowWin all{0, ny, w0.lo, w0.hi};
+    if (g_mom_mode == 1 && P->bc_kind != RMT_BC_PERIODIC) {
+        Rk4Args A = rk4_args(P, u, v, p, sxx, sxy, syy, W, u_new, v_new, ny, nx);
+        A.tlist = tiles; A.tcount = count; A.tiles_x = tiles_x;
+        A.olo = w0.jb; A.ohi = w0.je; A.rw = all;
+        RMT_TRY((launch_rk4<MOM_TX, MOM_TY, 640>(ctx, A, max_tiles)));
+    } else
     for (int s = 0; s < 4; ++s)
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, all, max_tiles,
                           tiles, count, grow(2 * (3 - s)).first, grow(2 * (3 - s)).second));
@@ -450,6 +674,12 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
 }  // namespace rmt
 
 using namespace rmt;
+
+extern "C" int rmt_momentum_set_mode(int mode) {
+    RMT_CHECK(mode >= 0 && mode <= 2, RMT_EINVAL, "momentum mode must be 0 .. 2");
+    rmt::g_mom_mode = mode;
+    return RMT_OK;
+}
 
 extern "C" int rmt_momentum_step_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u,
                                      const double *v, const double *p, const double *X1,

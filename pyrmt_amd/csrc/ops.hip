@@ -577,11 +577,11 @@ int rmt_ctx_kernel_ms(rmt_ctx *ctx, double *ms2) {
 
 int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (!ctx) return RMT_OK;
-    hipSetDevice(ctx->device);
-    if (ctx->scratch) hipFree(ctx->scratch);
-    if (ctx->red) hipFree(ctx->red);
-    if (ctx->rsum) hipFree(ctx->rsum);
-    if (ctx->bytes) hipFree(ctx->bytes);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    if (ctx->red) (void)hipFree(ctx->red);
+    if (ctx->rsum) (void)hipFree(ctx->rsum);
+    if (ctx->bytes) (void)hipFree(ctx->bytes);
     if (ctx->dct) dct_destroy(ctx->dct);
     if (ctx->dct2) dct2_destroy(ctx->dct2);
     if (ctx->per) per_destroy(ctx->per);

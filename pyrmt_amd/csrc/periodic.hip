@@ -35,8 +35,8 @@ void per_destroy(PerPlan *P) {
     if (P->fwd) rocfft_plan_destroy(P->fwd);
     if (P->inv) rocfft_plan_destroy(P->inv);
     if (P->info) rocfft_execution_info_destroy(P->info);
-    hipFree(P->work); hipFree(P->red); hipFree(P->C); hipFree(P->lamx); hipFree(P->lamy);
-    hipFree(P->g);
+    (void)hipFree(P->work); (void)hipFree(P->red); (void)hipFree(P->C); (void)hipFree(P->lamx); (void)hipFree(P->lamy);
+    (void)hipFree(P->g);
     delete P;
 }
 

@@ -71,9 +71,9 @@ void dct_destroy(DctPlan *P) {
     if (P->px) rocfft_plan_destroy(P->px);
     if (P->py) rocfft_plan_destroy(P->py);
     if (P->info) rocfft_execution_info_destroy(P->info);
-    hipFree(P->work); hipFree(P->E); hipFree(P->C); hipFree(P->T);
-    hipFree(P->lamx); hipFree(P->lamy);
-    hipFree(P->Wx); hipFree(P->Wy);
+    (void)hipFree(P->work); (void)hipFree(P->E); (void)hipFree(P->C); (void)hipFree(P->T);
+    (void)hipFree(P->lamx); (void)hipFree(P->lamy);
+    (void)hipFree(P->Wx); (void)hipFree(P->Wy);
     delete P;
 }
 
@@ -787,8 +787,8 @@ struct Dct2Plan {
 
 void dct2_destroy(Dct2Plan *P) {
     if (!P) return;
-    hipFree(P->Wx); hipFree(P->Wy); hipFree(P->Qx); hipFree(P->Qy);
-    hipFree(P->lamx); hipFree(P->lamy); hipFree(P->T);
+    (void)hipFree(P->Wx); (void)hipFree(P->Wy); (void)hipFree(P->Qx); (void)hipFree(P->Qy);
+    (void)hipFree(P->lamx); (void)hipFree(P->lamy); (void)hipFree(P->T);
     delete P;
 }
 

@@ -535,15 +535,15 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
 
 int rmt_sim_destroy(rmt_sim *S) {
     if (!S) return RMT_OK;
-    hipFree(S->block);
-    if (S->m2part) hipFree(S->m2part);
-    if (S->tiles) hipFree(S->tiles);
-    if (S->e_sl) hipEventDestroy(S->e_sl);
-    if (S->e_mom) hipEventDestroy(S->e_mom);
-    if (S->e_rows) hipEventDestroy(S->e_rows);
-    if (S->e_bits) hipEventDestroy(S->e_bits);
-    if (S->st2) hipStreamDestroy(S->st2);
-    for (auto e : S->pev) if (e) hipEventDestroy(e);
+    (void)hipFree(S->block);
+    if (S->m2part) (void)hipFree(S->m2part);
+    if (S->tiles) (void)hipFree(S->tiles);
+    if (S->e_sl) (void)hipEventDestroy(S->e_sl);
+    if (S->e_mom) (void)hipEventDestroy(S->e_mom);
+    if (S->e_rows) (void)hipEventDestroy(S->e_rows);
+    if (S->e_bits) (void)hipEventDestroy(S->e_bits);
+    if (S->st2) (void)hipStreamDestroy(S->st2);
+    for (auto e : S->pev) if (e) (void)hipEventDestroy(e);
     S->ctx->prof = false;
     delete S;
     return RMT_OK;
@@ -711,6 +711,17 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_TRY(es);
             if (overlap) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
+                // the fix-up tiles and the rows they reach depend on the known plane only
+                ctx->stream = S->st2;
+                const int fs = extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount);
+                ctx->stream = st;
+                RMT_TRY(fs);
+                if (S->split_proj) {
+                    RMT_HIP(hipMemsetAsync(S->rowmark, 0, ny, S->st2));
+                    k_mark_rows<<<S->max_tiles, 64, 0, S->st2>>>(
+                        S->tiles, S->tcount, (nx + MOM_TX - 1) / MOM_TX, ny, S->rowmark);
+                    RMT_LAUNCHED();
+                }
                 if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits) {
                     // the advection of every non-rim cell, once the chain has started (earlier
                     // its blocks would crowd out the one-workgroup band passes)
@@ -736,7 +747,6 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 RMT_TRY(ms);
                 RMT_HIP(hipEventRecord(S->e_rows, S->st2));
             }
-            if (overlap) RMT_TRY(extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount));
             if (S->prof) RMT_HIP(hipEventRecord(S->pev[3], st));
             // the flags (non-finite velocity, sweep aborted) are read with the diagnostics at
             // the end of the step: no host round trip between the chain and the projection
@@ -769,10 +779,6 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (overlap && S->split_proj) {
             // redo the rhs on the fix-up tiles (+1 cell) and the row DCT of the rows they
             // reach, then the column pass and the rest
-            const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
-            RMT_HIP(hipMemsetAsync(S->rowmark, 0, ny, st));
-            k_mark_rows<<<S->max_tiles, 64, 0, st>>>(S->tiles, S->tcount, tiles_x, ny, S->rowmark);
-            RMT_LAUNCHED();
             RMT_HIP(hipStreamWaitEvent(st, S->e_rows, 0));
             RMT_TRY(projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
                                     S->rowmark, S->tiles, S->tcount, S->max_tiles));

@@ -475,12 +475,12 @@ int rmt_slab_create(rmt_ctx *ctx, const rmt_sim_params *prm, int G, int rank,
 
 int rmt_slab_destroy(rmt_slab *S) {
     if (!S) return RMT_OK;
-    if (S->st2) hipStreamSynchronize(S->st2);
-    hipFree(S->block);
-    if (S->tiles) hipFree(S->tiles);
-    if (S->e_chain) hipEventDestroy(S->e_chain);
-    if (S->e_mom) hipEventDestroy(S->e_mom);
-    if (S->st2) hipStreamDestroy(S->st2);
+    if (S->st2) (void)hipStreamSynchronize(S->st2);
+    (void)hipFree(S->block);
+    if (S->tiles) (void)hipFree(S->tiles);
+    if (S->e_chain) (void)hipEventDestroy(S->e_chain);
+    if (S->e_mom) (void)hipEventDestroy(S->e_mom);
+    if (S->st2) (void)hipStreamDestroy(S->st2);
     delete S;
     return RMT_OK;
 }

@@ -354,6 +354,12 @@ def momentum_step_rk4(u, v, p, X1, X2, velocity_bc, mu_s, kappa, eta_s, dx, dy, 
     return tuple(io.out(o) for o in outs)
 
 
+def momentum_mode(mode):
+    """librmt diagnostic: 0 one kernel per RK4 stage (default), 1 temporally blocked RK4,
+    2 unfused per-cell passes (all bit-identical)."""
+    L.check(L.lib().rmt_momentum_set_mode(int(mode)), "rmt_momentum_set_mode")
+
+
 def velocity_rhs_blended_optimized(u, v, p, sigma_sxx_s_elastic, sigma_sxy_s_elastic,
                                    sigma_syy_s_elastic, dx, dy, phi, mu_f, H, dH_dx, dH_dy,
                                    rho_local, st_force_x, st_force_y):

@@ -389,3 +389,32 @@ def test_energy_exports(gpu, oracle):
     np.testing.assert_allclose(gpu.compute_viscous_dissipation(a, b, 0.01, phi, 2 * dx, dx, dy, 0.05),
                                oracle.compute_viscous_dissipation(a, b, 0.01, phi, 2 * dx, dx, dy, 0.05),
                                rtol=1e-14)
+
+
+@pytest.mark.parametrize("shape", [(40, 37), (97, 130), (257, 129), (300, 1001)])
+@pytest.mark.parametrize("bc", ["lid", "freeslip", "periodic"])
+def test_momentum_modes_bitwise(gpu, shape, bc):
+    """The per-stage kernels (mode 0), the temporally blocked RK4 kernel (mode 1) and the
+    unfused passes (mode 2) give the same bits: solid disc with viscosity (eta_s > 0) and the
+    stress band, tiles that straddle the grid edges."""
+    ny, nx = shape
+    rng = np.random.default_rng(ny * 7 + nx)
+    X, Y, dx, dy = gpu.create_grid(nx, ny, 1.0, 1.0)
+    u = rng.standard_normal((ny, nx)) * 0.1
+    v = rng.standard_normal((ny, nx)) * 0.1
+    p = rng.standard_normal((ny, nx))
+    X1 = X + 1e-3 * rng.standard_normal((ny, nx))
+    X2 = Y + 1e-3 * rng.standard_normal((ny, nx))
+    phi = np.sqrt((X - 0.5) ** 2 + (Y - 0.45) ** 2) - 0.2
+    kind = {"lid": gpu.NoSlipLid(1.0), "freeslip": gpu.FreeSlipBox(), "periodic": gpu.Periodic()}[bc]
+    outs = []
+    try:
+        for mode in (0, 1, 2):
+            gpu.momentum_mode(mode)
+            outs.append(gpu.momentum_step_rk4(u, v, p, X1, X2, kind, 0.7, 0.3, 0.05, dx, dy, 2e-3,
+                                              1.5, 1.0, phi, 0.01, 2 * dx, stress_band=True,
+                                              detg_clamp=3.0))
+    finally:
+        gpu.momentum_mode(0)
+    for o in outs[1:]:
+        _eq(o[0], outs[0][0]); _eq(o[1], outs[0][1])
