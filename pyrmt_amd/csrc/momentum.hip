@@ -28,7 +28,7 @@ __global__ void k_mom_prep(const double *__restrict__ X1, const double *__restri
     sxx[c] = s.sxx; sxy[c] = s.sxy; syy[c] = s.syy; J[c] = s.J;
     double pc = phi[c], h = heaviside(pc, w_t);
     H[c] = h;
-    rho[c] = (1 - h) * rho_s + h * rho_f;
+    if (rho) rho[c] = (1 - h) * rho_s + h * rho_f;   // read by the unfused passes only
     solid[c] = pc <= 0.0;
 }
 
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(256) k_mom_prep_tiles(
         sxx[c] = s.sxx; sxy[c] = s.sxy; syy[c] = s.syy; J[c] = s.J;
         const double pc = phi[c], h = heaviside(pc, w_t);
         H[c] = h;
-        rho[c] = (1 - h) * rho_s + h * rho_f;
+        if (rho) rho[c] = (1 - h) * rho_s + h * rho_f;
         solid[c] = pc <= 0.0;
     }
 }
@@ -588,7 +588,7 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     const RowWin wp = grow(7);
     k_mom_prep<<<grid1d((long)(wp.je - wp.jb) * nx, 256), 256, 0, ctx->stream>>>(
         X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
-        P->rho_f, sxx, sxy, syy, J, W.H, W.rho, W.solid, wp.jb, wp.je);
+        P->rho_f, sxx, sxy, syy, J, W.H, g_mom_mode == 2 ? W.rho : nullptr, W.solid, wp.jb, wp.je);
     RMT_LAUNCHED();
     // visc = eta_s > 0 and any(solid): cells with no solid contribute nothing anyway, so
     // the per-cell solid test reproduces the reference's np.any guard.
@@ -652,7 +652,7 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
     auto grow = [&](int m) { return std::pair<int, int>{std::max(w0.jb - m, 0), std::min(w0.je + m, ny)}; };
     k_mom_prep_tiles<<<max_tiles, 256, 0, ctx->stream>>>(
         X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
-        P->rho_f, sxx, sxy, syy, J, W.H, W.rho, W.solid, tiles, count, tiles_x, grow(7).first,
+        P->rho_f, sxx, sxy, syy, J, W.H, nullptr, W.solid, tiles, count, tiles_x, grow(7).first,
         grow(7).second);
     RMT_LAUNCHED();
     const RowWin all{0, ny, w0.lo, w0.hi};

@@ -62,6 +62,7 @@ struct rmt_sim {
     unsigned long long *kbits_next = nullptr;
     bool bits_ready = false;
     int *segs = nullptr;     // rim row segments (k_rim_segments): ny * ceil(nx / 256) + count
+    unsigned long long *m2acc = nullptr;   // k_dt_part's atomic max + block counter (zeroed)
     bool prof = false;
     hipEvent_t pev[7] = {};
     double ms[8] = {};
@@ -288,19 +289,24 @@ __global__ void k_dt(const double *m2, double dt_const, double cfl, double dx, d
     *out = fmin(dt_const, cfl * dx / (sqrt(*m2) + 1e-6));
 }
 // the same dt with max |u|^2 folded from the projection's per-block partials (NaN-propagating
-// max, exact in any order): sc[0] = max |u|^2, sc[1] = dt; both stay on the device
-__global__ void __launch_bounds__(1024) k_dt_part(const double *__restrict__ part, int np,
-                                                  double dt_const, double cfl, double dx,
-                                                  double *__restrict__ sc) {
-    __shared__ double s[1024];
-    double acc = -INFINITY;
-    for (int k = threadIdx.x; k < np; k += 1024) {
+// max, exact in any order): DTP_BLOCKS blocks fold their share and merge with a 64-bit atomic
+// max on the bit patterns (values are +0.0 .. +inf or NaN, which orders them as doubles with
+// every NaN on top); the last block writes sc[0] = max |u|^2, sc[1] = dt and re-arms acc.
+constexpr int DTP_BLOCKS = 64;
+__global__ void __launch_bounds__(256) k_dt_part(const double *__restrict__ part, int np,
+                                                 double dt_const, double cfl, double dx,
+                                                 double *__restrict__ sc,
+                                                 unsigned long long *__restrict__ acc) {
+    __shared__ double s[256];
+    __shared__ bool last;
+    double m = 0.0;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k < np; k += DTP_BLOCKS * 256) {
         const double y = part[k];
-        if (y > acc || y != y) acc = y;
+        if (y > m || y != y) m = y;
     }
-    s[threadIdx.x] = acc;
+    s[threadIdx.x] = m;
     __syncthreads();
-    for (int w = 512; w > 0; w >>= 1) {
+    for (int w = 128; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) {
             const double y = s[threadIdx.x + w];
             if (y > s[threadIdx.x] || y != y) s[threadIdx.x] = y;
@@ -308,7 +314,15 @@ __global__ void __launch_bounds__(1024) k_dt_part(const double *__restrict__ par
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const double m2 = s[0];
+        atomicMax(acc, (unsigned long long)__double_as_longlong(s[0]));
+        __threadfence();
+        last = atomicAdd((unsigned long long *)(acc + 1), 1ull) == DTP_BLOCKS - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        const double m2 = __longlong_as_double((long long)atomicExch(acc, 0ull));
+        atomicExch((unsigned long long *)(acc + 1), 0ull);
         sc[0] = m2;
         sc[1] = fmin(dt_const, cfl * dx / (sqrt(m2) + 1e-6));
     }
@@ -516,13 +530,15 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     const size_t Wn = (size_t)(nx + 63) / 64;
     RMT_HIP(hipMalloc(&S->m2part, ((size_t)S->m2n + (size_t)RING_N * RING_VALS + ny / 8 + 8 +
                                    (size_t)ny * Wn + ny / 2 + 8 + (size_t)ny * Wn +
-                                   (size_t)ny * ((nx + 255) / 256) / 2 + 8) * sizeof(double)));
+                                   (size_t)ny * ((nx + 255) / 256) / 2 + 8 + 8) * sizeof(double)));
     S->ring = S->m2part + S->m2n;
     S->rowmark = (unsigned char *)(S->ring + (size_t)RING_N * RING_VALS);
     S->rimw = (unsigned long long *)(S->ring + (size_t)RING_N * RING_VALS + ny / 8 + 8);
     S->rimcnt = (int *)(S->rimw + (size_t)ny * Wn);
     S->kbits_next = (unsigned long long *)((double *)S->rimcnt + ny / 2 + 8);
     S->segs = (int *)(S->kbits_next + (size_t)ny * Wn);
+    S->m2acc = (unsigned long long *)(S->segs + (((size_t)ny * ((nx + 255) / 256) + 3) & ~(size_t)1));
+    RMT_HIP(hipMemsetAsync(S->m2acc, 0, 2 * sizeof(unsigned long long), ctx->stream));
     if (S->st2) RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
     if (S->st2 && prm->rho_f > 0) {
         RMT_TRY(dct_plan(ctx, prm->dx, prm->dy));
@@ -622,7 +638,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // also bounds the velocities for the SL block skip
         double hv[2] = {0.0, 0.0}, dt = NAN;
         if (async && it > 0) {
-            k_dt_part<<<1, 1024, 0, st>>>(S->m2part, S->m2n, S->dt_const, P.cfl, P.dx, sc);
+            k_dt_part<<<DTP_BLOCKS, 256, 0, st>>>(S->m2part, S->m2n, S->dt_const, P.cfl, P.dx,
+                                                  sc, S->m2acc);
             RMT_LAUNCHED();
         } else {
             RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, n, sc));
