@@ -174,7 +174,8 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     const double *__restrict__ ainu, const double *__restrict__ ainv, double *__restrict__ accu,
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
-    int olo, int ohi) {
+    int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
+    const unsigned char *__restrict__ fluid_rows) {
     __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
     if (dtp) {   // the same roundings as mom_stage's host constants
         const double dt = *dtp;
@@ -187,6 +188,17 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     const int tile = tlist ? tlist[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
     const double h2x = 2 * dx, h2y = 2 * dy;
+    // pure-fluid tile (k_fluid_rows): every cell the blended stress is formed on has
+    // phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not solid
+    // exactly -- those constants replace the loads of sxx, sxy, syy, H and solid below (the
+    // arithmetic is unchanged).  Rows outside the resident window are never loaded anyway.
+    int fpred = 0;
+    if (fluid_rows) {
+        fpred = 1;
+        const int r = j0 - 2 + (int)threadIdx.x;
+        if (threadIdx.x < MS_GY && r >= rw.lo && r < rw.hi)
+            fpred = fluid_rows[(long)(r - rw.lo) * tiles_x + i0 / MS_TX];
+    }
     // 1. stage velocity (functions.py:714), BC applied; all loads issued before the LDS stores
     {
         double a[MS_NU], b[MS_NU], ka[MS_NU], kb[MS_NU];
@@ -213,7 +225,7 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             (&sv[0][0])[q] = !ok[it] ? 0.0 : vc[it] ? 0.0 : rv;
         }
     }
-    __syncthreads();
+    const bool fluid = __syncthreads_and(fpred) != 0;
     // 2. blended stress (functions.py:717-735, 906-921)
     {
         double ex[MS_NG], ey[MS_NG], exy[MS_NG], hh[MS_NG];
@@ -224,8 +236,12 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             const int j = j0 - 2 + ry, i = i0 - 2 + rx;
             ok[it] = q < MS_GX * MS_GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
             const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
-            ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh[it] = H[c];
-            sol[it] = solid[c] != 0;
+            if (fluid) {
+                ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh[it] = 1.0; sol[it] = false;
+            } else {
+                ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh[it] = H[c];
+                sol[it] = solid[c] != 0;
+            }
         }
 #pragma unroll
         for (int it = 0; it < MS_NG; ++it) {
@@ -271,10 +287,14 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             pc[it] = p[c];
             pxp[it] = ok[it] ? p[c + sx] : 0.0; pxm[it] = ok[it] && !ex ? p[c - 1] : 0.0;
             pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !ey ? p[c - nx] : 0.0;
-            hh[it] = H[c];
-            // accumulation operands
-            x0[it] = stage == 1 ? kpu[c] : (stage >= 2 ? ainu[c] : 0.0);
-            y0[it] = stage == 1 ? kpv[c] : (stage >= 2 ? ainv[c] : 0.0);
+            hh[it] = fluid ? 1.0 : H[c];
+            // stage 3: acc = (k1 + 2 k2) + 2 k3, formed here from the three k planes
+            // (functions.py:758's left-to-right order; no accumulation planes in HBM)
+            x0[it] = 0.0; y0[it] = 0.0;
+            if (stage == 3 && ok[it]) {
+                x0[it] = (ainu[c] + 2 * k2u[c]) + 2 * kpu[c];
+                y0[it] = (ainv[c] + 2 * k2v[c]) + 2 * kpv[c];
+            }
             x1[it] = stage == 3 ? u[c] : 0.0;
             y1[it] = stage == 3 ? v[c] : 0.0;
         }
@@ -304,13 +324,7 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             const double den = ((1 - h) * rho_s + h * rho_f) + 1e-12;
             const double k1 = uadv + (divx + 0.0 - dpx) / den;
             const double k2 = vadv + (divy + 0.0 - dpy) / den;
-            if (stage == 0) {
-                ku[c] = k1; kv[c] = k2;
-            } else if (stage == 1) {
-                accu[c] = x0[it] + 2 * k1; accv[c] = y0[it] + 2 * k2;
-                ku[c] = k1; kv[c] = k2;
-            } else if (stage == 2) {
-                accu[c] = x0[it] + 2 * k1; accv[c] = y0[it] + 2 * k2;
+            if (stage < 3) {
                 ku[c] = k1; kv[c] = k2;
             } else {
                 outu[c] = x1[it] + dt6 * (x0[it] + k1);
@@ -320,6 +334,28 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     }
 }
 
+// per row j of [jlo, jhi) (out row j - jlo) and 64-column tile tx: all of phi[j][64 tx - 2 .. 64 tx + 66) (the
+// columns a stage tile's blended stress is formed on) > thr = max(w_t, w_cut, 0).  One wave
+// per (row, tile); NaN phi is not fluid.
+__global__ void __launch_bounds__(256) k_fluid_rows(const double *__restrict__ phi, double thr,
+                                                    int nx, int tiles_x, int jlo, int jhi,
+                                                    unsigned char *__restrict__ out) {
+    const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long nw = (long)(jhi - jlo) * tiles_x;
+    if (w >= nw) return;
+    const int j = jlo + (int)(w / tiles_x), tx = (int)(w % tiles_x);
+    const int i = MS_TX * tx + lane;
+    const double *row = phi + (long)j * nx;
+    bool ok = i >= nx || row[i] > thr;
+    if (lane < 4) {
+        const int e = lane < 2 ? MS_TX * tx - 2 + lane : MS_TX * tx + 62 + lane;
+        if (e >= 0 && e < nx) ok = ok && row[e] > thr;
+    }
+    const unsigned long long all = __ballot(ok);
+    if (lane == 0) out[(long)(j - jlo) * tiles_x + tx] = all == ~0ull;
+}
+
 // One fused stage launch: k_{s+1} -> (k1 | k2 | k3)[s], acc1 / acc2 / u* (see MomWork)
 // tlist: tiles of the whole grid (ws.jb = 0), outputs on rows [olo, ohi); else the tiles of
 // rows [ws.jb, ws.je)
@@ -327,18 +363,17 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
                      const double *v, const double *p, const double *sxx, const double *sxy,
                      const double *syy, const MomWork &W, double *u_new, double *v_new,
                      RowWin ws, int ntiles, const int *tlist, const int *tcount, int olo,
-                     int ohi) {
+                     int ohi, const unsigned char *fluid_rows) {
     const int nx = ctx->nx, ny = ctx->ny, tiles_x = (nx + MS_TX - 1) / MS_TX;
     const double coef[4] = {0.0, 0.5 * P->dt, 0.5 * P->dt, P->dt}, dt6 = P->dt / 6.0;
     double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
     const double *kpu = s ? ku[s - 1] : u, *kpv = s ? kv[s - 1] : v;
-    const double *ainu = s == 3 ? W.acc2u : W.accu, *ainv = s == 3 ? W.acc2v : W.accv;
-    double *aou = s == 2 ? W.acc2u : W.accu, *aov = s == 2 ? W.acc2v : W.accv;
     k_mom_stage<<<ntiles, MS_T, 0, ctx->stream>>>(
         u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid,
         P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx,
-        tiles_x, ntiles, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, ainu, ainv, aou, aov,
-        u_new, v_new, ws, tlist, tcount, W.dtp, olo, ohi);
+        tiles_x, ntiles, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, W.k1u, W.k1v,
+        nullptr, nullptr, u_new, v_new, ws, tlist, tcount, W.dtp, olo, ohi, W.k2u, W.k2v,
+        fluid_rows);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -607,11 +642,22 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
         A.olo = w0.jb; A.ohi = w0.je; A.rw = w0;
         RMT_TRY((launch_rk4<RK_TX, RK_TY, RK_T>(ctx, A, A.ntiles)));
     }
+    // pure-fluid tile rows for the stage kernels, on every resident row (a stage tile's
+    // stress region may reach past its window; rows prep did not write only feed halo cells
+    // that never reach the window's outputs)
+    unsigned char *fluid_rows = (unsigned char *)(W.acc2u + (long)w0.lo * nx);   // row w0.lo first
+    if (!unfused && !blocked) {
+        const double thr = std::max({P->w_t, w_cut, 0.0});
+        const long nw = (long)(w0.hi - w0.lo) * tiles_x;
+        k_fluid_rows<<<grid1d(nw, 4), 256, 0, ctx->stream>>>(phi, thr, nx, tiles_x, w0.lo,
+                                                              w0.hi, fluid_rows);
+        RMT_LAUNCHED();
+    }
     for (int s = 0; s < 4 && !unfused && !blocked; ++s) {
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
-                          nullptr, nullptr, ws.jb, ws.je));
+                          nullptr, nullptr, ws.jb, ws.je, fluid_rows));
     }
     RMT_CHECK(!unfused || (!win && !W.dtp), RMT_ENOTSUP,
               "RMT_MOM_UNFUSED: single-domain, host-dt only");
@@ -664,7 +710,8 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
     } else
     for (int s = 0; s < 4; ++s)
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, all, max_tiles,
-                          tiles, count, grow(2 * (3 - s)).first, grow(2 * (3 - s)).second));
+                          tiles, count, grow(2 * (3 - s)).first, grow(2 * (3 - s)).second,
+                          nullptr));
     k_bc_edges<<<grid1d(2 * (nx + ny), 256), 256, 0, ctx->stream>>>(P->bc_kind, P->lid, u_new,
                                                                      v_new, ny, nx, w0.jb, w0.je);
     RMT_LAUNCHED();

@@ -483,8 +483,9 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 double *phi_pre, int *bad, const double *dev_m2 = nullptr);
 
 // --------------------------------------------------------------------- momentum --
-// every stage keeps its own k and accumulation planes (k1, k2, k3, acc1 = k1 + 2 k2,
-// acc2 = acc1 + 2 k3), so a tile-list re-run of any stage (momentum_fixup) finds its inputs
+// every stage keeps its own k plane (k1, k2, k3; the last stage forms (k1 + 2 k2) + 2 k3
+// itself), so a tile-list re-run of any stage (momentum_fixup) finds its inputs.  accu/accv
+// serve the unfused mode only; acc2u holds the stage kernels' pure-fluid tile-row flags
 constexpr int MOM_WORK_PLANES = 17;
 struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + flag
     double *H, *rho, *k1u, *k1v, *k2u, *k2v, *accu, *accv, *us, *vs, *gxx, *gxy, *gyy;
