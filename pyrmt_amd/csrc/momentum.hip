@@ -163,7 +163,28 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
     return b < 8 * per ? (b % 8) * per + b / 8 : b;
 }
 
-__global__ void __launch_bounds__(MS_T) k_mom_stage(
+// interior-tile stencils (IN): the centred branch of grad2 / upwind3 only; upwind3's
+// two numerators are both formed and the one its velocity sign picks is divided (one
+// division, no divergent branch) -- each the expression of rmt_internal.hpp, operand for operand
+template <bool IN>
+__device__ __forceinline__ double g2(const double *f, long s, int k, int n, double h2) {
+    if constexpr (IN) return (f[s] - f[-s]) / h2;
+    else return grad2(f, s, k, n, h2);
+}
+template <bool IN>
+__device__ __forceinline__ double u3(const double *f, long s, int k, int n, double vel, double h) {
+    if constexpr (IN) {
+        const double a = 2 * f[s] + 3 * f[0] - 6 * f[-s] + f[-2 * s];
+        const double b = -f[2 * s] + 6 * f[s] - 3 * f[0] - 2 * f[-s];
+        return (vel > 0 ? a : b) / (6 * h);
+    } else {
+        return upwind3(f, s, k, n, vel, h);
+    }
+}
+
+// one stage tile (k_mom_stage); IN: an interior tile (see the kernel)
+template <bool IN>
+__device__ __forceinline__ void ms_tile(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
     const double *__restrict__ sxx, const double *__restrict__ sxy,
@@ -175,18 +196,8 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
-    const unsigned char *__restrict__ fluid_rows) {
-    __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
-    if (dtp) {   // the same roundings as mom_stage's host constants
-        const double dt = *dtp;
-        coef = stage == 0 ? 0.0 : stage == 3 ? dt : 0.5 * dt;
-        dt6 = dt / 6.0;
-    }
-    __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
-    // tlist: the listed tiles only (momentum_fixup); otherwise every tile of rows [jb, je)
-    if (tlist && (int)blockIdx.x >= *tcount) return;
-    const int tile = tlist ? tlist[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
-    const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
+    const unsigned char *__restrict__ fluid_rows, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
+    double (&gx)[MS_GY][MS_GX], double (&gm)[MS_GY][MS_GX], double (&gy)[MS_GY][MS_GX]) {
     const double h2x = 2 * dx, h2y = 2 * dy;
     // pure-fluid tile (k_fluid_rows): every cell the blended stress is formed on has
     // phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not solid
@@ -209,9 +220,15 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q % MS_UX;
             const int j = j0 - 3 + ry, i = i0 - 3 + rx;
             ok[it] = q < MS_UX * MS_UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
-            const BCSrc s = bc_source(bc, lid, ok[it] ? j : 1, ok[it] ? i : 1, ny, nx);
-            uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
-            const long cu = ok[it] ? s.u_src : (long)rw.lo * nx, cv = ok[it] ? s.v_src : (long)rw.lo * nx;
+            long cu, cv;
+            if constexpr (IN) {   // interior cell: every BC kind is the identity there
+                uc[it] = false; vc[it] = false; uval[it] = 0.0;
+                cu = cv = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
+            } else {
+                const BCSrc s = bc_source(bc, lid, ok[it] ? j : 1, ok[it] ? i : 1, ny, nx);
+                uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
+                cu = ok[it] ? s.u_src : (long)rw.lo * nx; cv = ok[it] ? s.v_src : (long)rw.lo * nx;
+            }
             a[it] = u[cu]; b[it] = v[cv];
             ka[it] = stage ? kpu[cu] : 0.0; kb[it] = stage ? kpv[cv] : 0.0;
         }
@@ -251,8 +268,8 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
             if (ok[it]) {
                 const double *pu = &su[ry + 1][rx + 1], *pv = &sv[ry + 1][rx + 1];
-                const double dudx = grad2(pu, 1, i, nx, h2x), dvdy = grad2(pv, MS_UX, j, ny, h2y);
-                const double dudy = grad2(pu, MS_UX, j, ny, h2y), dvdx = grad2(pv, 1, i, nx, h2x);
+                const double dudx = g2<IN>(pu, 1, i, nx, h2x), dvdy = g2<IN>(pv, MS_UX, j, ny, h2y);
+                const double dudy = g2<IN>(pu, MS_UX, j, ny, h2y), dvdx = g2<IN>(pv, 1, i, nx, h2x);
                 double e1 = ex[it], e2 = ey[it], e3 = exy[it];
                 if (visc && sol[it]) {
                     e1 = e1 + eta_s * dudx;
@@ -304,22 +321,27 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             const int j = j0 + ry, i = i0 + rx;
             if (!ok[it]) continue;
             const long c = (long)j * nx + i;
-            const double divx = grad2(&gx[ry + 2][rx + 2], 1, i, nx, h2x) +
-                                grad2(&gm[ry + 2][rx + 2], MS_GX, j, ny, h2y);
-            const double divy = grad2(&gm[ry + 2][rx + 2], 1, i, nx, h2x) +
-                                grad2(&gy[ry + 2][rx + 2], MS_GX, j, ny, h2y);
+            const double divx = g2<IN>(&gx[ry + 2][rx + 2], 1, i, nx, h2x) +
+                                g2<IN>(&gm[ry + 2][rx + 2], MS_GX, j, ny, h2y);
+            const double divy = g2<IN>(&gm[ry + 2][rx + 2], 1, i, nx, h2x) +
+                                g2<IN>(&gy[ry + 2][rx + 2], MS_GX, j, ny, h2y);
             const double *pu = &su[ry + 3][rx + 3], *pv = &sv[ry + 3][rx + 3];
             const double uc = *pu, vc = *pv;
-            const double uadv = -uc * upwind3(pu, 1, i, nx, uc, dx) - vc * upwind3(pu, MS_UX, j, ny, vc, dy);
-            const double vadv = -uc * upwind3(pv, 1, i, nx, uc, dx) - vc * upwind3(pv, MS_UX, j, ny, vc, dy);
+            const double uadv = -uc * u3<IN>(pu, 1, i, nx, uc, dx) - vc * u3<IN>(pu, MS_UX, j, ny, vc, dy);
+            const double vadv = -uc * u3<IN>(pv, 1, i, nx, uc, dx) - vc * u3<IN>(pv, MS_UX, j, ny, vc, dy);
             // grad2 of p with the operands loaded above (same expressions as grad2)
             double dpx, dpy;
+            if (IN) {
+                dpx = (pxp[it] - pxm[it]) / h2x;
+                dpy = (pyp[it] - pym[it]) / h2y;
+            } else {
             if (i == 0) dpx = (-3 * pc[it] + 4 * pxp[it] - p[c + 2]) / h2x;
             else if (i == nx - 1) dpx = (3 * pc[it] - 4 * pxp[it] + p[c - 2]) / h2x;
             else dpx = (pxp[it] - pxm[it]) / h2x;
             if (j == 0) dpy = (-3 * pc[it] + 4 * pyp[it] - p[c + 2L * nx]) / h2y;
             else if (j == ny - 1) dpy = (3 * pc[it] - 4 * pyp[it] + p[c - 2L * nx]) / h2y;
             else dpy = (pyp[it] - pym[it]) / h2y;
+            }
             const double h = hh[it];
             const double den = ((1 - h) * rho_s + h * rho_f) + 1e-12;
             const double k1 = uadv + (divx + 0.0 - dpx) / den;
@@ -332,6 +354,40 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
             }
         }
     }
+}
+
+__global__ void __launch_bounds__(MS_T) k_mom_stage(
+    const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
+    const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
+    const double *__restrict__ sxx, const double *__restrict__ sxy,
+    const double *__restrict__ syy, const double *__restrict__ H,
+    const unsigned char *__restrict__ solid, int visc, double mu_f, double eta_s, double rho_s,
+    double rho_f, const double *__restrict__ p, double dt6, double dx, double dy, int ny, int nx,
+    int tiles_x, int ntiles, double *__restrict__ ku, double *__restrict__ kv,
+    const double *__restrict__ ainu, const double *__restrict__ ainv, double *__restrict__ accu,
+    double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
+    const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
+    int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
+    const unsigned char *__restrict__ fluid_rows) {
+    __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
+    if (dtp) {   // the same roundings as mom_stage's host constants
+        const double dt = *dtp;
+        coef = stage == 0 ? 0.0 : stage == 3 ? dt : 0.5 * dt;
+        dt6 = dt / 6.0;
+    }
+    __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
+    // tlist: the listed tiles only (momentum_fixup); otherwise every tile of rows [jb, je)
+    if (tlist && (int)blockIdx.x >= *tcount) return;
+    const int tile = tlist ? tlist[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
+    const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
+    // interior tile: its whole 3-cell halo lies inside the grid's interior and the resident
+    // rows, so no BC copy and no one-sided edge stencil is ever taken (same arithmetic)
+    const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 && j0 - 3 >= max(rw.lo, 2) &&
+                          j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
+    if (interior)
+        ms_tile<true>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_rows, i0, j0, su, sv, gx, gm, gy);
+    else
+        ms_tile<false>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_rows, i0, j0, su, sv, gx, gm, gy);
 }
 
 // per row j of [jlo, jhi) (out row j - jlo) and 64-column tile tx: all of phi[j][64 tx - 2 .. 64 tx + 66) (the

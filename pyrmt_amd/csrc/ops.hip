@@ -818,7 +818,7 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,
-                      double *m2part) {
+                      double *m2part, bool sub_mean) {
     const long n = (long)ctx->ny * ctx->nx;
     double *pc = ctx->scratch + n, *root = ctx->red + RED_BLOCKS + 17;
     RMT_TRY(dct_solve_after_rows(ctx, pc, root));
@@ -826,7 +826,7 @@ int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, 
         a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt / rho, bc_kind, lid, a, b, p, 0,
         ctx->ny, root, (double)n, dtp, rho, m2part);
     RMT_LAUNCHED();
-    return sub_mean_rows(ctx, p, ctx->ny, ctx->nx);
+    return sub_mean ? sub_mean_rows(ctx, p, ctx->ny, ctx->nx) : RMT_OK;
 }
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                    double dy, const double *dtp, double rho, int bc_kind, double lid,

@@ -450,7 +450,7 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,
-                      double *m2part);
+                      double *m2part, bool sub_mean = true);
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                    double dy, const double *dtp, double rho, int bc_kind, double lid,
                    const double *p_prev, double *a, double *b, double *p, double *m2part);

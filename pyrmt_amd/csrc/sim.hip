@@ -56,7 +56,7 @@ struct rmt_sim {
     // extrapolation reads) before the chain, the rest beside it on the second stream
     unsigned long long *rimw = nullptr;
     int *rimcnt = nullptr;
-    hipEvent_t e_bits = nullptr;
+    hipEvent_t e_bits = nullptr, e_proj = nullptr, e_tail = nullptr;
     // the next step's known plane, written by the phi kernels of this step (nx % 64 == 0):
     // double-buffered with kbits, valid from the second step of a call on
     unsigned long long *kbits_next = nullptr;
@@ -539,7 +539,11 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     S->segs = (int *)(S->kbits_next + (size_t)ny * Wn);
     S->m2acc = (unsigned long long *)(S->segs + (((size_t)ny * ((nx + 255) / 256) + 3) & ~(size_t)1));
     RMT_HIP(hipMemsetAsync(S->m2acc, 0, 2 * sizeof(unsigned long long), ctx->stream));
-    if (S->st2) RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
+    if (S->st2) {
+        RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_proj, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_tail, hipEventDisableTiming));
+    }
     if (S->st2 && prm->rho_f > 0) {
         RMT_TRY(dct_plan(ctx, prm->dx, prm->dy));
         S->split_proj = dct_lds_ready(ctx) && ny <= ctx->rsum_len;
@@ -558,6 +562,8 @@ int rmt_sim_destroy(rmt_sim *S) {
     if (S->e_mom) (void)hipEventDestroy(S->e_mom);
     if (S->e_rows) (void)hipEventDestroy(S->e_rows);
     if (S->e_bits) (void)hipEventDestroy(S->e_bits);
+    if (S->e_proj) (void)hipEventDestroy(S->e_proj);
+    if (S->e_tail) (void)hipEventDestroy(S->e_tail);
     if (S->st2) (void)hipStreamDestroy(S->st2);
     for (auto e : S->pev) if (e) (void)hipEventDestroy(e);
     S->ctx->prof = false;
@@ -614,7 +620,16 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     const bool async = !force_sync && !S->prof && std::isinf(t_end) && t_end > 0 &&
                        P.scheme == RMT_SCHEME_SEMILAGRANGIAN;
     int slot = 0;
+    // the step's tail (p -= mean(p), the diagnostics) may run on the second stream beside the
+    // next step's band passes; joined before the ring is read and when the call returns
+    bool tail = false;
+    auto join = [&]() -> int {
+        if (tail) RMT_HIP(hipStreamWaitEvent(st, S->e_tail, 0));
+        tail = false;
+        return RMT_OK;
+    };
     auto flush = [&]() -> int {
+        RMT_TRY(join());
         if (!slot) return RMT_OK;
         std::vector<double> h((size_t)slot * RING_VALS);
         RMT_HIP(hipMemcpyAsync(h.data(), S->ring, h.size() * sizeof(double),
@@ -668,6 +683,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // feed runs beside it: the momentum of every cell, from the pre-extrapolation map, on
         // a second stream, re-run afterwards on the tiles within reach of a target
         static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
+        static const bool side_tail = !(getenv("RMT_SIDE_TAIL") && !atoi(getenv("RMT_SIDE_TAIL")));
         const bool overlap = solid && S->st2 && !no_overlap;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
@@ -801,7 +817,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                     S->rowmark, S->tiles, S->tcount, S->max_tiles));
             RMT_TRY(projection_finish(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, P.bc_kind,
                                       P.lid, S->p, S->u, S->v, S->p,
-                                      async ? S->m2part : nullptr));
+                                      async ? S->m2part : nullptr, !(async && side_tail)));
         } else if (async)
             RMT_TRY(projection_dev(ctx, S->us, S->vs, P.dx, P.dy, dtp, P.rho_f, P.bc_kind, P.lid,
                                    S->p, S->u, S->v, S->p, S->m2part));
@@ -813,6 +829,28 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // no gain: both are HBM-bound)
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
                    P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa, 0, ny};
+        if (async && overlap && S->split_proj && side_tail) {
+            // p -= mean(p) and the diagnostics on the second stream: nothing before the next
+            // step's chain reads p or writes what they read (that stream's next work -- the
+            // speculative phi, momentum -- is queued behind them)
+            double *e = S->ring + (size_t)slot * RING_VALS;
+            RMT_HIP(hipEventRecord(S->e_proj, st));
+            RMT_HIP(hipStreamWaitEvent(S->st2, S->e_proj, 0));
+            ctx->stream = S->st2;
+            const int ts = sub_mean_rows(ctx, S->p, ny, nx);
+            ctx->stream = st;
+            RMT_TRY(ts);
+            k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
+            k_diag_p2<<<1, DIAG_T, 0, S->st2>>>(S->dscr, e);
+            RMT_LAUNCHED();
+            RMT_HIP(hipEventRecord(S->e_tail, S->st2));
+            tail = true;
+            k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
+            RMT_LAUNCHED();
+            if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
+            if (++slot == RING_N) RMT_TRY(flush());
+            continue;
+        }
         k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, S->dscr);
         if (async) {
             double *e = S->ring + (size_t)slot * RING_VALS;
