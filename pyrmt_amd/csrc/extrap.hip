@@ -686,20 +686,18 @@ size_t extrap_workspace(int ny, int nx, int max_layers) {
     return b;
 }
 
-int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
-                double dy, int max_layers, double *X1o, double *X2o, int *dev_status,
-                const u64 *kin) {
+// The geometry half of the extrapolation: everything the known plane decides (targets,
+// acceptance, chain order, record layouts, the fallback sweep's candidate rows).  In place
+// (X1o == X1) with a known plane kin, it reads no map value, so the fused step runs it for the
+// next step beside the projection (sim.hip); otherwise (copy or phi-derived known set) the
+// map is copied / read here and the call is simply the first half of extrapolate().
+int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi,
+                    double dx, double dy, int max_layers, double *X1o, double *X2o,
+                    const u64 *kin) {
     const int ny = ctx->ny, nx = ctx->nx;
-    const long n = (long)ny * nx;
     const int W = (nx + 63) / 64;
-    if (max_layers <= 0) {
-        if (X1o != X1) RMT_HIP(hipMemcpyAsync(X1o, X1, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        if (X2o != X2) RMT_HIP(hipMemcpyAsync(X2o, X2, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        if (dev_status) RMT_HIP(hipMemsetAsync(dev_status, 0, 2 * sizeof(int), ctx->stream));
-        return RMT_OK;
-    }
-    RMT_CHECK(ny >= 3 && nx >= 3 && ny < (1 << 20) && nx < (1 << 30), RMT_EINVAL,
-              "extrapolation grid size");
+    RMT_CHECK(max_layers > 0 && ny >= 3 && nx >= 3 && ny < (1 << 20) && nx < (1 << 30),
+              RMT_EINVAL, "extrapolation grid size");
     RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, max_layers)));
     const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
     const int force = g_ex_mode;
@@ -733,6 +731,21 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
     const int *ctl = chain ? ws.ctl : nullptr;
     k_ex_dilate<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(
         ws.kbits, ny, nx, W, max_layers, ws.cbits, ws.rowcand, ws.jrange, ctl);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+// The value half after extrap_geometry (same ctx, same map, same layers): the static terms of
+// the records, the fallback sweep (an early exit unless a capacity limit tripped), the chain.
+int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
+                  int *dev_status) {
+    const int ny = ctx->ny, nx = ctx->nx;
+    const int W = (nx + 63) / 64;
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
+    const int force = g_ex_mode;
+    const bool chain = ctx->ex_chain;
+    const int *ctl = chain ? ws.ctl : nullptr;
+    if (chain) RMT_TRY(extrap_chain_values(ctx, ws, X1o, X2o, dx, dy, max_layers));
     if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
     ExSweep A{X1o, X2o, ws.kbits, ws.cbits, ws.Kold, ws.rowcand, ws.jrange, ny, nx, W,
               max_layers, dx, dy, ws.status, ctl};
@@ -777,6 +790,20 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                                ctx->stream));
     if (ctx->ev_chain && !chain) RMT_HIP(hipEventRecord(ctx->ev_chain, ctx->stream));
     return RMT_OK;
+}
+
+int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
+                double dy, int max_layers, double *X1o, double *X2o, int *dev_status,
+                const u64 *kin) {
+    const long n = (long)ctx->ny * ctx->nx;
+    if (max_layers <= 0) {
+        if (X1o != X1) RMT_HIP(hipMemcpyAsync(X1o, X1, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        if (X2o != X2) RMT_HIP(hipMemcpyAsync(X2o, X2, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        if (dev_status) RMT_HIP(hipMemsetAsync(dev_status, 0, 2 * sizeof(int), ctx->stream));
+        return RMT_OK;
+    }
+    RMT_TRY(extrap_geometry(ctx, X1, X2, phi, dx, dy, max_layers, X1o, X2o, kin));
+    return extrap_finish(ctx, dx, dy, max_layers, X1o, X2o, dev_status);
 }
 
 }  // namespace rmt

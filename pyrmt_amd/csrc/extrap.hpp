@@ -56,6 +56,8 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes);
 // chain path: queue the kernels; they check ctl[EXC_FALLBACK] themselves
 int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
                       double dx, double dy, int ML);
+int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
+                        double dx, double dy, int ML);
 int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o, int ML);
 bool extrap_chain_supported(int ny, int nx, int ML);
 

@@ -159,7 +159,10 @@ struct ExGeoArgs {
 
 // One wave fits target `id` of layer A.L.  Same-layer acceptance of earlier targets is read
 // from T (FIX = false: speculation) or from ACC through L2 (FIX = true: k_ex_fix, where ACC
-// changes inside the launch).  Emits the record if accepted; returns acceptance (uniform).
+// changes inside the launch).  Emits the record's geometry if accepted (Cramer constants, the
+// term layout, the dynamic sources and their coefficients -- everything the known plane
+// decides); the values of the static terms (P and the static products) are filled in by
+// k_ex_vals once the map is advected.  Returns acceptance (uniform).
 template <bool FIX>
 __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, int lane) {
     const ExWs &ws = A.ws;
@@ -170,13 +173,13 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
     const u64 *SL = (FIX ? ws.ACC : ws.T) + (long)L * plane;
     const double x0 = A.dx * i, y0 = A.dy * j;
     bool inc[2], st[2];
-    double w[2], xi[2], yi[2], b1[2], b2[2];
+    double w[2], xi[2], yi[2];
     int src[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
         inc[h] = false; st[h] = false;
-        w[h] = 0.0; b1[h] = 0.0; b2[h] = 0.0; src[h] = -1;
+        w[h] = 0.0; src[h] = -1;
         xi[h] = A.dx * ii; yi[h] = A.dy * jj;
         if (q < 81 && jj >= 0 && jj < ny && ii >= 0 && ii < nx) {
             const double ax = xi[h] - x0, ay = yi[h] - y0, d2 = ax * ax + ay * ay;
@@ -191,10 +194,7 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
                 if (inc[h]) {
                     w[h] = exp_glibc_tab(-d2 / A.r2, tab);   // libm exp, bit for bit
                     st[h] = (ws.kbits[o] & bit) != 0;
-                    if (st[h]) {
-                        const long cc = (long)jj * nx + ii;
-                        b1[h] = A.X1[cc]; b2[h] = A.X2[cc];
-                    } else {
+                    if (!st[h]) {
                         int Ls = L;
                         if (!sl)
                             for (Ls = 0; Ls < L; ++Ls)
@@ -208,33 +208,26 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
     // first dynamic window position (the static prefix before it is pre-summed)
     const u64 dl = __ballot(inc[0] && !st[0]), dh = __ballot(inc[1] && !st[1] && lane < 17);
     const int qf = dl ? __builtin_ctzll(dl) : (dh ? 64 + __builtin_ctzll(dh) : 81);
-    // terms of functions.py:128-145: rows 0-5 Aw (every included cell), rows 6-11 the
-    // Bw prefix (static cells before qf); excluded cells contribute +0.0 (exact)
+    // terms of functions.py:140-145: Aw over every included cell; excluded cells contribute
+    // +0.0 (exact)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int q = lane + 64 * h;
         if (q >= 81) break;
         const double wa0 = w[h] * 1.0, wa1 = w[h] * xi[h], wa2 = w[h] * yi[h];
-        const bool pre = st[h] && q < qf;
         tb[0 * EXS + q] = inc[h] ? wa0 * 1.0 : 0.0;
         tb[1 * EXS + q] = inc[h] ? wa0 * xi[h] : 0.0;
         tb[2 * EXS + q] = inc[h] ? wa0 * yi[h] : 0.0;
         tb[3 * EXS + q] = inc[h] ? wa1 * xi[h] : 0.0;
         tb[4 * EXS + q] = inc[h] ? wa1 * yi[h] : 0.0;
         tb[5 * EXS + q] = inc[h] ? wa2 * yi[h] : 0.0;
-        tb[6 * EXS + q] = pre ? wa0 * b1[h] : 0.0;
-        tb[7 * EXS + q] = pre ? wa1 * b1[h] : 0.0;
-        tb[8 * EXS + q] = pre ? wa2 * b1[h] : 0.0;
-        tb[9 * EXS + q] = pre ? wa0 * b2[h] : 0.0;
-        tb[10 * EXS + q] = pre ? wa1 * b2[h] : 0.0;
-        tb[11 * EXS + q] = pre ? wa2 * b2[h] : 0.0;
     }
     const u64 il = __ballot(inc[0]), ih = __ballot(inc[1] && lane < 17);
     const int count = __popcll(il) + __popcll(ih);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     double acc = 0.0;
-    if (lane < 12) {
+    if (lane < 6) {
         const double2 *t2 = (const double2 *)(tb + lane * EXS);
         double2 t[40];
 #pragma unroll
@@ -291,11 +284,7 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
         if (!term) continue;
         const int k = h ? __popcll(tl) + __popcll(th & lt) : __popcll(tl & lt);
         const double wa0 = w[h] * 1.0, wa1 = w[h] * xi[h], wa2 = w[h] * yi[h];
-        if (st[h]) {
-            tv[0 * npad + k] = wa0 * b1[h]; tv[1 * npad + k] = wa1 * b1[h];
-            tv[2 * npad + k] = wa2 * b1[h]; tv[3 * npad + k] = wa0 * b2[h];
-            tv[4 * npad + k] = wa1 * b2[h]; tv[5 * npad + k] = wa2 * b2[h];
-        } else {
+        if (!st[h]) {   // (static products: k_ex_vals)
             const int dk = h ? __popcll(dl) + __popcll(dh & lt) : __popcll(dl & lt);
             dyn[4 * dk] = __longlong_as_double(((long long)src[h] << 32) | (unsigned)k);
             dyn[4 * dk + 1] = wa0; dyn[4 * dk + 2] = wa1; dyn[4 * dk + 3] = wa2;
@@ -313,14 +302,13 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
         rec[16] = 1.0 / det;
         rec[23] = 0.0;
     }
-    if (lane >= 6 && lane < 12) rec[17 + lane - 6] = acc;   // P[0..5]
     if (lane == 0) ws.recoff[id] = ((long long)(bytes >> 6) << 32) | (long long)(off >> 6);
     return true;
 }
 
 __global__ void __launch_bounds__(256) k_ex_geom(ExGeoArgs A) {
     __shared__ u64 tab[256];
-    __shared__ __attribute__((aligned(16))) double tb[4][12 * EXS];
+    __shared__ __attribute__((aligned(16))) double tb[4][6 * EXS];
     for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
     __syncthreads();
     const ExWs &ws = A.ws;
@@ -335,6 +323,117 @@ __global__ void __launch_bounds__(256) k_ex_geom(ExGeoArgs A) {
         const int r = atomicAdd(ws.ctl + EXC_REJ + A.L, 1);
         if (r < EX_MAXREJ) ws.rej[A.L * EX_MAXREJ + r] = id;
         else ws.ctl[EXC_FALLBACK] = 1;
+    }
+}
+
+
+// ------------------------------------------------------------------ 1. values ------
+// The value half of a record (k_ex_geom wrote the geometry): P[0..5] = the ordered sums of
+// the static terms before the first dynamic one (functions.py:128-138, window order), and
+// the 6 products w*a*X of every static term from there on, at the record's term slots.  The
+// same window analysis as ex_geom (final same-layer acceptance from ACC), the same operands.
+// One wave per accepted fit, every layer in one launch.
+__global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML) {
+    __shared__ u64 tab[256];
+    __shared__ __attribute__((aligned(16))) double tb[4][6 * EXS];
+    for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
+    __syncthreads();
+    const ExWs &ws = A.ws;
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int total = ws.ctl[EXC_BASE + ML];
+    const int W = A.W, nx = A.nx, ny = A.ny;
+    const long plane = ws.plane;
+    double *T = tb[wv];
+    for (int id = blockIdx.x * 4 + wv; id < total; id += gridDim.x * 4) {
+        const long long r = ws.recoff[id];
+        if (r < 0) continue;
+        int L = ML - 1;
+        while (L > 0 && id < ws.ctl[EXC_BASE + L]) --L;
+        const long c = ws.tcell[id];
+        const int j = (int)(c / nx), i = (int)(c % nx);
+        const u64 *Kst = L == 0 ? ws.kbits : ws.KN + (long)(L - 1) * plane;
+        const u64 *SL = ws.ACC + (long)L * plane;
+        const double x0 = A.dx * i, y0 = A.dy * j;
+        bool inc[2], st[2];
+        double w[2], xi[2], yi[2], b1[2], b2[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
+            inc[h] = false; st[h] = false;
+            w[h] = 0.0; b1[h] = 0.0; b2[h] = 0.0;
+            xi[h] = A.dx * ii; yi[h] = A.dy * jj;
+            if (q < 81 && jj >= 0 && jj < ny && ii >= 0 && ii < nx) {
+                const double ax = xi[h] - x0, ay = yi[h] - y0, d2 = ax * ax + ay * ay;
+                if (d2 <= A.r2) {
+                    const long o = (long)jj * W + (ii >> 6);
+                    const u64 bit = 1ull << (ii & 63);
+                    const bool ks = (Kst[o] & bit) != 0;
+                    bool sl = false;
+                    if (!ks && (jj < j || (jj == j && ii < i))) sl = (SL[o] & bit) != 0;
+                    inc[h] = ks || sl;
+                    if (inc[h]) {
+                        st[h] = (ws.kbits[o] & bit) != 0;
+                        if (st[h]) {
+                            w[h] = exp_glibc_tab(-d2 / A.r2, tab);   // libm exp, bit for bit
+                            const long cc = (long)jj * nx + ii;
+                            b1[h] = A.X1[cc]; b2[h] = A.X2[cc];
+                        }
+                    }
+                }
+            }
+        }
+        const u64 dl = __ballot(inc[0] && !st[0]), dh = __ballot(inc[1] && !st[1] && lane < 17);
+        const int qf = dl ? __builtin_ctzll(dl) : (dh ? 64 + __builtin_ctzll(dh) : 81);
+        // the Bw prefix: static cells before qf (functions.py:133-138 order), +0.0 elsewhere
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = lane + 64 * h;
+            if (q >= 81) break;
+            const double wa0 = w[h] * 1.0, wa1 = w[h] * xi[h], wa2 = w[h] * yi[h];
+            const bool pre = st[h] && q < qf;
+            T[0 * EXS + q] = pre ? wa0 * b1[h] : 0.0;
+            T[1 * EXS + q] = pre ? wa1 * b1[h] : 0.0;
+            T[2 * EXS + q] = pre ? wa2 * b1[h] : 0.0;
+            T[3 * EXS + q] = pre ? wa0 * b2[h] : 0.0;
+            T[4 * EXS + q] = pre ? wa1 * b2[h] : 0.0;
+            T[5 * EXS + q] = pre ? wa2 * b2[h] : 0.0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        double acc = 0.0;
+        if (lane < 6) {
+            const double2 *t2 = (const double2 *)(T + lane * EXS);
+            double2 t[40];
+#pragma unroll
+            for (int q2 = 0; q2 < 40; ++q2) t[q2] = t2[q2];
+            const double last = T[lane * EXS + 80];
+#pragma unroll
+            for (int q2 = 0; q2 < 40; ++q2) { acc += t[q2].x; acc += t[q2].y; }
+            acc += last;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // static products from qf on, at the compact term slots of ex_geom's record
+        double *rec = (double *)(ws.arena + ((r & 0xffffffffLL) << 6));
+        const long long meta = __double_as_longlong(rec[1]);
+        const int npad = (int)(meta & 0xffffffff), nd = (int)((meta >> 32) & 0x7fffffff);
+        double *tv = rec + CH_HDR + 4 * nd;
+        const u64 il = __ballot(inc[0]), ih = __ballot(inc[1] && lane < 17);
+        const u64 lt = (1ull << lane) - 1;
+        const u64 tl = il & ~((qf >= 64) ? ~0ull : ((1ull << qf) - 1));
+        const u64 th = ih & ~((qf >= 64) ? ((1ull << (qf - 64)) - 1) : 0ull);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const bool term = h ? ((th >> lane) & 1) && lane < 17 : (tl >> lane) & 1;
+            if (!term || !st[h]) continue;
+            const int k = h ? __popcll(tl) + __popcll(th & lt) : __popcll(tl & lt);
+            const double wa0 = w[h] * 1.0, wa1 = w[h] * xi[h], wa2 = w[h] * yi[h];
+            tv[0 * npad + k] = wa0 * b1[h]; tv[1 * npad + k] = wa1 * b1[h];
+            tv[2 * npad + k] = wa2 * b1[h]; tv[3 * npad + k] = wa0 * b2[h];
+            tv[4 * npad + k] = wa1 * b2[h]; tv[5 * npad + k] = wa2 * b2[h];
+        }
+        if (lane < 6) rec[17 + lane] = acc;   // P[0..5]
     }
 }
 
@@ -363,7 +462,7 @@ __device__ void ex_add_dependents(const ExGeoArgs &A, int id, int *dlist, int *d
 // Jacobi re-fits of the targets downstream of rejections until acceptance is a fixed point.
 __global__ void __launch_bounds__(FIXW * 64) k_ex_fix(ExGeoArgs A) {
     __shared__ u64 tab[256];
-    __shared__ __attribute__((aligned(16))) double tb[FIXW][12 * EXS];
+    __shared__ __attribute__((aligned(16))) double tb[FIXW][6 * EXS];
     __shared__ int dlist[EX_DCAP];
     __shared__ unsigned char dres[EX_DCAP];
     __shared__ int dn, nflip;
@@ -954,6 +1053,18 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
     k_ex_local<<<1, 1024, 0, st>>>(ws, ML);
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+// the value half of the records (after the map is advected; k_ex_vals)
+int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
+                        double dx, double dy, int ML) {
+    const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
+    const double r = 4 * std::sqrt(dx * dx + dy * dy);
+    ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r};
+    const unsigned gblocks = (unsigned)std::min<long>(1024, std::max<long>(1, ws.maxt / 4));
+    k_ex_vals<<<gblocks, 256, 0, ctx->stream>>>(A, ML);
     RMT_LAUNCHED();
     return RMT_OK;
 }

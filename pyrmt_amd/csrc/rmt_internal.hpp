@@ -548,6 +548,14 @@ void dct_destroy(DctPlan *);
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
                 double dy, int max_layers, double *X1o, double *X2o, int *dev_status = nullptr,
                 const unsigned long long *kin = nullptr);
+// extrapolate() in two halves: the geometry (reads no map value when kin is given and the
+// call is in place) and the values + chain (max_layers > 0; same ctx, nothing else may use
+// ctx->bytes in between)
+int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi,
+                    double dx, double dy, int max_layers, double *X1o, double *X2o,
+                    const unsigned long long *kin);
+int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
+                  int *dev_status);
 size_t extrap_workspace(int ny, int nx, int max_layers);   // bytes of ctx->bytes it uses
 // the exact no-op test of extrapolate() (k_ex_none) on rows [jb, je) of a whole known plane:
 // ctl[EXC_ANY] (extrap.hpp; zeroed by the caller) set iff a first-layer target there fits
