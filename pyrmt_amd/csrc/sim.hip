@@ -56,7 +56,7 @@ struct rmt_sim {
     // extrapolation reads) before the chain, the rest beside it on the second stream
     unsigned long long *rimw = nullptr;
     int *rimcnt = nullptr;
-    hipEvent_t e_bits = nullptr, e_proj = nullptr, e_tail = nullptr;
+    hipEvent_t e_bits = nullptr, e_proj = nullptr, e_tail = nullptr, e_kb = nullptr, e_geo = nullptr;
     // the next step's known plane, written by the phi kernels of this step (nx % 64 == 0):
     // double-buffered with kbits, valid from the second step of a call on
     unsigned long long *kbits_next = nullptr;
@@ -543,6 +543,8 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
         RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_proj, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_tail, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_kb, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_geo, hipEventDisableTiming));
     }
     if (S->st2 && prm->rho_f > 0) {
         RMT_TRY(dct_plan(ctx, prm->dx, prm->dy));
@@ -564,6 +566,8 @@ int rmt_sim_destroy(rmt_sim *S) {
     if (S->e_bits) (void)hipEventDestroy(S->e_bits);
     if (S->e_proj) (void)hipEventDestroy(S->e_proj);
     if (S->e_tail) (void)hipEventDestroy(S->e_tail);
+    if (S->e_kb) (void)hipEventDestroy(S->e_kb);
+    if (S->e_geo) (void)hipEventDestroy(S->e_geo);
     if (S->st2) (void)hipStreamDestroy(S->st2);
     for (auto e : S->pev) if (e) (void)hipEventDestroy(e);
     S->ctx->prof = false;
@@ -622,8 +626,29 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     int slot = 0;
     // the step's tail (p -= mean(p), the diagnostics) may run on the second stream beside the
     // next step's band passes; joined before the ring is read and when the call returns
-    bool tail = false;
+    // Deferred to the second stream's next start (the next chain's launch), so that it does
+    // not crowd the next step's rim advection and record values either.
+    bool tail = false, pending = false;
+    double *pend_e = nullptr;
+    auto emit_tail = [&]() -> int {
+        if (!pending) return RMT_OK;
+        pending = false;
+        DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
+                   P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa, 0, ny};
+        RMT_HIP(hipStreamWaitEvent(S->st2, S->e_proj, 0));
+        ctx->stream = S->st2;
+        const int ts = sub_mean_rows(ctx, S->p, ny, nx);
+        ctx->stream = st;
+        RMT_TRY(ts);
+        k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
+        k_diag_p2<<<1, DIAG_T, 0, S->st2>>>(S->dscr, pend_e);
+        RMT_LAUNCHED();
+        RMT_HIP(hipEventRecord(S->e_tail, S->st2));
+        tail = true;
+        return RMT_OK;
+    };
     auto join = [&]() -> int {
+        RMT_TRY(emit_tail());
         if (tail) RMT_HIP(hipStreamWaitEvent(st, S->e_tail, 0));
         tail = false;
         return RMT_OK;
@@ -646,6 +671,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         return RMT_OK;
     };
     S->bits_ready = false;   // the caller may have changed the map between calls
+    // the next step's rim words and extrapolation geometry, prepared on the second stream
+    // beside this step's projection (they depend on the known plane alone)
+    static const bool geo_env = !(getenv("RMT_EARLY_GEOMETRY") && !atoi(getenv("RMT_EARLY_GEOMETRY")));
+    bool geo_ready = false;
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end)) break;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[0], st));
@@ -697,12 +726,17 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     k_sim_bits<<<gsl, 256, 0, st>>>(S->X1, S->X2, nx, P.x0, P.y0, P.R, S->kbits);
                     RMT_LAUNCHED();
                 }
-                RMT_TRY(rim_words(ctx, S->kbits, ny, nx, (nx + 63) / 64, S->rimw, S->rimcnt));
-                RMT_HIP(hipEventRecord(S->e_bits, st));
                 const long nseg = (long)ny * ((nx + 255) / 256);
                 int *scount = S->segs + nseg;
-                RMT_HIP(hipMemsetAsync(scount, 0, sizeof(int), st));
-                k_rim_segments<<<grid1d(nseg, 256), 256, 0, st>>>(S->rimw, ny, nx, S->segs, scount);
+                if (geo_ready) {
+                    RMT_HIP(hipStreamWaitEvent(st, S->e_geo, 0));
+                } else {
+                    RMT_TRY(rim_words(ctx, S->kbits, ny, nx, (nx + 63) / 64, S->rimw, S->rimcnt));
+                    RMT_HIP(hipMemsetAsync(scount, 0, sizeof(int), st));
+                    k_rim_segments<<<grid1d(nseg, 256), 256, 0, st>>>(S->rimw, ny, nx, S->segs,
+                                                                       scount);
+                }
+                RMT_HIP(hipEventRecord(S->e_bits, st));
                 k_sim_sl_rim<<<1024, 256, 0, st>>>(
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.x0, P.y0,
                     P.R, S->X1n, S->X2n, S->flag, sc, dtp, S->rimw, S->segs, scount);
@@ -738,12 +772,16 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // chip-wide passes are done and the one-workgroup chain kernel is launched
             if (overlap) ctx->ev_chain = S->e_sl;
             const bool kb = P.scheme == RMT_SCHEME_SEMILAGRANGIAN;   // k_sim_sl wrote kbits
-            const int es = extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
-                                       S->X1n, S->X2n, S->flag + 2, kb ? S->kbits : nullptr);
+            const int es = geo_ready && P.layers > 0
+                               ? extrap_finish(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->flag + 2)
+                               : extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
+                                             S->X1n, S->X2n, S->flag + 2, kb ? S->kbits : nullptr);
+            geo_ready = false;
             ctx->ev_chain = nullptr;
             RMT_TRY(es);
             if (overlap) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
+                RMT_TRY(emit_tail());   // the previous step's tail, beside the chain
                 // the fix-up tiles and the rows they reach depend on the known plane only
                 ctx->stream = S->st2;
                 const int fs = extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount);
@@ -796,6 +834,29 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                                        S->phi, S->X1, S->X2, S->tiles, S->tcount,
                                                        tiles_x, nb);
             RMT_LAUNCHED();
+            if (async && geo_env && nb && P.layers > 0 && it + 1 < nsteps) {
+                // the next step's known plane is final (k_phi_tiles): its rim words, rim
+                // segments and extrapolation geometry on the second stream, beside the rest of
+                // this step (nothing there uses them or the extrapolation workspace)
+                RMT_HIP(hipEventRecord(S->e_kb, st));
+                RMT_HIP(hipStreamWaitEvent(S->st2, S->e_kb, 0));
+                const long nseg = (long)ny * ((nx + 255) / 256);
+                int *scount = S->segs + nseg;
+                ctx->stream = S->st2;
+                int gs = rim_words(ctx, nb, ny, nx, (nx + 63) / 64, S->rimw, S->rimcnt);
+                if (gs == RMT_OK)
+                    gs = hipMemsetAsync(scount, 0, sizeof(int), S->st2) ? RMT_EDEVICE : RMT_OK;
+                if (gs == RMT_OK) {
+                    k_rim_segments<<<grid1d(nseg, 256), 256, 0, S->st2>>>(S->rimw, ny, nx,
+                                                                           S->segs, scount);
+                    gs = extrap_geometry(ctx, S->X1n, S->X2n, nullptr, P.dx, P.dy, P.layers,
+                                         S->X1n, S->X2n, nb);
+                }
+                ctx->stream = st;
+                RMT_TRY(gs);
+                RMT_HIP(hipEventRecord(S->e_geo, S->st2));
+                geo_ready = true;
+            }
             RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
                                    S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,
                                    S->max_tiles));
@@ -835,16 +896,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // speculative phi, momentum -- is queued behind them)
             double *e = S->ring + (size_t)slot * RING_VALS;
             RMT_HIP(hipEventRecord(S->e_proj, st));
-            RMT_HIP(hipStreamWaitEvent(S->st2, S->e_proj, 0));
-            ctx->stream = S->st2;
-            const int ts = sub_mean_rows(ctx, S->p, ny, nx);
-            ctx->stream = st;
-            RMT_TRY(ts);
-            k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
-            k_diag_p2<<<1, DIAG_T, 0, S->st2>>>(S->dscr, e);
-            RMT_LAUNCHED();
-            RMT_HIP(hipEventRecord(S->e_tail, S->st2));
-            tail = true;
+            pend_e = e;
+            pending = true;
             k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
             RMT_LAUNCHED();
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
