@@ -196,77 +196,93 @@ __device__ __forceinline__ void ms_tile(
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
-    const unsigned char *__restrict__ fluid_rows, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
+    const unsigned char *__restrict__ fluid_tiles, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
     double (&gx)[MS_GY][MS_GX], double (&gm)[MS_GY][MS_GX], double (&gy)[MS_GY][MS_GX]) {
     const double h2x = 2 * dx, h2y = 2 * dy;
-    // pure-fluid tile (k_fluid_rows): every cell the blended stress is formed on has
-    // phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not solid
-    // exactly -- those constants replace the loads of sxx, sxy, syy, H and solid below (the
-    // arithmetic is unchanged).  Rows outside the resident window are never loaded anyway.
-    int fpred = 0;
-    if (fluid_rows) {
-        fpred = 1;
-        const int r = j0 - 2 + (int)threadIdx.x;
-        if (threadIdx.x < MS_GY && r >= rw.lo && r < rw.hi)
-            fpred = fluid_rows[(long)(r - rw.lo) * tiles_x + i0 / MS_TX];
-    }
-    // 1. stage velocity (functions.py:714), BC applied; all loads issued before the LDS stores
+    // pure-fluid tile (k_fluid_rows / k_fluid_win): every cell the blended stress is formed
+    // on has phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not
+    // solid exactly -- those constants replace the loads of sxx, sxy, syy, H and solid below
+    // (the arithmetic is unchanged).  One uniform flag per tile.
+    const bool fluid = fluid_tiles && fluid_tiles[(long)(j0 - rw.lo) * tiles_x + i0 / MS_TX];
+    // every global load of the three phases is issued first (one exposed latency per tile),
+    // then the LDS phases run
+    double a[MS_NU], b[MS_NU], ka[MS_NU], kb[MS_NU];
+    bool ok1[MS_NU], uc[MS_NU], vc[MS_NU];
+    double uval[MS_NU];
+    double ex[MS_NG], ey[MS_NG], exy[MS_NG], hh2[MS_NG];
+    bool sol[MS_NG], ok2[MS_NG];
+    double pc[MS_NO], pxm[MS_NO], pxp[MS_NO], pym[MS_NO], pyp[MS_NO], hh[MS_NO];
+    bool ok[MS_NO];
     {
-        double a[MS_NU], b[MS_NU], ka[MS_NU], kb[MS_NU];
-        bool ok[MS_NU], uc[MS_NU], vc[MS_NU];
-        double uval[MS_NU];
 #pragma unroll
         for (int it = 0; it < MS_NU; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q % MS_UX;
             const int j = j0 - 3 + ry, i = i0 - 3 + rx;
-            ok[it] = q < MS_UX * MS_UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
+            ok1[it] = q < MS_UX * MS_UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
             long cu, cv;
             if constexpr (IN) {   // interior cell: every BC kind is the identity there
                 uc[it] = false; vc[it] = false; uval[it] = 0.0;
-                cu = cv = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
+                cu = cv = ok1[it] ? (long)j * nx + i : (long)rw.lo * nx;
             } else {
-                const BCSrc s = bc_source(bc, lid, ok[it] ? j : 1, ok[it] ? i : 1, ny, nx);
+                const BCSrc s = bc_source(bc, lid, ok1[it] ? j : 1, ok1[it] ? i : 1, ny, nx);
                 uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
-                cu = ok[it] ? s.u_src : (long)rw.lo * nx; cv = ok[it] ? s.v_src : (long)rw.lo * nx;
+                cu = ok1[it] ? s.u_src : (long)rw.lo * nx; cv = ok1[it] ? s.v_src : (long)rw.lo * nx;
             }
             a[it] = u[cu]; b[it] = v[cv];
             ka[it] = stage ? kpu[cu] : 0.0; kb[it] = stage ? kpv[cv] : 0.0;
         }
+    }
+    // phase-2 operands: the elastic stress, H and the solid mask on the tile + 2 halo
 #pragma unroll
-        for (int it = 0; it < MS_NU; ++it) {
-            const int q = threadIdx.x + it * MS_T;
-            if (q >= MS_UX * MS_UY) break;
-            const double ru = stage == 0 ? a[it] : a[it] + coef * ka[it];
-            const double rv = stage == 0 ? b[it] : b[it] + coef * kb[it];
-            (&su[0][0])[q] = !ok[it] ? 0.0 : uc[it] ? uval[it] : ru;
-            (&sv[0][0])[q] = !ok[it] ? 0.0 : vc[it] ? 0.0 : rv;
+    for (int it = 0; it < MS_NG; ++it) {
+        const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
+        const int j = j0 - 2 + ry, i = i0 - 2 + rx;
+        ok2[it] = q < MS_GX * MS_GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
+        const long c = ok2[it] ? (long)j * nx + i : (long)rw.lo * nx;
+        if (fluid) {
+            ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh2[it] = 1.0; sol[it] = false;
+        } else {
+            ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh2[it] = H[c];
+            sol[it] = solid[c] != 0;
         }
     }
-    const bool fluid = __syncthreads_and(fpred) != 0;
+    // phase-3 operands on the output cells
+#pragma unroll
+    for (int it = 0; it < MS_NO; ++it) {
+        const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+        const int j = j0 + ry, i = i0 + rx;
+        ok[it] = q < MS_TX * MS_TY && j >= olo && j < ohi && i < nx;   // output rows
+        const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
+        // grad2(p) operands (functions.py:941): centred inside, one-sided at the edges
+        // (inside: c+1 / c-1; i == 0: c+1; i == nx-1: c-1 as the "+s" operand; the "-s"
+        // operand only inside) -- every index stays in the grid
+        const bool exd = i == 0 || i == nx - 1, eyd = j == 0 || j == ny - 1;
+        const long sx = i == nx - 1 ? -1 : 1, sy = j == ny - 1 ? -(long)nx : (long)nx;
+        pc[it] = p[c];
+        pxp[it] = ok[it] ? p[c + sx] : 0.0; pxm[it] = ok[it] && !exd ? p[c - 1] : 0.0;
+        pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !eyd ? p[c - nx] : 0.0;
+        hh[it] = fluid ? 1.0 : H[c];
+    }
+    // 1. stage velocity (functions.py:714), BC applied
+#pragma unroll
+    for (int it = 0; it < MS_NU; ++it) {
+        const int q = threadIdx.x + it * MS_T;
+        if (q >= MS_UX * MS_UY) break;
+        const double ru = stage == 0 ? a[it] : a[it] + coef * ka[it];
+        const double rv = stage == 0 ? b[it] : b[it] + coef * kb[it];
+        (&su[0][0])[q] = !ok1[it] ? 0.0 : uc[it] ? uval[it] : ru;
+        (&sv[0][0])[q] = !ok1[it] ? 0.0 : vc[it] ? 0.0 : rv;
+    }
+    __syncthreads();
     // 2. blended stress (functions.py:717-735, 906-921)
     {
-        double ex[MS_NG], ey[MS_NG], exy[MS_NG], hh[MS_NG];
-        bool sol[MS_NG], ok[MS_NG];
-#pragma unroll
-        for (int it = 0; it < MS_NG; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
-            const int j = j0 - 2 + ry, i = i0 - 2 + rx;
-            ok[it] = q < MS_GX * MS_GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
-            const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
-            if (fluid) {
-                ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh[it] = 1.0; sol[it] = false;
-            } else {
-                ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh[it] = H[c];
-                sol[it] = solid[c] != 0;
-            }
-        }
 #pragma unroll
         for (int it = 0; it < MS_NG; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
             if (q >= MS_GX * MS_GY) break;
             const int j = j0 - 2 + ry, i = i0 - 2 + rx;
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
-            if (ok[it]) {
+            if (ok2[it]) {
                 const double *pu = &su[ry + 1][rx + 1], *pv = &sv[ry + 1][rx + 1];
                 const double dudx = g2<IN>(pu, 1, i, nx, h2x), dvdy = g2<IN>(pv, MS_UX, j, ny, h2y);
                 const double dudy = g2<IN>(pu, MS_UX, j, ny, h2y), dvdx = g2<IN>(pv, 1, i, nx, h2x);
@@ -276,7 +292,7 @@ __device__ __forceinline__ void ms_tile(
                     e2 = e2 + eta_s * dvdy;
                     e3 = e3 + eta_s * 0.5 * (dudy + dvdx);
                 }
-                const double h = hh[it], omh = 1 - h;
+                const double h = hh2[it], omh = 1 - h;
                 oxx = h * (2 * mu_f * dudx) + omh * e1;
                 oyy = h * (2 * mu_f * dvdy) + omh * e2;
                 oxy = h * (mu_f * (dudy + dvdx)) + omh * e3;
@@ -285,35 +301,20 @@ __device__ __forceinline__ void ms_tile(
         }
     }
     __syncthreads();
-    // 3. RHS and RK4 accumulation (functions.py:923-944, 743-758)
+    // 3. RHS and RK4 accumulation (functions.py:923-944, 743-758); stage 3 forms
+    // acc = (k1 + 2 k2) + 2 k3 from the three k planes (loaded here: registers)
     {
-        double pc[MS_NO], pxm[MS_NO], pxp[MS_NO], pym[MS_NO], pyp[MS_NO], hh[MS_NO];
-        double x0[MS_NO], x1[MS_NO], y0[MS_NO], y1[MS_NO];
-        bool ok[MS_NO];
+        double x0[MS_NO], y0[MS_NO], x1[MS_NO], y1[MS_NO];
 #pragma unroll
         for (int it = 0; it < MS_NO; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
-            const int j = j0 + ry, i = i0 + rx;
-            ok[it] = q < MS_TX * MS_TY && j >= olo && j < ohi && i < nx;   // output rows
-            const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
-            // grad2(p) operands (functions.py:941): centred inside, one-sided at the edges
-            // (inside: c+1 / c-1; i == 0: c+1; i == nx-1: c-1 as the "+s" operand; the "-s"
-            // operand only inside) -- every index stays in the grid
-            const bool ex = i == 0 || i == nx - 1, ey = j == 0 || j == ny - 1;
-            const long sx = i == nx - 1 ? -1 : 1, sy = j == ny - 1 ? -(long)nx : (long)nx;
-            pc[it] = p[c];
-            pxp[it] = ok[it] ? p[c + sx] : 0.0; pxm[it] = ok[it] && !ex ? p[c - 1] : 0.0;
-            pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !ey ? p[c - nx] : 0.0;
-            hh[it] = fluid ? 1.0 : H[c];
-            // stage 3: acc = (k1 + 2 k2) + 2 k3, formed here from the three k planes
-            // (functions.py:758's left-to-right order; no accumulation planes in HBM)
-            x0[it] = 0.0; y0[it] = 0.0;
+            const long c = ok[it] ? (long)(j0 + ry) * nx + i0 + rx : (long)rw.lo * nx;
+            x0[it] = 0.0; y0[it] = 0.0; x1[it] = 0.0; y1[it] = 0.0;
             if (stage == 3 && ok[it]) {
                 x0[it] = (ainu[c] + 2 * k2u[c]) + 2 * kpu[c];
                 y0[it] = (ainv[c] + 2 * k2v[c]) + 2 * kpv[c];
+                x1[it] = u[c]; y1[it] = v[c];
             }
-            x1[it] = stage == 3 ? u[c] : 0.0;
-            y1[it] = stage == 3 ? v[c] : 0.0;
         }
 #pragma unroll
         for (int it = 0; it < MS_NO; ++it) {
@@ -356,7 +357,7 @@ __device__ __forceinline__ void ms_tile(
     }
 }
 
-__global__ void __launch_bounds__(MS_T) k_mom_stage(
+__global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
     const double *__restrict__ sxx, const double *__restrict__ sxy,
@@ -368,7 +369,7 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
-    const unsigned char *__restrict__ fluid_rows) {
+    const unsigned char *__restrict__ fluid_tiles) {
     __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
     if (dtp) {   // the same roundings as mom_stage's host constants
         const double dt = *dtp;
@@ -385,9 +386,9 @@ __global__ void __launch_bounds__(MS_T) k_mom_stage(
     const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 && j0 - 3 >= max(rw.lo, 2) &&
                           j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
     if (interior)
-        ms_tile<true>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_rows, i0, j0, su, sv, gx, gm, gy);
+        ms_tile<true>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, i0, j0, su, sv, gx, gm, gy);
     else
-        ms_tile<false>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_rows, i0, j0, su, sv, gx, gm, gy);
+        ms_tile<false>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, i0, j0, su, sv, gx, gm, gy);
 }
 
 // per row j of [jlo, jhi) (out row j - jlo) and 64-column tile tx: all of phi[j][64 tx - 2 .. 64 tx + 66) (the
@@ -410,6 +411,19 @@ __global__ void __launch_bounds__(256) k_fluid_rows(const double *__restrict__ p
     }
     const unsigned long long all = __ballot(ok);
     if (lane == 0) out[(long)(j - jlo) * tiles_x + tx] = all == ~0ull;
+}
+
+// tile flag for a stage tile whose first output row is j: rows [j - 2, j + MS_TY + 2) of
+// [jlo, jhi) all fluid (k_fluid_rows); rows outside the window are never loaded
+__global__ void __launch_bounds__(256) k_fluid_win(const unsigned char *__restrict__ rows,
+                                                   int tiles_x, int jlo, int jhi,
+                                                   unsigned char *__restrict__ out) {
+    const long w = (long)blockIdx.x * 256 + threadIdx.x;
+    if (w >= (long)(jhi - jlo) * tiles_x) return;
+    const int j = jlo + (int)(w / tiles_x), tx = (int)(w % tiles_x);
+    unsigned char f = 1;
+    for (int r = max(j - 2, jlo); r < min(j + MS_TY + 2, jhi); ++r) f &= rows[(long)(r - jlo) * tiles_x + tx];
+    out[w] = f;
 }
 
 // One fused stage launch: k_{s+1} -> (k1 | k2 | k3)[s], acc1 / acc2 / u* (see MomWork)
@@ -707,13 +721,16 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
         const long nw = (long)(w0.hi - w0.lo) * tiles_x;
         k_fluid_rows<<<grid1d(nw, 4), 256, 0, ctx->stream>>>(phi, thr, nx, tiles_x, w0.lo,
                                                               w0.hi, fluid_rows);
+        k_fluid_win<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(fluid_rows, tiles_x, w0.lo, w0.hi,
+                                                               fluid_rows + nw);
         RMT_LAUNCHED();
     }
     for (int s = 0; s < 4 && !unfused && !blocked; ++s) {
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
-                          nullptr, nullptr, ws.jb, ws.je, fluid_rows));
+                          nullptr, nullptr, ws.jb, ws.je,
+                          fluid_rows + (long)(w0.hi - w0.lo) * tiles_x));
     }
     RMT_CHECK(!unfused || (!win && !W.dtp), RMT_ENOTSUP,
               "RMT_MOM_UNFUSED: single-domain, host-dt only");
