@@ -358,6 +358,24 @@ int rmt_mac_momentum_predictor(rmt_ctx *ctx, const double *u, const double *v, d
 int rmt_mac_contact_stress(rmt_ctx *ctx, const double *phi_a, const double *phi_b, double eta,
                            double Gsum, double eps, double dx, double dy, double *txx,
                            double *txy, double *tyy);                     /* mac.py:729-749 */
+/* MAC IMEX tier (imex.hip), square N x N cell grid (ctx ny = nx = N).  kind 0: u faces, full
+ * (N, N+1), interior (N, N-1); kind 1: v faces, full (N+1, N), interior (N-1, N).
+ * rmt_mac_lap_lid_hom: the homogeneous-BC Laplacian of a full field on the interior faces,
+ *   mac.py:243-250 _lap_u_lid_hom (kind 0) / :253-260 _lap_v_lid_hom (kind 1).
+ * rmt_mac_helmholtz: (I - coef Lap_hom) x = rhs on the interior faces by scipy's cg
+ *   (x0 = rhs, atol = rtol ||rhs||), precond 0: mac.py:263-275 _cg_helmholtz, precond 1:
+ *   mac.py:287-316 _pcg_helmholtz (DST-II preconditioner); *iters = iterations run.
+ * rmt_mac_momentum_predictor_lid_imex: mac.py:319-369; fu / fv full face forces or NULL;
+ *   iters[2] (optional): the u and v PCG iteration counts. */
+int rmt_mac_lap_lid_hom(rmt_ctx *ctx, int kind, const double *f, double dx, double dy,
+                        double *out);
+int rmt_mac_helmholtz(rmt_ctx *ctx, int kind, const double *rhs, double coef, double dx,
+                      double dy, double rtol, int maxiter, int precond, double *x, int *iters);
+int rmt_mac_momentum_predictor_lid_imex(rmt_ctx *ctx, const double *u, const double *v,
+                                        double nu, double dx, double dy, double dt,
+                                        double U_lid, const double *fu, const double *fv,
+                                        double rho, double rtol, double cs2, double *u_star,
+                                        double *v_star, int *iters);
 
 /* The loop body of benchmarks/mac_multi_disc_lid.py:62-98 (K soft discs with contact, lid
  * U_lid, fixed dt), device-resident.  Fields: 0 u, 1 v, 2 p (disc ignored); 3 X1, 4 X2,

@@ -5,7 +5,10 @@ pyRMT/mac.py is pure NumPy in the reference; it is restated here with the same N
 operations in the same order (so bit-exact with the reference), the DCT-II through
 scipy.fft like mac.py:118-123.  The per-disc reference-map advection / extrapolation /
 stress reuse the C restatement in oracle.py.  Pinned by tests/golden/mac_ops.npz and
-mac_trace.npz (tests/test_oracle_golden.py).
+mac_trace.npz (tests/test_oracle_golden.py).  The IMEX tier (mac.py:243-369): the ghost-cell
+Laplacians with the same NumPy expressions, scipy 1.15's cg restated (oracle.cg's loop with
+x0 = rhs) and the DST preconditioner through scipy.fft.dstn / idstn as mac.py:304-306;
+pinned by tests/golden/imex.npz.
 """
 import numpy as np
 
@@ -191,3 +194,122 @@ class MacMultiDisc:
         cents = [(self.Xc[q <= 0].mean(), self.Yc[q <= 0].mean()) for q in phis]
         return dict(t=self.t, dt=dt, minJ=Jmin, maxJ=Jmax,
                     cx=np.array([c[0] for c in cents]), cy=np.array([c[1] for c in cents]))
+
+
+# ------------------------------------------------------------------ IMEX tier --------
+def lap_u_lid_hom(u, dx, dy):
+    """mac.py:243-250: Laplacian of u (Ny, Nx+1) on the interior faces, walls u = 0 and
+    reflected (homogeneous) ghost rows."""
+    up = np.empty((u.shape[0] + 2, u.shape[1])); up[1:-1] = u; up[0] = -u[0]; up[-1] = -u[-1]
+    uc = u[:, 1:-1]
+    return ((u[:, 2:] - 2 * uc + u[:, :-2]) / dx ** 2
+            + (up[2:, 1:-1] - 2 * up[1:-1, 1:-1] + up[:-2, 1:-1]) / dy ** 2)
+
+
+def lap_v_lid_hom(v, dx, dy):
+    """mac.py:253-260: Laplacian of v (Ny+1, Nx) on the interior faces, reflected ghost
+    columns."""
+    vp = np.empty((v.shape[0], v.shape[1] + 2)); vp[:, 1:-1] = v
+    vp[:, 0] = -v[:, 0]; vp[:, -1] = -v[:, -1]
+    vc = v[1:-1, :]
+    return ((vp[1:-1, 2:] - 2 * vp[1:-1, 1:-1] + vp[1:-1, :-2]) / dx ** 2
+            + (v[2:, :] - 2 * vc + v[:-2, :]) / dy ** 2)
+
+
+def dst_helmholtz_eigs(shp, dx, dy):
+    """mac.py:278-284: homogeneous-Dirichlet Laplacian eigenvalues of the DST-II."""
+    Ny, Nx = shp
+    lx = -2.0 * (1.0 - np.cos(np.pi * (np.arange(Nx) + 1) / Nx)) / dx ** 2
+    ly = -2.0 * (1.0 - np.cos(np.pi * (np.arange(Ny) + 1) / Ny)) / dy ** 2
+    return ly[:, None] + lx[None, :]
+
+
+def cg_x0(matvec, b, psolve, rtol, maxiter):
+    """scipy.sparse.linalg.cg (scipy 1.15) with x0 = b and atol = 0 (mac.py:274, 312):
+    r = b - A x0, then the loop of oracle.cg.  Returns (x, iterations run)."""
+    x = b.copy()
+    bnrm2 = np.linalg.norm(b)
+    if bnrm2 == 0:
+        return b.copy(), 0
+    atol = rtol * bnrm2
+    r = b - matvec(x) if x.any() else b.copy()
+    rho_prev, p = None, None
+    for it in range(maxiter):
+        if np.linalg.norm(r) < atol:
+            return x, it
+        z = psolve(r)
+        rho_cur = np.dot(r, z)
+        if it > 0:
+            beta = rho_cur / rho_prev
+            p *= beta
+            p += z
+        else:
+            p = np.empty_like(r)
+            p[:] = z[:]
+        q = matvec(p)
+        alpha = rho_cur / np.dot(p, q)
+        x += alpha * p
+        r -= alpha * q
+        rho_prev = rho_cur
+    return x, maxiter
+
+
+def helmholtz(rhs, kind, coef, dx, dy, rtol, maxiter=500, precond=True):
+    """mac.py:263-316: (I - coef Lap_hom) x = rhs on the u (kind 0) or v (kind 1) interior
+    faces; CG, or PCG with the DST-II preconditioner (I - coef Lap_Dirichlet)^-1.
+    Returns (x, iterations)."""
+    from scipy.fft import dstn, idstn
+    shp = rhs.shape
+    if kind == 0:
+        emb = lambda x: np.pad(x, ((0, 0), (1, 1)))
+        lap = lambda w: lap_u_lid_hom(w, dx, dy)
+    else:
+        emb = lambda x: np.pad(x, ((1, 1), (0, 0)))
+        lap = lambda w: lap_v_lid_hom(w, dx, dy)
+    denom = 1.0 - coef * dst_helmholtz_eigs(shp, dx, dy)
+
+    def matvec(xf):
+        x = xf.reshape(shp)
+        return (x - coef * lap(emb(x))).ravel()
+
+    def prec(rf):
+        return idstn(dstn(rf.reshape(shp), type=2, norm='ortho') / denom, type=2,
+                     norm='ortho').ravel()
+
+    x, it = cg_x0(matvec, rhs.ravel().copy(), prec if precond else (lambda r: r), rtol, maxiter)
+    return x.reshape(shp), it
+
+
+def momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0,
+                                rtol=1e-8, cs2=0.0):
+    """mac.py:319-369: explicit central advection + face forces, implicit viscosity (+ the
+    trapezoidal elastic term for cs2 > 0) by DST-preconditioned CG.  Returns (u*, v*)."""
+    Ny, Nx = u.shape[0], u.shape[1] - 1
+    up = np.empty((Ny + 2, Nx + 1)); up[1:-1] = u; up[0] = -u[0]; up[-1] = 2.0 * U_lid - u[-1]
+    vp = np.empty((Ny + 1, Nx + 2)); vp[:, 1:-1] = v; vp[:, 0] = -v[:, 0]; vp[:, -1] = -v[:, -1]
+    c_el = 0.25 * dt * dt * cs2
+    coef = dt * nu + c_el
+    uc = u[:, 1:-1]
+    dudx = (u[:, 2:] - u[:, :-2]) / (2 * dx)
+    dudy = (up[2:, 1:-1] - up[:-2, 1:-1]) / (2 * dy)
+    v_u = 0.25 * (v[:-1, :-1] + v[:-1, 1:] + v[1:, :-1] + v[1:, 1:])
+    rhs_u = uc + dt * (-(uc * dudx + v_u * dudy))
+    if fu is not None:
+        rhs_u = rhs_u + dt * fu[:, 1:-1] / rho
+    if c_el > 0.0:
+        rhs_u = rhs_u + c_el * lap_u_lid_hom(u, dx, dy)
+    rhs_u[-1, :] += coef * (2.0 * U_lid / dy ** 2)
+    sol_u, _ = helmholtz(rhs_u, 0, coef, dx, dy, rtol)
+    ustar = u.copy(); ustar[:, 1:-1] = sol_u; ustar[:, 0] = 0.0; ustar[:, -1] = 0.0
+    vc = v[1:-1, :]
+    dvdy = (v[2:, :] - v[:-2, :]) / (2 * dy)
+    dvdx = (vp[1:-1, 2:] - vp[1:-1, :-2]) / (2 * dx)
+    u_v = 0.25 * (u[:-1, :-1] + u[:-1, 1:] + u[1:, :-1] + u[1:, 1:])
+    rhs_v = vc + dt * (-(u_v * dvdx + vc * dvdy))
+    if fv is not None:
+        rhs_v = rhs_v + dt * fv[1:-1, :] / rho
+    if c_el > 0.0:
+        rhs_v = rhs_v + c_el * lap_v_lid_hom(v, dx, dy)
+    sol_v, _ = helmholtz(rhs_v, 1, coef, dx, dy, rtol)
+    vstar = v.copy(); vstar[1:-1, :] = sol_v; vstar[0, :] = 0.0; vstar[-1, :] = 0.0
+    return ustar, vstar

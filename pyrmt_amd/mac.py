@@ -114,6 +114,127 @@ def momentum_predictor(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0):
     return io.out(us), io.out(vs)
 
 
+# ------------------------------------------------------------------ IMEX tier --------
+# mac.py:243-442 through imex.hip: the homogeneous ghost-cell Laplacians,
+# CG / DST-preconditioned CG Helmholtz solves and the IMEX lid-cavity predictor.
+def _lap_hom(kind, f, dx, dy):
+    io = _IO(f); fd = io.dev(f)
+    N = fd.shape[0] if kind == 0 else fd.shape[1]
+    out = io.empty((N, N - 1) if kind == 0 else (N - 1, N))
+    L.check(L.lib().rmt_mac_lap_lid_hom(_ctx(N), kind, _p(fd), float(dx), float(dy), _p(out)),
+            "_lap_lid_hom")
+    return io.out(out)
+
+
+def _lap_u_lid_hom(u, dx, dy):
+    """mac.py:243-250: Laplacian of u (Ny, Nx+1) on the interior faces (Ny, Nx-1)."""
+    return _lap_hom(0, u, dx, dy)
+
+
+def _lap_v_lid_hom(v, dx, dy):
+    """mac.py:253-260: Laplacian of v (Ny+1, Nx) on the interior faces (Ny-1, Nx)."""
+    return _lap_hom(1, v, dx, dy)
+
+
+def _dst_helmholtz_eigs(shp, dx, dy):
+    """mac.py:278-284 (setup, host): DST-II eigenvalues of the Dirichlet Laplacian."""
+    Ny, Nx = shp
+    lx = -2.0 * (1.0 - np.cos(np.pi * (np.arange(Nx) + 1) / Nx)) / dx ** 2
+    ly = -2.0 * (1.0 - np.cos(np.pi * (np.arange(Ny) + 1) / Ny)) / dy ** 2
+    return ly[:, None] + lx[None, :]
+
+
+def _helmholtz_operator(apply_lap_hom, embed, shp):
+    """The reference hands the operator over as callables (mac.py:351, 366 and its tests:
+    ``lambda w: _lap_u_lid_hom(w, dx, dy)``, ``np.pad`` embeddings).  Identify the face kind
+    and (dx, dy) from the lambda's closure and verify both on a probe (the embedding pads
+    the kind's wall axis with zeros, the operator equals this module's kernel bit for bit);
+    anything else raises NotImplementedError -- there is no host fallback."""
+    code = getattr(apply_lap_hom, "__code__", None)
+    names = code.co_names if code is not None else ()
+    kind = 0 if "_lap_u_lid_hom" in names else 1 if "_lap_v_lid_hom" in names else None
+    cells = {}
+    if code is not None and apply_lap_hom.__closure__:
+        cells = {k: c.cell_contents for k, c in zip(code.co_freevars, apply_lap_hom.__closure__)}
+    dx, dy = cells.get("dx"), cells.get("dy")
+    Ny, Nx = shp
+    if kind is None or dx is None or dy is None or (kind == 0 and Nx != Ny - 1) or \
+            (kind == 1 and Ny != Nx - 1):
+        raise NotImplementedError("helmholtz: apply_lap_hom must be the reference's "
+                                  "lambda w: _lap_u_lid_hom / _lap_v_lid_hom(w, dx, dy)")
+    probe = np.random.default_rng(0).standard_normal(shp)
+    e = np.asarray(embed(probe), dtype=np.float64)
+    pad = np.pad(probe, ((0, 0), (1, 1)) if kind == 0 else ((1, 1), (0, 0)))
+    if not np.array_equal(e, pad):
+        raise NotImplementedError("helmholtz: embed must zero-pad the walls as mac.py:350/365")
+    host = np.asarray(apply_lap_hom(e), dtype=np.float64)
+    if not np.array_equal(host, _lap_hom(kind, e, dx, dy)):
+        raise NotImplementedError("helmholtz: apply_lap_hom is not the homogeneous lid Laplacian")
+    return kind, float(dx), float(dy)
+
+
+def _solve_helmholtz(rhs_int, kind, coef, dx, dy, rtol, maxiter, precond):
+    io = _IO(rhs_int); b = io.dev(rhs_int)
+    N = b.shape[0] if kind == 0 else b.shape[1]
+    x = io.empty(b.shape)
+    it = ctypes.c_int(0)
+    L.check(L.lib().rmt_mac_helmholtz(_ctx(N), kind, _p(b), float(coef), dx, dy, float(rtol),
+                                      int(maxiter), int(precond), _p(x), ctypes.byref(it)),
+            "helmholtz")
+    return io.out(x), it.value
+
+
+def _cg_helmholtz(rhs_int, apply_lap_hom, embed, coef, rtol=1e-10, maxiter=500):
+    """mac.py:263-275: (I - coef Lap_hom) x = rhs_int by CG (x0 = rhs_int)."""
+    kind, dx, dy = _helmholtz_operator(apply_lap_hom, embed, tuple(rhs_int.shape))
+    return _solve_helmholtz(rhs_int, kind, coef, dx, dy, rtol, maxiter, 0)[0]
+
+
+def _pcg_helmholtz(rhs_int, apply_lap_hom, embed, coef, dx, dy, rtol=1e-8, maxiter=500,
+                   count=None):
+    """mac.py:287-316: DST-II-preconditioned CG; appends the iteration count to `count`."""
+    kind, ldx, ldy = _helmholtz_operator(apply_lap_hom, embed, tuple(rhs_int.shape))
+    if (ldx, ldy) != (float(dx), float(dy)):
+        raise NotImplementedError("_pcg_helmholtz: the preconditioner's (dx, dy) differ from "
+                                  "the operator's")
+    x, it = _solve_helmholtz(rhs_int, kind, coef, ldx, ldy, rtol, maxiter, 1)
+    if count is not None:
+        count.append(it)
+    return x
+
+
+def momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0,
+                                rtol=1e-8, cs2=0.0):
+    """mac.py:319-369: explicit central advection + face forces, implicit (backward-Euler)
+    viscosity (+ the trapezoidal elastic term, cs2 > 0) by DST-preconditioned CG."""
+    if (fu is None) != (fv is None):
+        raise NotImplementedError("momentum_predictor_lid_imex: give both face forces or neither")
+    io = _IO(u, v); ud = io.dev(u); vd = io.dev(v)
+    fud, fvd = io.dev(fu), io.dev(fv)
+    us = io.empty(ud.shape); vs = io.empty(vd.shape)
+    it = (ctypes.c_int * 2)()
+    L.check(L.lib().rmt_mac_momentum_predictor_lid_imex(
+        _ctx(ud.shape[0]), _p(ud), _p(vd), float(nu), float(dx), float(dy), float(dt),
+        float(U_lid), _p(fud), _p(fvd), float(rho), float(rtol), float(cs2), _p(us), _p(vs),
+        ctypes.cast(it, ctypes.c_void_p)), "momentum_predictor_lid_imex")
+    return io.out(us), io.out(vs)
+
+
+def momentum_predictor_lid_semilag(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0,
+                                   cs2=0.0, rtol=1e-8, cfl_switch=0.9):
+    """mac.py:381-442: adaptive predictor.  At an advective CFL <= cfl_switch the reference
+    takes momentum_predictor_lid_imex (mac.py:387-390), as here; its semi-Lagrangian branch
+    (scipy.ndimage.map_coordinates cubic-spline backtrace) is not built and raises."""
+    uh = np.asarray(u.detach().cpu() if hasattr(u, "detach") else u)
+    vh = np.asarray(v.detach().cpu() if hasattr(v, "detach") else v)
+    cfl = dt * max(np.max(np.abs(uh)) / dx, np.max(np.abs(vh)) / dy)
+    if cfl <= cfl_switch:
+        return momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=fu, fv=fv, rho=rho,
+                                           rtol=rtol, cs2=cs2)
+    raise NotImplementedError("momentum_predictor_lid_semilag: the semi-Lagrangian branch "
+                              "(CFL > cfl_switch) is not built")
+
+
 def contact_stress(phi_a, phi_b, eta, Gsum, eps, dx, dy):
     """mac.py:729-749: (txx, txy, tyy)."""
     io = _IO(phi_a, phi_b); a = io.dev(phi_a); b = io.dev(phi_b)

@@ -634,6 +634,42 @@ def gen_mac_trace(N=64, nsteps=8, n_discs=3, seed=3):
          **{k: np.array(val) for k, val in rec.items()})
 
 
+def gen_imex(N=32):
+    """mac.py:243-369 (the MAC IMEX tier): the homogeneous-BC ghost-cell
+    Laplacians, the DST-II Helmholtz eigenvalues, CG and DST-preconditioned CG Helmholtz
+    solves (with scipy's own callback counting the PCG iterations, as the reference's
+    `count`), and momentum_predictor_lid_imex with and without forces / the trapezoidal
+    elastic term, on seeded lid-cavity-like fields."""
+    rng = np.random.default_rng(77)
+    dx, dy = M.mac_grid(N, N)
+    u = 0.3 * rng.standard_normal((N, N + 1)); u[:, 0] = 0.0; u[:, -1] = 0.0
+    v = 0.3 * rng.standard_normal((N + 1, N)); v[0, :] = 0.0; v[-1, :] = 0.0
+    lap_u = M._lap_u_lid_hom(u, dx, dy)
+    lap_v = M._lap_v_lid_hom(v, dx, dy)
+    eig_u = M._dst_helmholtz_eigs((N, N - 1), dx, dy)
+    eig_v = M._dst_helmholtz_eigs((N - 1, N), dx, dy)
+    rhs_u = rng.standard_normal((N, N - 1))
+    rhs_v = rng.standard_normal((N - 1, N))
+    emb_u = lambda x: np.pad(x, ((0, 0), (1, 1)))
+    emb_v = lambda x: np.pad(x, ((1, 1), (0, 0)))
+    lu = lambda w: M._lap_u_lid_hom(w, dx, dy)
+    lv = lambda w: M._lap_v_lid_hom(w, dx, dy)
+    coef = 0.5e-3
+    cg_u = M._cg_helmholtz(rhs_u, lu, emb_u, coef)
+    cnt_u, cnt_v = [], []
+    pcg_u = M._pcg_helmholtz(rhs_u, lu, emb_u, coef, dx, dy, rtol=1e-8, count=cnt_u)
+    pcg_v = M._pcg_helmholtz(rhs_v, lv, emb_v, coef, dx, dy, rtol=1e-8, count=cnt_v)
+    nu, dt, U_lid = 0.01, 2e-3, 1.0
+    us0, vs0 = M.momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid)
+    fu = 0.1 * rng.standard_normal((N, N + 1)); fv = 0.1 * rng.standard_normal((N + 1, N))
+    us1, vs1 = M.momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=fu, fv=fv,
+                                             rho=1.3, cs2=4.0)
+    save("imex", N=N, dx=dx, dy=dy, u=u, v=v, lap_u=lap_u, lap_v=lap_v, eig_u=eig_u,
+         eig_v=eig_v, rhs_u=rhs_u, rhs_v=rhs_v, coef=coef, cg_u=cg_u, pcg_u=pcg_u, pcg_v=pcg_v,
+         cnt_u=cnt_u[0], cnt_v=cnt_v[0], nu=nu, dt=dt, U_lid=U_lid, us0=us0, vs0=vs0, fu=fu,
+         fv=fv, us1=us1, vs1=vs1)
+
+
 if __name__ == "__main__":
     if "--only" in sys.argv:     # regenerate the named fixtures only
         for name in sys.argv[sys.argv.index("--only") + 1:]:
