@@ -376,6 +376,15 @@ int rmt_mac_momentum_predictor_lid_imex(rmt_ctx *ctx, const double *u, const dou
                                         double U_lid, const double *fu, const double *fv,
                                         double rho, double rtol, double cs2, double *u_star,
                                         double *v_star, int *iters);
+/* mac.py:381-442 momentum_predictor_lid_semilag, its semi-Lagrangian branch (the caller
+ * checked CFL > cfl_switch, mac.py:387-390): midpoint backtrace through cubic-spline
+ * interpolation (scipy.ndimage.map_coordinates order 3, mode 'nearest', mac.py:374-378),
+ * then the implicit viscosity by PCG; iters as above. */
+int rmt_mac_momentum_predictor_lid_semilag(rmt_ctx *ctx, const double *u, const double *v,
+                                           double nu, double dx, double dy, double dt,
+                                           double U_lid, const double *fu, const double *fv,
+                                           double rho, double cs2, double rtol, double *u_star,
+                                           double *v_star, int *iters);
 
 /* The loop body of benchmarks/mac_multi_disc_lid.py:62-98 (K soft discs with contact, lid
  * U_lid, fixed dt), device-resident.  Fields: 0 u, 1 v, 2 p (disc ignored); 3 X1, 4 X2,

@@ -313,3 +313,55 @@ def momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, r
     sol_v, _ = helmholtz(rhs_v, 1, coef, dx, dy, rtol)
     vstar = v.copy(); vstar[1:-1, :] = sol_v; vstar[0, :] = 0.0; vstar[-1, :] = 0.0
     return ustar, vstar
+
+
+def momentum_predictor_lid_semilag(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0,
+                                   cs2=0.0, rtol=1e-8, cfl_switch=0.9):
+    """mac.py:381-442: IMEX below cfl_switch, else the midpoint semi-Lagrangian backtrace
+    through scipy.ndimage.map_coordinates(order=3, mode='nearest') (the reference's own
+    call, mac.py:374-378) and the PCG viscosity solve."""
+    from scipy.ndimage import map_coordinates
+    interp = lambda f, iq, jq: map_coordinates(f, [jq, iq], order=3, mode="nearest")
+    cfl = dt * max(np.max(np.abs(u)) / dx, np.max(np.abs(v)) / dy)
+    if cfl <= cfl_switch:
+        return momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=fu, fv=fv, rho=rho,
+                                           rtol=rtol, cs2=cs2)
+    Ny, Nx = u.shape[0], u.shape[1] - 1
+    up = np.empty((Ny + 2, Nx + 1)); up[1:-1] = u; up[0] = -u[0]; up[-1] = 2.0 * U_lid - u[-1]
+    vp = np.empty((Ny + 1, Nx + 2)); vp[:, 1:-1] = v; vp[:, 0] = -v[:, 0]; vp[:, -1] = -v[:, -1]
+    Ii, Jj = np.meshgrid(np.arange(1, Nx), np.arange(Ny))
+    xf = Ii * dx; yf = (Jj + 0.5) * dy
+    velx = u[:, 1:-1]; vely = 0.25 * (v[:-1, :-1] + v[:-1, 1:] + v[1:, :-1] + v[1:, 1:])
+    xm = xf - 0.5 * dt * velx; ym = yf - 0.5 * dt * vely
+    vxm = interp(u, xm / dx, ym / dy)
+    vym = interp(vp, xm / dx + 0.5, ym / dy - 0.0)
+    xd = xf - dt * vxm; yd = yf - dt * vym
+    u_adv = np.zeros_like(u)
+    u_adv[:, 1:-1] = interp(up, xd / dx, yd / dy + 0.5)
+    Iv, Jv = np.meshgrid(np.arange(Nx), np.arange(1, Ny))
+    xfv = (Iv + 0.5) * dx; yfv = Jv * dy
+    velxv = 0.25 * (u[:-1, :-1] + u[:-1, 1:] + u[1:, :-1] + u[1:, 1:]); velyv = v[1:-1, :]
+    xmv = xfv - 0.5 * dt * velxv; ymv = yfv - 0.5 * dt * velyv
+    vxmv = interp(up, xmv / dx, ymv / dy + 0.5)
+    vymv = interp(v, xmv / dx - 0.5, ymv / dy)
+    xdv = xfv - dt * vxmv; ydv = yfv - dt * vymv
+    v_adv = np.zeros_like(v)
+    v_adv[1:-1, :] = interp(vp, xdv / dx + 0.5, ydv / dy)
+    c_el = 0.25 * dt * dt * cs2
+    coef = dt * nu + c_el
+    rhs_u = u_adv[:, 1:-1].copy()
+    if fu is not None:
+        rhs_u = rhs_u + dt * fu[:, 1:-1] / rho
+    if c_el > 0.0:
+        rhs_u = rhs_u + c_el * lap_u_lid_hom(u, dx, dy)
+    rhs_u[-1, :] += coef * (2.0 * U_lid / dy ** 2)
+    sol_u, _ = helmholtz(rhs_u, 0, coef, dx, dy, rtol)
+    ustar = u.copy(); ustar[:, 1:-1] = sol_u; ustar[:, 0] = 0.0; ustar[:, -1] = 0.0
+    rhs_v = v_adv[1:-1, :].copy()
+    if fv is not None:
+        rhs_v = rhs_v + dt * fv[1:-1, :] / rho
+    if c_el > 0.0:
+        rhs_v = rhs_v + c_el * lap_v_lid_hom(v, dx, dy)
+    sol_v, _ = helmholtz(rhs_v, 1, coef, dx, dy, rtol)
+    vstar = v.copy(); vstar[1:-1, :] = sol_v; vstar[0, :] = 0.0; vstar[-1, :] = 0.0
+    return ustar, vstar

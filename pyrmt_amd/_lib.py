@@ -163,6 +163,8 @@ SIGNATURES = {
     "rmt_mac_helmholtz": (_I, [_P, _I, _P, _D, _D, _D, _D, _I, _I, _P, ctypes.POINTER(_I)]),
     "rmt_mac_momentum_predictor_lid_imex": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _P, _P, _D, _D,
                                                  _D, _P, _P, _P]),
+    "rmt_mac_momentum_predictor_lid_semilag": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _P, _P, _D,
+                                                    _D, _D, _P, _P, _P]),
     "rmt_mac_contact_stress": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _P, _P, _P]),
     "rmt_mac_sim_create": (_I, [_P, ctypes.POINTER(rmt_mac_params), ctypes.POINTER(_P)]),
     "rmt_mac_sim_destroy": (_I, [_P]),

@@ -484,6 +484,150 @@ __global__ void k_im_scatter(int kind, const double *__restrict__ sol, int ny, i
     }
 }
 
+
+// ------------------------------------------------- semi-Lagrangian branch (mac.py:381-442) --
+// scipy.ndimage.map_coordinates(f, [jq, iq], order=3, mode='nearest') (mac.py:374-378) as
+// scipy 1.15 computes it: f edge-padded by 12 (_prepad_for_spline_filter), the cubic
+// B-spline prefilter along axis 0 then axis 1 (gain 6, pole sqrt(3) - 2, the 'reflect'
+// causal / anticausal initialisation scipy uses for 'nearest'), then the 4 x 4 tap spline
+// sum at (jq + 12, iq + 12) with the taps clamped to the padded array.
+constexpr int SPL_PAD = 12;
+
+__global__ void k_spl_pad(const double *__restrict__ f, int R, int C, double *__restrict__ o) {
+    const int P = R + 2 * SPL_PAD, Q = C + 2 * SPL_PAD;
+    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k >= (long)P * Q) return;
+    const int a = (int)(k / Q), b = (int)(k % Q);
+    const int j = min(max(a - SPL_PAD, 0), R - 1), i = min(max(b - SPL_PAD, 0), C - 1);
+    o[k] = f[(long)j * C + i];
+}
+// in-place cubic B-spline prefilter of the line c[0], c[s], ..., c[(n-1) s]
+__device__ void spl_line(double *c, int n, long s) {
+    const double z = sqrt(3.0) - 2.0;
+    for (int k = 0; k < n; ++k) c[k * s] *= 6.0;
+    // causal init ('reflect')
+    double zi = z;
+    const double zn = pow(z, (double)n), c0 = c[0];
+    double a = c[0] + zn * c[(n - 1) * s];
+    for (int k = 1; k < n; ++k) {
+        a += zi * (c[k * s] + zn * c[(n - 1 - k) * s]);
+        zi *= z;
+    }
+    a *= z / (1.0 - zn * zn);
+    c[0] = a + c0;
+    for (int k = 1; k < n; ++k) c[k * s] += z * c[(k - 1) * s];
+    c[(n - 1) * s] *= z / (z - 1.0);
+    for (int k = n - 2; k >= 0; --k) c[k * s] = z * (c[(k + 1) * s] - c[k * s]);
+}
+__global__ void k_spl_cols(double *__restrict__ c, int P, int Q) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < Q) spl_line(c + i, P, Q);
+}
+__global__ void k_spl_rows(double *__restrict__ c, int P, int Q) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < P) spl_line(c + (long)j * Q, Q, 1);
+}
+// the spline value at index coordinates (jq, iq) of the unpadded field (R x C)
+__device__ double spl_eval(const double *__restrict__ c, int R, int C, double jq, double iq) {
+    const int P = R + 2 * SPL_PAD, Q = C + 2 * SPL_PAD;
+    const double tj = jq + SPL_PAD, ti = iq + SPL_PAD;
+    const double fj = floor(tj), fi = floor(ti);
+    double wj[4], wi[4];
+    {
+        const double y = tj - fj, z = 1.0 - y;
+        wj[0] = z * z * z / 6.0; wj[1] = (y * y * (y - 2.0) * 3.0 + 4.0) / 6.0;
+        wj[2] = (z * z * (z - 2.0) * 3.0 + 4.0) / 6.0; wj[3] = y * y * y / 6.0;
+    }
+    {
+        const double y = ti - fi, z = 1.0 - y;
+        wi[0] = z * z * z / 6.0; wi[1] = (y * y * (y - 2.0) * 3.0 + 4.0) / 6.0;
+        wi[2] = (z * z * (z - 2.0) * 3.0 + 4.0) / 6.0; wi[3] = y * y * y / 6.0;
+    }
+    // a NaN / huge coordinate: clamp the base index (the weights carry the NaN)
+    const double bj = fmin(fmax(fj, -4.0), (double)P), bi = fmin(fmax(fi, -4.0), (double)Q);
+    const int j0 = (int)bj - 1, i0 = (int)bi - 1;
+    double s = 0.0;
+    for (int a = 0; a < 4; ++a) {
+        const long row = (long)min(max(j0 + a, 0), P - 1) * Q;
+        double r = 0.0;
+        for (int b = 0; b < 4; ++b) r += wi[b] * c[row + min(max(i0 + b, 0), Q - 1)];
+        s += wj[a] * r;
+    }
+    return s;
+}
+struct SplFields {           // prefiltered coefficients (padded) of the four grids
+    const double *u, *v, *up, *vp;
+};
+// mac.py:395-405 (u faces) / 407-417 (v faces): midpoint backtrace and the departure value,
+// written as the interior array (the implicit solve's rhs before forces)
+__global__ void k_sl_faces(int kind, const double *__restrict__ u, const double *__restrict__ v,
+                           SplFields S, int ny, int nx, double dx, double dy, double dt,
+                           double *__restrict__ out) {
+    const long n = kind == 0 ? (long)ny * (nx - 1) : (long)(ny - 1) * nx;
+    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int j, i;
+    face_of(kind, k, ny, nx, j, i);
+    const long U = nx + 1;
+    if (kind == 0) {
+        const double xf = i * dx, yf = (j + 0.5) * dy;
+        const double velx = u[j * U + i];
+        const double vely = 0.25 * (v[(long)j * nx + i - 1] + v[(long)j * nx + i] +
+                                    v[(long)(j + 1) * nx + i - 1] + v[(long)(j + 1) * nx + i]);
+        const double xm = xf - 0.5 * dt * velx, ym = yf - 0.5 * dt * vely;
+        const double vxm = spl_eval(S.u, ny, nx + 1, ym / dy, xm / dx);
+        const double vym = spl_eval(S.vp, ny + 1, nx + 2, ym / dy - 0.0, xm / dx + 0.5);
+        const double xd = xf - dt * vxm, yd = yf - dt * vym;
+        out[k] = spl_eval(S.up, ny + 2, nx + 1, yd / dy + 0.5, xd / dx);
+    } else {
+        const double xf = (i + 0.5) * dx, yf = j * dy;
+        const double velx = 0.25 * (u[(j - 1) * U + i] + u[(j - 1) * U + i + 1] + u[j * U + i] +
+                                    u[j * U + i + 1]);
+        const double vely = v[(long)j * nx + i];
+        const double xm = xf - 0.5 * dt * velx, ym = yf - 0.5 * dt * vely;
+        const double vxm = spl_eval(S.up, ny + 2, nx + 1, ym / dy + 0.5, xm / dx);
+        const double vym = spl_eval(S.v, ny + 1, nx, ym / dy, xm / dx - 0.5);
+        const double xd = xf - dt * vxm, yd = yf - dt * vym;
+        out[k] = spl_eval(S.vp, ny + 1, nx + 2, yd / dy, xd / dx + 0.5);
+    }
+}
+// mac.py:420-440: rhs = advected interior (+ dt f / rho) (+ c_el Lap_hom(u^n)) (+ lid term)
+__global__ void k_sl_rhs(int kind, const double *f0, const double *__restrict__ full,
+                         const double *__restrict__ f, int ny, int nx, double dt, double rho,
+                         double c_el, double dx2, double dy2, double lid_term, double *rhs) {
+    const long n = kind == 0 ? (long)ny * (nx - 1) : (long)(ny - 1) * nx;
+    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int j, i;
+    face_of(kind, k, ny, nx, j, i);
+    double r = f0[k];
+    if (kind == 0) {
+        if (f) r = r + dt * f[(long)j * (nx + 1) + i] / rho;
+        if (c_el > 0.0) r = r + c_el * lap_u<true>(full, j, i, ny, nx, dx2, dy2);
+        if (j == ny - 1) r += lid_term;
+    } else {
+        if (f) r = r + dt * f[(long)j * nx + i] / rho;
+        if (c_el > 0.0) r = r + c_el * lap_v<true>(full, j, i, ny, nx, dx2, dy2);
+    }
+    rhs[k] = r;
+}
+// _u_ghost_y / _v_ghost_x (mac.py:147-165)
+__global__ void k_ghosts(const double *__restrict__ u, const double *__restrict__ v, int ny,
+                         int nx, double U_lid, double *__restrict__ up, double *__restrict__ vp) {
+    const long nu = (long)(ny + 2) * (nx + 1), nvp = (long)(ny + 1) * (nx + 2);
+    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < nu) {
+        const int r = (int)(k / (nx + 1)), i = (int)(k % (nx + 1));
+        up[k] = r == 0 ? -u[i] : r == ny + 1 ? 2.0 * U_lid - u[(long)(ny - 1) * (nx + 1) + i]
+                                             : u[(long)(r - 1) * (nx + 1) + i];
+    }
+    if (k < nvp) {
+        const int j = (int)(k / (nx + 2)), c = (int)(k % (nx + 2));
+        vp[k] = c == 0 ? -v[(long)j * nx] : c == nx + 1 ? -v[(long)j * nx + nx - 1]
+                                                        : v[(long)j * nx + c - 1];
+    }
+}
+
 }  // namespace rmt
 
 using namespace rmt;
@@ -536,6 +680,59 @@ int rmt_mac_momentum_predictor_lid_imex(rmt_ctx *ctx, const double *u, const dou
         RMT_LAUNCHED();
         if ((status = helmholtz(ctx, 0, ru, coef, dx, dy, rtol, 500, 1, xu, &it[0]))) break;
         if ((status = helmholtz(ctx, 1, rv, coef, dx, dy, rtol, 500, 1, xv, &it[1]))) break;
+        k_im_scatter<<<grid1d((long)ny * (nx + 1), 256), 256, 0, st>>>(0, xu, ny, nx, ustar);
+        k_im_scatter<<<grid1d((long)(ny + 1) * nx, 256), 256, 0, st>>>(1, xv, ny, nx, vstar);
+        RMT_LAUNCHED();
+    } while (false);
+    (void)hipFreeAsync(w, st);
+    if (iters) { iters[0] = it[0]; iters[1] = it[1]; }
+    if (!status) RMT_HIP(hipStreamSynchronize(st));
+    return status;
+}
+
+// mac.py:381-442 semi-Lagrangian branch (the caller took it: CFL > cfl_switch)
+int rmt_mac_momentum_predictor_lid_semilag(rmt_ctx *ctx, const double *u, const double *v,
+                                           double nu, double dx, double dy, double dt,
+                                           double U_lid, const double *fu, const double *fv,
+                                           double rho, double cs2, double rtol, double *ustar,
+                                           double *vstar, int *iters) {
+    RMT_CHECK(ctx && u && v && ustar && vstar && ctx->ny >= 2 && ctx->nx >= 2, RMT_EINVAL,
+              "bad argument");
+    const int ny = ctx->ny, nx = ctx->nx;
+    const long nu_i = (long)ny * (nx - 1), nv_i = (long)(ny - 1) * nx;
+    hipStream_t st = ctx->stream;
+    const double c_el = 0.25 * dt * dt * cs2, coef = dt * nu + c_el;
+    const double dx2 = std::pow(dx, 2.0), dy2 = std::pow(dy, 2.0);
+    const double lid_term = coef * (2.0 * U_lid / dy2);
+    const int R[4] = {ny, ny + 1, ny + 2, ny + 1}, C[4] = {nx + 1, nx, nx + 1, nx + 2};
+    long off[5] = {0};
+    for (int q = 0; q < 4; ++q) off[q + 1] = off[q] + (long)(R[q] + 2 * SPL_PAD) * (C[q] + 2 * SPL_PAD);
+    const long ng = (long)(ny + 2) * (nx + 1) + (long)(ny + 1) * (nx + 2);
+    double *w = nullptr;
+    RMT_HIP(hipMallocAsync((void **)&w, (off[4] + ng + 2 * (nu_i + nv_i)) * sizeof(double), st));
+    double *up = w + off[4], *vp = up + (long)(ny + 2) * (nx + 1);
+    double *au = w + off[4] + ng, *av = au + nu_i, *xu = av + nv_i, *xv = xu + nu_i;
+    int status = RMT_OK, it[2] = {0, 0};
+    do {
+        k_ghosts<<<grid1d(std::max((long)(ny + 2) * (nx + 1), (long)(ny + 1) * (nx + 2)), 256), 256, 0,
+                   st>>>(u, v, ny, nx, U_lid, up, vp);
+        const double *src[4] = {u, v, up, vp};
+        for (int q = 0; q < 4; ++q) {
+            const int P = R[q] + 2 * SPL_PAD, Q = C[q] + 2 * SPL_PAD;
+            k_spl_pad<<<grid1d((long)P * Q, 256), 256, 0, st>>>(src[q], R[q], C[q], w + off[q]);
+            k_spl_cols<<<grid1d(Q, 64), 64, 0, st>>>(w + off[q], P, Q);
+            k_spl_rows<<<grid1d(P, 64), 64, 0, st>>>(w + off[q], P, Q);
+        }
+        const SplFields S{w + off[0], w + off[1], w + off[2], w + off[3]};
+        k_sl_faces<<<grid1d(nu_i, 256), 256, 0, st>>>(0, u, v, S, ny, nx, dx, dy, dt, au);
+        k_sl_faces<<<grid1d(nv_i, 256), 256, 0, st>>>(1, u, v, S, ny, nx, dx, dy, dt, av);
+        k_sl_rhs<<<grid1d(nu_i, 256), 256, 0, st>>>(0, au, u, fu, ny, nx, dt, rho, c_el, dx2, dy2,
+                                                   lid_term, au);
+        k_sl_rhs<<<grid1d(nv_i, 256), 256, 0, st>>>(1, av, v, fv, ny, nx, dt, rho, c_el, dx2, dy2,
+                                                   0.0, av);
+        RMT_LAUNCHED();
+        if ((status = helmholtz(ctx, 0, au, coef, dx, dy, rtol, 500, 1, xu, &it[0]))) break;
+        if ((status = helmholtz(ctx, 1, av, coef, dx, dy, rtol, 500, 1, xv, &it[1]))) break;
         k_im_scatter<<<grid1d((long)ny * (nx + 1), 256), 256, 0, st>>>(0, xu, ny, nx, ustar);
         k_im_scatter<<<grid1d((long)(ny + 1) * nx, 256), 256, 0, st>>>(1, xv, ny, nx, vstar);
         RMT_LAUNCHED();

@@ -222,17 +222,26 @@ def momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, r
 
 def momentum_predictor_lid_semilag(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, rho=1.0,
                                    cs2=0.0, rtol=1e-8, cfl_switch=0.9):
-    """mac.py:381-442: adaptive predictor.  At an advective CFL <= cfl_switch the reference
-    takes momentum_predictor_lid_imex (mac.py:387-390), as here; its semi-Lagrangian branch
-    (scipy.ndimage.map_coordinates cubic-spline backtrace) is not built and raises."""
-    uh = np.asarray(u.detach().cpu() if hasattr(u, "detach") else u)
-    vh = np.asarray(v.detach().cpu() if hasattr(v, "detach") else v)
-    cfl = dt * max(np.max(np.abs(uh)) / dx, np.max(np.abs(vh)) / dy)
+    """mac.py:381-442: adaptive predictor -- momentum_predictor_lid_imex at an advective
+    CFL <= cfl_switch (mac.py:387-390), else the semi-Lagrangian midpoint backtrace through
+    cubic-spline interpolation (map_coordinates order 3, 'nearest') and the same PCG
+    viscosity solve."""
+    if (fu is None) != (fv is None):
+        raise NotImplementedError("momentum_predictor_lid_semilag: give both face forces or "
+                                  "neither")
+    io = _IO(u, v); ud = io.dev(u); vd = io.dev(v)
+    cfl = dt * max(float(ud.abs().max()) / dx, float(vd.abs().max()) / dy)
     if cfl <= cfl_switch:
         return momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=fu, fv=fv, rho=rho,
                                            rtol=rtol, cs2=cs2)
-    raise NotImplementedError("momentum_predictor_lid_semilag: the semi-Lagrangian branch "
-                              "(CFL > cfl_switch) is not built")
+    fud, fvd = io.dev(fu), io.dev(fv)
+    us = io.empty(ud.shape); vs = io.empty(vd.shape)
+    it = (ctypes.c_int * 2)()
+    L.check(L.lib().rmt_mac_momentum_predictor_lid_semilag(
+        _ctx(ud.shape[0]), _p(ud), _p(vd), float(nu), float(dx), float(dy), float(dt),
+        float(U_lid), _p(fud), _p(fvd), float(rho), float(cs2), float(rtol), _p(us), _p(vs),
+        ctypes.cast(it, ctypes.c_void_p)), "momentum_predictor_lid_semilag")
+    return io.out(us), io.out(vs)
 
 
 def contact_stress(phi_a, phi_b, eta, Gsum, eps, dx, dy):

@@ -664,6 +664,13 @@ def gen_imex(N=32):
     fu = 0.1 * rng.standard_normal((N, N + 1)); fv = 0.1 * rng.standard_normal((N + 1, N))
     us1, vs1 = M.momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=fu, fv=fv,
                                              rho=1.3, cs2=4.0)
+    # the semi-Lagrangian branch (CFL > 0.9 at this dt), with forces and the elastic term
+    dts = 0.05
+    sl0 = M.momentum_predictor_lid_semilag(u, v, nu, dx, dy, dts, U_lid)
+    sl1 = M.momentum_predictor_lid_semilag(u, v, nu, dx, dy, dts, U_lid, fu=fu, fv=fv, rho=1.3,
+                                           cs2=4.0)
+    save("imex_sl", N=N, dx=dx, dy=dy, u=u, v=v, nu=nu, dt=dts, U_lid=U_lid, fu=fu, fv=fv,
+         us0=sl0[0], vs0=sl0[1], us1=sl1[0], vs1=sl1[1])
     save("imex", N=N, dx=dx, dy=dy, u=u, v=v, lap_u=lap_u, lap_v=lap_v, eig_u=eig_u,
          eig_v=eig_v, rhs_u=rhs_u, rhs_v=rhs_v, coef=coef, cg_u=cg_u, pcg_u=pcg_u, pcg_v=pcg_v,
          cnt_u=cnt_u[0], cnt_v=cnt_v[0], nu=nu, dt=dt, U_lid=U_lid, us0=us0, vs0=vs0, fu=fu,

@@ -116,3 +116,28 @@ def test_helmholtz_rejects_unknown_operator(M):
     rhs = np.ones((N, N - 1))
     with pytest.raises(NotImplementedError):
         M._cg_helmholtz(rhs, lambda w: w[:, 1:-1], lambda x: np.pad(x, ((0, 0), (1, 1))), 0.1)
+
+
+def test_semilag_branch_vs_reference(M):
+    """mac.py:381-442 at CFL 1.76 (> cfl_switch): the cubic-spline midpoint backtrace
+    (map_coordinates order 3, 'nearest': prefilter + 16-tap sums here, scipy's C there) and
+    the PCG viscosity, with and without forces / the elastic term, to 1e-12 of scale."""
+    g = golden("imex_sl")
+    args = (g["u"], g["v"], float(g["nu"]), float(g["dx"]), float(g["dy"]), float(g["dt"]),
+            float(g["U_lid"]))
+    us, vs = M.momentum_predictor_lid_semilag(*args)
+    _close(us, g["us0"]); _close(vs, g["vs0"])
+    us, vs = M.momentum_predictor_lid_semilag(*args, fu=g["fu"], fv=g["fv"], rho=1.3, cs2=4.0)
+    _close(us, g["us1"]); _close(vs, g["vs1"])
+
+
+@pytest.mark.parametrize("N", [48, 96])
+def test_semilag_vs_oracle_sizes(M, MO, N):
+    rng = np.random.default_rng(N + 1)
+    dx = dy = 1.0 / N
+    u = rng.standard_normal((N, N + 1)); u[:, 0] = 0.0; u[:, -1] = 0.0
+    v = rng.standard_normal((N + 1, N)); v[0, :] = 0.0; v[-1, :] = 0.0
+    args = (u, v, 0.01, dx, dy, 4.0 * dx, 1.0)          # CFL ~ 4 x max|u|: backtraces leave
+    us, vs = M.momentum_predictor_lid_semilag(*args)     # the grid (clamped taps)
+    uo, vo = MO.momentum_predictor_lid_semilag(*args)
+    _close(us, uo, 1e-11); _close(vs, vo, 1e-11)
