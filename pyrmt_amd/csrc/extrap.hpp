@@ -43,6 +43,11 @@ struct ExWs {
     unsigned char *part;                      // MAXT
     int *loc, *inv, *gtag;                    // MAXT each
     double *gval;                             // 2 * MAXT
+    int2 *crit;                               // MAXT by global slot: the fit's latest source
+                                              // in chain order {ring tag, or -1 when it
+                                              // lies in another part or none; its cell}
+    double2 *pred;                            // MAXT by global slot: that source's predicted
+                                              // (X1, X2) (k_ex_vals)
     int *rej;                                 // ML * EX_MAXREJ
     int *ctl;                                 // EXC_WORDS
     char *arena;

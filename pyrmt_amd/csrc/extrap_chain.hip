@@ -327,13 +327,16 @@ __global__ void __launch_bounds__(256) k_ex_geom(ExGeoArgs A) {
 }
 
 
+__device__ __forceinline__ int ch_base(const int *ctl, int p);
+
 // ------------------------------------------------------------------ 1. values ------
 // The value half of a record (k_ex_geom wrote the geometry): P[0..5] = the ordered sums of
 // the static terms before the first dynamic one (functions.py:128-138, window order), and
 // the 6 products w*a*X of every static term from there on, at the record's term slots.  The
 // same window analysis as ex_geom (final same-layer acceptance from ACC), the same operands.
 // One wave per accepted fit, every layer in one launch.
-__global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML) {
+__global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML, const double *P1,
+                                                 const double *P2) {
     __shared__ u64 tab[256];
     __shared__ __attribute__((aligned(16))) double tb[4][6 * EXS];
     for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
@@ -434,6 +437,11 @@ __global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML) {
             tv[4 * npad + k] = wa1 * b2[h]; tv[5 * npad + k] = wa2 * b2[h];
         }
         if (lane < 6) rec[17 + lane] = acc;   // P[0..5]
+        if (lane == 0) {   // the prediction of the fit's latest source (k_ex_chain fast fold)
+            const int x = ws.chain_of[id], g = ch_base(ws.ctl, ws.part[x]) + ws.loc[x];
+            const int cc = ws.crit[g].y;
+            ws.pred[g] = cc >= 0 ? make_double2(P1[cc], P2[cc]) : make_double2(0.0, 0.0);
+        }
     }
 }
 
@@ -663,8 +671,14 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
     int2 *dyn = (int2 *)(rec + CH_HDR);   // entry d at int2 index 2d: (k, src)
     const int x = ws.chain_of[id], p = ws.part[x], l = ws.loc[x];
     const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
+    int2 crit = make_int2(-1, -1);   // the latest source in chain order (k_ex_chain fast fold)
+    int xmax = -1;
     for (int d = 0; d < nd; ++d) {
         const int xs = ws.chain_of[dyn[4 * d].y];
+        if (xs > xmax) {
+            xmax = xs;
+            crit = make_int2(ws.part[xs] == p ? ws.loc[xs] : -1, (int)ws.tcell[dyn[4 * d].y]);
+        }
         if (xs >= x) { ws.ctl[EXC_ABORT] = 1; atomicExch(ws.status + 1, 1); }   // a bug
         if (ws.part[xs] == p) {
             const int ls = ws.loc[xs];
@@ -678,6 +692,7 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
             atomicOr((unsigned long long *)&srec[1], 1ull << 63);
         }
     }
+    ws.crit[base + l] = crit;
     int ln = l + CH_W;
     while (ln < np && ws.rec_by_chain[ws.inv[base + ln]] < 0) ln += CH_W;
     const long long rn = ln < np ? ws.rec_by_chain[ws.inv[base + ln]] : 0;   // (size64 << 32) | off64
@@ -772,6 +787,135 @@ __device__ __forceinline__ double ch_fold(double acc, const double *row, int c0,
     return acc;
 }
 
+
+// Fast fold (VAR bit 5): the sums after a fit's latest source c, F(a) = fl(..fl(a + t1) ..
+// + tn), folded BEFORE c arrives.  a = fl(S_pre + cf X_c) is predicted as a^ from X^_c (the
+// previous step's map at c, k_ex_vals); lane 8k + r (sum k < 6, r < 8) folds the trailing
+// terms from a^ with its 3 low mantissa bits replaced by r.  If a and a^ share the binade and
+// every partial sum of lane (k, r = a mod 8 ulp) stays >= 2^-14 of its binade from the
+// binade's edges, at most 2 binades above a's, then rounding commutes with the shift
+// d = a - a_r (a multiple of 8 ulp(a), >= 2 ulp of every binade passed):
+// F(a) = F(a_r) + d exactly.  Otherwise the terms are folded after the arrival as before.
+// Returns 0: not taken (nothing changed), 1: the sums are in acc (lanes 0-5), -1: timeout.
+__device__ __forceinline__ double d_hl(unsigned h, unsigned l) {
+    return __hiloint2double((int)h, (int)l);
+}
+__device__ __forceinline__ int ch_fast(int lane, double *B, const double2 *val, const int *tag,
+                                       double *tv, int npad, int2 e, const double *cf,
+                                       bool &done, double &acc, int2 cr, double2 pr) {
+    if (cr.x < 0) return 0;
+    const u64 cl = __ballot(!done && e.y == cr.x);
+    if (!cl) return 0;
+    const int clane = __builtin_ctzll(cl);
+    const int slot = e.y & (CH_R - 1);
+    // every other missing source first (their products into tv, as pass 2 writes them)
+    long sp = 0;
+    while (__ballot(!done && lane != clane)) {
+        if (!done && lane != clane &&
+            __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
+            asm volatile("" ::: "memory");
+            const double2 v = val[slot];
+#pragma unroll
+            for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+            done = true;
+        }
+        if (++sp > CH_SPIN_LIMIT) return -1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int kc = __builtin_amdgcn_readlane(e.x, clane);
+    const double c0 = rlf(cf[0], clane), c1 = rlf(cf[1], clane), c2 = rlf(cf[2], clane);
+    const int m3 = lane % 3;
+    const double cfl = m3 == 0 ? c0 : (m3 == 1 ? c1 : c2);
+    // the sums up to the latest source's term, in the reference's order
+    if (lane < 6) {
+        const double *row = tv + lane * npad;
+        acc = ch_fold(acc, row, 0, kc >> 3);
+        for (int j = kc & ~7; j < kc; ++j) acc += row[j];
+    }
+    double *sc = B + CH_BUFD - 8;
+    if (lane < 6) sc[lane] = acc + cfl * (lane < 3 ? pr.x : pr.y);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int kk = (lane >> 3) < 6 ? (lane >> 3) : 5, rr = lane & 7;
+    const double ah = sc[kk];
+    const unsigned hA = (unsigned)__double2hiint(ah), lA = (unsigned)__double2loint(ah);
+    double f = d_hl(hA, (lA & ~7u) | (unsigned)rr);
+    unsigned mx = hA, mn = hA;
+    bool nr = false;
+    const double *trow = tv + kk * npad;
+    auto trk = [&](double t) {
+        f += t;
+        const unsigned h = (unsigned)__double2hiint(f);
+        mx = max(mx, h); mn = min(mn, h);
+        nr = nr || ((h + 0x40u) & 0xFFF80u) == 0u;
+    };
+    const int t1 = (kc >> 3) + 1, nch = npad >> 3;
+    for (int j = kc + 1; j < 8 * t1; ++j) trk(trow[j]);
+    if (t1 < nch) {   // whole chunks, the next chunk's reads in flight (as ch_fold)
+        const double2 *r2 = (const double2 *)trow;
+        double2 a0 = r2[4 * t1], a1 = r2[4 * t1 + 1], a2 = r2[4 * t1 + 2], a3 = r2[4 * t1 + 3];
+        for (int c = t1; c < nch; ++c) {
+            double2 b0, b1, b2, b3;
+            const bool more = c + 1 < nch;
+            if (more) {
+                b0 = r2[4 * c + 4]; b1 = r2[4 * c + 5]; b2 = r2[4 * c + 6]; b3 = r2[4 * c + 7];
+            }
+            trk(a0.x); trk(a0.y); trk(a1.x); trk(a1.y);
+            trk(a2.x); trk(a2.y); trk(a3.x); trk(a3.y);
+            if (more) { a0 = b0; a1 = b1; a2 = b2; a3 = b3; }
+        }
+    }
+    // the latest source (low priority while polling, as pass 2)
+    double2 vc = make_double2(0.0, 0.0);
+    sp = 0;
+    __builtin_amdgcn_s_setprio(0);
+    for (;;) {
+        if (lane == clane && !done &&
+            __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
+            asm volatile("" ::: "memory");
+            vc = val[slot];
+            done = true;
+        }
+        if (__ballot(!done) == 0) break;
+        if (++sp > CH_SPIN_LIMIT) return -1;
+    }
+    __builtin_amdgcn_s_setprio(3);
+    const double v1 = rlf(vc.x, clane), v2 = rlf(vc.y, clane);
+    double a = 0.0;
+    if (lane < 6) a = acc + cfl * (lane < 3 ? v1 : v2);   // the reference's next operation
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane < 6) sc[lane] = a;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const double ak = sc[kk];
+    const unsigned hB = (unsigned)__double2hiint(ak), lB = (unsigned)__double2loint(ak);
+    const bool match = lane < 48 && (lB & 7u) == (unsigned)rr;
+    const unsigned e0 = hA & 0x7FF00000u, emn = (mn >> 20) & 0x7FFu;
+    const bool same = (hB & 0xFFF00000u) == (hA & 0xFFF00000u) && (hA >> 31) == 0u &&
+                      e0 >= (0x100u << 20) && e0 <= (0x700u << 20);
+    const bool okb = !nr && (mx >> 31) == 0u && (mx & 0x7FF00000u) <= e0 + (2u << 20) && emn > 64u;
+    const double del = d_hl(hB, lB & ~7u) - d_hl(hA, lA & ~7u);
+    const double lim = d_hl((emn - 15u) << 20, 0u);
+    const bool good = same && okb && fabs(del) <= lim;
+    const u64 mm = __ballot(match), mg = __ballot(match && good);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (mm == mg && __popcll(mm) == 6) {
+        if (match) sc[kk] = f + del;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane < 6) acc = sc[lane];
+    } else if (lane < 6) {
+        acc = a;
+        const double *row = tv + lane * npad;
+        for (int j = kc + 1; j < 8 * t1; ++j) acc += row[j];
+        acc = ch_fold(acc, row, t1, nch);
+    }
+    return 1;
+}
+
 __device__ __forceinline__ double dpp_shl(double v, int ctrl) {
     // row_shl:1 = 0x101, row_shl:2 = 0x102 (lanes read lane + k within their 16-lane row)
     const int lo = __double2loint(v), hi = __double2hiint(v);
@@ -796,7 +940,8 @@ template <bool PROF, int VAR>
 __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                        int *cur, int &wm, double &o_out, long &c_out,
                                        long long *pr, long long &tl, int *gtag, double *gval,
-                                       int gslot, long long *trace = nullptr, int base = 0) {
+                                       int gslot, long long *trace = nullptr, int base = 0,
+                                       const int2 *crit = nullptr, const double2 *pred = nullptr) {
     long long tr_start = 0, tr_ready = 0;
     int tr_crit = -1;
     // ring reuse: every fit < x - CH_R/2 is done (all their readers are < x)
@@ -875,6 +1020,13 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         }
     }
     // first window term whose source is still missing: sources are listed in window order
+    int fastr = 0;
+    if constexpr ((VAR & 32) != 0 && !PROF) {
+        if (__ballot(!done))
+            fastr = ch_fast(lane, B, val, tag, tv, npad, e, cf, done, acc, crit[gslot], pred[gslot]);
+        if (fastr < 0) return false;
+    }
+    if (!fastr) {
     const u64 pend = __ballot(!done);
     const int kmiss = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : npad;
     __builtin_amdgcn_wave_barrier();
@@ -914,6 +1066,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     if (lane < 6) acc = ch_fold(acc, tv + lane * npad, c1, nch);
+    }
     if constexpr (PROF) asm volatile("" : "+v"(acc));
     CH_STAMP(4);
     // utils.py:134-166 on lanes 0 (X1) and 3 (X2) with the precomputed cofactors
@@ -1006,7 +1159,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
         if (!ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag, C.ws.gval,
-                               base + x, C.trace, base)) { ok = false; break; }
+                               base + x, C.trace, base, C.ws.crit, C.ws.pred)) { ok = false; break; }
         x = x2; r = r2;
     }
     if constexpr (PROF)
@@ -1064,7 +1217,8 @@ int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     const double r = 4 * std::sqrt(dx * dx + dy * dy);
     ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r};
     const unsigned gblocks = (unsigned)std::min<long>(1024, std::max<long>(1, ws.maxt / 4));
-    k_ex_vals<<<gblocks, 256, 0, ctx->stream>>>(A, ML);
+    k_ex_vals<<<gblocks, 256, 0, ctx->stream>>>(A, ML, ctx->ex_pred1 ? ctx->ex_pred1 : X1o,
+                                                ctx->ex_pred2 ? ctx->ex_pred2 : X2o);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -1084,6 +1238,7 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
             case 0: k_ex_chain<false, 0><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 1: k_ex_chain<false, 1><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 2: k_ex_chain<false, 2><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
+            case 35: k_ex_chain<false, 35><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             default:
                 if (nparts == 1) k_ex_chain<false, 19><<<1, CH_W * 64, 0, st>>>(C, nullptr);
                 else k_ex_chain<false, 3><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);

@@ -772,11 +772,15 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // chip-wide passes are done and the one-workgroup chain kernel is launched
             if (overlap) ctx->ev_chain = S->e_sl;
             const bool kb = P.scheme == RMT_SCHEME_SEMILAGRANGIAN;   // k_sim_sl wrote kbits
+            // the previous step's map (intact until the second stream's phi rebuild, which
+            // starts at the chain's launch) predicts the chain's latest sources
+            ctx->ex_pred1 = S->X1; ctx->ex_pred2 = S->X2;
             const int es = geo_ready && P.layers > 0
                                ? extrap_finish(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->flag + 2)
                                : extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
                                              S->X1n, S->X2n, S->flag + 2, kb ? S->kbits : nullptr);
             geo_ready = false;
+            ctx->ex_pred1 = ctx->ex_pred2 = nullptr;
             ctx->ev_chain = nullptr;
             RMT_TRY(es);
             if (overlap) {

@@ -39,6 +39,33 @@ static Res fold(double s, const double *t, int n) {
     return r;
 }
 
+
+/* the k_ex_chain fast fold's acceptance (VAR 35): residues mod 8 ulp, near test on the top 14
+ * mantissa bits, max binade <= e0 + 2, |d| <= 2^(Emin - 15); returns 1 and *out on success */
+static unsigned hiw(double v) { unsigned long long b; memcpy(&b, &v, 8); return (unsigned)(b >> 32); }
+static unsigned low(double v) { unsigned long long b; memcpy(&b, &v, 8); return (unsigned)b; }
+static double mk(unsigned h, unsigned l) { unsigned long long b = ((unsigned long long)h << 32) | l; double v; memcpy(&v, &b, 8); return v; }
+static int kernel_fast(double ah, double a, const double *t, int nt, double *out) {
+    unsigned hA = hiw(ah), lA = low(ah), hB = hiw(a), lB = low(a);
+    unsigned rr = lB & 7u;
+    double f = mk(hA, (lA & ~7u) | rr);
+    unsigned mx = hA, mn = hA; int nr = 0;
+    for (int j = 0; j < nt; ++j) {
+        f += t[j];
+        unsigned h = hiw(f);
+        if (h > mx) mx = h; if (h < mn) mn = h;
+        nr = nr || ((h + 0x40u) & 0xFFF80u) == 0u;
+    }
+    unsigned e0 = hA & 0x7FF00000u, emn = (mn >> 20) & 0x7FFu;
+    int same = (hB & 0xFFF00000u) == (hA & 0xFFF00000u) && (hA >> 31) == 0u && e0 >= (0x100u << 20) && e0 <= (0x700u << 20);
+    int okb = !nr && (mx >> 31) == 0u && (mx & 0x7FF00000u) <= e0 + (2u << 20) && emn > 64u;
+    double del = mk(hB, lB & ~7u) - mk(hA, lA & ~7u);
+    double lim = mk((emn - 15u) << 20, 0u);
+    if (!(same && okb && fabs(del) <= lim)) return 0;
+    *out = f + del;
+    return 1;
+}
+
 int main(int argc, char **argv) {
     int N = argc > 1 ? atoi(argv[1]) : 4096, ML = argc > 2 ? atoi(argv[2]) : 3;
     int ny = N, nx = N;
@@ -59,7 +86,7 @@ int main(int argc, char **argv) {
         }
     double r = 4 * sqrt(dx * dx + dy * dy), r2 = r * r;
     long nfit = 0, nstatic = 0, npass = 0, nlane_ok = 0, nbad = 0, hist[9] = {0};
-    long sum_fail_exp = 0, sum_fail_slack = 0, sum_fail_neg = 0;
+    long sum_fail_exp = 0, sum_fail_slack = 0, sum_fail_neg = 0, kfits = 0, kok = 0, kbad = 0;
     for (int L = 0; L < ML; ++L) {
         memset(target, 0, n);
         for (int j = 1; j < ny - 1; ++j)
@@ -106,7 +133,7 @@ int main(int argc, char **argv) {
                 /* the 6 sums: the shortcut against the sequential fold */
                 if (crit < 0) { ++nstatic; }
                 else {
-                    int lanes = 0, ok = 1;
+                    int lanes = 0, ok = 1, kall = 1;
                     for (int k = 0; k < 6; ++k) {
                         const double *bb = k < 3 ? b1 : b2, *pp = k < 3 ? p1 : p2;
                         double s = 0.0, t[81];
@@ -122,6 +149,7 @@ int main(int argc, char **argv) {
                         }
                         double seq = a;
                         for (int q = 0; q < nt; ++q) seq += t[q];
+                        { double kr; if (kernel_fast(ah, a, t, nt, &kr)) { if (memcmp(&kr, &seq, 8)) ++kbad; } else kall = 0; }
                         if (!(ah > 0) || !(a > 0)) { ok = 0; ++sum_fail_neg; continue; }
                         up *= 1 + 1e-12;
                         const int e0 = ex_of(ah), em = ex_of(up), m = em - e0;
@@ -145,6 +173,7 @@ int main(int argc, char **argv) {
                     hist[lb]++;
                     if (lanes <= 64) ++nlane_ok;
                     if (ok) ++npass;
+                    ++kfits; if (kall) ++kok;
                 }
                 /* the fit itself (serial semantics) */
                 double B1[3] = {0}, B2[3] = {0};
@@ -166,6 +195,7 @@ int main(int argc, char **argv) {
     printf("N=%d fits %ld (no dynamic source %ld); shortcut passes %ld (%.1f%% of dynamic), "
            "lanes<=64 %ld; mismatches %ld\n", N, nfit, nstatic, npass,
            100.0 * npass / (nfit - nstatic), nlane_ok, nbad);
+    printf("kernel fast fold: %ld of %ld fits (%.1f%%), wrong results %ld\n", kok, kfits, 100.0 * kok / kfits, kbad);
     printf("per-sum failures: binade of a %ld, slack %ld, non-positive %ld\n", sum_fail_exp,
            sum_fail_slack, sum_fail_neg);
     printf("lanes histogram (<=8, 16, 32, 64, 128, 256, ...):");
