@@ -447,12 +447,24 @@ __device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__r
 // (launch bounds: two workgroups per CU -- 4 waves per SIMD at 512 threads, 128 VGPRs)
 template <int BIG> struct K1T { static constexpr int T = BIG ? 256 : 512; };
 
+// every load issued before the first LDS write: a dynamic-trip loop here compiled to one
+// HBM round trip per iteration (load, wait, write), ~8 serial misses per row
 template <int NT>
 __device__ __forceinline__ void put_row_even(double *d, int N, const double *__restrict__ x) {
-    for (int j = threadIdx.x; j <= N; j += NT) {
-        const double v = x[j];
-        d[j] = v;
-        if (j >= 1 && j < N) d[2 * N - j] = v;
+    constexpr int L = (K1_MAXN + NT) / NT;   // j <= N <= K1_MAXN
+    double v[L];
+#pragma unroll
+    for (int t = 0; t < L; ++t) {
+        const int j = threadIdx.x + t * NT;
+        if (j <= N) v[t] = x[j];
+    }
+#pragma unroll
+    for (int t = 0; t < L; ++t) {
+        const int j = threadIdx.x + t * NT;
+        if (j <= N) {
+            d[j] = v[t];
+            if (j >= 1 && j < N) d[2 * N - j] = v[t];
+        }
     }
 }
 
