@@ -30,6 +30,9 @@ STEP_ALG_BYTES_PER_CELL = 208  # the whole step (SURVEY.md 8(d), configs 2 and 4
 # HBM bytes per launch and per step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
 # bench (scripts/gpu.sh pmc -> tools/pmc_traffic.py; FETCH x2 per the gfx950 calibration)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_n4096.json")
+# fp64 VALU counts of the same kernel and the measured FMA peak (scripts/pmc_f64.sh ->
+# tools/f64_roof.py): k_mom_stage is VALU-issue-bound, not HBM-bound
+F64_ROOF = os.path.join(ROOT, "profiles", "r02", "f64_roof_n4096.json")
 # dependent fits on the critical path of the bench-state extrapolation at N=4096 (per-fit
 # trace of the chain kernel, tools/chain_trace.py; profiles/r02/chain_trace/)
 CHAIN_DEPTH_4096 = 3257
@@ -56,6 +59,20 @@ def _pmc(n, ws):
     d = json.load(open(PMC_TRAFFIC))
     k = d["kernels"].get("k_mom_stage")     # the full-grid stage launches the events time
     return (k["bytes_per_full_launch"] if k else None), d["per_step"].get("total"), d.get("git_rev")
+
+
+def _f64_roof(n, ws, launch_s):
+    """k_mom_stage against its fp64 VALU roof (committed counter pass), or None."""
+    if n != 4096 or ws != 1 or not os.path.exists(F64_ROOF):
+        return None
+    d = json.load(open(F64_ROOF))
+    achieved = d["flop_per_launch"] / launch_s / 1e12
+    return {"bound": "valu-f64", "kernel": d["kernel"], "achieved": achieved,
+            "peak": d["fma_peak_tflops_measured"], "unit": "TFLOP/s",
+            "frac": achieved / d["fma_peak_tflops_measured"],
+            "issue_floor_ms": d["valu_issue_floor_ms"],
+            "issue_frac": d["valu_issue_floor_ms"] / (launch_s * 1e3),
+            "counters_rev": d["git_rev"]}
 
 
 def _dist():
@@ -192,6 +209,8 @@ def main():
                          "traffic": traffic, "traffic_rev": pmc_rev,
                          "launch_ms": per_launch_s * 1e3,
                          "alg_bytes_per_launch": alg_per_launch},
+            # ... whose own bound is the fp64 VALU issue rate (SQ counters)
+            "compute_roofline": _f64_roof(N, ws, per_launch_s),
             # the dominant kernel by time is not HBM-bound: the exact raster-order extrapolation
             # chain runs on one workgroup, bounded by its dependency depth
             "latency_bound": {"kernel": "k_ex_chain (exact serial-order extrapolation chain)",
