@@ -63,6 +63,7 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
                       double dx, double dy, int ML);
 int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
                         double dx, double dy, int ML);
+int ch_variant();   // RMT_CH_VARIANT (extrap_chain.hip)
 int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o, int ML);
 bool extrap_chain_supported(int ny, int nx, int ML);
 

@@ -329,6 +329,12 @@ __global__ void __launch_bounds__(256) k_ex_geom(ExGeoArgs A) {
 
 __device__ __forceinline__ int ch_base(const int *ctl, int p);
 
+// RMT_CH_VARIANT (default 3; see ch_fit): read once per process
+int ch_variant() {
+    static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 3;
+    return var;
+}
+
 // ------------------------------------------------------------------ 1. values ------
 // The value half of a record (k_ex_geom wrote the geometry): P[0..5] = the ordered sums of
 // the static terms before the first dynamic one (functions.py:128-138, window order), and
@@ -437,7 +443,7 @@ __global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML, const doub
             tv[4 * npad + k] = wa1 * b2[h]; tv[5 * npad + k] = wa2 * b2[h];
         }
         if (lane < 6) rec[17 + lane] = acc;   // P[0..5]
-        if (lane == 0) {   // the prediction of the fit's latest source (k_ex_chain fast fold)
+        if (lane == 0 && ws.pred) {   // the prediction of the fit's latest source (variant 35)
             const int x = ws.chain_of[id], g = ch_base(ws.ctl, ws.part[x]) + ws.loc[x];
             const int cc = ws.crit[g].y;
             ws.pred[g] = cc >= 0 ? make_double2(P1[cc], P2[cc]) : make_double2(0.0, 0.0);
@@ -675,7 +681,7 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
     int xmax = -1;
     for (int d = 0; d < nd; ++d) {
         const int xs = ws.chain_of[dyn[4 * d].y];
-        if (xs > xmax) {
+        if (ws.crit && xs > xmax) {   // (variant 35 only: ws.crit is null otherwise)
             xmax = xs;
             crit = make_int2(ws.part[xs] == p ? ws.loc[xs] : -1, (int)ws.tcell[dyn[4 * d].y]);
         }
@@ -692,7 +698,7 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
             atomicOr((unsigned long long *)&srec[1], 1ull << 63);
         }
     }
-    ws.crit[base + l] = crit;
+    if (ws.crit) ws.crit[base + l] = crit;
     int ln = l + CH_W;
     while (ln < np && ws.rec_by_chain[ws.inv[base + ln]] < 0) ln += CH_W;
     const long long rn = ln < np ? ws.rec_by_chain[ws.inv[base + ln]] : 0;   // (size64 << 32) | off64
@@ -1187,7 +1193,7 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     const unsigned rows = grid1d(ny, 4);
     double r = 4 * std::sqrt(dx * dx + dy * dy);
     ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r};
-    const unsigned gblocks = (unsigned)std::min<long>(1024, std::max<long>(1, ws.maxt / 4));
+    const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
     for (int L = 0; L < ML; ++L) {
         A.L = L;
         k_tg_rows<<<rows, 256, 0, st>>>(ws, ny, nx, W, L);
@@ -1216,7 +1222,7 @@ int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
     const double r = 4 * std::sqrt(dx * dx + dy * dy);
     ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r};
-    const unsigned gblocks = (unsigned)std::min<long>(1024, std::max<long>(1, ws.maxt / 4));
+    const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
     k_ex_vals<<<gblocks, 256, 0, ctx->stream>>>(A, ML, ctx->ex_pred1 ? ctx->ex_pred1 : X1o,
                                                 ctx->ex_pred2 ? ctx->ex_pred2 : X2o);
     RMT_LAUNCHED();
@@ -1232,7 +1238,7 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
     if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status, nullptr};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
-    static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 3;
+    const int var = ch_variant();
     if (!prof) {
         switch (var) {
             case 0: k_ex_chain<false, 0><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;

@@ -737,7 +737,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                                                        scount);
                 }
                 RMT_HIP(hipEventRecord(S->e_bits, st));
-                k_sim_sl_rim<<<1024, 256, 0, st>>>(
+                k_sim_sl_rim<<<4096, 256, 0, st>>>(   // ~one rim segment per block
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.x0, P.y0,
                     P.R, S->X1n, S->X2n, S->flag, sc, dtp, S->rimw, S->segs, scount);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
