@@ -484,18 +484,21 @@ __global__ void k_project_correct(const double *__restrict__ a_s, const double *
     }
     if (m2part) {
         // max of u^2 + v^2 over the block, NaN-propagating (k_reduce_p1<3>'s rule; a max is
-        // exact in any order)
-        __shared__ double s[256];
-        s[threadIdx.x] = q;
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if ((int)threadIdx.x < w) {
-                const double y = s[threadIdx.x + w];
-                if (y > s[threadIdx.x] || y != y) s[threadIdx.x] = y;
-            }
-            __syncthreads();
+        // exact in any order): across each wave by shuffles, then the 4 wave results
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double y = __shfl_xor(q, off);
+            if (y > q || y != y) q = y;
         }
-        if (threadIdx.x == 0) m2part[(long)blockIdx.y * gridDim.x + blockIdx.x] = s[0];
+        __shared__ double s[4];
+        if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = q;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double m = s[0];
+            for (int w = 1; w < 4; ++w)
+                if (s[w] > m || s[w] != s[w]) m = s[w];
+            m2part[(long)blockIdx.y * gridDim.x + blockIdx.x] = m;
+        }
     }
 }
 __global__ void k_scale_copy(const double *__restrict__ x, long n, double s,
