@@ -41,6 +41,11 @@ struct rmt_sim {
     void *block = nullptr;
     // overlap of the (one-CU) extrapolation chain with a speculative momentum pass
     hipStream_t st2 = nullptr;
+    // the step's own stream at the highest priority (RMT_SIM_HIPRIO, default on), joined to the
+    // caller's stream at entry and exit: the critical path's kernels are dispatched ahead of
+    // the second stream's whenever both have work ready
+    hipStream_t st1 = nullptr;
+    hipEvent_t e_in = nullptr, e_out = nullptr;
     hipEvent_t e_sl = nullptr, e_mom = nullptr, e_rows = nullptr;
     int *tiles = nullptr, *tcount = nullptr, max_tiles = 0;
     // device-resident dt and diagnostics (rmt_sim_step's asynchronous path): per-block
@@ -519,6 +524,12 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
         int least = 0, greatest = 0;
         RMT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         RMT_HIP(hipStreamCreateWithPriority(&S->st2, hipStreamNonBlocking, least));
+        static const bool hiprio = !getenv("RMT_SIM_HIPRIO") || atoi(getenv("RMT_SIM_HIPRIO"));
+        if (hiprio && greatest != least) {
+            RMT_HIP(hipStreamCreateWithPriority(&S->st1, hipStreamNonBlocking, greatest));
+            RMT_HIP(hipEventCreateWithFlags(&S->e_in, hipEventDisableTiming));
+            RMT_HIP(hipEventCreateWithFlags(&S->e_out, hipEventDisableTiming));
+        }
         RMT_HIP(hipEventCreateWithFlags(&S->e_sl, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_mom, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_rows, hipEventDisableTiming));
@@ -569,6 +580,9 @@ int rmt_sim_destroy(rmt_sim *S) {
     if (S->e_kb) (void)hipEventDestroy(S->e_kb);
     if (S->e_geo) (void)hipEventDestroy(S->e_geo);
     if (S->st2) (void)hipStreamDestroy(S->st2);
+    if (S->st1) (void)hipStreamDestroy(S->st1);
+    if (S->e_in) (void)hipEventDestroy(S->e_in);
+    if (S->e_out) (void)hipEventDestroy(S->e_out);
     for (auto e : S->pev) if (e) (void)hipEventDestroy(e);
     S->ctx->prof = false;
     delete S;
@@ -614,6 +628,22 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     const int ny = P.ny, nx = P.nx;
     const long n = (long)ny * nx;
     const unsigned g = grid1d(n, 256);
+    // run on S->st1 (highest priority) when it exists: ordered after the caller's stream on
+    // entry, the caller's stream ordered after it on every return
+    struct OnHi {
+        rmt_ctx *c; hipStream_t user; rmt_sim *S;
+        ~OnHi() {
+            if (!S->st1) return;
+            (void)hipEventRecord(S->e_out, S->st1);
+            (void)hipStreamWaitEvent(user, S->e_out, 0);
+            c->stream = user;
+        }
+    } on_hi{ctx, ctx->stream, S};
+    if (S->st1) {
+        RMT_HIP(hipEventRecord(S->e_in, ctx->stream));
+        RMT_HIP(hipStreamWaitEvent(S->st1, S->e_in, 0));
+        ctx->stream = S->st1;
+    }
     hipStream_t st = ctx->stream;
     double *sc = S->dscr + DIAG_BLOCKS * DIAG_VALS;   // [0] maxsq, [1] dt, [2..11] diag
     // Asynchronous path (no t_end: nothing to clip): dt is computed and consumed on the
