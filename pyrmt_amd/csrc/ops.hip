@@ -821,10 +821,10 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,
-                      double *m2part, bool sub_mean) {
+                      double *m2part, bool sub_mean, const unsigned char *early_marks) {
     const long n = (long)ctx->ny * ctx->nx;
     double *pc = ctx->scratch + n, *root = ctx->red + RED_BLOCKS + 17;
-    RMT_TRY(dct_solve_after_rows(ctx, pc, root));
+    RMT_TRY(dct_solve_after_rows(ctx, pc, root, early_marks));
     k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
         a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt / rho, bc_kind, lid, a, b, p, 0,
         ctx->ny, root, (double)n, dtp, rho, m2part);

@@ -567,11 +567,18 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
     }
 }
 
-// out (C x R) = in (R x C) transposed, 64 x 64 tiles through LDS
+// out (C x R) = in (R x C) transposed, 64 x 64 tiles through LDS.  rowmark (nullable) with
+// mode 1: only the 64-row blocks of in holding no marked row; mode 2: only those holding one
 __global__ void __launch_bounds__(256) k_transpose(const double *__restrict__ in, int R, int C,
-                                                   double *__restrict__ out) {
+                                                   double *__restrict__ out,
+                                                   const unsigned char *__restrict__ rowmark = nullptr,
+                                                   int mode = 0) {
     __shared__ double t[64][65];
     const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64, tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    if (rowmark) {
+        const bool any = __syncthreads_or(threadIdx.x < 64 && r0 + tx < R && rowmark[r0 + tx] != 0);
+        if (any != (mode == 2)) return;
+    }
     for (int rr = ty; rr < 64; rr += 4) {
         const int r = r0 + rr, c = c0 + tx;
         if (r < R && c < C) t[rr][tx] = in[(long)r * C + c];
@@ -634,8 +641,9 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
 
 bool dct_lds_ready(rmt_ctx *ctx) { return ctx->dct && ctx->dct->lds; }
 
-void transpose(hipStream_t st, const double *in, int R, int C, double *out) {
-    k_transpose<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out);
+void transpose(hipStream_t st, const double *in, int R, int C, double *out,
+               const unsigned char *rowmark, int mode) {
+    k_transpose<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out, rowmark, mode);
 }
 
 static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p, double *rs) {
@@ -653,12 +661,24 @@ static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p,
     return RMT_OK;
 }
 
-int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root) {
+// the row blocks of pc whose rows are all unmarked are final before the marked rows are
+// redone: transposed ahead (beside the extrapolation chain); dct_solve_after_rows with the
+// same marks then transposes only the others
+int dct_transpose_unmarked(rmt_ctx *ctx, const double *pc, const unsigned char *rowmark) {
+    DctPlan *P = ctx->dct;
+    RMT_CHECK(P && P->lds && rowmark, RMT_ENOTSUP, "dct_transpose_unmarked: LDS DCT plan needed");
+    transpose(ctx->stream, pc, P->ny, P->nx, P->T, rowmark, 1);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root,
+                         const unsigned char *early_marks) {
     DctPlan *P = ctx->dct;
     RMT_CHECK(P && P->lds && P->ny <= ctx->rsum_len, RMT_ENOTSUP,
               "dct_solve_after_rows: LDS DCT plan needed");
     const int ny = P->ny, nx = P->nx;
-    transpose(ctx->stream, pc, ny, nx, P->T);
+    transpose(ctx->stream, pc, ny, nx, P->T, early_marks, early_marks ? 2 : 0);
     RMT_TRY(dct_pass(ctx, true, 1, P->T, P->T, nx, 0, 1.0 / (2.0 * (ny - 1))));
     transpose(ctx->stream, P->T, nx, ny, pc);
     RMT_TRY(dct_pass(ctx, false, 0, pc, pc, ny, 0, 1.0 / (2.0 * (nx - 1)), ctx->rsum));

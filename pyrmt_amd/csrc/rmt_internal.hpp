@@ -454,7 +454,8 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,
-                      double *m2part, bool sub_mean = true);
+                      double *m2part, bool sub_mean = true,
+                      const unsigned char *early_marks = nullptr);
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                    double dy, const double *dtp, double rho, int bc_kind, double lid,
                    const double *p_prev, double *a, double *b, double *p, double *m2part);
@@ -532,8 +533,13 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
              const unsigned char *rowmark = nullptr);
 // the LDS solve after its forward row pass (pc holds DCT_x of the rhs): columns, inverse rows,
 // the row-tree sum of the result into *dev_root (mean not subtracted)
-int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root);
-void transpose(hipStream_t st, const double *in, int R, int C, double *out);
+int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root,
+                         const unsigned char *early_marks = nullptr);
+// the row blocks of pc without a marked row, transposed into the plan's column buffer ahead
+// of dct_solve_after_rows(..., rowmark) (which then transposes only the others)
+int dct_transpose_unmarked(rmt_ctx *ctx, const double *pc, const unsigned char *rowmark);
+void transpose(hipStream_t st, const double *in, int R, int C, double *out,
+               const unsigned char *rowmark = nullptr, int mode = 0);
 // MAC grid (mac.py:104-123): DCT-II Neumann solve on a (ny, nx) cell grid, (0,0) -> 0
 int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);
 int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p);

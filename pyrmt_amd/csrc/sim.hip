@@ -704,6 +704,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     // the next step's rim words and extrapolation geometry, prepared on the second stream
     // beside this step's projection (they depend on the known plane alone)
     static const bool geo_env = !(getenv("RMT_EARLY_GEOMETRY") && !atoi(getenv("RMT_EARLY_GEOMETRY")));
+    // the column pass's transpose of the row blocks without fix-up rows beside the chain
+    // (RMT_EARLY_TRANSPOSE, default on)
+    static const bool early_t_env = !(getenv("RMT_EARLY_TRANSPOSE") && !atoi(getenv("RMT_EARLY_TRANSPOSE")));
+    bool early_t = false;
     bool geo_ready = false;
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end)) break;
@@ -848,6 +852,11 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 if (ms == RMT_OK && S->split_proj)
                     ms = projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
                                          nullptr);
+                // and the row blocks no fix-up row falls in, transposed for the column pass
+                if (ms == RMT_OK && S->split_proj && early_t_env) {
+                    ms = dct_transpose_unmarked(ctx, ctx->scratch + n, S->rowmark);
+                    early_t = ms == RMT_OK;
+                }
                 ctx->stream = st;
                 RMT_TRY(ms);
                 RMT_HIP(hipEventRecord(S->e_rows, S->st2));
@@ -912,7 +921,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                     S->rowmark, S->tiles, S->tcount, S->max_tiles));
             RMT_TRY(projection_finish(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, P.bc_kind,
                                       P.lid, S->p, S->u, S->v, S->p,
-                                      async ? S->m2part : nullptr, !(async && side_tail)));
+                                      async ? S->m2part : nullptr, !(async && side_tail),
+                                      early_t ? S->rowmark : nullptr));
+            early_t = false;
         } else if (async)
             RMT_TRY(projection_dev(ctx, S->us, S->vs, P.dx, P.dy, dtp, P.rho_f, P.bc_kind, P.lid,
                                    S->p, S->u, S->v, S->p, S->m2part));
