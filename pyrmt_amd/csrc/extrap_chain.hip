@@ -775,20 +775,31 @@ __device__ __forceinline__ bool ch_probe(int ey, const int *tag, const double2 *
         const long long t_ = __builtin_amdgcn_s_memtime();             \
         pr[k] += t_ - tl; tl = t_;                                     \
     }
-// fold row[8*c0 .. 8*c1) into acc in order; two 8-term chunks of reads in flight
+// fold row[8*c0 .. 8*c1) into acc in order: 4-term groups, three groups of reads in flight
+// (a group's 4 dependent adds, 32 clk, against an LDS read latency of ~70-100 clk).  The
+// reads run up to two groups past the end unconditionally (unused; LDS reads never fault):
+// conditional reads made the compiler copy registers and drain every read at each copy.
 __device__ __forceinline__ double ch_fold(double acc, const double *row, int c0, int c1) {
     if (c0 >= c1) return acc;
     const double2 *r2 = (const double2 *)row;
-    double2 a0 = r2[4 * c0], a1 = r2[4 * c0 + 1], a2 = r2[4 * c0 + 2], a3 = r2[4 * c0 + 3];
-    for (int c = c0; c < c1; ++c) {
-        double2 b0, b1, b2, b3;
-        const bool more = c + 1 < c1;
-        if (more) {
-            b0 = r2[4 * c + 4]; b1 = r2[4 * c + 5]; b2 = r2[4 * c + 6]; b3 = r2[4 * c + 7];
-        }
-        acc += a0.x; acc += a0.y; acc += a1.x; acc += a1.y;
-        acc += a2.x; acc += a2.y; acc += a3.x; acc += a3.y;
-        if (more) { a0 = b0; a1 = b1; a2 = b2; a3 = b3; }
+    const int g0 = 2 * c0, g1 = 2 * c1;   // 4-term groups: double2 pairs 2g, 2g + 1
+    double2 s0a = r2[2 * g0], s0b = r2[2 * g0 + 1];
+    double2 s1a = r2[2 * g0 + 2], s1b = r2[2 * g0 + 3];
+    double2 s2a = r2[2 * g0 + 4], s2b = r2[2 * g0 + 5];
+    __builtin_amdgcn_sched_barrier(0);
+    for (int g = g0;; g += 3) {
+        acc += s0a.x; acc += s0a.y; acc += s0b.x; acc += s0b.y;
+        if (g + 1 >= g1) break;
+        s0a = r2[2 * g + 6]; s0b = r2[2 * g + 7];
+        __builtin_amdgcn_sched_barrier(0);   // the reads stay issued here, ahead of use
+        acc += s1a.x; acc += s1a.y; acc += s1b.x; acc += s1b.y;
+        if (g + 2 >= g1) break;
+        s1a = r2[2 * g + 8]; s1b = r2[2 * g + 9];
+        __builtin_amdgcn_sched_barrier(0);
+        acc += s2a.x; acc += s2a.y; acc += s2b.x; acc += s2b.y;
+        if (g + 3 >= g1) break;
+        s2a = r2[2 * g + 10]; s2b = r2[2 * g + 11];
+        __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
 }
