@@ -775,9 +775,9 @@ __device__ __forceinline__ bool ch_probe(int ey, const int *tag, const double2 *
         const long long t_ = __builtin_amdgcn_s_memtime();             \
         pr[k] += t_ - tl; tl = t_;                                     \
     }
-// fold row[8*c0 .. 8*c1) into acc in order: 4-term groups, three groups of reads in flight
+// fold row[8*c0 .. 8*c1) into acc in order: 4-term groups, four groups of reads in flight
 // (a group's 4 dependent adds, 32 clk, against an LDS read latency of ~70-100 clk).  The
-// reads run up to two groups past the end unconditionally (unused; LDS reads never fault):
+// reads run up to three groups past the end unconditionally (unused; LDS reads never fault):
 // conditional reads made the compiler copy registers and drain every read at each copy.
 __device__ __forceinline__ double ch_fold(double acc, const double *row, int c0, int c1) {
     if (c0 >= c1) return acc;
@@ -786,19 +786,24 @@ __device__ __forceinline__ double ch_fold(double acc, const double *row, int c0,
     double2 s0a = r2[2 * g0], s0b = r2[2 * g0 + 1];
     double2 s1a = r2[2 * g0 + 2], s1b = r2[2 * g0 + 3];
     double2 s2a = r2[2 * g0 + 4], s2b = r2[2 * g0 + 5];
+    double2 s3a = r2[2 * g0 + 6], s3b = r2[2 * g0 + 7];
     __builtin_amdgcn_sched_barrier(0);
-    for (int g = g0;; g += 3) {
+    for (int g = g0;; g += 4) {
         acc += s0a.x; acc += s0a.y; acc += s0b.x; acc += s0b.y;
         if (g + 1 >= g1) break;
-        s0a = r2[2 * g + 6]; s0b = r2[2 * g + 7];
+        s0a = r2[2 * g + 8]; s0b = r2[2 * g + 9];
         __builtin_amdgcn_sched_barrier(0);   // the reads stay issued here, ahead of use
         acc += s1a.x; acc += s1a.y; acc += s1b.x; acc += s1b.y;
         if (g + 2 >= g1) break;
-        s1a = r2[2 * g + 8]; s1b = r2[2 * g + 9];
+        s1a = r2[2 * g + 10]; s1b = r2[2 * g + 11];
         __builtin_amdgcn_sched_barrier(0);
         acc += s2a.x; acc += s2a.y; acc += s2b.x; acc += s2b.y;
         if (g + 3 >= g1) break;
-        s2a = r2[2 * g + 10]; s2b = r2[2 * g + 11];
+        s2a = r2[2 * g + 12]; s2b = r2[2 * g + 13];
+        __builtin_amdgcn_sched_barrier(0);
+        acc += s3a.x; acc += s3a.y; acc += s3b.x; acc += s3b.y;
+        if (g + 4 >= g1) break;
+        s3a = r2[2 * g + 14]; s3b = r2[2 * g + 15];
         __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
