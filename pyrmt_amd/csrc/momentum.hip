@@ -715,12 +715,14 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     // pure-fluid tile rows for the stage kernels, on every resident row (a stage tile's
     // stress region may reach past its window; rows prep did not write only feed halo cells
     // that never reach the window's outputs)
-    unsigned char *fluid_rows = (unsigned char *)(W.acc2u + (long)w0.lo * nx);   // row w0.lo first
+    unsigned char *fluid_rows = fluid_rows_buf(W, w0.lo, nx);   // row w0.lo first
     if (!unfused && !blocked) {
-        const double thr = std::max({P->w_t, w_cut, 0.0});
+        (void)w_cut;
+        const double thr = fluid_threshold(P);
         const long nw = (long)(w0.hi - w0.lo) * tiles_x;
-        k_fluid_rows<<<grid1d(nw, 4), 256, 0, ctx->stream>>>(phi, thr, nx, tiles_x, w0.lo,
-                                                              w0.hi, fluid_rows);
+        if (!W.fluid_rows_ready)
+            k_fluid_rows<<<grid1d(nw, 4), 256, 0, ctx->stream>>>(phi, thr, nx, tiles_x, w0.lo,
+                                                                  w0.hi, fluid_rows);
         k_fluid_win<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(fluid_rows, tiles_x, w0.lo, w0.hi,
                                                                fluid_rows + nw);
         RMT_LAUNCHED();

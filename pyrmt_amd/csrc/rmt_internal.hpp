@@ -7,6 +7,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rocfft/rocfft.h>
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -498,12 +499,24 @@ struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + 
     unsigned char *solid;
     int *any_solid;
     const double *dtp;           // device dt (the fused step's k_dt output), or null: P->dt
+    // the pure-fluid row flags (k_fluid_rows' output, at fluid_rows_buf) were already written
+    // by the producer of phi (the fused step's k_phi_rebuild): momentum_rk4 skips that pass
+    bool fluid_rows_ready = false;
 };
 inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
     return MomWork{w,          w + n,      w + 2 * n,  w + 3 * n,  w + 4 * n,  w + 5 * n,
                    w + 6 * n,  w + 7 * n,  w + 8 * n,  w + 9 * n,  w + 10 * n, w + 11 * n,
                    w + 12 * n, w + 13 * n, w + 14 * n, w + 15 * n, w + 16 * n, solid, flag,
-                   nullptr};
+                   nullptr, false};
+}
+// where momentum_rk4 keeps the per-(row, 64-column tile) pure-fluid flags of rows [lo, ...)
+inline unsigned char *fluid_rows_buf(const MomWork &W, int lo, int nx) {
+    return (unsigned char *)(W.acc2u + (long)lo * nx);
+}
+// the flags' threshold: a stage tile is pure fluid where every phi > max(w_t, w_cut, 0)
+inline double fluid_threshold(const rmt_momentum_params *P) {
+    const double w_cut = P->stress_band ? P->w_t : 0.0;
+    return std::max({P->w_t, w_cut, 0.0});
 }
 int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                  const double *p, const double *X1, const double *X2, const double *phi,

@@ -258,6 +258,40 @@ __global__ void k_phi_rebuild(const double *__restrict__ X1n, const double *__re
     }
 }
 
+// k_phi_rebuild (disc, nx % 64 == 0) that also writes k_fluid_rows' pure-fluid flags: a wave
+// holds 64 cells of one row, i.e. one stage tile's columns; lanes 0-3 add the 2-column halo
+// on each side (phi recomputed from the same map, the same disc_phi) -- the flags equal
+// k_fluid_rows' on this phi, and the momentum's pass over the phi plane is saved
+__global__ void __launch_bounds__(256) k_phi_rebuild_fluid(
+    const double *__restrict__ X1n, const double *__restrict__ X2n, long n, int nx, int tiles_x,
+    double x0, double y0, double R, double *__restrict__ phi, double *__restrict__ X1,
+    double *__restrict__ X2, unsigned long long *__restrict__ nbits, double thr,
+    unsigned char *__restrict__ frows) {
+    const long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    if (c - lane >= n) return;   // wave-uniform (n is a multiple of 64)
+    const double a = X1n[c], b = X2n[c];
+    X1[c] = a; X2[c] = b;
+    const double ph = disc_phi(a, b, x0, y0, R);
+    phi[c] = ph;
+    if (nbits) {
+        const unsigned long long w = __ballot(ph < 0);
+        if (lane == 0) nbits[c >> 6] = w;
+    }
+    const long j = c / nx;
+    const int i = (int)(c - j * nx), tx = i >> 6;
+    bool ok = ph > thr;   // (k_fluid_rows: NaN phi is not fluid)
+    if (lane < 4) {
+        const int e = lane < 2 ? 64 * tx - 2 + lane : 64 * tx + 62 + lane;
+        if (e >= 0 && e < nx) {
+            const long ce = j * nx + e;
+            ok = ok && disc_phi(X1n[ce], X2n[ce], x0, y0, R) > thr;
+        }
+    }
+    const unsigned long long all = __ballot(ok);
+    if (lane == 0) frows[j * tiles_x + tx] = all == ~0ull;
+}
+
 // k_phi_rebuild on the listed tiles (after the chain: the targets all lie inside them)
 __global__ void __launch_bounds__(256) k_phi_tiles(const double *__restrict__ X1n,
                                                    const double *__restrict__ X2n, int ny, int nx,
@@ -708,6 +742,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     // (RMT_EARLY_TRANSPOSE, default on)
     static const bool early_t_env = !(getenv("RMT_EARLY_TRANSPOSE") && !atoi(getenv("RMT_EARLY_TRANSPOSE")));
     bool early_t = false;
+    // k_phi_rebuild writes the momentum's pure-fluid flags (RMT_FUSED_FLUID, default on)
+    static const bool fluid_env = !(getenv("RMT_FUSED_FLUID") && !atoi(getenv("RMT_FUSED_FLUID")));
     bool geo_ready = false;
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end)) break;
@@ -840,12 +876,21 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                         S->rimw);
                     RMT_LAUNCHED();
                 }
-                k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R,
-                                                      S->phi, S->X1, S->X2, nb);
+                MomWork Wf = W;
+                if (fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 && MOM_TX == 64) {
+                    // phi and the stage kernels' pure-fluid flags in one pass
+                    k_phi_rebuild_fluid<<<g, 256, 0, S->st2>>>(
+                        S->X1n, S->X2n, n, nx, (nx + 63) / 64, P.x0, P.y0, P.R, S->phi, S->X1,
+                        S->X2, nb, fluid_threshold(&M), fluid_rows_buf(W, 0, nx));
+                    Wf.fluid_rows_ready = true;
+                } else {
+                    k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0,
+                                                          P.R, S->phi, S->X1, S->X2, nb);
+                }
                 RMT_LAUNCHED();
                 ctx->stream = S->st2;
                 int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi,
-                                      S->us, S->vs, S->sxx, S->sxy, S->syy, S->J, W);
+                                      S->us, S->vs, S->sxx, S->sxy, S->syy, S->J, Wf);
                 if (ms == RMT_OK) ms = hipEventRecord(S->e_mom, S->st2) ? RMT_EDEVICE : RMT_OK;
                 // and the projection's rows from the speculative u*, v* (the fix-up tiles the
                 // main stream re-runs meanwhile only feed rows it redoes afterwards)

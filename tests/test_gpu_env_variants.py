@@ -11,6 +11,7 @@ projection (LDS DCT plan: 255 = 3 5 17) and with it the early transpose are on.
   RMT_SIM_SYNC=1          dt read back on the host every step
   RMT_CH_PARTS=1          the chain in one workgroup
   RMT_CH_VARIANT=35       the chain's residue fast fold (sim.hip / extrap_chain.hip ch_fast)
+  RMT_FUSED_FLUID=0       the momentum's pure-fluid flags from their own pass over phi
 """
 import os
 import subprocess
@@ -54,7 +55,7 @@ def default_run(tmp_path_factory, gpu):
 @pytest.mark.parametrize("env", [
     {"RMT_SIM_HIPRIO": "0"}, {"RMT_EARLY_TRANSPOSE": "0"}, {"RMT_EARLY_GEOMETRY": "0"},
     {"RMT_SIDE_TAIL": "0"}, {"RMT_NO_OVERLAP": "1"}, {"RMT_SIM_SYNC": "1"},
-    {"RMT_CH_PARTS": "1"}, {"RMT_CH_VARIANT": "35"},
+    {"RMT_CH_PARTS": "1"}, {"RMT_CH_VARIANT": "35"}, {"RMT_FUSED_FLUID": "0"},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(tmp_path, default_run, env):
     got = _run(tmp_path, "variant", env)
