@@ -110,6 +110,11 @@ int rmt_advect_sl_cubic_rk4(rmt_ctx *ctx, const double *q, const double *a, cons
                             const double *X, const double *Y, double dt, double dx, double dy,
                             double *out);
 int rmt_all_finite2(rmt_ctx *ctx, const double *a, const double *b, int *finite);
+/* Test hook (no reference counterpart): q = divk(x, d), the correctly rounded division by a
+ * precomputed divisor that the stencil kernels use for x / (2h), x / (6h), xq / dx, ...
+ * (pyrmt_amd/csrc/divk.hpp), and q_ieee = x / d, both on the device (device pointers). */
+int rmt_selftest_divk(rmt_ctx *ctx, const double *x, long n, double d, double *q,
+                      double *q_ieee);
 
 /* functions.py:48-163 extrapolate_reference_map: exact raster-order (Gauss-Seidel)
  * semantics of the reference; outputs may alias the inputs.  Blocks until the result is
@@ -124,6 +129,15 @@ int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, const double *
  * abort status is raised (exercises the callers' error paths).  rmt_extrap_last_path
  * (blocks) reports what the last call on ctx ran: 0 chain, 1 sweep. */
 int rmt_extrap_set_mode(int mode);
+/* Parallel extrapolation (no reference counterpart; default off, or RMT_EXTRAP_PARALLEL=1):
+ * every fit of functions.py:95-161 -- the same targets, acceptance, weights and raster-order
+ * known sets -- evaluated as the weighted least-squares plane in offsets from the target and
+ * the layer solved as one sparse triangular system by segments (extrap_par.hip), instead of
+ * the exact raster-order chain.  Not bit-exact: each fit differs from the reference by the
+ * reference's own rounding of Cramer's rule on absolute coordinates (~1e-7 at N = 4096,
+ * the size of 1-ulp weight noise).  Process-wide; applies to the
+ * extrapolations started after the call. */
+int rmt_extrap_set_parallel(int on);
 int rmt_extrap_last_path(rmt_ctx *ctx, int *path);
 
 /* functions.py:1366-1367 with benchmarks/common.py:55-57: phi = |xi - (x0,y0)| - R */

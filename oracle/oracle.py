@@ -61,6 +61,7 @@ def _load():
         "rmto_pairwise_sum": (D, [P, L]),
         "rmto_bicubic": (None, [P, P, P, L, D, D, I, I, P]),
         "rmto_set_pow_mode": (None, [I]),
+        "rmto_set_ex_mode": (None, [I]),
         "rmto_advect_sl_cubic_rk4": (None, [P, P, P, P, P, I, I, D, D, D, P]),
         "rmto_central_rhs": (None, [P, P, P, I, I, D, D, P, D, I, P]),
     }
@@ -83,6 +84,12 @@ def set_all_cores(on):
     """All-cores mode: OpenMP also on the per-cell loops the reference runs serially (same
     results bit for bit; the extrapolation sweep stays serial).  Off = faithful threading."""
     _lib.rmto_set_all_cores(int(bool(on)))
+
+
+def set_ex_mode(m):
+    """Extrapolation fit arithmetic: 0 the reference's; 1 weights nudged +1 ulp (noise-floor
+    experiment); 2 the centred restatement librmt's parallel mode computes (rmt_oracle.c)."""
+    _lib.rmto_set_ex_mode(int(m))
 
 
 def _c(a):

@@ -75,12 +75,14 @@ SIGNATURES = {
     "rmt_weno5_rhs": (_I, [_P, _P, _P, _P, _D, _D, _P, _D, _P]),
     "rmt_advect_weno5_rk3": (_I, [_P, _P, _P, _P, _D, _D, _D, _P, _D, _P]),
     "rmt_all_finite2": (_I, [_P, _P, _P, ctypes.POINTER(_I)]),
+    "rmt_selftest_divk": (_I, [_P, _P, _L, _D, _P, _P]),
     "rmt_central_rhs": (_I, [_P, _P, _P, _P, _D, _D, _P, _D, _I, _P]),
     "rmt_advect_central_rk3": (_I, [_P, _P, _P, _P, _D, _D, _D, _P, _D, _I, _P]),
     "rmt_bicubic_interpolate": (_I, [_P, _P, _P, _P, _L, _D, _D, _P]),
     "rmt_advect_sl_cubic_rk4": (_I, [_P, _P, _P, _P, _P, _P, _D, _D, _D, _P]),
     "rmt_extrapolate_reference_map": (_I, [_P, _P, _P, _P, _D, _D, _I, _P, _P]),
     "rmt_extrap_set_mode": (_I, [_I]),
+    "rmt_extrap_set_parallel": (_I, [_I]),
     "rmt_momentum_set_mode": (_I, [_I]),
     "rmt_extrap_last_path": (_I, [_P, ctypes.POINTER(_I)]),
     "rmt_rebuild_phi_disc": (_I, [_P, _P, _P, _D, _D, _D, _P]),

@@ -620,7 +620,7 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A, long long *gpr
 static int g_ex_mode = 0;   // rmt_extrap_set_mode
 
 // byte workspace: both paths' bit planes, the chain path's tables and its record arena
-ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes) {
+ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bool px) {
     const int ML = std::max(max_layers, 1), W = (nx + 63) / 64;
     const long plane = (long)ny * W;
     const long interior = (long)std::max(ny - 2, 0) * std::max(nx - 2, 0);
@@ -667,6 +667,21 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes) {
     w.arena = take(w.arena_bytes);
     w.maxt = maxt;
     w.plane = plane;
+    w.maxseg = maxt / PX_K + EX_MAXL + 2;
+    if (px) {
+        w.pns = (int *)take(maxt * 4);
+        w.pnd = (int *)take(maxt * 4);
+        w.pkey = (int *)take(maxt * PX_S * 4);
+        w.pbeta = (double *)take(maxt * PX_S * 8);
+        w.pval = (double2 *)take(maxt * 16);
+        w.pc = (double2 *)take(maxt * 16);
+        w.live = (unsigned char *)take(maxt);
+        w.shdr = (int *)take(w.maxseg * PX_H * 4);
+        w.sF = (int *)take(w.maxseg * PX_F * 4);
+        w.sMT = (double *)take(w.maxseg * PX_F * PX_K * 8);
+        w.sNT = (double *)take(w.maxseg * PX_K * PX_K * 8);
+        w.sd = (double2 *)take(w.maxseg * PX_K * 16);
+    }
     if (bytes) *bytes = o;
     return w;
 }
@@ -683,9 +698,9 @@ int extrap_none_rows(rmt_ctx *ctx, const u64 *kbits, int ny, int nx, double dx, 
     return RMT_OK;
 }
 
-size_t extrap_workspace(int ny, int nx, int max_layers) {
+size_t extrap_workspace(int ny, int nx, int max_layers, bool px) {
     size_t b = 0;
-    extrap_layout(nullptr, ny, nx, max_layers, &b);
+    extrap_layout(nullptr, ny, nx, max_layers, &b, px);
     return b;
 }
 
@@ -701,12 +716,15 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
     const int W = (nx + 63) / 64;
     RMT_CHECK(max_layers > 0 && ny >= 3 && nx >= 3 && ny < (1 << 20) && nx < (1 << 30),
               RMT_EINVAL, "extrapolation grid size");
-    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, max_layers)));
-    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
     const int force = g_ex_mode;
     const bool chain = force != 1 && extrap_chain_supported(ny, nx, max_layers);
+    // the parallel mode replaces the chain (never the diagnostic sweep modes)
+    const bool par = chain && force == 0 && extrap_par_enabled();
+    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, max_layers, par)));
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, par);
     ctx->ex_layers = max_layers;
     ctx->ex_chain = chain;
+    ctx->ex_par = par;
     const int copy = (X1o != X1) || (X2o != X2);
     if (kin && !copy)
         k_ex_bits_w<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(
@@ -729,7 +747,12 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
                                                            ws.ctl, 0, ny);
         k_ex_none_fin<<<1, 1, 0, ctx->stream>>>(ws.ctl);
         RMT_LAUNCHED();
-        RMT_TRY(extrap_chain_prep(ctx, ws, X1o, X2o, dx, dy, max_layers));
+        if (par) {
+            RMT_TRY(extrap_chain_prep_px(ctx, ws, dx, dy, max_layers));
+            RMT_TRY(extrap_par_geometry(ctx, ws, dx, dy, max_layers));
+        } else {
+            RMT_TRY(extrap_chain_prep(ctx, ws, X1o, X2o, dx, dy, max_layers));
+        }
     }
     const int *ctl = chain ? ws.ctl : nullptr;
     k_ex_dilate<<<grid1d((long)ny * W, 256), 256, 0, ctx->stream>>>(
@@ -744,12 +767,13 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
                   int *dev_status) {
     const int ny = ctx->ny, nx = ctx->nx;
     const int W = (nx + 63) / 64;
-    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
+    const bool par = ctx->ex_par;
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, par);
     const int force = g_ex_mode;
-    const bool chain = ctx->ex_chain;
-    const int *ctl = chain ? ws.ctl : nullptr;
+    const bool chain = ctx->ex_chain && !par;
+    const int *ctl = ctx->ex_chain ? ws.ctl : nullptr;
     if (chain) RMT_TRY(extrap_chain_values(ctx, ws, X1o, X2o, dx, dy, max_layers));
-    if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
+    if (ctx->prof && !chain && !par) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
     ExSweep A{X1o, X2o, ws.kbits, ws.cbits, ws.Kold, ws.rowcand, ws.jrange, ny, nx, W,
               max_layers, dx, dy, ws.status, ctl};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
@@ -779,9 +803,14 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
                 hp[3] / 1e6, hp[4] / 1e6, hp[5] / 1e6);
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1); (void)hipFree(gp);
     }
-    if (ctx->prof && !chain) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
+    if (ctx->prof && !chain && !par) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
     // the chain after the sweep: both read the fallback flag the chain prep settled
     if (chain) RMT_TRY(extrap_chain_run(ctx, ws, X1o, X2o, max_layers));
+    if (par) {
+        if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
+        RMT_TRY(extrap_par_values(ctx, ws, X1o, X2o, max_layers));
+        if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
+    }
     if (force == 3) {   // diagnostic: report an abort (tests of the callers' error paths)
         const int one = 1;
         RMT_HIP(hipMemcpyAsync(ws.status + 1, &one, sizeof(int), hipMemcpyHostToDevice,

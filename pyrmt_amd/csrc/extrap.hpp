@@ -25,6 +25,10 @@ enum { EXC_FALLBACK = 0, EXC_ABORT = 1, EXC_FILLED = 2, EXC_ARENA = 4, EXC_REJ =
        EXC_CMIN = EXC_ANY + 2, EXC_CMAX = EXC_ANY + 3, EXC_NPART = EXC_ANY + 4,
        EXC_WORDS = 8 + 2 * EX_MAXL + 16 };
 constexpr int CH_MAXP = 4;          // chain parts (workgroups), split by target column
+constexpr int PX_K = 64;            // parallel mode: fits per segment
+constexpr int PX_F = 64;            // frontier capacity (more: the segment is solved serially)
+constexpr int PX_S = 81;            // window sources per fit
+constexpr int PX_H = 8;             // segment header ints
 
 struct ExWs {
     // band detection (both paths) and the fallback sweep
@@ -50,6 +54,20 @@ struct ExWs {
                                               // (X1, X2) (k_ex_vals)
     int *rej;                                 // ML * EX_MAXREJ
     int *ctl;                                 // EXC_WORDS
+    // parallel mode (extrap_par.hip; laid out after everything else, only when requested):
+    // per fit id the window sources in window order -- first the static ones (solid cells:
+    // key = cell; earlier layers' fits: key = -(id + 1)), then the same-layer fits -- with
+    // their coefficients beta; the fit values; per segment of PX_K consecutive ids of a layer
+    // its frontier and its affine response (M^T, N^T) and the constants d = N c
+    int *pns, *pnd;                           // MAXT each: static / same-layer source counts
+    int *pkey;                                // MAXT * PX_S
+    double *pbeta;                            // MAXT * PX_S
+    double2 *pval, *pc;                       // MAXT each: fit values, static sums c
+    unsigned char *live;                      // MAXT: read by a later segment's frontier
+    int *shdr, *sF;                           // maxseg * PX_H, maxseg * PX_F
+    double *sMT, *sNT;                        // maxseg * PX_F * PX_K, maxseg * PX_K * PX_K
+    double2 *sd;                              // maxseg * PX_K
+    long maxseg;
     char *arena;
     long long arena_bytes;
     int slots;                                // 1: record of fit id at id * CH_MAXREC
@@ -57,7 +75,9 @@ struct ExWs {
     long plane;                               // ny * W
 };
 
-ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes);
+// px: also lay out the parallel mode's arrays (after everything else: the other offsets do
+// not depend on it)
+ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bool px = false);
 // chain path: queue the kernels; they check ctl[EXC_FALLBACK] themselves
 int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
                       double dx, double dy, int ML);
@@ -66,5 +86,12 @@ int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
 int ch_variant();   // RMT_CH_VARIANT (extrap_chain.hip)
 int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o, int ML);
 bool extrap_chain_supported(int ny, int nx, int ML);
+// chain prep without the chain-order passes and with no records (the parallel mode only
+// needs targets and acceptance)
+int extrap_chain_prep_px(rmt_ctx *ctx, const ExWs &ws, double dx, double dy, int ML);
+// the parallel mode (extrap_par.hip): geometry after the acceptance passes, values after
+// the map is advected
+int extrap_par_geometry(rmt_ctx *ctx, const ExWs &ws, double dx, double dy, int ML);
+int extrap_par_values(rmt_ctx *ctx, const ExWs &ws, double *X1o, double *X2o, int ML);
 
 }  // namespace rmt

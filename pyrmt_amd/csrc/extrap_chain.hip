@@ -155,6 +155,7 @@ struct ExGeoArgs {
     const double *X1, *X2;   // static values (phi < 0 cells are never written)
     int ny, nx, W, L;
     double dx, dy, r2;
+    int norec;               // acceptance only, no record (the parallel mode)
 };
 
 // One wave fits target `id` of layer A.L.  Same-layer acceptance of earlier targets is read
@@ -250,6 +251,7 @@ __device__ bool ex_geom(const ExGeoArgs &A, int id, double *tb, const u64 *tab, 
         if (lane == 0) ws.recoff[id] = -1;
         return false;
     }
+    if (A.norec) return true;
     // record: compact the included cells from qf on (static: 6 products; dynamic: 3 coefs)
     const u64 lt = (1ull << lane) - 1;
     const u64 tl = il & ~((qf >= 64) ? ~0ull : ((1ull << qf) - 1));
@@ -1208,7 +1210,7 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     hipStream_t st = ctx->stream;
     const unsigned rows = grid1d(ny, 4);
     double r = 4 * std::sqrt(dx * dx + dy * dy);
-    ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r};
+    ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r, 0};
     const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
     for (int L = 0; L < ML; ++L) {
         A.L = L;
@@ -1232,12 +1234,32 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     return RMT_OK;
 }
 
+// the parallel mode's half of the prep: targets and final acceptance per layer, no records
+int extrap_chain_prep_px(rmt_ctx *ctx, const ExWs &ws, double dx, double dy, int ML) {
+    const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
+    hipStream_t st = ctx->stream;
+    const unsigned rows = grid1d(ny, 4);
+    double r = 4 * std::sqrt(dx * dx + dy * dy);
+    ExGeoArgs A{ws, nullptr, nullptr, ny, nx, W, 0, dx, dy, r * r, 1};
+    const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
+    for (int L = 0; L < ML; ++L) {
+        A.L = L;
+        k_tg_rows<<<rows, 256, 0, st>>>(ws, ny, nx, W, L);
+        k_tg_scan<<<1, 1024, 0, st>>>(ws, ny, L);
+        k_tg_emit<<<rows, 256, 0, st>>>(ws, ny, nx, W, L);
+        k_ex_geom<<<gblocks, 256, 0, st>>>(A);
+        k_ex_fix<<<1, FIXW * 64, 0, st>>>(A);
+        RMT_LAUNCHED();
+    }
+    return RMT_OK;
+}
+
 // the value half of the records (after the map is advected; k_ex_vals)
 int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
                         double dx, double dy, int ML) {
     const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
     const double r = 4 * std::sqrt(dx * dx + dy * dy);
-    ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r};
+    ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r, 0};
     const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
     k_ex_vals<<<gblocks, 256, 0, ctx->stream>>>(A, ML, ctx->ex_pred1 ? ctx->ex_pred1 : X1o,
                                                 ctx->ex_pred2 ? ctx->ex_pred2 : X2o);

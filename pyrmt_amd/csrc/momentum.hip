@@ -167,19 +167,40 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 // two numerators are both formed and the one its velocity sign picks is divided (one
 // division, no divergent branch) -- each the expression of rmt_internal.hpp, operand for operand
 template <bool IN>
-__device__ __forceinline__ double g2(const double *f, long s, int k, int n, double h2) {
-    if constexpr (IN) return (f[s] - f[-s]) / h2;
-    else return grad2(f, s, k, n, h2);
+__device__ __forceinline__ double g2(const double *f, long s, int k, int n, const DivK &K2) {
+    if constexpr (IN) return divk(f[s] - f[-s], K2);
+    else return grad2k(f, s, k, n, K2);
 }
 template <bool IN>
-__device__ __forceinline__ double u3(const double *f, long s, int k, int n, double vel, double h) {
+__device__ __forceinline__ double u3(const double *f, long s, int k, int n, double vel,
+                                     const DivK &K6, const DivK &K1) {
     if constexpr (IN) {
         const double a = 2 * f[s] + 3 * f[0] - 6 * f[-s] + f[-2 * s];
         const double b = -f[2 * s] + 6 * f[s] - 3 * f[0] - 2 * f[-s];
-        return (vel > 0 ? a : b) / (6 * h);
+        return divk(vel > 0 ? a : b, K6);
     } else {
-        return upwind3(f, s, k, n, vel, h);
+        return upwind3k(f, s, k, n, vel, K6, K1);
     }
+}
+
+// The stage's divisors (divk.hpp): 2h, 6h, h per axis, and rho + 1e-12 when it is one constant:
+// rho_s == rho_f == 2^k makes (1 - H) rho_s + H rho_f == rho exactly for every H in [0, 1]
+// ((1 - H) + H rounds to 1; scaling by 2^k is exact), so den = fl(rho + 1e-12) everywhere
+// (a NaN H still yields NaN: the numerator is replaced by H).
+struct MomDiv {
+    DivK x2, y2, x6, y6, x1, y1, den;
+    int den_const;
+};
+static MomDiv mom_div(double dx, double dy, double rho_s, double rho_f) {
+    MomDiv m;
+    m.x2 = divk_make(2 * dx); m.y2 = divk_make(2 * dy);
+    m.x6 = divk_make(6 * dx); m.y6 = divk_make(6 * dy);
+    m.x1 = divk_make(dx); m.y1 = divk_make(dy);
+    int e;
+    m.den_const = rho_s == rho_f && rho_s > 0.0 && std::isnormal(rho_s) &&
+                  std::frexp(rho_s, &e) == 0.5;
+    m.den = divk_make(rho_s + 1e-12);
+    return m;
 }
 
 // one stage tile (k_mom_stage); IN: an interior tile (see the kernel)
@@ -196,9 +217,8 @@ __device__ __forceinline__ void ms_tile(
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
-    const unsigned char *__restrict__ fluid_tiles, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
+    const unsigned char *__restrict__ fluid_tiles, const MomDiv &K, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
     double (&gx)[MS_GY][MS_GX], double (&gm)[MS_GY][MS_GX], double (&gy)[MS_GY][MS_GX]) {
-    const double h2x = 2 * dx, h2y = 2 * dy;
     // pure-fluid tile (k_fluid_rows / k_fluid_win): every cell the blended stress is formed
     // on has phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not
     // solid exactly -- those constants replace the loads of sxx, sxy, syy, H and solid below
@@ -284,8 +304,8 @@ __device__ __forceinline__ void ms_tile(
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
             if (ok2[it]) {
                 const double *pu = &su[ry + 1][rx + 1], *pv = &sv[ry + 1][rx + 1];
-                const double dudx = g2<IN>(pu, 1, i, nx, h2x), dvdy = g2<IN>(pv, MS_UX, j, ny, h2y);
-                const double dudy = g2<IN>(pu, MS_UX, j, ny, h2y), dvdx = g2<IN>(pv, 1, i, nx, h2x);
+                const double dudx = g2<IN>(pu, 1, i, nx, K.x2), dvdy = g2<IN>(pv, MS_UX, j, ny, K.y2);
+                const double dudy = g2<IN>(pu, MS_UX, j, ny, K.y2), dvdx = g2<IN>(pv, 1, i, nx, K.x2);
                 double e1 = ex[it], e2 = ey[it], e3 = exy[it];
                 if (visc && sol[it]) {
                     e1 = e1 + eta_s * dudx;
@@ -322,31 +342,40 @@ __device__ __forceinline__ void ms_tile(
             const int j = j0 + ry, i = i0 + rx;
             if (!ok[it]) continue;
             const long c = (long)j * nx + i;
-            const double divx = g2<IN>(&gx[ry + 2][rx + 2], 1, i, nx, h2x) +
-                                g2<IN>(&gm[ry + 2][rx + 2], MS_GX, j, ny, h2y);
-            const double divy = g2<IN>(&gm[ry + 2][rx + 2], 1, i, nx, h2x) +
-                                g2<IN>(&gy[ry + 2][rx + 2], MS_GX, j, ny, h2y);
+            const double divx = g2<IN>(&gx[ry + 2][rx + 2], 1, i, nx, K.x2) +
+                                g2<IN>(&gm[ry + 2][rx + 2], MS_GX, j, ny, K.y2);
+            const double divy = g2<IN>(&gm[ry + 2][rx + 2], 1, i, nx, K.x2) +
+                                g2<IN>(&gy[ry + 2][rx + 2], MS_GX, j, ny, K.y2);
             const double *pu = &su[ry + 3][rx + 3], *pv = &sv[ry + 3][rx + 3];
             const double uc = *pu, vc = *pv;
-            const double uadv = -uc * u3<IN>(pu, 1, i, nx, uc, dx) - vc * u3<IN>(pu, MS_UX, j, ny, vc, dy);
-            const double vadv = -uc * u3<IN>(pv, 1, i, nx, uc, dx) - vc * u3<IN>(pv, MS_UX, j, ny, vc, dy);
+            const double uadv = -uc * u3<IN>(pu, 1, i, nx, uc, K.x6, K.x1) -
+                                vc * u3<IN>(pu, MS_UX, j, ny, vc, K.y6, K.y1);
+            const double vadv = -uc * u3<IN>(pv, 1, i, nx, uc, K.x6, K.x1) -
+                                vc * u3<IN>(pv, MS_UX, j, ny, vc, K.y6, K.y1);
             // grad2 of p with the operands loaded above (same expressions as grad2)
             double dpx, dpy;
             if (IN) {
-                dpx = (pxp[it] - pxm[it]) / h2x;
-                dpy = (pyp[it] - pym[it]) / h2y;
+                dpx = divk(pxp[it] - pxm[it], K.x2);
+                dpy = divk(pyp[it] - pym[it], K.y2);
             } else {
-            if (i == 0) dpx = (-3 * pc[it] + 4 * pxp[it] - p[c + 2]) / h2x;
-            else if (i == nx - 1) dpx = (3 * pc[it] - 4 * pxp[it] + p[c - 2]) / h2x;
-            else dpx = (pxp[it] - pxm[it]) / h2x;
-            if (j == 0) dpy = (-3 * pc[it] + 4 * pyp[it] - p[c + 2L * nx]) / h2y;
-            else if (j == ny - 1) dpy = (3 * pc[it] - 4 * pyp[it] + p[c - 2L * nx]) / h2y;
-            else dpy = (pyp[it] - pym[it]) / h2y;
+            if (i == 0) dpx = divk(-3 * pc[it] + 4 * pxp[it] - p[c + 2], K.x2);
+            else if (i == nx - 1) dpx = divk(3 * pc[it] - 4 * pxp[it] + p[c - 2], K.x2);
+            else dpx = divk(pxp[it] - pxm[it], K.x2);
+            if (j == 0) dpy = divk(-3 * pc[it] + 4 * pyp[it] - p[c + 2L * nx], K.y2);
+            else if (j == ny - 1) dpy = divk(3 * pc[it] - 4 * pyp[it] + p[c - 2L * nx], K.y2);
+            else dpy = divk(pyp[it] - pym[it], K.y2);
             }
             const double h = hh[it];
-            const double den = ((1 - h) * rho_s + h * rho_f) + 1e-12;
-            const double k1 = uadv + (divx + 0.0 - dpx) / den;
-            const double k2 = vadv + (divy + 0.0 - dpy) / den;
+            double k1, k2;
+            if (K.den_const) {   // uniform: (1 - h) rho + h rho == rho (MomDiv)
+                const double nu = divx + 0.0 - dpx, nv = divy + 0.0 - dpy;
+                k1 = uadv + divk(h == h ? nu : h, K.den);
+                k2 = vadv + divk(h == h ? nv : h, K.den);
+            } else {
+                const double den = ((1 - h) * rho_s + h * rho_f) + 1e-12;
+                k1 = uadv + (divx + 0.0 - dpx) / den;
+                k2 = vadv + (divy + 0.0 - dpy) / den;
+            }
             if (stage < 3) {
                 ku[c] = k1; kv[c] = k2;
             } else {
@@ -369,7 +398,7 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
-    const unsigned char *__restrict__ fluid_tiles) {
+    const unsigned char *__restrict__ fluid_tiles, MomDiv K) {
     __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
     if (dtp) {   // the same roundings as mom_stage's host constants
         const double dt = *dtp;
@@ -386,9 +415,9 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 && j0 - 3 >= max(rw.lo, 2) &&
                           j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
     if (interior)
-        ms_tile<true>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, i0, j0, su, sv, gx, gm, gy);
+        ms_tile<true>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy);
     else
-        ms_tile<false>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, i0, j0, su, sv, gx, gm, gy);
+        ms_tile<false>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy);
 }
 
 // per row j of [jlo, jhi) (out row j - jlo) and 64-column tile tx: all of phi[j][64 tx - 2 .. 64 tx + 66) (the
@@ -443,7 +472,7 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
         P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx,
         tiles_x, ntiles, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, W.k1u, W.k1v,
         nullptr, nullptr, u_new, v_new, ws, tlist, tcount, W.dtp, olo, ohi, W.k2u, W.k2v,
-        fluid_rows);
+        fluid_rows, mom_div(P->dx, P->dy, P->rho_s, P->rho_f));
     RMT_LAUNCHED();
     return RMT_OK;
 }

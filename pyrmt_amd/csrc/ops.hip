@@ -373,10 +373,14 @@ __global__ void k_apply_bc(int kind, double lid, double *u, double *v, int ny, i
 static inline dim3 rows_grid(int nx, int jb, int je) { return dim3((nx + 255) / 256, je - jb); }
 // rho > 0: the projection's rhs = (rho * divU) / dt (functions.py:1331, the same two
 // roundings as the separate scale and divide passes)
+struct RcDiv { DivK x2, y2, x1, y1; };   // 2dx, 2dy, dx, dy (divk.hpp)
+static RcDiv rc_div(double dx, double dy) {
+    return RcDiv{divk_make(2.0 * dx), divk_make(2.0 * dy), divk_make(dx), divk_make(dy)};
+}
 __device__ __forceinline__ void div_rc_cell(const double *__restrict__ a,
                                             const double *__restrict__ b,
                                             const double *__restrict__ p, int ny, int nx,
-                                            double d_f, double dx, double dy,
+                                            double d_f, const RcDiv &K,
                                             double *__restrict__ divU, double rho, double dt,
                                             int j, int i) {
     const long c = (long)j * nx + i;
@@ -384,21 +388,20 @@ __device__ __forceinline__ void div_rc_cell(const double *__restrict__ a,
         divU[c] = rho > 0 ? (rho * 0.0) / dt : 0.0;
         return;
     }
-    const double h2x = 2.0 * dx, h2y = 2.0 * dy;
-    double gxl = grad2(p + c - 1, 1, i - 1, nx, h2x), gxc = grad2(p + c, 1, i, nx, h2x),
-           gxr = grad2(p + c + 1, 1, i + 1, nx, h2x);
-    double gyd = grad2(p + c - nx, nx, j - 1, ny, h2y), gyc = grad2(p + c, nx, j, ny, h2y),
-           gyu = grad2(p + c + nx, nx, j + 1, ny, h2y);
-    double ue = 0.5 * (a[c] + a[c + 1]) - d_f * ((p[c + 1] - p[c]) / dx - 0.5 * (gxc + gxr));
-    double uw = 0.5 * (a[c - 1] + a[c]) - d_f * ((p[c] - p[c - 1]) / dx - 0.5 * (gxl + gxc));
-    double vn = 0.5 * (b[c] + b[c + nx]) - d_f * ((p[c + nx] - p[c]) / dy - 0.5 * (gyc + gyu));
-    double vs = 0.5 * (b[c - nx] + b[c]) - d_f * ((p[c] - p[c - nx]) / dy - 0.5 * (gyd + gyc));
-    const double d = (ue - uw) / dx + (vn - vs) / dy;
+    double gxl = grad2k(p + c - 1, 1, i - 1, nx, K.x2), gxc = grad2k(p + c, 1, i, nx, K.x2),
+           gxr = grad2k(p + c + 1, 1, i + 1, nx, K.x2);
+    double gyd = grad2k(p + c - nx, nx, j - 1, ny, K.y2), gyc = grad2k(p + c, nx, j, ny, K.y2),
+           gyu = grad2k(p + c + nx, nx, j + 1, ny, K.y2);
+    double ue = 0.5 * (a[c] + a[c + 1]) - d_f * (divk(p[c + 1] - p[c], K.x1) - 0.5 * (gxc + gxr));
+    double uw = 0.5 * (a[c - 1] + a[c]) - d_f * (divk(p[c] - p[c - 1], K.x1) - 0.5 * (gxl + gxc));
+    double vn = 0.5 * (b[c] + b[c + nx]) - d_f * (divk(p[c + nx] - p[c], K.y1) - 0.5 * (gyc + gyu));
+    double vs = 0.5 * (b[c - nx] + b[c]) - d_f * (divk(p[c] - p[c - nx], K.y1) - 0.5 * (gyd + gyc));
+    const double d = divk(ue - uw, K.x1) + divk(vn - vs, K.y1);
     divU[c] = rho > 0 ? (rho * d) / dt : d;
 }
 __global__ void k_divergence_rc(const double *__restrict__ a, const double *__restrict__ b,
                                 const double *__restrict__ p, int ny, int nx, double d_f,
-                                double dx, double dy, double *__restrict__ divU, int jb, int je,
+                                RcDiv K, double *__restrict__ divU, int jb, int je,
                                 double rho = 0.0, double dt = 1.0,
                                 const double *__restrict__ dtp = nullptr,
                                 const unsigned char *__restrict__ rowmark = nullptr) {
@@ -407,14 +410,14 @@ __global__ void k_divergence_rc(const double *__restrict__ a, const double *__re
     // Grid: rows_grid (one block row per grid row, no per-cell division).
     const int j = jb + (int)blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nx || j >= je) return;
-    div_rc_cell(a, b, p, ny, nx, d_f, dx, dy, divU, rho, dt, j, i);
+    div_rc_cell(a, b, p, ny, nx, d_f, K, divU, rho, dt, j, i);
 }
 // The rhs on the listed MOM_TX x MOM_TY tiles grown by one cell (the cells whose stencil
 // reads a u*, v* the momentum fix-up rewrote); one block per tile.  Overlapping grown tiles
 // write the same value twice.
 __global__ void __launch_bounds__(256) k_divergence_tiles(
     const double *__restrict__ a, const double *__restrict__ b, const double *__restrict__ p,
-    int ny, int nx, double dx, double dy, double *__restrict__ divU, double rho, double dt,
+    int ny, int nx, RcDiv K, double *__restrict__ divU, double rho, double dt,
     const double *__restrict__ dtp, const int *__restrict__ tiles,
     const int *__restrict__ count, int tiles_x) {
     if ((int)blockIdx.x >= *count) return;
@@ -426,7 +429,7 @@ __global__ void __launch_bounds__(256) k_divergence_tiles(
     for (int e = threadIdx.x; e < TW * TH; e += blockDim.x) {
         const int j = j0 + e / TW, i = i0 + e % TW;
         if (j >= 0 && j < ny && i >= 0 && i < nx)
-            div_rc_cell(a, b, p, ny, nx, d_f, dx, dy, divU, rho, dt, j, i);
+            div_rc_cell(a, b, p, ny, nx, d_f, K, divU, rho, dt, j, i);
     }
 }
 __global__ void k_divergence_central(const double *__restrict__ a, const double *__restrict__ b,
@@ -454,16 +457,17 @@ __global__ void k_pressure_gradient(const double *__restrict__ p, int ny, int nx
 // pc - m is the mean-free correction (m: the solve's mean, subtracted here as pc is read)
 __device__ __forceinline__ double corrected(const double *__restrict__ s,
                                             const double *__restrict__ pc, long c, int ny, int nx,
-                                            double dx, double dy, double dt_rho, int comp, double m) {
+                                            const DivK &Kx2, const DivK &Ky2, double dt_rho,
+                                            int comp, double m) {
     int j = (int)(c / nx), i = (int)(c % nx);
     double gx, gy;
-    pgrad_cell(pc, c, j, i, ny, nx, dx, dy, gx, gy, m);
+    pgrad_cellk(pc, c, j, i, ny, nx, Kx2, Ky2, gx, gy, m);
     return s[c] - dt_rho * (comp == 0 ? gx : gy);
 }
 // root (nullable): the row-tree sum of pc (dct_solve's dev_root), mean = root / count
 __global__ void k_project_correct(const double *__restrict__ a_s, const double *__restrict__ b_s,
                                   const double *__restrict__ pc, const double *__restrict__ p_prev,
-                                  int ny, int nx, double dx, double dy, double dt_rho, int bc,
+                                  int ny, int nx, DivK Kx2, DivK Ky2, double dt_rho, int bc,
                                   double lid, double *__restrict__ a, double *__restrict__ b,
                                   double *__restrict__ p, int jb, int je,
                                   const double *__restrict__ root, double count,
@@ -476,8 +480,8 @@ __global__ void k_project_correct(const double *__restrict__ a_s, const double *
         const double m = root ? *root / count : 0.0;
         const long c = (long)j * nx + i;
         BCSrc s = bc_source(bc, lid, j, i, ny, nx);
-        const double ua = s.u_const ? s.u_val : corrected(a_s, pc, s.u_src, ny, nx, dx, dy, dt_rho, 0, m);
-        const double vb = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, dx, dy, dt_rho, 1, m);
+        const double ua = s.u_const ? s.u_val : corrected(a_s, pc, s.u_src, ny, nx, Kx2, Ky2, dt_rho, 0, m);
+        const double vb = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, Kx2, Ky2, dt_rho, 1, m);
         a[c] = ua; b[c] = vb;
         p[c] = p_prev ? p_prev[c] + (pc[c] - m) : (pc[c] - m);
         q = ua * ua + vb * vb;
@@ -516,7 +520,7 @@ int divergence_rc_rows(rmt_ctx *ctx, const double *a, const double *b, const dou
                        double d_f, double dx, double dy, double *divU, int jb, int je) {
     if (je > jb)
         k_divergence_rc<<<rows_grid(ctx->nx, jb, je), 256, 0, ctx->stream>>>(
-            a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU, jb, je);
+            a, b, p, ctx->ny, ctx->nx, d_f, rc_div(dx, dy), divU, jb, je);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -525,7 +529,7 @@ int project_correct_rows(rmt_ctx *ctx, const double *a_s, const double *b_s, con
                          double lid, double *a, double *b, double *p, int jb, int je) {
     if (je > jb)
         k_project_correct<<<rows_grid(ctx->nx, jb, je), 256, 0, ctx->stream>>>(
-            a_s, b_s, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt_rho, bc, lid, a, b, p, jb, je,
+            a_s, b_s, pc, p_prev, ctx->ny, ctx->nx, divk_make(2 * dx), divk_make(2 * dy), dt_rho, bc, lid, a, b, p, jb, je,
             nullptr, 1.0);
     RMT_LAUNCHED();
     return RMT_OK;
@@ -626,6 +630,18 @@ int rmt_advect_sl_rk4(rmt_ctx *ctx, const double *q, const double *a, const doub
     RMT_LAUNCHED();
     return RMT_OK;
 }
+__global__ void k_divk_selftest(const double *__restrict__ x, long n, DivK K,
+                                double *__restrict__ q, double *__restrict__ qi) {
+    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (k < n) { q[k] = divk(x[k], K); qi[k] = x[k] / K.d; }
+}
+int rmt_selftest_divk(rmt_ctx *ctx, const double *x, long n, double d, double *q,
+                      double *q_ieee) {
+    RMT_CHECK(n >= 0, RMT_EINVAL, "rmt_selftest_divk: n < 0");
+    if (n) k_divk_selftest<<<grid1d(n, 256), 256, 0, ctx->stream>>>(x, n, divk_make(d), q, q_ieee);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
 int rmt_all_finite2(rmt_ctx *ctx, const double *a, const double *b, int *finite) {
     RMT_TRY(ensure_bytes(ctx, 64));
     int *bad = (int *)ctx->bytes;
@@ -723,7 +739,7 @@ int rmt_apply_velocity_bc(rmt_ctx *ctx, int bc_kind, double lid, double *u, doub
 }
 int rmt_divergence_rc(rmt_ctx *ctx, const double *a, const double *b, const double *p,
                       double d_f, double dx, double dy, double *divU) {
-    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a, b, p, ctx->ny, ctx->nx, d_f, dx, dy, divU, 0, ctx->ny);
+    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a, b, p, ctx->ny, ctx->nx, d_f, rc_div(dx, dy), divU, 0, ctx->ny);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -751,8 +767,8 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
     double *rhs = ctx->scratch, *pc = rhs + n;
     // functions.py:1292-1295 + :1331: rhs = rho * divU / dt, d_f = dt / mean(rho)
     if (p_prev && rho > 0) {
-        k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx,
-                                         dy, rhs, 0, ctx->ny, rho, dt);
+        k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho,
+                                         rc_div(dx, dy), rhs, 0, ctx->ny, rho, dt);
         RMT_LAUNCHED();
     } else {
         if (p_prev) RMT_TRY(rmt_divergence_rc(ctx, a_star, b_star, p_prev, dt / rho, dx, dy, rhs));
@@ -763,7 +779,7 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
     // pc = the raw solve; its mean (functions.py:1119) is subtracted inside the correction
     double *root = ctx->red + RED_BLOCKS + 17;
     RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc, root));
-    k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy,
+    k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, divk_make(2 * dx), divk_make(2 * dy),
                                        dt / rho, bc_kind, lid, a, b, p, 0, ctx->ny, root, (double)n);
     RMT_LAUNCHED();
     RMT_TRY(sub_mean_rows(ctx, p, ctx->ny, ctx->nx));
@@ -808,11 +824,11 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
     double *rhs = ctx->scratch, *pc = rhs + n;
     if (tiles)   // the rhs of the other cells of the marked rows is still in scratch
         k_divergence_tiles<<<max_tiles, 256, 0, ctx->stream>>>(
-            a_star, b_star, p_prev, ctx->ny, ctx->nx, dx, dy, rhs, rho, dt, dtp, tiles, tcount,
+            a_star, b_star, p_prev, ctx->ny, ctx->nx, rc_div(dx, dy), rhs, rho, dt, dtp, tiles, tcount,
             (ctx->nx + MOM_TX - 1) / MOM_TX);
     else
         k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
-            a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, dx, dy, rhs, 0, ctx->ny, rho, dt,
+            a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, rc_div(dx, dy), rhs, 0, ctx->ny, rho, dt,
             dtp, rowmark);
     RMT_LAUNCHED();
     RMT_TRY(dct_plan(ctx, dx, dy));
@@ -826,7 +842,7 @@ int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, 
     double *pc = ctx->scratch + n, *root = ctx->red + RED_BLOCKS + 17;
     RMT_TRY(dct_solve_after_rows(ctx, pc, root, early_marks));
     k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
-        a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy, dt / rho, bc_kind, lid, a, b, p, 0,
+        a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, divk_make(2 * dx), divk_make(2 * dy), dt / rho, bc_kind, lid, a, b, p, 0,
         ctx->ny, root, (double)n, dtp, rho, m2part);
     RMT_LAUNCHED();
     return sub_mean ? sub_mean_rows(ctx, p, ctx->ny, ctx->nx) : RMT_OK;
@@ -840,12 +856,12 @@ int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, dou
     RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
     double *rhs = ctx->scratch, *pc = rhs + n;
     k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
-        a_star, b_star, p_prev, ctx->ny, ctx->nx, 0.0, dx, dy, rhs, 0, ctx->ny, rho, 1.0, dtp);
+        a_star, b_star, p_prev, ctx->ny, ctx->nx, 0.0, rc_div(dx, dy), rhs, 0, ctx->ny, rho, 1.0, dtp);
     RMT_LAUNCHED();
     double *root = ctx->red + RED_BLOCKS + 17;
     RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc, root));
     k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
-        a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, dx, dy, 0.0, bc_kind, lid, a, b, p, 0,
+        a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, divk_make(2 * dx), divk_make(2 * dy), 0.0, bc_kind, lid, a, b, p, 0,
         ctx->ny, root, (double)n, dtp, rho, m2part);
     RMT_LAUNCHED();
     return sub_mean_rows(ctx, p, ctx->ny, ctx->nx);

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <string>
 #include "../../include/rmt.h"
+#include "divk.hpp"
 
 namespace rmt {
 
@@ -73,6 +74,7 @@ struct rmt_ctx {
     bool prof = false;
     int ex_layers = 0;          // last extrapolation call (rmt_extrap_last_path)
     bool ex_chain = false;
+    bool ex_par = false;        // the last geometry laid out the parallel mode (extrap_par.hip)
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // optional (sim.hip overlap): recorded on the stream right before the extrapolation's
     // serial chain kernel starts (or after the call when no chain kernel runs)
@@ -112,14 +114,34 @@ __device__ __forceinline__ double upwind3(const double *f, long s, int k, int n,
     return 0.0;
 }
 
+// The same two stencils with every division by a precomputed divisor (divk.hpp: correctly
+// rounded, so bit-identical): K2 = 2h, K6 = 6h, K1 = h
+__device__ __forceinline__ double grad2k(const double *f, long s, int k, int n, const DivK &K2) {
+    if (k == 0) return divk(-3 * f[0] + 4 * f[s] - f[2 * s], K2);
+    if (k == n - 1) return divk(3 * f[0] - 4 * f[-s] + f[-2 * s], K2);
+    return divk(f[s] - f[-s], K2);
+}
+__device__ __forceinline__ double upwind3k(const double *f, long s, int k, int n, double vel,
+                                           const DivK &K6, const DivK &K1) {
+    if (k >= 2 && k < n - 2) {
+        if (vel > 0) return divk(2 * f[s] + 3 * f[0] - 6 * f[-s] + f[-2 * s], K6);
+        return divk(-f[2 * s] + 6 * f[s] - 3 * f[0] - 2 * f[-s], K6);
+    }
+    if (vel > 0 && k > 0) return divk(f[0] - f[-s], K1);
+    if (vel <= 0 && k < n - 1) return divk(f[s] - f[0], K1);
+    if (k > 0) return divk(f[0] - f[-s], K1);
+    if (k < n - 1) return divk(f[s] - f[0], K1);
+    return 0.0;
+}
+
 // interpolators.py:4-61 bilinear_interpolate at one query point.  CHK (slab-decomposed
 // step): the two rows read must be resident, rows [lo, hi); otherwise *oob is set and the
 // result is NaN (a departure point farther than the halo: never at CFL <= 1).
 template <bool CHK>
 __device__ __forceinline__ double bilinear_t(const double *__restrict__ u, double xq, double yq,
-                                             double dx, double dy, int nx, int ny, int lo,
-                                             int hi, bool *oob) {
-    double x = xq / dx, y = yq / dy;
+                                             const DivK &Kx, const DivK &Ky, int nx, int ny,
+                                             int lo, int hi, bool *oob) {
+    double x = divk(xq, Kx), y = divk(yq, Ky);
     if (!(isfinite(x) && isfinite(y))) return __builtin_nan("");
     if (x < 0.0) x = 0.0; else if (x > nx - 1.0) x = nx - 1.0;
     if (y < 0.0) y = 0.0; else if (y > ny - 1.0) y = ny - 1.0;
@@ -132,19 +154,20 @@ __device__ __forceinline__ double bilinear_t(const double *__restrict__ u, doubl
     return (1 - fx) * (1 - fy) * r0[ix] + fx * (1 - fy) * r0[ix + 1] +
            (1 - fx) * fy * r1[ix] + fx * fy * r1[ix + 1];
 }
+// dx, dy entry (the standalone operators): the divisors made per call
 __device__ __forceinline__ double bilinear(const double *__restrict__ u, double xq, double yq,
                                            double dx, double dy, int nx, int ny) {
-    return bilinear_t<false>(u, xq, yq, dx, dy, nx, ny, 0, ny, nullptr);
+    return bilinear_t<false>(u, xq, yq, divk_make(dx), divk_make(dy), nx, ny, 0, ny, nullptr);
 }
 
 // functions.py:194-227: RK4 backtrace of one point; returns the foot (xb, yb).
 template <bool CHK>
 __device__ __forceinline__ void sl_backtrace_t(const double *__restrict__ a,
                                                const double *__restrict__ b, double x, double y,
-                                               double dt, double dx, double dy, int nx, int ny,
-                                               int lo, int hi, bool *oob, double &xb,
+                                               double dt, const DivK &Kx, const DivK &Ky, int nx,
+                                               int ny, int lo, int hi, bool *oob, double &xb,
                                                double &yb) {
-#define BL_(f, X, Y) bilinear_t<CHK>(f, X, Y, dx, dy, nx, ny, lo, hi, oob)
+#define BL_(f, X, Y) bilinear_t<CHK>(f, X, Y, Kx, Ky, nx, ny, lo, hi, oob)
     const double hdt = 0.5 * dt, dt6 = dt / 6.0;
     double k1x = BL_(a, x, y), k1y = BL_(b, x, y);
     double x2 = x - hdt * k1x, y2 = y - hdt * k1y;
@@ -161,7 +184,8 @@ __device__ __forceinline__ void sl_backtrace(const double *__restrict__ a,
                                              const double *__restrict__ b, double x, double y,
                                              double dt, double dx, double dy, int nx, int ny,
                                              double &xb, double &yb) {
-    sl_backtrace_t<false>(a, b, x, y, dt, dx, dy, nx, ny, 0, ny, nullptr, xb, yb);
+    sl_backtrace_t<false>(a, b, x, y, dt, divk_make(dx), divk_make(dy), nx, ny, 0, ny, nullptr,
+                          xb, yb);
 }
 
 // Semi-Lagrangian block skip.  With every velocity sample bounded by sqrt(m2) and
@@ -400,6 +424,24 @@ __device__ __forceinline__ void pgrad_cell(const double *__restrict__ p, long c,
         gy = (3.0 * (col[(long)(ny - 1) * nx] - m) - 4.0 * (col[(long)(ny - 2) * nx] - m) +
               (col[(long)(ny - 3) * nx] - m)) / (2.0 * dy);
 }
+// pgrad_cell with the divisions by 2dx, 2dy precomputed (divk.hpp, bit-identical)
+__device__ __forceinline__ void pgrad_cellk(const double *__restrict__ p, long c, int j, int i,
+                                            int ny, int nx, const DivK &Kx2, const DivK &Ky2,
+                                            double &gx, double &gy, double m = 0.0) {
+    const double *row = p + (c - i), *col = p + i;
+    gx = 0.0; gy = 0.0;
+    if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1) {
+        gx = divk((p[c + 1] - m) - (p[c - 1] - m), Kx2);
+        gy = divk((p[c + nx] - m) - (p[c - nx] - m), Ky2);
+    }
+    if (i == 0) gx = divk(-3.0 * (row[0] - m) + 4.0 * (row[1] - m) - (row[2] - m), Kx2);
+    if (i == nx - 1)
+        gx = divk(3.0 * (row[nx - 1] - m) - 4.0 * (row[nx - 2] - m) + (row[nx - 3] - m), Kx2);
+    if (j == 0) gy = divk(-3.0 * (col[0] - m) + 4.0 * (col[nx] - m) - (col[2L * nx] - m), Ky2);
+    if (j == ny - 1)
+        gy = divk(3.0 * (col[(long)(ny - 1) * nx] - m) - 4.0 * (col[(long)(ny - 2) * nx] - m) +
+                  (col[(long)(ny - 3) * nx] - m), Ky2);
+}
 struct BCSrc {
     bool u_const, v_const;
     double u_val, v_val;
@@ -579,7 +621,11 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
                     const unsigned long long *kin);
 int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
                   int *dev_status);
-size_t extrap_workspace(int ny, int nx, int max_layers);   // bytes of ctx->bytes it uses
+size_t extrap_workspace(int ny, int nx, int max_layers, bool px = false);   // ctx->bytes used
+// the parallel extrapolation mode (extrap_par.hip; rmt_extrap_set_parallel or the environment
+// variable RMT_EXTRAP_PARALLEL=1): the fits solved as one sparse triangular system by
+// segments instead of the exact raster-order chain -- not bit-exact, see extrap_par.hip
+bool extrap_par_enabled();
 // the exact no-op test of extrapolate() (k_ex_none) on rows [jb, je) of a whole known plane:
 // ctl[EXC_ANY] (extrap.hpp; zeroed by the caller) set iff a first-layer target there fits
 int extrap_none_rows(rmt_ctx *ctx, const unsigned long long *kbits, int ny, int nx, double dx,

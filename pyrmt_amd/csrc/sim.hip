@@ -86,7 +86,7 @@ namespace rmt {
 __device__ __forceinline__ void sl_segment(
     const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ a,
     const double *__restrict__ b, const double *__restrict__ xs, const double *__restrict__ ys,
-    int ny, int nx, double dt, double dx, double dy, double x0, double y0, double R,
+    int ny, int nx, double dt, const DivK &Kx, const DivK &Ky, double x0, double y0, double R,
     double *__restrict__ X1n, double *__restrict__ X2n, double *__restrict__ phi_pre, int *bad,
     unsigned long long *__restrict__ kbits, const double *m2, int mode,
     const unsigned long long *__restrict__ rimw, int j, int i0) {
@@ -98,7 +98,7 @@ __device__ __forceinline__ void sl_segment(
         const bool rim = in && ((rimw[(long)j * ((nx + 63) / 64) + (i >> 6)] >> (i & 63)) & 1);
         mine = (mode == 1) == rim;
     }
-    const bool zero = sl_skip_ok(m2, dt, fmin(dx, dy)) &&
+    const bool zero = sl_skip_ok(m2, dt, fmin(Kx.d, Ky.d)) &&
                       sl_zero_block(X1, X2, ny, nx, j, i0, 256, 0, ny);
     bool known = false;
     if (in && zero) {
@@ -117,9 +117,9 @@ __device__ __forceinline__ void sl_segment(
         {
             double m = ph <= 0 ? 1.0 : 0.0;
             double xb, yb;
-            sl_backtrace(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, xb, yb);
-            X1n[c] = bilinear(X1, xb, yb, dx, dy, nx, ny) * m;
-            X2n[c] = bilinear(X2, xb, yb, dx, dy, nx, ny) * m;
+            sl_backtrace_t<false>(a, b, xs[i], ys[j], dt, Kx, Ky, nx, ny, 0, ny, nullptr, xb, yb);
+            X1n[c] = bilinear_t<false>(X1, xb, yb, Kx, Ky, nx, ny, 0, ny, nullptr) * m;
+            X2n[c] = bilinear_t<false>(X2, xb, yb, Kx, Ky, nx, ny, 0, ny, nullptr) * m;
         }
     }
     if (kbits) {
@@ -133,7 +133,7 @@ __device__ __forceinline__ void sl_segment(
 __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict__ X2,
                          const double *__restrict__ a, const double *__restrict__ b,
                          const double *__restrict__ xs, const double *__restrict__ ys, int ny,
-                         int nx, double dt_arg, double dx, double dy, int shape, double x0,
+                         int nx, double dt_arg, DivK Kx, DivK Ky, int shape, double x0,
                          double y0, double R, double *__restrict__ X1n, double *__restrict__ X2n,
                          double *__restrict__ phi_pre, int *bad,
                          unsigned long long *__restrict__ kbits, const double *m2,
@@ -141,7 +141,7 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
                          const unsigned long long *__restrict__ rimw = nullptr) {
     (void)shape;
     const double dt = dtp ? *dtp : dt_arg;
-    sl_segment(X1, X2, a, b, xs, ys, ny, nx, dt, dx, dy, x0, y0, R, X1n, X2n, phi_pre, bad, kbits,
+    sl_segment(X1, X2, a, b, xs, ys, ny, nx, dt, Kx, Ky, x0, y0, R, X1n, X2n, phi_pre, bad, kbits,
                m2, mode, rimw, blockIdx.y, blockIdx.x * 256);
 }
 
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) k_rim_segments(const unsigned long long *
 __global__ void k_sim_sl_rim(const double *__restrict__ X1, const double *__restrict__ X2,
                              const double *__restrict__ a, const double *__restrict__ b,
                              const double *__restrict__ xs, const double *__restrict__ ys,
-                             int ny, int nx, double dt_arg, double dx, double dy, double x0,
+                             int ny, int nx, double dt_arg, DivK Kx, DivK Ky, double x0,
                              double y0, double R, double *__restrict__ X1n,
                              double *__restrict__ X2n, int *bad, const double *m2,
                              const double *__restrict__ dtp,
@@ -172,7 +172,7 @@ __global__ void k_sim_sl_rim(const double *__restrict__ X1, const double *__rest
     const int nbx = (nx + 255) / 256, cnt = *count;
     for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
         const int id = list[k];
-        sl_segment(X1, X2, a, b, xs, ys, ny, nx, dt, dx, dy, x0, y0, R, X1n, X2n, nullptr, bad,
+        sl_segment(X1, X2, a, b, xs, ys, ny, nx, dt, Kx, Ky, x0, y0, R, X1n, X2n, nullptr, bad,
                    nullptr, m2, 1, rimw, id / nbx, (id % nbx) * 256);
     }
 }
@@ -479,7 +479,7 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
                 double *phi_pre, int *bad, const double *dev_m2) {
     k_sim_sl<<<dim3((ctx->nx + 255) / 256, ctx->ny), 256, 0, ctx->stream>>>(
-        X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, dx, dy, RMT_SHAPE_DISC, x0, y0, R, X1n, X2n,
+        X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx), divk_make(dy), RMT_SHAPE_DISC, x0, y0, R, X1n, X2n,
         phi_pre, bad, nullptr, dev_m2);
     RMT_LAUNCHED();
     return RMT_OK;
@@ -550,7 +550,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     // size the shared scratch once (WENO5: 3 planes, projection: 2) and the extrapolation's
     // byte workspace, so nothing is reallocated while kernels are queued
     RMT_TRY(ensure_scratch(ctx, 3 * n * sizeof(double)));
-    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, prm->layers)));
+    RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, prm->layers, extrap_par_enabled())));
     if (prm->shape == RMT_SHAPE_DISC && prm->scheme == RMT_SCHEME_SEMILAGRANGIAN &&
         prm->layers >= 1 && prm->layers <= 12) {
         // the speculative momentum stream at the lowest priority: the extrapolation's own
@@ -783,7 +783,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // a second stream, re-run afterwards on the tiles within reach of a target
         static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
         static const bool side_tail = !(getenv("RMT_SIDE_TAIL") && !atoi(getenv("RMT_SIDE_TAIL")));
-        const bool overlap = solid && S->st2 && !no_overlap;
+        // the parallel extrapolation takes ~0.2 ms: nothing to hide it behind, so the step
+        // runs in order (its geometry still beside the previous step's projection)
+        const bool par = extrap_par_enabled();
+        const bool overlap = solid && S->st2 && !no_overlap && !par;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
             // 2. advect the reference map with the pre-advection level set and mask
@@ -808,11 +811,11 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 }
                 RMT_HIP(hipEventRecord(S->e_bits, st));
                 k_sim_sl_rim<<<4096, 256, 0, st>>>(   // ~one rim segment per block
-                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.x0, P.y0,
+                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.x0, P.y0,
                     P.R, S->X1n, S->X2n, S->flag, sc, dtp, S->rimw, S->segs, scount);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
                 k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, st>>>(
-                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
+                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.shape,
                     P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits, sc, dtp);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN_CUBIC) {
                 k_sim_sl_cubic<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx,
@@ -845,6 +848,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // the previous step's map (intact until the second stream's phi rebuild, which
             // starts at the chain's launch) predicts the chain's latest sources
             ctx->ex_pred1 = S->X1; ctx->ex_pred2 = S->X2;
+            if (geo_ready && !overlap) RMT_HIP(hipStreamWaitEvent(st, S->e_geo, 0));
             const int es = geo_ready && P.layers > 0
                                ? extrap_finish(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->flag + 2)
                                : extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
@@ -871,7 +875,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     // the advection of every non-rim cell, once the chain has started (earlier
                     // its blocks would crowd out the one-workgroup band passes)
                     k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, S->st2>>>(
-                        S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, P.dx, P.dy, P.shape,
+                        S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.shape,
                         P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, nullptr, sc, dtp, 2,
                         S->rimw);
                     RMT_LAUNCHED();
@@ -952,6 +956,20 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // 4. phi from the advected + extrapolated map
             k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R, S->phi,
                                               S->X1, S->X2, nb);
+            RMT_LAUNCHED();
+            if (par && async && geo_env && nb && P.layers > 0 && S->st2 && it + 1 < nsteps) {
+                // the next step's extrapolation geometry (known plane nb) beside this step's
+                // momentum and projection
+                RMT_HIP(hipEventRecord(S->e_kb, st));
+                RMT_HIP(hipStreamWaitEvent(S->st2, S->e_kb, 0));
+                ctx->stream = S->st2;
+                const int gs = extrap_geometry(ctx, S->X1n, S->X2n, nullptr, P.dx, P.dy,
+                                               P.layers, S->X1n, S->X2n, nb);
+                ctx->stream = st;
+                RMT_TRY(gs);
+                RMT_HIP(hipEventRecord(S->e_geo, S->st2));
+                geo_ready = true;
+            }
             // 5. momentum (RK4)
             RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
                                  S->sxx, S->sxy, S->syy, S->J, W));

@@ -88,14 +88,14 @@ namespace rmt {
 __global__ void k_slab_sl(const double *__restrict__ X1, const double *__restrict__ X2,
                           const double *__restrict__ a, const double *__restrict__ b,
                           const double *__restrict__ xs, const double *__restrict__ ys, int ny,
-                          int nx, double dt, double dx, double dy, double x0, double y0, double R,
+                          int nx, double dt, DivK Kx, DivK Ky, double x0, double y0, double R,
                           double *__restrict__ X1n, double *__restrict__ X2n,
                           double *__restrict__ phi_pre, int *flags, int jb, int je, int lo,
                           int hi, const double *m2) {
     // grid (ceil(nx / 256), je - jb); the block skip of sl_zero_block (rmt_internal.hpp) with
     // m2 bounding the velocities of the resident rows
     const int j = jb + blockIdx.y, i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
-    const bool zero = sl_skip_ok(m2, dt, fmin(dx, dy)) &&
+    const bool zero = sl_skip_ok(m2, dt, fmin(Kx.d, Ky.d)) &&
                       sl_zero_block(X1, X2, ny, nx, j, i0, 256, lo, hi);
     if (i >= nx) return;
     const long c = (long)j * nx + i;
@@ -110,9 +110,9 @@ __global__ void k_slab_sl(const double *__restrict__ X1, const double *__restric
     const double m = ph <= 0 ? 1.0 : 0.0;
     bool oob = false;
     double xb, yb;
-    sl_backtrace_t<true>(a, b, xs[i], ys[j], dt, dx, dy, nx, ny, lo, hi, &oob, xb, yb);
-    X1n[c] = bilinear_t<true>(X1, xb, yb, dx, dy, nx, ny, lo, hi, &oob) * m;
-    X2n[c] = bilinear_t<true>(X2, xb, yb, dx, dy, nx, ny, lo, hi, &oob) * m;
+    sl_backtrace_t<true>(a, b, xs[i], ys[j], dt, Kx, Ky, nx, ny, lo, hi, &oob, xb, yb);
+    X1n[c] = bilinear_t<true>(X1, xb, yb, Kx, Ky, nx, ny, lo, hi, &oob) * m;
+    X2n[c] = bilinear_t<true>(X2, xb, yb, Kx, Ky, nx, ny, lo, hi, &oob) * m;
     if (oob) atomicOr(flags, FL_HALO);
 }
 
@@ -317,7 +317,7 @@ int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, c
             int *flags, int jb, int je, int lo, int hi, const double *dev_m2) {
     if (je <= jb) return RMT_OK;
     k_slab_sl<<<dim3((nx + 255) / 256, je - jb), 256, 0, ctx->stream>>>(
-        X1, X2, a, b, xs, ys, ny, nx, dt, dx, dy, x0, y0, R, X1n, X2n, phi_pre, flags, jb, je,
+        X1, X2, a, b, xs, ys, ny, nx, dt, divk_make(dx), divk_make(dy), x0, y0, R, X1n, X2n, phi_pre, flags, jb, je,
         lo, hi, dev_m2);
     RMT_LAUNCHED();
     return RMT_OK;
@@ -457,7 +457,7 @@ int rmt_slab_create(rmt_ctx *ctx, const rmt_sim_params *prm, int G, int rank,
     if (mu_max > 1e-12 && rho_min > 1e-12)
         d = std::fmin(d, CFL * rho_min * std::pow(dx, 2.0) / (4.0 * mu_max));
     S->dt_const = std::fmin(d, prm->dt_cap);
-    RMT_TRY(ensure_bytes(ctx, extrap_workspace(S->NY, S->NX, prm->layers)));
+    RMT_TRY(ensure_bytes(ctx, extrap_workspace(S->NY, S->NX, prm->layers, extrap_par_enabled())));
     if (prm->layers >= 1 && prm->layers <= 12) {
         int least = 0, greatest = 0;
         RMT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -530,7 +530,7 @@ int rmt_slab_advect_interior(rmt_slab *S, double dt) {
         RMT_TRY(reduce_maxsq2_nan(ctx, S->u + o, S->v + o, no, S->scal + SC_M2OWN));
         k_slab_sl<<<dim3((NX + 255) / 256, ie - ib), 256, 0, ctx->stream>>>(
             S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt,
-            P.dx, P.dy, P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
+            divk_make(P.dx), divk_make(P.dy), P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
             S->flags, ib, ie, S->r0, S->r1, S->scal + SC_M2OWN);
         RMT_LAUNCHED();
     }
@@ -557,7 +557,7 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
         if (b <= a) continue;
         k_slab_sl<<<dim3((NX + 255) / 256, b - a), 256, 0, ctx->stream>>>(
             S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt,
-            P.dx, P.dy, P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
+            divk_make(P.dx), divk_make(P.dy), P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
             S->flags, a, b, S->lo, S->hi, S->scal + SC_M2RES);
         RMT_LAUNCHED();
     }

@@ -168,6 +168,15 @@ def extrapolation_mode(mode):
     L.check(L.lib().rmt_extrap_set_mode(int(mode)), "rmt_extrap_set_mode")
 
 
+def extrapolation_parallel(on=True):
+    """librmt option (no reference counterpart): the parallel extrapolation (extrap_par.hip)
+    instead of the exact raster-order chain -- the same targets, acceptance and weights, each
+    fit evaluated in offsets from its target (not bit-exact: within the reference's own
+    rounding noise).  Process-wide, for the extrapolations that start
+    afterwards (a simulation created afterwards also schedules its step for it)."""
+    L.check(L.lib().rmt_extrap_set_parallel(int(bool(on))), "rmt_extrap_set_parallel")
+
+
 def extrapolation_last_path(ny, nx):
     """librmt diagnostic: 0 if the last extrapolation on this grid ran the chain path,
     1 if it ran the row-ticket sweep."""

@@ -1,0 +1,39 @@
+#!/bin/bash
+# round-3 GPU steps: scripts/r03_run.sh OUT STEP [STEP ...]; each step under its own limit,
+# the first failure ends the call.
+#   suite          pytest -m gpu without the parallel-extrapolation tests
+#   par            tests/test_gpu_extrap_par.py
+#   t:EXPR         pytest -m gpu -k EXPR
+#   bench          20-step bench line (no CPU baseline)
+#   benchpar       the same with RMT_EXTRAP_PARALLEL=1
+#   kt / ktpar     rocprofv3 kernel trace + stats of the 20-step bench (exact / parallel)
+set -o pipefail
+O=gpurun_out/${1:?out}; shift; mkdir -p "$O"; export TMPDIR=/tmp
+PYT="python -u -m pytest -v --timeout 240 --timeout-method thread"
+for s in "$@"; do
+    echo "== $s $(date +%T)"
+    case "$s" in
+        suite) timeout -k 10 900 $PYT tests -m gpu --ignore=tests/test_gpu_extrap_par.py -x > "$O/suite.log" 2>&1 \
+                   || { grep -E "FAIL|Error|error" "$O/suite.log" | head -20; tail -30 "$O/suite.log"; exit 1; }
+               tail -2 "$O/suite.log" ;;
+        par) timeout -k 10 900 $PYT -s tests/test_gpu_extrap_par.py > "$O/par.log" 2>&1 \
+                   || { grep -E "^\[|FAIL|Error" "$O/par.log" | head -30; tail -30 "$O/par.log"; exit 1; }
+             grep -E "^\[|passed|failed" "$O/par.log" | tail -20 ;;
+        t:*) timeout -k 10 900 $PYT -s tests -m gpu -k "${s#t:}" > "$O/t.log" 2>&1 \
+                   || { tail -40 "$O/t.log"; exit 1; }
+             grep -E "^\[|passed|failed" "$O/t.log" | tail -20 ;;
+        bench) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/bench.log" 2>&1 \
+                   || { tail -20 "$O/bench.log"; exit 1; }
+               tail -1 "$O/bench.log" | cut -c1-400 ;;
+        benchpar) RMT_EXTRAP_PARALLEL=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/benchpar.log" 2>&1 \
+                   || { tail -20 "$O/benchpar.log"; exit 1; }
+               tail -1 "$O/benchpar.log" | cut -c1-400 ;;
+        kt|ktpar) [ "$s" = ktpar ] && export RMT_EXTRAP_PARALLEL=1
+            timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/$s" -o bench -- \
+                python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/$s.log" 2>&1 || exit 1
+            unset RMT_EXTRAP_PARALLEL
+            f=$(find "$O/$s" -name "*kernel_stats.csv" | head -1); cp "$f" "$O/${s}_stats.csv"
+            cut -d, -f1-4 "$f" | head -16 ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done
