@@ -234,6 +234,10 @@ int rmt_compute_strain_energy(rmt_ctx *ctx, const double *X1, const double *X2, 
 int rmt_compute_viscous_dissipation(rmt_ctx *ctx, const double *a, const double *b, double mu_f,
                                     const double *phi, double w_t, double dx, double dy,
                                     double eta_s, double *diss);
+/* output.py:195-211 divergence_2d_interior (the div_vel dataset of output_simulation_data,
+ * pad = 4 there): central differences on the cells >= pad from every edge, 0 elsewhere */
+int rmt_divergence_2d_interior(rmt_ctx *ctx, const double *u, const double *v, double dx,
+                               double dy, int pad, double *div);
 /* functions.py:897-944 velocity_rhs_blended_optimized: H, rho_local device arrays; the
  * surface-tension force fx, fy device arrays or both NULL (the scalar 0.0 of the gamma = 0
  * path).  (phi, dH_dx, dH_dy of the reference signature are unused by its body.) */

@@ -521,6 +521,14 @@ def disc_centroid(phi, X, Y):
     return (X[m].mean(), Y[m].mean()) if np.any(m) else (np.nan, np.nan)
 
 
+def divergence_2d_interior(u, v, dx, dy, pad=3):
+    """output.py:195-211 (the same slices and operation order)."""
+    d = np.zeros_like(u)
+    d[pad:-pad, pad:-pad] = ((u[pad:-pad, pad + 1:-pad + 1] - u[pad:-pad, pad - 1:-pad - 1]) / (2 * dx)
+                             + (v[pad + 1:-pad + 1, pad:-pad] - v[pad - 1:-pad - 1, pad:-pad]) / (2 * dy))
+    return d, d[pad:-pad, pad:-pad]
+
+
 def compute_kinetic_energy(a, b, rho_f, rho_s, phi, w_t, dx, dy):
     H = smoothed_heaviside(phi, w_t)
     rho = (1 - H) * rho_s + H * rho_f

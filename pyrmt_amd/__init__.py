@@ -13,6 +13,7 @@ from .functions import (_precompute_poisson_eigenvalues, _solve_poisson_dct,  # 
                         _tile_overlap, _solve_poisson_fft, _compute_divergence_periodic,
                         _compute_pressure_gradient_periodic, _central2_rhs,
                         _conservative_rhs)
+from .output import output_simulation_data  # noqa: F401  (pyRMT/__init__.py:32)
 from . import simulation
 from . import mac
 

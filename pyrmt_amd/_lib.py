@@ -102,6 +102,7 @@ SIGNATURES = {
     "rmt_divergence_rc_variable": (_I, [_P, _P, _P, _P, _D, _P, _D, _D, _P]),
     "rmt_compute_timestep": (_I, [_P, _P, _P, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D,
                                   ctypes.POINTER(_D)]),
+    "rmt_divergence_2d_interior": (_I, [_P, _P, _P, _D, _D, _I, _P]),
     "rmt_compute_kinetic_energy": (_I, [_P, _P, _P, _D, _D, _P, _D, _D, _D, ctypes.POINTER(_D)]),
     "rmt_compute_strain_energy": (_I, [_P, _P, _P, _P, _D, _D, _D, _D, ctypes.POINTER(_D)]),
     "rmt_compute_viscous_dissipation": (_I, [_P, _P, _P, _D, _P, _D, _D, _D, _D,

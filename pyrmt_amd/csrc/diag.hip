@@ -200,7 +200,32 @@ __global__ void k_vrhs(const double *__restrict__ u, const double *__restrict__ 
 
 using namespace rmt;
 
+// output.py:195-211 divergence_2d_interior: central differences on [pad, N - pad)^2,
+// (u[j, i+1] - u[j, i-1]) / (2dx) + (v[j+1, i] - v[j-1, i]) / (2dy); 0 elsewhere
+__global__ void k_div_interior(const double *__restrict__ u, const double *__restrict__ v,
+                               int ny, int nx, DivK Kx2, DivK Ky2, int pad,
+                               double *__restrict__ out) {
+    const long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (c >= (long)ny * nx) return;
+    const int j = (int)(c / nx), i = (int)(c % nx);
+    double d = 0.0;
+    if (j >= pad && j < ny - pad && i >= pad && i < nx - pad)
+        d = divk(u[c + 1] - u[c - 1], Kx2) + divk(v[c + nx] - v[c - nx], Ky2);
+    out[c] = d;
+}
+
 extern "C" {
+
+int rmt_divergence_2d_interior(rmt_ctx *ctx, const double *u, const double *v, double dx,
+                               double dy, int pad, double *div) {
+    RMT_CHECK(pad >= 1, RMT_EINVAL, "divergence_2d_interior: pad >= 1");
+    const long n = (long)ctx->ny * ctx->nx;
+    k_div_interior<<<grid1d(n, 256), 256, 0, ctx->stream>>>(u, v, ctx->ny, ctx->nx,
+                                                              divk_make(2 * dx), divk_make(2 * dy),
+                                                              pad, div);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
 
 int rmt_compute_kinetic_energy(rmt_ctx *ctx, const double *a, const double *b, double rho_f,
                                double rho_s, const double *phi, double w_t, double dx, double dy,

@@ -39,7 +39,7 @@ namespace rmt {
 
 struct DivK {
     double d, yh, yl;
-    unsigned rlo, rspan;   // certified |x| high words [rlo, rlo + rspan); rspan = 0: IEEE only
+    unsigned rspan;   // certified |x| high words [DIVK_HI_LO, DIVK_HI_LO + rspan); 0: IEEE only
 };
 
 // 2^-900 and 2^1000 as high words of |x| (exponent field in bits 20..30)
@@ -47,7 +47,7 @@ constexpr unsigned DIVK_HI_LO = (unsigned)(1023 - 900) << 20;
 constexpr unsigned DIVK_HI_HI = (unsigned)(1023 + 1000) << 20;
 
 __host__ __device__ inline DivK divk_make(double d) {
-    DivK k{d, 0.0, 0.0, 0u, 0u};
+    DivK k{d, 0.0, 0.0, 0u};
     if (!(d > 0.0) || !std::isfinite(d) || !std::isnormal(d)) return k;   // IEEE only
     int e;
     const double D = 2.0 * std::frexp(d, &e);            // significand in [1, 2)
@@ -55,7 +55,6 @@ __host__ __device__ inline DivK divk_make(double d) {
     k.yh = 1.0 / d;
     const double r = std::fma(-d, k.yh, 1.0);             // 1 - d*yh, exact
     k.yl = r / d;                                         // RN(r / d) = RN(1/d - yh)
-    k.rlo = DIVK_HI_LO;
     k.rspan = DIVK_HI_HI - DIVK_HI_LO;
     return k;
 }
@@ -85,7 +84,7 @@ __host__ __device__ __forceinline__ double divk(double x, const DivK &K) {
     const double t = std::fma(q0, K.d, -x);
     double q = std::fma(-t, K.yh, q0);
     const unsigned hi = divk_hiword(x) & 0x7fffffffu, lo = divk_loword(x);
-    const bool ok = (hi - K.rlo) < K.rspan || (hi | lo) == 0u;
+    const bool ok = (hi - DIVK_HI_LO) < K.rspan || (hi | lo) == 0u;
     if (__builtin_expect(!ok, 0)) q = x / K.d;
     return std::copysign(q, x);   // x = -0 with yl < 0: RN(x*yl) = +0 makes q0 = +0
 }

@@ -681,6 +681,7 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bo
         w.sMT = (double *)take(w.maxseg * PX_F * PX_K * 8);
         w.sNT = (double *)take(w.maxseg * PX_K * PX_K * 8);
         w.sd = (double2 *)take(w.maxseg * PX_K * 16);
+        w.spk = (double *)take(w.maxseg * PX_PB * 8);
     }
     if (bytes) *bytes = o;
     return w;

@@ -29,6 +29,7 @@ constexpr int PX_K = 64;            // parallel mode: fits per segment
 constexpr int PX_F = 64;            // frontier capacity (more: the segment is solved serially)
 constexpr int PX_S = 81;            // window sources per fit
 constexpr int PX_H = 8;             // segment header ints
+constexpr int PX_PB = 768;          // packed block of a segment for k_px_comb (doubles)
 
 struct ExWs {
     // band detection (both paths) and the fallback sweep
@@ -67,6 +68,7 @@ struct ExWs {
     int *shdr, *sF;                           // maxseg * PX_H, maxseg * PX_F
     double *sMT, *sNT;                        // maxseg * PX_F * PX_K, maxseg * PX_K * PX_K
     double2 *sd;                              // maxseg * PX_K
+    double *spk;                              // maxseg * PX_PB: k_px_comb's packed blocks
     long maxseg;
     char *arena;
     long long arena_bytes;

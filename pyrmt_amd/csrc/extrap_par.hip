@@ -26,11 +26,15 @@
 //     k_px_seg    one wave per segment: its frontier F (earlier same-layer fits it reads,
 //                 ~13 at N = 4096, <= PX_F or the segment is solved serially), and its
 //                 affine response x_seg = M f_F + N c_seg by forward substitution
+//     k_px_pack   one wave per segment: the rows a later frontier reads ("live", ~13) and
+//                 their M rows, packed into one contiguous block for the sequential pass
 //   values, per layer (critical path):
 //     k_px_c      one wave per fit: c_t = sum over static sources beta X
-//     k_px_d      one wave per segment: d = N c
-//     k_px_comb   ONE wave, sequential over the layer's segments: only the fits a later
-//                 frontier reads ("live"), x = d + M f (~13 x 13 FMAs per segment)
+//     k_px_d      one wave per segment: d = N c (and d of the live rows into the block)
+//     k_px_comb   one workgroup, sequential over the layer's segments: wave 0 computes the
+//                 live rows, x = d + M f (~13 x 13 FMAs per segment) from an LDS value ring;
+//                 15 producer waves stream the next segments' blocks into LDS slots ahead
+//                 of it (intra-workgroup flags), so its ~0.2 us per segment is not HBM latency
 //     k_px_out    one wave per segment: every fit, x = d + M f, written to the map
 // tools/pex_proto.py restates the algorithm in numpy (segment solve = serial forward
 // substitution to 7e-16 at N = 4096; frontier sizes); oracle/rmt_oracle.c mode 2 computes the
@@ -284,6 +288,38 @@ __global__ void __launch_bounds__(64) k_px_seg(ExWs ws, int ML) {
     for (int q = 0; q < n; ++q) NT[q * PX_K + lane] = lane < n ? S.N[lane][q] : 0.0;
 }
 
+// packed block of segment g (doubles): [0] nF, [1] nL, [2] kind (0 packed, 1 serial, 2 too
+// large: k_px_comb reads M and d from their own arrays), [3] lo, [4] n, [8, 72) frontier ids,
+// [72, 136) live rows, [136, 264) d of the live rows (k_px_d), [264, PX_PB) M of the live
+// rows, column-major: M[r_k][c] at 264 + c nL + k
+constexpr int PXB_F = 8, PXB_R = 72, PXB_D = 136, PXB_M = 264;
+__global__ void __launch_bounds__(64) k_px_pack(ExWs ws, int ML) {
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int g = blockIdx.x, lane = threadIdx.x;
+    int L = -1, s0 = 0, ns = 0;
+    for (int q = 0; q < ML; ++q) {
+        px_segs(ws.ctl, q, s0, ns);
+        if (g >= s0 && g < s0 + ns) { L = q; break; }
+    }
+    if (L < 0) return;
+    const int *hdr = ws.shdr + (long)g * PX_H;
+    const int lo = hdr[0], n = hdr[1] - lo, nF = hdr[3], serial = hdr[4];
+    double *B = ws.spk + (long)g * PX_PB;
+    const bool lv = !serial && lane < n && ws.live[lo + lane];
+    const u64 lm = __ballot(lv);
+    const int nL = __popcll(lm);
+    const int kind = serial ? 1 : (PXB_M + nF * nL > PX_PB ? 2 : 0);
+    if (lane == 0) { B[0] = nF; B[1] = nL; B[2] = kind; B[3] = lo; B[4] = n; }
+    if (serial) return;
+    if (lane < nF) B[PXB_F + lane] = ws.sF[(long)g * PX_F + lane];
+    const int k = __popcll(lm & ((1ull << lane) - 1));
+    if (lv) B[PXB_R + k] = lane;
+    if (kind != 0) return;
+    const double *MT = ws.sMT + (long)g * PX_F * PX_K;
+    for (int c = 0; c < nF; ++c)
+        if (lv) B[PXB_M + c * nL + k] = MT[c * PX_K + lane];
+}
+
 // ------------------------------------------------------------------ values ---------
 // c_t = sum over the static sources (solid: the advected map; earlier layers: their fits)
 // of beta X, one wave per fit of layer L (butterfly sum)
@@ -327,6 +363,13 @@ __global__ void __launch_bounds__(64) k_px_d(ExWs ws, int L) {
         d2 += nq * px_rl(cr.y, q);
     }
     if (lane < n) ws.sd[(long)g * PX_K + lane] = make_double2(d1, d2);
+    const bool lv = lane < n && ws.live[lo + lane];
+    const u64 lm = __ballot(lv);
+    if (lv) {
+        double *B = ws.spk + (long)g * PX_PB + PXB_D;
+        const int k = __popcll(lm & ((1ull << lane) - 1));
+        B[2 * k] = d1; B[2 * k + 1] = d2;
+    }
 }
 
 // x = d + M f for one row (lane): the same operation order in k_px_comb and k_px_out
@@ -341,34 +384,67 @@ __device__ __forceinline__ double2 px_row(const double *__restrict__ MT, int nF,
     return make_double2(x1, x2);
 }
 
-// ONE wave: the layer's segments in order.  Values live in an LDS ring by fit id (a frontier
-// id more than PX_RING behind its segment is read through L2 after a fence: this wave wrote it
-// to pval earlier).
-constexpr int PX_RING = 4096;
+// The layer's segments in order, one workgroup: wave 0 (the consumer) computes each
+// segment's live rows from an LDS value ring by fit id; waves 1..PX_NP (producers) copy the
+// segments' packed blocks into PX_NS LDS slots ahead of it.  A slot is handed over by LDS flags
+// (a wave's LDS operations complete in order, so the flag written after the data orders it);
+// all waves of a workgroup are resident, so the spins terminate; a bug guard caps them and
+// reports an abort (dev_status[1]).  A frontier id more than PX_RING behind its segment is
+// read through L2 after a fence (the consumer wrote it to pval).
+constexpr int PX_RING = 4096, PX_NS = 10, PX_NP = 15;
+constexpr size_t PX_COMB_LDS = PX_RING * 16 + (size_t)PX_NS * PX_PB * 8 + 2 * PX_NS * 4;
 __device__ __forceinline__ double2 px_far(const double2 *p) {
     const double *q = (const double *)p;
     return make_double2(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                         __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-__global__ void __launch_bounds__(64) k_px_comb(ExWs ws, int L, double *__restrict__ X1,
-                                                double *__restrict__ X2, int nx) {
-    __shared__ double2 ring[PX_RING];
+__global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
+                                                             double *__restrict__ X1,
+                                                             double *__restrict__ X2) {
+    extern __shared__ double px_lds[];
+    double2 *ring = (double2 *)px_lds;
+    double *slots = px_lds + 2 * PX_RING;
+    volatile int *ready = (volatile int *)(slots + (size_t)PX_NS * PX_PB);
+    volatile int *freeg = ready + PX_NS;
     if (ws.ctl[EXC_FALLBACK]) return;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int s0, ns;
     px_segs(ws.ctl, L, s0, ns);
-    const int b0 = ws.ctl[EXC_BASE + L];
-    for (int gi = 0; gi < ns; ++gi) {
-        const int g = s0 + gi;
-        const int *hdr = ws.shdr + (long)g * PX_H;
-        const int lo = hdr[0], hi = hdr[1], nF = hdr[3], serial = hdr[4], n = hi - lo;
-        if (serial) {
-            // fit by fit: x_t = c_t + sum over same-layer sources (window order) beta x_s
+    if (threadIdx.x < PX_NS) { ready[threadIdx.x] = -1; freeg[threadIdx.x] = threadIdx.x; }
+    __syncthreads();
+    constexpr long SPIN = 1L << 26;
+    if (wv > 0) {   // producer
+        for (int gi = wv - 1; gi < ns; gi += PX_NP) {
+            const int slot = gi % PX_NS;
+            long spin = 0;
+            while (freeg[slot] != gi) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spin > SPIN) { if (lane == 0) atomicExch(ws.status + 1, 1); return; }
+            }
+            const double *src = ws.spk + (long)(s0 + gi) * PX_PB;
+            double v[PX_PB / 64];
+#pragma unroll
+            for (int q = 0; q < PX_PB / 64; ++q) v[q] = src[q * 64 + lane];
+            double *dst = slots + (size_t)slot * PX_PB;
+#pragma unroll
+            for (int q = 0; q < PX_PB / 64; ++q) dst[q * 64 + lane] = v[q];
+            if (lane == 0) ready[slot] = gi;
+        }
+        return;
+    }
+    for (int gi = 0; gi < ns; ++gi) {   // consumer (wave 0)
+        const int slot = gi % PX_NS, g = s0 + gi;
+        long spin = 0;
+        while (ready[slot] != gi)
+            if (++spin > SPIN) { if (lane == 0) atomicExch(ws.status + 1, 1); return; }
+        const double *B = slots + (size_t)slot * PX_PB;
+        const int nF = (int)B[0], nL = (int)B[1], kind = (int)B[2], lo = (int)B[3], n = (int)B[4];
+        if (kind == 1) {
+            // serial segment, fit by fit: x_t = c_t + sum over same-layer sources beta x_s
             for (int r = 0; r < n; ++r) {
                 const int t = lo + r, nst = ws.pns[t], nd = ws.pnd[t];
-                double a1 = 0.0, a2 = 0.0;
                 int s = 0;
-                double b = 0.0;
+                double b = 0.0, a1 = 0.0, a2 = 0.0;
                 if (lane < nd) {
                     s = -ws.pkey[(long)t * PX_S + nst + lane] - 1;
                     b = ws.pbeta[(long)t * PX_S + nst + lane];
@@ -388,32 +464,40 @@ __global__ void __launch_bounds__(64) k_px_comb(ExWs ws, int L, double *__restri
                     const long cell = ws.tcell[t];
                     X1[cell] = x.x; X2[cell] = x.y;
                 }
-                __syncthreads();
             }
-            continue;
-        }
-        double f1 = 0.0, f2 = 0.0;
-        {
-            const int s = lane < nF ? ws.sF[(long)g * PX_F + lane] : lo;
-            const bool far = lane < nF && lo - s > PX_RING;
-            if (__ballot(far)) __threadfence();
-            if (lane < nF) {
-                const double2 v = far ? px_far(&ws.pval[s]) : ring[s & (PX_RING - 1)];
-                f1 = v.x; f2 = v.y;
+        } else if (nL > 0) {
+            double f1 = 0.0, f2 = 0.0;
+            {
+                const int s = lane < nF ? (int)B[PXB_F + lane] : lo;
+                const bool far = lane < nF && lo - s > PX_RING;
+                if (__ballot(far)) __threadfence();
+                if (lane < nF) {
+                    const double2 v = far ? px_far(&ws.pval[s]) : ring[s & (PX_RING - 1)];
+                    f1 = v.x; f2 = v.y;
+                }
+            }
+            const int r = lane < nL ? (int)B[PXB_R + lane] : 0;
+            double2 x;
+            if (kind == 0) {
+                x = lane < nL ? make_double2(B[PXB_D + 2 * lane], B[PXB_D + 2 * lane + 1])
+                              : make_double2(0.0, 0.0);
+                for (int c = 0; c < nF; ++c) {
+                    const double m = lane < nL ? B[PXB_M + c * nL + lane] : 0.0;
+                    x.x += m * px_rl(f1, c);
+                    x.y += m * px_rl(f2, c);
+                }
+            } else {   // block too small for this segment's M: its own arrays (same order)
+                x = px_row(ws.sMT + (long)g * PX_F * PX_K, nF, ws.sd[(long)g * PX_K + r], f1, f2,
+                           r);
+            }
+            if (lane < nL) {
+                ring[(lo + r) & (PX_RING - 1)] = x;
+                ws.pval[lo + r] = x;
             }
         }
-        const bool lv = lane < n && ws.live[lo + lane];
-        if (__ballot(lv)) {
-            const double2 d = lane < n ? ws.sd[(long)g * PX_K + lane] : make_double2(0.0, 0.0);
-            const double2 x = px_row(ws.sMT + (long)g * PX_F * PX_K, nF, d, f1, f2, lane);
-            if (lv) {
-                ring[(lo + lane) & (PX_RING - 1)] = x;
-                ws.pval[lo + lane] = x;
-            }
-        }
-        __syncthreads();
+        // every read of the slot is issued: hand it back (LDS operations stay in order)
+        if (lane == 0) freeg[slot] = gi + PX_NS;
     }
-    (void)b0; (void)nx;
 }
 
 // every fit of the (non-serial) segments of layer L: x = d + M f, into the map
@@ -450,18 +534,25 @@ int extrap_par_geometry(rmt_ctx *ctx, const ExWs &ws, double dx, double dy, int 
     const unsigned gb = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
     k_px_beta<<<gb, 256, 0, st>>>(ws, ny, nx, W, ML, dx, dy, r * r);
     k_px_seg<<<(unsigned)ws.maxseg, 64, 0, st>>>(ws, ML);
+    k_px_pack<<<(unsigned)ws.maxseg, 64, 0, st>>>(ws, ML);
     RMT_LAUNCHED();
     return RMT_OK;
 }
 
 int extrap_par_values(rmt_ctx *ctx, const ExWs &ws, double *X1o, double *X2o, int ML) {
     hipStream_t st = ctx->stream;
+    static bool attr = false;
+    if (!attr) {
+        RMT_HIP(hipFuncSetAttribute((const void *)k_px_comb,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, PX_COMB_LDS));
+        attr = true;
+    }
     const unsigned gb = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
     const unsigned sb = (unsigned)ws.maxseg;
     for (int L = 0; L < ML; ++L) {
         k_px_c<<<gb, 256, 0, st>>>(ws, L, X1o, X2o);
         k_px_d<<<sb, 64, 0, st>>>(ws, L);
-        k_px_comb<<<1, 64, 0, st>>>(ws, L, X1o, X2o, ctx->nx);
+        k_px_comb<<<1, 64 * (PX_NP + 1), PX_COMB_LDS, st>>>(ws, L, X1o, X2o);
         k_px_out<<<sb, 64, 0, st>>>(ws, L, X1o, X2o);
         RMT_LAUNCHED();
     }

@@ -8,6 +8,7 @@
 #include "rmt_internal.hpp"
 #include <utility>
 #include <algorithm>
+#include <vector>
 
 namespace rmt {
 
@@ -203,8 +204,9 @@ static MomDiv mom_div(double dx, double dy, double rho_s, double rho_f) {
     return m;
 }
 
-// one stage tile (k_mom_stage); IN: an interior tile (see the kernel)
-template <bool IN>
+// one stage tile (k_mom_stage); IN: an interior tile (see the kernel); SQ: dx == dy (the
+// y divisors are the x ones: fewer live scalar registers)
+template <bool IN, bool SQ>
 __device__ __forceinline__ void ms_tile(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
@@ -219,6 +221,7 @@ __device__ __forceinline__ void ms_tile(
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
     const unsigned char *__restrict__ fluid_tiles, const MomDiv &K, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
     double (&gx)[MS_GY][MS_GX], double (&gm)[MS_GY][MS_GX], double (&gy)[MS_GY][MS_GX]) {
+    const DivK &Ky2 = SQ ? K.x2 : K.y2, &Ky6 = SQ ? K.x6 : K.y6, &Ky1 = SQ ? K.x1 : K.y1;
     // pure-fluid tile (k_fluid_rows / k_fluid_win): every cell the blended stress is formed
     // on has phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not
     // solid exactly -- those constants replace the loads of sxx, sxy, syy, H and solid below
@@ -304,8 +307,8 @@ __device__ __forceinline__ void ms_tile(
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
             if (ok2[it]) {
                 const double *pu = &su[ry + 1][rx + 1], *pv = &sv[ry + 1][rx + 1];
-                const double dudx = g2<IN>(pu, 1, i, nx, K.x2), dvdy = g2<IN>(pv, MS_UX, j, ny, K.y2);
-                const double dudy = g2<IN>(pu, MS_UX, j, ny, K.y2), dvdx = g2<IN>(pv, 1, i, nx, K.x2);
+                const double dudx = g2<IN>(pu, 1, i, nx, K.x2), dvdy = g2<IN>(pv, MS_UX, j, ny, Ky2);
+                const double dudy = g2<IN>(pu, MS_UX, j, ny, Ky2), dvdx = g2<IN>(pv, 1, i, nx, K.x2);
                 double e1 = ex[it], e2 = ey[it], e3 = exy[it];
                 if (visc && sol[it]) {
                     e1 = e1 + eta_s * dudx;
@@ -343,27 +346,27 @@ __device__ __forceinline__ void ms_tile(
             if (!ok[it]) continue;
             const long c = (long)j * nx + i;
             const double divx = g2<IN>(&gx[ry + 2][rx + 2], 1, i, nx, K.x2) +
-                                g2<IN>(&gm[ry + 2][rx + 2], MS_GX, j, ny, K.y2);
+                                g2<IN>(&gm[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
             const double divy = g2<IN>(&gm[ry + 2][rx + 2], 1, i, nx, K.x2) +
-                                g2<IN>(&gy[ry + 2][rx + 2], MS_GX, j, ny, K.y2);
+                                g2<IN>(&gy[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
             const double *pu = &su[ry + 3][rx + 3], *pv = &sv[ry + 3][rx + 3];
             const double uc = *pu, vc = *pv;
             const double uadv = -uc * u3<IN>(pu, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * u3<IN>(pu, MS_UX, j, ny, vc, K.y6, K.y1);
+                                vc * u3<IN>(pu, MS_UX, j, ny, vc, Ky6, Ky1);
             const double vadv = -uc * u3<IN>(pv, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * u3<IN>(pv, MS_UX, j, ny, vc, K.y6, K.y1);
+                                vc * u3<IN>(pv, MS_UX, j, ny, vc, Ky6, Ky1);
             // grad2 of p with the operands loaded above (same expressions as grad2)
             double dpx, dpy;
             if (IN) {
                 dpx = divk(pxp[it] - pxm[it], K.x2);
-                dpy = divk(pyp[it] - pym[it], K.y2);
+                dpy = divk(pyp[it] - pym[it], Ky2);
             } else {
             if (i == 0) dpx = divk(-3 * pc[it] + 4 * pxp[it] - p[c + 2], K.x2);
             else if (i == nx - 1) dpx = divk(3 * pc[it] - 4 * pxp[it] + p[c - 2], K.x2);
             else dpx = divk(pxp[it] - pxm[it], K.x2);
-            if (j == 0) dpy = divk(-3 * pc[it] + 4 * pyp[it] - p[c + 2L * nx], K.y2);
-            else if (j == ny - 1) dpy = divk(3 * pc[it] - 4 * pyp[it] + p[c - 2L * nx], K.y2);
-            else dpy = divk(pyp[it] - pym[it], K.y2);
+            if (j == 0) dpy = divk(-3 * pc[it] + 4 * pyp[it] - p[c + 2L * nx], Ky2);
+            else if (j == ny - 1) dpy = divk(3 * pc[it] - 4 * pyp[it] + p[c - 2L * nx], Ky2);
+            else dpy = divk(pyp[it] - pym[it], Ky2);
             }
             const double h = hh[it];
             double k1, k2;
@@ -386,6 +389,10 @@ __device__ __forceinline__ void ms_tile(
     }
 }
 
+// IN: the interior tiles only (the others return), !IN: the others (a host-built list of the
+// tiles a full launch does not cover, or the fix-up list).  Two kernels instead of a branch:
+// the interior body alone fits its registers (no scalar spills).
+template <bool IN, bool SQ>
 __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
@@ -407,17 +414,15 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     }
     __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
     // tlist: the listed tiles only (momentum_fixup); otherwise every tile of rows [jb, je)
-    if (tlist && (int)blockIdx.x >= *tcount) return;
+    if (tlist && (int)blockIdx.x >= (tcount ? *tcount : ntiles)) return;
     const int tile = tlist ? tlist[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
     const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
     // interior tile: its whole 3-cell halo lies inside the grid's interior and the resident
     // rows, so no BC copy and no one-sided edge stencil is ever taken (same arithmetic)
     const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 && j0 - 3 >= max(rw.lo, 2) &&
                           j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
-    if (interior)
-        ms_tile<true>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy);
-    else
-        ms_tile<false>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy);
+    if (interior != IN) return;
+    ms_tile<IN, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy);
 }
 
 // per row j of [jlo, jhi) (out row j - jlo) and 64-column tile tx: all of phi[j][64 tx - 2 .. 64 tx + 66) (the
@@ -455,6 +460,40 @@ __global__ void __launch_bounds__(256) k_fluid_win(const unsigned char *__restri
     out[w] = f;
 }
 
+// The tiles of rows [ws.jb, ws.je) that are not interior (k_mom_stage's test), listed once per
+// (grid, window) on the host and kept on the device (ctx->edge_*).
+static int stage_edge_tiles(rmt_ctx *ctx, RowWin ws, int ntiles, int tiles_x, const int **list,
+                            int *count) {
+    const int nx = ctx->nx, ny = ctx->ny;
+    const long key[6] = {ws.jb, ws.je, ws.lo, ws.hi, nx, ny};
+    int slot = -1;
+    for (int k = 0; k < RMT_EDGE_SLOTS; ++k)
+        if (ctx->edge[k].list && std::equal(key, key + 6, ctx->edge[k].key)) slot = k;
+    if (slot < 0) {
+        std::vector<int> v;
+        for (int t = 0; t < ntiles; ++t) {
+            const int i0 = (t % tiles_x) * MS_TX, j0 = ws.jb + (t / tiles_x) * MS_TY;
+            const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 &&
+                                  j0 - 3 >= std::max(ws.lo, 2) &&
+                                  j0 + MS_TY + 3 <= std::min(ws.hi, ny - 2);
+            if (!interior) v.push_back(t);
+        }
+        slot = ctx->edge_next;
+        ctx->edge_next = (ctx->edge_next + 1) % RMT_EDGE_SLOTS;
+        if (ctx->edge[slot].list) RMT_HIP(hipFree(ctx->edge[slot].list));
+        ctx->edge[slot].list = nullptr;
+        RMT_HIP(hipMalloc(&ctx->edge[slot].list, std::max<size_t>(1, v.size()) * sizeof(int)));
+        if (!v.empty())
+            RMT_HIP(hipMemcpy(ctx->edge[slot].list, v.data(), v.size() * sizeof(int),
+                              hipMemcpyHostToDevice));
+        ctx->edge[slot].n = (int)v.size();
+        std::copy(key, key + 6, ctx->edge[slot].key);
+    }
+    *list = ctx->edge[slot].list;
+    *count = ctx->edge[slot].n;
+    return RMT_OK;
+}
+
 // One fused stage launch: k_{s+1} -> (k1 | k2 | k3)[s], acc1 / acc2 / u* (see MomWork)
 // tlist: tiles of the whole grid (ws.jb = 0), outputs on rows [olo, ohi); else the tiles of
 // rows [ws.jb, ws.je)
@@ -467,12 +506,24 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
     const double coef[4] = {0.0, 0.5 * P->dt, 0.5 * P->dt, P->dt}, dt6 = P->dt / 6.0;
     double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
     const double *kpu = s ? ku[s - 1] : u, *kpv = s ? kv[s - 1] : v;
-    k_mom_stage<<<ntiles, MS_T, 0, ctx->stream>>>(
-        u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, W.solid,
-        P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, nx,
-        tiles_x, ntiles, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, W.k1u, W.k1v,
-        nullptr, nullptr, u_new, v_new, ws, tlist, tcount, W.dtp, olo, ohi, W.k2u, W.k2v,
-        fluid_rows, mom_div(P->dx, P->dy, P->rho_s, P->rho_f));
+    const bool sq = P->dx == P->dy;
+    auto kin = sq ? k_mom_stage<true, true> : k_mom_stage<true, false>;
+    auto kedge = sq ? k_mom_stage<false, true> : k_mom_stage<false, false>;
+    const MomDiv K = mom_div(P->dx, P->dy, P->rho_s, P->rho_f);
+    // the tiles a full launch's interior kernel skips (host list, per row window)
+    const int *elist = tlist, *ecount = tcount;
+    int enb = ntiles;
+    if (!tlist) {
+        RMT_TRY(stage_edge_tiles(ctx, ws, ntiles, tiles_x, &elist, &enb));
+        ecount = nullptr;
+    }
+#define MS_ARGS(TL, TC, NT) u, v, kpu, kpv, coef[s], s, P->bc_kind, P->lid, sxx, sxy, syy, W.H, \
+        W.solid, P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, \
+        nx, tiles_x, NT, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, W.k1u, W.k1v, nullptr, \
+        nullptr, u_new, v_new, ws, TL, TC, W.dtp, olo, ohi, W.k2u, W.k2v, fluid_rows, K
+    kin<<<ntiles, MS_T, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
+    if (enb > 0) kedge<<<enb, MS_T, 0, ctx->stream>>>(MS_ARGS(elist, ecount, enb));
+#undef MS_ARGS
     RMT_LAUNCHED();
     return RMT_OK;
 }

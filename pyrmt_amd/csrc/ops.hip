@@ -592,6 +592,8 @@ int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (ctx->dct) dct_destroy(ctx->dct);
     if (ctx->dct2) dct2_destroy(ctx->dct2);
     if (ctx->per) per_destroy(ctx->per);
+    for (auto &e : ctx->edge)
+        if (e.list) (void)hipFree(e.list);
     delete ctx;
     return RMT_OK;
 }

@@ -83,7 +83,12 @@ struct rmt_ctx {
     // chain's prediction of each fit's latest source (extrap_chain.hip, fast fold); null:
     // the input map
     const double *ex_pred1 = nullptr, *ex_pred2 = nullptr;
+    // momentum.hip: the stage tiles a full launch's interior kernel skips, per row window
+    struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
+    EdgeTiles edge[8];
+    int edge_next = 0;
 };
+#define RMT_EDGE_SLOTS 8
 
 namespace rmt {
 

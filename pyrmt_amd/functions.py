@@ -432,6 +432,18 @@ def compute_viscous_dissipation(a, b, mu_f, phi, w_t, dx, dy, eta_s=0.0):
     return out.value
 
 
+def divergence_2d_interior(u, v, dx, dy, pad=3):
+    """output.py:195-211: (divU, its interior [pad:-pad, pad:-pad]); central differences on
+    the device, 0 within pad cells of every edge."""
+    io = _IO(u, v); u, v = io.dev(u), io.dev(v)
+    out = io.empty(u.shape)
+    c = ctx_for(*u.shape)
+    L.check(L.lib().rmt_divergence_2d_interior(c.bind(), _p(u), _p(v), dx, dy, int(pad), _p(out)),
+            "divergence_2d_interior")
+    d = io.out(out)
+    return d, d[pad:-pad, pad:-pad]
+
+
 # ── projection (functions.py:1005-1364) ──────────────────────────────────────────
 def _rho_scalar(rho):
     """The constant-density branch (functions.py:1298): rho scalar, or an array whose

@@ -677,6 +677,60 @@ def gen_imex(N=32):
          fv=fv, us1=us1, vs1=vs1)
 
 
+# ── 11. output.py:213-321 output_simulation_data (HDF5 writer recorded, not written) ─
+def gen_output(N=33):
+    """The reference's writer on a synthetic deformed-disc state; h5py is replaced by a
+    recorder of its datasets / attrs (h5py is absent here), the CSV and the log line are
+    kept as text."""
+    import contextlib
+    import io
+    rng = np.random.default_rng(11)
+    X, Y, dx, dy = F.create_grid(N, N, 1.0, 1.0)
+    X1 = X + 0.02 * np.sin(2 * np.pi * Y); X2 = Y + 0.015 * np.sin(2 * np.pi * X)
+    phi = np.sqrt((X1 - 0.5) ** 2 + (X2 - 0.5) ** 2) - 0.25
+    solid = (phi <= 0).astype(float)
+    k = 2 * np.pi
+    a = 0.05 * np.sin(k * X) * np.cos(k * Y) + 0.01 * rng.standard_normal((N, N))
+    b = -0.05 * np.cos(k * X) * np.sin(k * Y) + 0.01 * rng.standard_normal((N, N))
+    p = rng.standard_normal((N, N))
+    sxx, sxy, syy, J = (rng.standard_normal((N, N)) for _ in range(4))
+    rec = {}
+
+    class _File:
+        def __init__(self, path, mode):
+            self.path = os.path.basename(path); self.ds = {}; self.attrs = {}
+        def __enter__(self):
+            return self
+        def __exit__(self, *a):
+            rec[self.path] = (self.ds, self.attrs)
+        def create_dataset(self, name, data):
+            self.ds[name] = np.array(data)
+    O.h5py = types.SimpleNamespace(File=_File)
+    kw = dict(mu_s=0.7, mu_f=1e-3, rho_s=1.0, rho_f=1.0, w_t=2 * dx, eta_s=0.02, kappa=0.3,
+              time=0.125, integrated_dissipation=3.5e-4)
+    cwd = os.getcwd()
+    tmp = tempfile.mkdtemp(prefix="rmt_out_")
+    os.chdir(tmp)
+    try:
+        log = io.StringIO()
+        with contextlib.redirect_stdout(log):
+            ret = O.output_simulation_data(dx, dy, phi, solid, X1, X2, a, b, p, 5, "case", 1, 2.5e-3,
+                                           sxx, sxy, syy, J, **kw)
+            O.output_simulation_data(dx, dy, phi, solid, X1, X2, a, b, p, 5, "case", 7, 2.5e-3,
+                                     sxx, sxy, syy, J, **kw)   # not an output step
+            O.output_simulation_data(dx, dy, phi, solid, X1, X2, a, b, p, 5, "case", 10, 2.5e-3,
+                                     sxx, sxy, syy, J, **kw)
+        csv_text = open(os.path.join("outputs", "case", "energy_history.csv")).read()
+    finally:
+        os.chdir(cwd)
+    ds, at = rec["data_000001.h5"]
+    assert set(rec) == {"data_000001.h5", "data_000010.h5"}
+    save("output_sim", N=N, dx=dx, dy=dy, phi=phi, solid=solid, X1=X1, X2=X2, a=a, b=b, p=p,
+         sxx=sxx, sxy=sxy, syy=syy, J=J, ret=ret, csv=csv_text, log=log.getvalue(),
+         **{"kw_" + k: v for k, v in kw.items()},
+         **{"ds_" + k: v for k, v in ds.items()}, **{"at_" + k: v for k, v in at.items()})
+
+
 if __name__ == "__main__":
     if "--only" in sys.argv:     # regenerate the named fixtures only
         for name in sys.argv[sys.argv.index("--only") + 1:]:

@@ -58,3 +58,60 @@ def test_snapshot_of_device_state(gpu, tmp_path):
     assert attrs["t"] == sim.diagnostics()["t"][-1]
     tr = trajectory(sim)
     assert tr.shape == (3, 5) and np.all(np.isfinite(tr))
+
+
+def _osd_args(z):
+    kw = {k[3:]: float(z[k]) for k in z.files if k.startswith("kw_")}
+    return (float(z["dx"]), float(z["dy"]), z["phi"], z["solid"], z["X1"], z["X2"], z["a"],
+            z["b"], z["p"]), (z["sxx"], z["sxy"], z["syy"], z["J"]), kw
+
+
+def test_output_simulation_data_oracle_vs_reference_fixture(oracle):
+    """The fixture (tests/golden/gen_golden.py gen_output: the reference's writer with a
+    recording h5py) against the oracle's restatement: div_vel and the energies bit-exact."""
+    from conftest import golden
+    z = golden("output_sim")
+    (dx, dy, phi, solid, X1, X2, a, b, p), (sxx, sxy, syy, J), kw = _osd_args(z)
+    d, _ = oracle.divergence_2d_interior(a, b, dx, dy, pad=4)
+    np.testing.assert_array_equal(d, z["ds_div_vel"])
+    assert oracle.compute_kinetic_energy(a, b, kw["rho_f"], kw["rho_s"], phi, kw["w_t"], dx, dy) \
+        == float(z["at_kinetic_energy"])
+    assert oracle.compute_strain_energy(X1, X2, phi, kw["mu_s"], dx, dy, kappa=kw["kappa"]) \
+        == float(z["at_strain_energy"])
+
+
+@pytest.mark.gpu
+def test_output_simulation_data_vs_reference(gpu, tmp_path, monkeypatch, capsys):
+    """output.py:213-321 under its own name: the data_NNNNNN file's datasets (div_vel from
+    the device, bit-exact) and attrs (energies at the A26 bars: KE / dissipation 1e-14
+    relative -- device sin in the Heaviside --, SE bit-exact), the CSV rows and the log line
+    against the reference's own output on the same inputs."""
+    from conftest import golden
+    from pyrmt_amd.output import output_simulation_data, read_snapshot
+    z = golden("output_sim")
+    args, tail, kw = _osd_args(z)
+    monkeypatch.chdir(tmp_path)
+    kws = dict(kw)
+    ret = output_simulation_data(*args, 5, "case", 1, 2.5e-3, *tail, **kws)
+    output_simulation_data(*args, 5, "case", 7, 2.5e-3, *tail, **kws)
+    output_simulation_data(*args, 5, "case", 10, 2.5e-3, *tail, **kws)
+    assert ret == float(z["ret"])
+    out = capsys.readouterr().out
+    assert out == str(z["log"])
+    files = sorted(os.listdir(tmp_path / "outputs" / "case"))
+    assert files[0] == "data_000001.h5" or files[0] == "data_000001.npz"
+    assert len([f for f in files if f.startswith("data_")]) == 2
+    ds, at = read_snapshot(str(tmp_path / "outputs" / "case" / files[0]))
+    want_ds = {k[3:]: z[k] for k in z.files if k.startswith("ds_")}
+    assert set(ds) == set(want_ds)
+    for k, v in want_ds.items():
+        np.testing.assert_array_equal(ds[k], v, err_msg=k)
+    want_at = {k[3:]: float(z[k]) for k in z.files if k.startswith("at_")}
+    assert set(at) == set(want_at)
+    for k, v in want_at.items():
+        np.testing.assert_allclose(float(at[k]), v, rtol=1e-14, err_msg=k)
+    got_csv = list(csv.reader(open(tmp_path / "outputs" / "case" / "energy_history.csv")))
+    want_csv = list(csv.reader(io.StringIO(str(z["csv"]))))
+    assert got_csv[0] == want_csv[0] and len(got_csv) == len(want_csv)
+    for g, w in zip(got_csv[1:], want_csv[1:]):
+        np.testing.assert_allclose(np.array(g, float), np.array(w, float), rtol=1e-14)
