@@ -280,14 +280,19 @@ typedef struct {
 
 int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out);
 int rmt_sim_destroy(rmt_sim *sim);
+/* how often (steps, 1 .. 64) rmt_sim_step reads the device diagnostics back (see below) */
+int rmt_sim_set_sync_every(rmt_sim *sim, int k);
 /* field ids: 0 u (a), 1 v (b), 2 p, 3 X1, 4 X2, 5 phi (last rebuilt), 6 J, 7 sigma_xx,
  * 8 sigma_xy, 9 sigma_yy (the solid stress of the last momentum step) */
 int rmt_sim_field(rmt_sim *sim, int field, double **dev_ptr);
 /* Run nsteps loop bodies.  dt comes from compute_timestep on device and is clipped to
  * t_end - t as the drivers do; steps after t >= t_end are no-ops.  Blocks: the diagnostics
- * and flags of the enqueued steps are read back (see rmt_sim_set_sync_every) and errors
- * (non-finite velocity, extrapolation abort) are returned synchronously; the call returns once
- * the last step has finished on the stream. */
+ * and flags of the enqueued steps are read back every rmt_sim_set_sync_every steps (64 by
+ * default) and at the end of the call, and errors (non-finite velocity, extrapolation abort)
+ * are returned then: the diagnostics and t stop at the last good step, while the fields are
+ * those after the last ENQUEUED step (up to sync_every - 1 steps past the failing one; with
+ * sync_every = 1, or a finite t_end, they are the failing step's).  The call returns once the
+ * last step has finished on the stream. */
 int rmt_sim_step(rmt_sim *sim, int nsteps, double t_end);
 /* Phase timers (HIP events on the context stream, accumulated over steps while on):
  * ms[0] dt reduction, [1] advection, [2] extrapolation, [3] momentum (prep + 4 stages +

@@ -111,6 +111,7 @@ SIGNATURES = {
                                       _P, _P]),
     "rmt_sim_create": (_I, [_P, ctypes.POINTER(rmt_sim_params), ctypes.POINTER(_P)]),
     "rmt_sim_destroy": (_I, [_P]),
+    "rmt_sim_set_sync_every": (_I, [_P, _I]),
     "rmt_sim_field": (_I, [_P, _I, ctypes.POINTER(_P)]),
     "rmt_sim_step": (_I, [_P, _I, _D]),
     "rmt_sim_diagnostics": (_I, [_P, ctypes.POINTER(rmt_diag), _I, ctypes.POINTER(_I)]),

@@ -247,6 +247,7 @@ struct ImexPlan {
     double *denom = nullptr;  // 1 - coef * lambda (mac.py:297-298), (rows, cols)
     double2 *buf = nullptr;   // 2M complex per row, the larger axis
     double *T = nullptr;      // transpose scratch
+    std::vector<double> denom_h;   // host copy of denom (source of its async upload)
 };
 
 static bool g_rocfft = false;
@@ -293,25 +294,28 @@ static int axis_make(DstAxis &a, int M, long rows) {
     return RMT_OK;
 }
 
-static ImexPlan *g_plans[2] = {nullptr, nullptr};   // per kind (u, v); one device, one stream
-
+// the plans live on the context (ctx->imex[kind], kind 0 u, 1 v), freed with it
 static void plan_destroy(ImexPlan *P) {
     if (!P) return;
     axis_destroy(P->ax[0]); axis_destroy(P->ax[1]);
     (void)hipFree(P->denom); (void)hipFree(P->buf); (void)hipFree(P->T);
     delete P;
 }
+void imex_destroy(rmt_ctx *ctx) {
+    for (auto &p : ctx->imex) { plan_destroy((ImexPlan *)p); p = nullptr; }
+}
 
 // the plan of kind for (ny, nx, dx, dy, coef); denom as mac.py:278-298 (np.cos -> cos)
-static int imex_plan(int kind, int ny, int nx, double dx, double dy, double coef, ImexPlan **out) {
-    ImexPlan *P = g_plans[kind];
+static int imex_plan(rmt_ctx *ctx, int kind, int ny, int nx, double dx, double dy, double coef,
+                     ImexPlan **out) {
+    ImexPlan *P = (ImexPlan *)ctx->imex[kind];
     if (P && P->ny == ny && P->nx == nx && P->dx == dx && P->dy == dy && P->coef == coef) {
         *out = P;
         return RMT_OK;
     }
     if (!g_rocfft) { RMT_TRY(rfok(rocfft_setup(), "setup")); g_rocfft = true; }
     const bool keep = P && P->ny == ny && P->nx == nx;
-    if (!keep) { plan_destroy(P); P = new ImexPlan; g_plans[kind] = P; }
+    if (!keep) { plan_destroy(P); P = new ImexPlan; ctx->imex[kind] = P; }
     P->ny = ny; P->nx = nx; P->kind = kind; P->dx = dx; P->dy = dy; P->coef = coef;
     const int R = kind == 0 ? ny : ny - 1, C = kind == 0 ? nx - 1 : nx;   // interior shape
     if (!keep) {
@@ -322,13 +326,16 @@ static int imex_plan(int kind, int ny, int nx, double dx, double dy, double coef
         RMT_HIP(hipMalloc(&P->denom, (size_t)R * C * sizeof(double)));
     }
     // mac.py:278-284: lambda = ly[:, None] + lx[None, :], ly/lx = -2 (1 - cos(pi (k+1)/N)) / h**2
-    std::vector<double> lx(C), ly(R), d((size_t)R * C);
+    std::vector<double> lx(C), ly(R);
+    std::vector<double> &d = P->denom_h;   // kept: the async upload reads it
+    d.assign((size_t)R * C, 0.0);
     const double dx2 = std::pow(dx, 2.0), dy2 = std::pow(dy, 2.0);
     for (int k = 0; k < C; ++k) lx[k] = -2.0 * (1.0 - std::cos(M_PI * (k + 1) / C)) / dx2;
     for (int k = 0; k < R; ++k) ly[k] = -2.0 * (1.0 - std::cos(M_PI * (k + 1) / R)) / dy2;
     for (int r = 0; r < R; ++r)
         for (int c = 0; c < C; ++c) d[(size_t)r * C + c] = 1.0 - coef * (ly[r] + lx[c]);
-    RMT_HIP(hipMemcpy(P->denom, d.data(), d.size() * sizeof(double), hipMemcpyHostToDevice));
+    RMT_HIP(hipMemcpyAsync(P->denom, d.data(), d.size() * sizeof(double), hipMemcpyHostToDevice,
+                           ctx->stream));
     *out = P;
     return RMT_OK;
 }
@@ -380,7 +387,7 @@ static int helmholtz(rmt_ctx *ctx, int kind, const double *b, double coef, doubl
     const long n = kind == 0 ? (long)ny * (nx - 1) : (long)(ny - 1) * nx;
     hipStream_t st = ctx->stream;
     ImexPlan *P = nullptr;
-    if (precond) RMT_TRY(imex_plan(kind, ny, nx, dx, dy, coef, &P));
+    if (precond) RMT_TRY(imex_plan(ctx, kind, ny, nx, dx, dy, coef, &P));
     const double dx2 = std::pow(dx, 2.0), dy2 = std::pow(dy, 2.0);
     double *w = nullptr;
     RMT_HIP(hipMallocAsync((void **)&w, (4 * n + IM_BLOCKS + IS_N) * sizeof(double), st));

@@ -594,6 +594,7 @@ int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (ctx->per) per_destroy(ctx->per);
     for (auto &e : ctx->edge)
         if (e.list) (void)hipFree(e.list);
+    imex_destroy(ctx);
     delete ctx;
     return RMT_OK;
 }

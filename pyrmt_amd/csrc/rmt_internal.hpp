@@ -87,6 +87,7 @@ struct rmt_ctx {
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
     EdgeTiles edge[8];
     int edge_next = 0;
+    void *imex[2] = {nullptr, nullptr};   // imex.hip: the DST preconditioner plans (u, v)
 };
 #define RMT_EDGE_SLOTS 8
 
@@ -627,6 +628,7 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
 int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
                   int *dev_status);
 size_t extrap_workspace(int ny, int nx, int max_layers, bool px = false);   // ctx->bytes used
+void imex_destroy(rmt_ctx *ctx);   // imex.hip: the context's DST plans
 // the parallel extrapolation mode (extrap_par.hip; rmt_extrap_set_parallel or the environment
 // variable RMT_EXTRAP_PARALLEL=1): the fits solved as one sparse triangular system by
 // segments instead of the exact raster-order chain -- not bit-exact, see extrap_par.hip

@@ -69,6 +69,7 @@ struct rmt_sim {
     int *segs = nullptr;     // rim row segments (k_rim_segments): ny * ceil(nx / 256) + count
     unsigned long long *m2acc = nullptr;   // k_dt_part's atomic max + block counter (zeroed)
     bool prof = false;
+    int sync_every = rmt::RING_N;   // rmt_sim_set_sync_every
     hipEvent_t pev[7] = {};
     double ms[8] = {};
     long calls[8] = {};
@@ -1009,7 +1010,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
             RMT_LAUNCHED();
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
-            if (++slot == RING_N) RMT_TRY(flush());
+            if (++slot == S->sync_every) RMT_TRY(flush());
             continue;
         }
         k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, S->dscr);
@@ -1019,7 +1020,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
             RMT_LAUNCHED();
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
-            if (++slot == RING_N) RMT_TRY(flush());
+            if (++slot == S->sync_every) RMT_TRY(flush());
             continue;
         }
         k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, sc + 2);
@@ -1047,6 +1048,13 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         RMT_TRY(sim_record(S, dv, hv[0], dt, fl));
     }
     return flush();
+}
+
+int rmt_sim_set_sync_every(rmt_sim *S, int k) {
+    RMT_CHECK(S, RMT_EINVAL, "null sim");
+    RMT_CHECK(k >= 1 && k <= RING_N, RMT_EINVAL, "rmt_sim_set_sync_every: k must be 1 .. 64");
+    S->sync_every = k;
+    return RMT_OK;
 }
 
 int rmt_sim_set_profiling(rmt_sim *S, int on) {

@@ -542,9 +542,11 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
     rmt_ctx *ctx = S->ctx;
     const rmt_sim_params &P = S->P;
     const int NX = S->NX, jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
-    RMT_CHECK(!S->interior || dt == S->dt_cur, RMT_EINVAL, "slab advect: dt differs");
+    // the per-step state is consumed before any check, so a failed call cannot leak into the
+    // next step
     const bool in = S->interior;
     S->interior = false;
+    RMT_CHECK(!in || dt == S->dt_cur, RMT_EINVAL, "slab advect: dt differs");
     S->dt_cur = dt;
     if (!in) RMT_HIP(hipMemsetAsync(S->flags, 0, 8 * sizeof(int), ctx->stream));
     // max |u|^2 over the resident rows: bounds every velocity sample of the backtraces
@@ -586,7 +588,7 @@ int rmt_slab_extrapolate(rmt_slab *S, const double *gathered, const long long *c
                                         P.dx, P.dy, P.layers, S->flags + 4, S->gv(S->X1n),
                                         S->gv(S->X2n), (long)S->lo * S->NX, (long)S->hi * S->NX);
     ctx->ev_chain = nullptr;
-    RMT_TRY(es);
+    if (es != RMT_OK) { S->spec = false; return es; }
     if (!S->spec) {
         k_slab_phi<<<grid1d((long)(je - jb) * S->NX, 256), 256, 0, ctx->stream>>>(
             S->gv(S->X1n), S->gv(S->X2n), P.x0, P.y0, P.R, S->NX, jb, je, S->gv(S->phi),

@@ -381,7 +381,7 @@ def velocity_rhs_blended_optimized(u, v, p, sigma_sxx_s_elastic, sigma_sxy_s_ela
     def full(a):
         if isinstance(a, torch.Tensor):
             return a.expand(shape) if a.dim() < 2 else a
-        return np.broadcast_to(np.asarray(a, dtype=np.float64), shape)
+        return np.array(np.broadcast_to(np.asarray(a, dtype=np.float64), shape))   # writable copy
 
     zero_f = all(np.ndim(f) == 0 and float(f) == 0.0 and not isinstance(f, torch.Tensor)
                  for f in (st_force_x, st_force_y))

@@ -207,8 +207,6 @@ def momentum_predictor_lid_imex(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None, r
                                 rtol=1e-8, cs2=0.0):
     """mac.py:319-369: explicit central advection + face forces, implicit (backward-Euler)
     viscosity (+ the trapezoidal elastic term, cs2 > 0) by DST-preconditioned CG."""
-    if (fu is None) != (fv is None):
-        raise NotImplementedError("momentum_predictor_lid_imex: give both face forces or neither")
     io = _IO(u, v); ud = io.dev(u); vd = io.dev(v)
     fud, fvd = io.dev(fu), io.dev(fv)
     us = io.empty(ud.shape); vs = io.empty(vd.shape)
@@ -226,9 +224,6 @@ def momentum_predictor_lid_semilag(u, v, nu, dx, dy, dt, U_lid, fu=None, fv=None
     CFL <= cfl_switch (mac.py:387-390), else the semi-Lagrangian midpoint backtrace through
     cubic-spline interpolation (map_coordinates order 3, 'nearest') and the same PCG
     viscosity solve."""
-    if (fu is None) != (fv is None):
-        raise NotImplementedError("momentum_predictor_lid_semilag: give both face forces or "
-                                  "neither")
     io = _IO(u, v); ud = io.dev(u); vd = io.dev(v)
     cfl = dt * max(float(ud.abs().max()) / dx, float(vd.abs().max()) / dy)
     if cfl <= cfl_switch:

@@ -86,6 +86,12 @@ class Simulation:
     PHASES = ("dt", "advect", "extrapolate", "momentum", "projection", "diagnostics",
               "rk4_stage_kernels", "extrap_sweep_kernel")
 
+    def set_sync_every(self, k):
+        """Read the device diagnostics / error flags back every k steps (1..64; default 64).
+        An error is raised at the next read-back; the fields are then those of the last
+        enqueued step (k = 1: the failing step's)."""
+        L.check(L.lib().rmt_sim_set_sync_every(self.h, int(k)), "rmt_sim_set_sync_every")
+
     def set_profiling(self, on=True):
         L.check(L.lib().rmt_sim_set_profiling(self.h, int(bool(on))))
 

@@ -71,6 +71,18 @@ def test_imex_predictor_vs_reference(M):
     _close(us2, g["us0"]); _close(vs2, g["vs0"])
 
 
+def test_imex_predictor_one_force_vs_oracle(M, MO):
+    """mac.py:345 / :361 apply fu and fv independently: only one of them given (the other
+    face kind gets no force) against the oracle's restatement."""
+    g = golden("imex")
+    dx, dy = float(g["dx"]), float(g["dy"])
+    args = (g["u"], g["v"], float(g["nu"]), dx, dy, float(g["dt"]), float(g["U_lid"]))
+    for kw in (dict(fu=g["fu"]), dict(fv=g["fv"])):
+        us, vs = M.momentum_predictor_lid_imex(*args, rho=1.3, **kw)
+        uo, vo = MO.momentum_predictor_lid_imex(*args, rho=1.3, **kw)
+        _close(us, uo); _close(vs, vo)
+
+
 @pytest.mark.parametrize("N", [64, 128, 256])
 def test_pcg_vs_oracle_sizes(M, MO, N):
     """Odd interior extents (N - 1 = 63, 127 (prime), 255) through the rocFFT DST."""
