@@ -203,11 +203,12 @@ __global__ void __launch_bounds__(64) k_px_seg(ExWs ws, int ML) {
     const int lo = b0 + (g - s0) * PX_K, hi = min(b1, lo + PX_K), n = hi - lo;
     for (int k = lane; k < PX_HT; k += 64) S.tab[k] = -1;
     __syncthreads();
-    // 1. frontier: same-layer sources before lo
-    for (int r = 0; r < n; ++r) {
-        const int t = lo + r, nst = ws.pns[t], nd = ws.pnd[t];
-        for (int k = lane; k < nd; k += 64) {
-            const int s = -ws.pkey[(long)t * PX_S + nst + k] - 1;
+    // 1. frontier: same-layer sources before lo (lane = row: the rows' loads in parallel)
+    if (lane < n) {
+        const int t = lo + lane, nst = ws.pns[t], nd = ws.pnd[t];
+        const int *kb = ws.pkey + (long)t * PX_S + nst;
+        for (int k = 0; k < nd; ++k) {
+            const int s = -kb[k] - 1;
             if (s < lo) {
                 unsigned h = px_h(s) & (PX_HT - 1);
                 int probe = 0;
@@ -258,12 +259,21 @@ __global__ void __launch_bounds__(64) k_px_seg(ExWs ws, int ML) {
         S.pos[h] = rank;
     }
     __syncthreads();
-    // 2. forward substitution, one row per fit
-    for (int r = 0; r < n; ++r) {
-        const int t = lo + r, nst = ws.pns[t], nd = ws.pnd[t];
+    // 2. forward substitution, one row per fit (the next row's sources loaded ahead)
+    int nxt_nd = 0, nxt_key = 0;
+    double nxt_beta = 0.0;
+    auto load_row = [&](int r) {
+        const int t = lo + r, nst = ws.pns[t];
+        nxt_nd = ws.pnd[t];
         const long kb = (long)t * PX_S + nst;
-        const int mykey = lane < nd ? ws.pkey[kb + lane] : 0;
-        const double mybeta = lane < nd ? ws.pbeta[kb + lane] : 0.0;
+        nxt_key = lane < nxt_nd ? ws.pkey[kb + lane] : 0;
+        nxt_beta = lane < nxt_nd ? ws.pbeta[kb + lane] : 0.0;
+    };
+    if (n > 0) load_row(0);
+    for (int r = 0; r < n; ++r) {
+        const int nd = nxt_nd, mykey = nxt_key;
+        const double mybeta = nxt_beta;
+        if (r + 1 < n) load_row(r + 1);
         double m = 0.0, nn = lane == r ? 1.0 : 0.0;
         for (int k = 0; k < nd; ++k) {
             const int s = -__builtin_amdgcn_readlane(mykey, k) - 1;
@@ -344,24 +354,38 @@ __global__ void __launch_bounds__(256) k_px_c(ExWs ws, int L, const double *__re
     }
 }
 
-// d = N c per segment of layer L (lane = row)
-__global__ void __launch_bounds__(64) k_px_d(ExWs ws, int L) {
+// d = N c per segment of layer L: lane = row, the 64 columns split over 4 waves (16 each,
+// combined in wave order), the live rows' d also into the packed block
+__global__ void __launch_bounds__(256) k_px_d(ExWs ws, int L) {
+    __shared__ double part[4][2][64];
     if (ws.ctl[EXC_FALLBACK]) return;
     int s0, ns;
     px_segs(ws.ctl, L, s0, ns);
-    const int g = s0 + blockIdx.x, lane = threadIdx.x;
     if ((int)blockIdx.x >= ns) return;
+    const int g = s0 + blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int *hdr = ws.shdr + (long)g * PX_H;
     if (hdr[4]) return;
     const int lo = hdr[0], n = hdr[1] - lo;
-    const double2 cr = lane < n ? ws.pc[lo + lane] : make_double2(0.0, 0.0);
     const double *NT = ws.sNT + (long)g * PX_K * PX_K;
-    double d1 = 0.0, d2 = 0.0;
-    for (int q = 0; q < n; ++q) {
-        const double nq = NT[q * PX_K + lane];
-        d1 += nq * px_rl(cr.x, q);
-        d2 += nq * px_rl(cr.y, q);
+    double nq[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int q = wv * 16 + k;
+        nq[k] = q < n ? NT[q * PX_K + lane] : 0.0;
     }
+    const double2 cr = lane < n ? ws.pc[lo + lane] : make_double2(0.0, 0.0);
+    double d1 = 0.0, d2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int q = wv * 16 + k;
+        d1 += nq[k] * px_rl(cr.x, q);
+        d2 += nq[k] * px_rl(cr.y, q);
+    }
+    part[wv][0][lane] = d1; part[wv][1][lane] = d2;
+    __syncthreads();
+    if (wv) return;
+    d1 = ((part[0][0][lane] + part[1][0][lane]) + part[2][0][lane]) + part[3][0][lane];
+    d2 = ((part[0][1][lane] + part[1][1][lane]) + part[2][1][lane]) + part[3][1][lane];
     if (lane < n) ws.sd[(long)g * PX_K + lane] = make_double2(d1, d2);
     const bool lv = lane < n && ws.live[lo + lane];
     const u64 lm = __ballot(lv);
@@ -392,6 +416,7 @@ __device__ __forceinline__ double2 px_row(const double *__restrict__ MT, int nF,
 // reports an abort (dev_status[1]).  A frontier id more than PX_RING behind its segment is
 // read through L2 after a fence (the consumer wrote it to pval).
 constexpr int PX_RING = 4096, PX_NS = 10, PX_NP = 15;
+constexpr int PX_FR = 24;   // frontier columns the consumer holds in registers
 constexpr size_t PX_COMB_LDS = PX_RING * 16 + (size_t)PX_NS * PX_PB * 8 + 2 * PX_NS * 4;
 __device__ __forceinline__ double2 px_far(const double2 *p) {
     const double *q = (const double *)p;
@@ -466,9 +491,21 @@ __global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
                 }
             }
         } else if (nL > 0) {
+            // every LDS read of the segment is issued before the first use: the frontier ids,
+            // then (independent of each other) the ring values, the live rows, their d and up
+            // to PX_FR columns of M; the FMAs then run back to back in px_row's order
+            const int s = lane < nF ? (int)B[PXB_F + lane] : lo;
+            const int r = lane < nL ? (int)B[PXB_R + lane] : 0;
+            double2 x = make_double2(0.0, 0.0);
+            double m[PX_FR];
+            if (kind == 0) {
+                if (lane < nL) x = make_double2(B[PXB_D + 2 * lane], B[PXB_D + 2 * lane + 1]);
+#pragma unroll
+                for (int c = 0; c < PX_FR; ++c)
+                    m[c] = (c < nF && lane < nL) ? B[PXB_M + c * nL + lane] : 0.0;
+            }
             double f1 = 0.0, f2 = 0.0;
             {
-                const int s = lane < nF ? (int)B[PXB_F + lane] : lo;
                 const bool far = lane < nF && lo - s > PX_RING;
                 if (__ballot(far)) __threadfence();
                 if (lane < nF) {
@@ -476,15 +513,18 @@ __global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
                     f1 = v.x; f2 = v.y;
                 }
             }
-            const int r = lane < nL ? (int)B[PXB_R + lane] : 0;
-            double2 x;
             if (kind == 0) {
-                x = lane < nL ? make_double2(B[PXB_D + 2 * lane], B[PXB_D + 2 * lane + 1])
-                              : make_double2(0.0, 0.0);
-                for (int c = 0; c < nF; ++c) {
-                    const double m = lane < nL ? B[PXB_M + c * nL + lane] : 0.0;
-                    x.x += m * px_rl(f1, c);
-                    x.y += m * px_rl(f2, c);
+#pragma unroll
+                for (int c = 0; c < PX_FR; ++c) {
+                    if (c < nF) {
+                        x.x += m[c] * px_rl(f1, c);
+                        x.y += m[c] * px_rl(f2, c);
+                    }
+                }
+                for (int c = PX_FR; c < nF; ++c) {   // a wide frontier: the rest from LDS
+                    const double mc = lane < nL ? B[PXB_M + c * nL + lane] : 0.0;
+                    x.x += mc * px_rl(f1, c);
+                    x.y += mc * px_rl(f2, c);
                 }
             } else {   // block too small for this segment's M: its own arrays (same order)
                 x = px_row(ws.sMT + (long)g * PX_F * PX_K, nF, ws.sd[(long)g * PX_K + r], f1, f2,
@@ -551,7 +591,7 @@ int extrap_par_values(rmt_ctx *ctx, const ExWs &ws, double *X1o, double *X2o, in
     const unsigned sb = (unsigned)ws.maxseg;
     for (int L = 0; L < ML; ++L) {
         k_px_c<<<gb, 256, 0, st>>>(ws, L, X1o, X2o);
-        k_px_d<<<sb, 64, 0, st>>>(ws, L);
+        k_px_d<<<sb, 256, 0, st>>>(ws, L);
         k_px_comb<<<1, 64 * (PX_NP + 1), PX_COMB_LDS, st>>>(ws, L, X1o, X2o);
         k_px_out<<<sb, 64, 0, st>>>(ws, L, X1o, X2o);
         RMT_LAUNCHED();

@@ -34,6 +34,22 @@ for s in "$@"; do
             unset RMT_EXTRAP_PARALLEL
             f=$(find "$O/$s" -name "*kernel_stats.csv" | head -1); cp "$f" "$O/${s}_stats.csv"
             cut -d, -f1-4 "$f" | head -16 ;;
+        pmc|pmcpar)   # counter passes (one group each) over a short bench, stage / SL / DCT / px kernels
+            [ "$s" = pmcpar ] && export RMT_EXTRAP_PARALLEL=1
+            RX="k_mom_stage|k_sim_sl|k_dct1|k_px_|k_divergence_rc|k_project_correct|k_mom_prep|k_transpose"
+            timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+                SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES --kernel-include-regex "$RX" \
+                --kernel-trace -T -f csv -d "$O/${s}_sq" -o sq -- python3 bench.py --steps 2 --warmup 1 \
+                --no-cpu-baseline > "$O/${s}_sq.log" 2>&1 || exit 1
+            timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --kernel-trace -T -f csv \
+                -d "$O/${s}_fetch" -o fetch -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline \
+                > "$O/${s}_fetch.log" 2>&1 || exit 1
+            timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_FMA_F64 \
+                --kernel-include-regex "$RX" --kernel-trace -T -f csv \
+                -d "$O/${s}_write" -o write -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline \
+                > "$O/${s}_write.log" 2>&1 || exit 1
+            unset RMT_EXTRAP_PARALLEL
+            echo "pmc passes done" ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

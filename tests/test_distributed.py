@@ -101,3 +101,53 @@ def test_slab_step_two_processes_gloo(gpu):
     match the fused single-domain step."""
     out = _torchrun(2, "dist_step.py", 129, 4, "gloo", timeout=300)
     assert "dist_step ok" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_config4_slab_step_N4096(gpu, G):
+    """Config 4 (soft_disc_in_lid_driven N=4096, 2->4->8 slabs) at its own size: G virtual
+    slabs of 4096/G rows (tree-aligned) in one process, 2 steps, bit-identical to the fused
+    single-domain step (rmt_sim) -- the rim capacity (~70k entries), halo and all-to-all
+    paths at the bench size."""
+    from pyrmt_amd import distributed as D
+    N, K = 4096, 2
+    ref = _fused(gpu, N, K)
+    sim = D.soft_disc_in_lid_driven(N, D.LocalComm(G))
+    sim.step(K)
+    d, r = sim.diagnostics(), ref.diagnostics()
+    np.testing.assert_array_equal(d["dt"], r["dt"])
+    for f in ("u", "v", "p", "X1", "X2"):
+        np.testing.assert_array_equal(sim.gather(f), ref.get(f), err_msg=f)
+    np.testing.assert_array_equal(d["minJ"], r["minJ"])
+    np.testing.assert_array_equal(d["maxJ"], r["maxJ"])
+    np.testing.assert_allclose(d["cx"], r["cx"], rtol=1e-13)
+    assert d["fitted"][-1] > 0
+
+
+@pytest.mark.gpu
+def test_slab_step_two_processes_gloo_N1024(gpu):
+    """The TorchComm path at N=1024 (two processes on cuda:0 over gloo)."""
+    out = _torchrun(2, "dist_step.py", 1024, 3, "gloo", timeout=400)
+    assert "dist_step ok" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 4])
+def test_slab_step_parallel_extrapolation(gpu, G):
+    """The parallel extrapolation mode in the slab step (each rank solves the gathered band,
+    extrap_par.hip): bit-identical to the fused step in the same mode."""
+    from pyrmt_amd import distributed as D
+    N, K = 1024, 4
+    gpu.extrapolation_parallel(True)
+    try:
+        ref = _fused(gpu, N, K)
+        sim = D.soft_disc_in_lid_driven(N, D.LocalComm(G))
+        sim.step(K)
+    finally:
+        gpu.extrapolation_parallel(False)
+    d, r = sim.diagnostics(), ref.diagnostics()
+    np.testing.assert_array_equal(d["dt"], r["dt"])
+    for f in ("u", "v", "p", "X1", "X2"):
+        np.testing.assert_array_equal(sim.gather(f), ref.get(f), err_msg=f)
+    np.testing.assert_allclose(d["cx"], r["cx"], rtol=1e-13)
