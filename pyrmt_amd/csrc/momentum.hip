@@ -545,6 +545,7 @@ struct Rk4Args {
     double dt, lid, mu_f, eta_s, rho_s, rho_f, dx, dy;
     int bc, visc, ny, nx, tiles_x, ntiles, olo, ohi;   // outputs on rows [olo, ohi)
     RowWin rw;
+    MomDiv K;
 };
 constexpr int RK_HL = 8;
 template <int TX, int TY>
@@ -560,7 +561,7 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
     const int tile = A.tlist ? A.tlist[blockIdx.x] : xcd_tile(blockIdx.x, A.ntiles);
     const int ri = (tile % A.tiles_x) * TX - HL, rj = A.rw.jb + (tile / A.tiles_x) * TY - HL;
     const int nx = A.nx, ny = A.ny;
-    const double dx = A.dx, dy = A.dy, h2x = 2 * dx, h2y = 2 * dy;
+    const MomDiv &K = A.K;
     const double dt = A.dtp ? *A.dtp : A.dt;
     // mom_stage's constants: coef {0, dt/2, dt/2, dt}, dt / 6
     const double chalf = 0.5 * dt, dt6 = dt / 6.0;
@@ -589,8 +590,8 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
             ex[m] = A.sxx[c]; ey[m] = A.syy[c]; exy[m] = A.sxy[c]; hh[m] = A.H[c];
             solm |= (unsigned)(A.solid[c] != 0) << m;
             const bool k0 = ok && ly >= HL - 6 && ly < HL + TY + 6 && lx >= HL - 6 && lx < HL + TX + 6;
-            dpx[m] = k0 ? grad2(A.p + c, 1, i, nx, h2x) : 0.0;
-            dpy[m] = k0 ? grad2(A.p + c, nx, j, ny, h2y) : 0.0;
+            dpx[m] = k0 ? grad2k(A.p + c, 1, i, nx, K.x2) : 0.0;
+            dpy[m] = k0 ? grad2k(A.p + c, nx, j, ny, K.y2) : 0.0;
             au[m] = 0.0; av[m] = 0.0;
         }
 #pragma unroll
@@ -615,8 +616,8 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
             if ((okm >> m) & 1) {
                 const double *pu = U + q, *pv = V + q;
-                const double dudx = grad2(pu, 1, i, nx, h2x), dvdy = grad2(pv, RX, j, ny, h2y);
-                const double dudy = grad2(pu, RX, j, ny, h2y), dvdx = grad2(pv, 1, i, nx, h2x);
+                const double dudx = grad2k(pu, 1, i, nx, K.x2), dvdy = grad2k(pv, RX, j, ny, K.y2);
+                const double dudy = grad2k(pu, RX, j, ny, K.y2), dvdx = grad2k(pv, 1, i, nx, K.x2);
                 double e1 = ex[m], e2 = ey[m], e3 = exy[m];
                 if (A.visc && ((solm >> m) & 1)) {
                     e1 = e1 + A.eta_s * dudx;
@@ -642,16 +643,25 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
                 continue;
             const int j = rj + ly, i = ri + lx;
             if (st == 3 && (j < A.olo || j >= A.ohi)) continue;
-            const double divx = grad2(GX + q, 1, i, nx, h2x) + grad2(GM + q, RX, j, ny, h2y);
-            const double divy = grad2(GM + q, 1, i, nx, h2x) + grad2(GY + q, RX, j, ny, h2y);
+            const double divx = grad2k(GX + q, 1, i, nx, K.x2) + grad2k(GM + q, RX, j, ny, K.y2);
+            const double divy = grad2k(GM + q, 1, i, nx, K.x2) + grad2k(GY + q, RX, j, ny, K.y2);
             const double *pu = U + q, *pv = V + q;
             const double uc = *pu, vc = *pv;
-            const double uadv = -uc * upwind3(pu, 1, i, nx, uc, dx) - vc * upwind3(pu, RX, j, ny, vc, dy);
-            const double vadv = -uc * upwind3(pv, 1, i, nx, uc, dx) - vc * upwind3(pv, RX, j, ny, vc, dy);
+            const double uadv = -uc * upwind3k(pu, 1, i, nx, uc, K.x6, K.x1) -
+                                vc * upwind3k(pu, RX, j, ny, vc, K.y6, K.y1);
+            const double vadv = -uc * upwind3k(pv, 1, i, nx, uc, K.x6, K.x1) -
+                                vc * upwind3k(pv, RX, j, ny, vc, K.y6, K.y1);
             const double h = hh[m];
-            const double den = ((1 - h) * A.rho_s + h * A.rho_f) + 1e-12;
-            const double k1 = uadv + (divx + 0.0 - dpx[m]) / den;
-            const double k2 = vadv + (divy + 0.0 - dpy[m]) / den;
+            double k1, k2;
+            if (K.den_const) {   // (1 - h) rho + h rho == rho (MomDiv)
+                const double nu = divx + 0.0 - dpx[m], nv = divy + 0.0 - dpy[m];
+                k1 = uadv + divk(h == h ? nu : h, K.den);
+                k2 = vadv + divk(h == h ? nv : h, K.den);
+            } else {
+                const double den = ((1 - h) * A.rho_s + h * A.rho_f) + 1e-12;
+                k1 = uadv + (divx + 0.0 - dpx[m]) / den;
+                k2 = vadv + (divy + 0.0 - dpy[m]) / den;
+            }
             if (st == 0) {
                 au[m] = k1; av[m] = k2;
             } else if (st < 3) {
@@ -729,13 +739,16 @@ static Rk4Args rk4_args(const rmt_momentum_params *P, const double *u, const dou
     A.dt = P->dt; A.lid = P->lid; A.mu_f = P->mu_f; A.eta_s = P->eta_s; A.rho_s = P->rho_s;
     A.rho_f = P->rho_f; A.dx = P->dx; A.dy = P->dy; A.bc = P->bc_kind;
     A.visc = P->eta_s > 0.0; A.ny = ny; A.nx = nx;
+    A.K = mom_div(P->dx, P->dy, P->rho_s, P->rho_f);
     return A;
 }
 // 0: per-stage kernels (k_mom_stage), 1: temporally blocked RK4 (k_mom_rk4) where the BC
 // allows, 2: unfused per-cell passes (single domain).  Mode 1 moves ~9 planes per RK4 pass
 // instead of ~64 but measured slower at N = 4096 (2.50 vs 2.12 ms full pass, 0.36 vs 0.13 ms
 // fix-up): the fp64 divisions of ~1.7x halo recompute at 3 waves per SIMD are latency-bound.
-static int g_mom_mode = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED")) ? 2 : 0;
+// RMT_MOM_MODE=<mode> (benchmarking) or RMT_MOM_UNFUSED=1 (mode 2)
+static int g_mom_mode = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED")) ? 2 :
+                        getenv("RMT_MOM_MODE") ? atoi(getenv("RMT_MOM_MODE")) : 0;
 constexpr int RK_TX = 48, RK_TY = 32, RK_T = 768;   // full pass: region 64 x 48 (one row a wave)
 
 // Final BC (functions.py:760) on the boundary cells of rows [jb, je) only: the bottom / top
