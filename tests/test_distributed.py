@@ -126,9 +126,11 @@ def test_config4_slab_step_N4096(gpu, G):
 
 
 @pytest.mark.gpu
-def test_slab_step_two_processes_gloo_N1024(gpu):
-    """The TorchComm path at N=1024 (two processes on cuda:0 over gloo)."""
-    out = _torchrun(2, "dist_step.py", 1024, 3, "gloo", timeout=400)
+def test_slab_step_two_processes_gloo_N4096(gpu):
+    """The TorchComm path at config 4's own size (two processes on cuda:0 over gloo, 2 steps).
+    (The slab step's LDS DCT-I needs 2(N-1) to factor into radices <= 23: N = 4096 and 256
+    qualify, 1024 and 2048 do not.)"""
+    out = _torchrun(2, "dist_step.py", 4096, 2, "gloo", timeout=400)
     assert "dist_step ok" in out
 
 
@@ -138,7 +140,7 @@ def test_slab_step_parallel_extrapolation(gpu, G):
     """The parallel extrapolation mode in the slab step (each rank solves the gathered band,
     extrap_par.hip): bit-identical to the fused step in the same mode."""
     from pyrmt_amd import distributed as D
-    N, K = 1024, 4
+    N, K = 256, 6
     gpu.extrapolation_parallel(True)
     try:
         ref = _fused(gpu, N, K)
