@@ -528,6 +528,292 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
     return RMT_OK;
 }
 
+// ------------------------------------------------------------ row-streaming stage ----
+// mode 3: one RK4 stage with the same per-cell arithmetic, in the same order, as k_mom_stage
+// (bit-identical), organised for CDNA: one wave owns a strip of MR_OUT output columns and
+// walks MR_H rows down it.  Lane L holds column x0 - 2 + L (outputs on lanes 2..61); the
+// horizontal neighbours come from wave-wide DPP shifts, the vertical ones from rolling
+// register windows of rows (stage velocity: 7 rows, blended stress: 5, H: 3), so there is no
+// LDS, no barrier and no 2-D halo recompute (1.07x in x, (MR_H + 7) / MR_H in y).  Every
+// global load is issued one row ahead of its use.  Row r of the stage velocity arrives in
+// iteration r; the stress of row r - 2 and the RHS of row r - 4 follow in the same iteration.
+constexpr int MR_OUT = 60, MR_H = 64;
+
+struct MrArgs {
+    const double *u, *v, *kpu, *kpv, *p, *sxx, *sxy, *syy, *H;
+    const unsigned char *solid, *fluid;   // fluid: k_fluid_rows' flags, row lo first (or null)
+    const double *k1u, *k1v, *k2u, *k2v;  // stage 3: k1, k2 (k3 = kpu / kpv)
+    double *ku, *kv, *outu, *outv;
+    const double *dtp;
+    double coef, dt6, lid, mu_f, eta_s, rho_s, rho_f;
+    int stage, bc, visc, ny, nx, tiles_x, nstrips, nchunks;
+    RowWin rw;                            // outputs on rows [rw.jb, rw.je); resident [lo, hi)
+    MomDiv K;
+};
+
+// lane + 1 / lane - 1 of a double across the wave (DPP wave shifts; the edge lane gets 0)
+__device__ __forceinline__ double mr_next(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x130, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double mr_prev(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+// grad2 / upwind3 (rmt_internal.hpp) on the five values f[k-2 .. k+2] of a line, index k of n
+template <bool IN>
+__device__ __forceinline__ double mr_g2(double m2, double m1, double f0, double p1, double p2,
+                                        int k, int n, const DivK &K2) {
+    if (!IN) {
+        if (k == 0) return divk(-3 * f0 + 4 * p1 - p2, K2);
+        if (k == n - 1) return divk(3 * f0 - 4 * m1 + m2, K2);
+    }
+    return divk(p1 - m1, K2);
+}
+template <bool IN>
+__device__ __forceinline__ double mr_u3(double m2, double m1, double f0, double p1, double p2,
+                                        int k, int n, double vel, const DivK &K6,
+                                        const DivK &K1) {
+    if (IN || (k >= 2 && k < n - 2)) {
+        const double a = 2 * p1 + 3 * f0 - 6 * m1 + m2;
+        const double b = -p2 + 6 * p1 - 3 * f0 - 2 * m1;
+        return divk(vel > 0 ? a : b, K6);
+    }
+    if (vel > 0 && k > 0) return divk(f0 - m1, K1);
+    if (vel <= 0 && k < n - 1) return divk(p1 - f0, K1);
+    if (k > 0) return divk(f0 - m1, K1);
+    if (k < n - 1) return divk(p1 - f0, K1);
+    return 0.0;
+}
+
+template <bool IN, bool SQ, bool S3>
+__global__ void __launch_bounds__(256) k_mom_rows(MrArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wid >= A.nstrips * A.nchunks) return;
+    const int strip = wid % A.nstrips, chunk = wid / A.nstrips;
+    const int nx = A.nx, ny = A.ny, lo = A.rw.lo, hi = A.rw.hi;
+    const int x0 = strip * MR_OUT, i = x0 - 2 + lane;
+    const int y0 = A.rw.jb + chunk * MR_H, y1 = min(A.rw.je, y0 + MR_H);
+    // interior wave: every column / row it touches is >= 2 from the domain edges and inside
+    // the resident rows (no BC source, no one-sided stencil, no zero fill)
+    const bool interior = x0 - 2 >= 2 && x0 + 61 <= nx - 3 && y0 - 4 >= max(lo, 2) &&
+                          y1 + 3 <= min(hi, ny - 2) - 1;
+    if (interior != IN) return;
+    const MomDiv &K = A.K;
+    const DivK &Ky2 = SQ ? K.x2 : K.y2, &Ky6 = SQ ? K.x6 : K.y6, &Ky1 = SQ ? K.x1 : K.y1;
+    double coef = A.coef, dt6 = A.dt6;
+    if (A.dtp) {   // the same roundings as mom_stage's host constants
+        const double dt = *A.dtp;
+        coef = A.stage == 0 ? 0.0 : A.stage == 3 ? dt : 0.5 * dt;
+        dt6 = dt / 6.0;
+    }
+    const int stage = S3 ? 3 : A.stage;   // S3: the last stage (u* = u + dt/6 (acc + k4))
+    const bool col_ok = i >= 0 && i < nx;
+    // windows: Wu/Wv rows r-6 .. r (index 6 = newest), S* stress rows r-6 .. r-2, Hw rows
+    // r-6 .. r-2 of H at the stress cells (RHS row r-4 reads index 2)
+    double Wu[7], Wv[7], Sx[5], Sm[5], Sy[5], Hw[5];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) { Wu[q] = 0.0; Wv[q] = 0.0; }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) { Sx[q] = 0.0; Sm[q] = 0.0; Sy[q] = 0.0; Hw[q] = 1.0; }
+    // prefetched operands of the next iteration
+    double na = 0.0, nb = 0.0, nka = 0.0, nkb = 0.0;   // W row r + 1 (at its BC sources)
+    bool nuc = false, nvc = false, nok = false;
+    double nuval = 0.0;
+    double ne1 = 0.0, ne2 = 0.0, ne3 = 0.0, nh = 1.0;  // stress row r - 1 inputs
+    bool nsol = false, nsok = false;
+    auto load_w = [&](int r) {
+        nok = col_ok && r >= lo && r < hi;
+        long cu, cv;
+        if (IN) {
+            nuc = false; nvc = false; nuval = 0.0;
+            cu = cv = (long)r * nx + i;
+        } else {
+            const BCSrc b = bc_source(A.bc, A.lid, nok ? r : 1, nok ? i : 1, ny, nx);
+            nuc = b.u_const; nvc = b.v_const; nuval = b.u_val;
+            cu = nok ? b.u_src : (long)lo * nx; cv = nok ? b.v_src : (long)lo * nx;
+        }
+        na = A.u[cu]; nb = A.v[cv];
+        nka = stage ? A.kpu[cu] : 0.0; nkb = stage ? A.kpv[cv] : 0.0;
+    };
+    auto load_s = [&](int j) {   // stress-row inputs (pure-fluid rows: the constants)
+        nsok = col_ok && j >= lo && j < hi;
+        bool fluid = false;
+        if (A.fluid && j >= lo && j < hi) {
+            const int ta = max(x0 - 1, 0) / 64, tb = min(x0 + 60, nx - 1) / 64;
+            const unsigned char *fr = A.fluid + (long)(j - lo) * A.tiles_x;
+            fluid = fr[ta] && fr[tb];
+        }
+        if (fluid) {
+            ne1 = 0.0; ne2 = 0.0; ne3 = 0.0; nh = 1.0; nsol = false;
+        } else {
+            const long c = nsok ? (long)j * nx + i : (long)lo * nx;
+            ne1 = A.sxx[c]; ne2 = A.syy[c]; ne3 = A.sxy[c]; nh = A.H[c];
+            nsol = A.solid[c] != 0;
+        }
+    };
+    const int r0 = y0 - 4, r1 = y1 + 3;   // W rows [r0, r1], stress rows [y0 - 2, y1 + 1]
+    load_w(r0);
+    load_s(r0 - 2);
+    for (int r = r0; r <= r1; ++r) {
+        // 1. the stage velocity of row r (BC applied), into the window
+        {
+            const double a = na, b = nb, ka = nka, kb = nkb, uval = nuval;
+            const bool ok = nok, uc = nuc, vc = nvc;
+            if (r + 1 <= r1) load_w(r + 1);
+            const double ru = stage == 0 ? a : a + coef * ka;
+            const double rv = stage == 0 ? b : b + coef * kb;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) { Wu[q] = Wu[q + 1]; Wv[q] = Wv[q + 1]; }
+            Wu[6] = !ok ? 0.0 : uc ? uval : ru;
+            Wv[6] = !ok ? 0.0 : vc ? 0.0 : rv;
+        }
+        // 2. the blended stress of row j = r - 2 (rows j-2 .. j+2 of W at indices 2 .. 6)
+        {
+            const int j = r - 2;
+            const double e1i = ne1, e2i = ne2, e3i = ne3, hs = nh;
+            const bool sol = nsol, sok = nsok;
+            load_s(j + 1);
+            double oxx = 0.0, oxy = 0.0, oyy = 0.0;
+            const double u0 = Wu[4], v0 = Wv[4];
+            const double up1 = mr_next(u0), um1 = mr_prev(u0), vp1 = mr_next(v0), vm1 = mr_prev(v0);
+            // (every cross-lane read outside divergent code: all lanes active)
+            double up2 = 0.0, um2 = 0.0, vp2 = 0.0, vm2 = 0.0;
+            if (!IN) { up2 = mr_next(up1); um2 = mr_prev(um1); vp2 = mr_next(vp1); vm2 = mr_prev(vm1); }
+            if (sok && j >= y0 - 2) {
+                const double dudx = mr_g2<IN>(um2, um1, u0, up1, up2, i, nx, K.x2);
+                const double dvdy = mr_g2<IN>(Wv[2], Wv[3], v0, Wv[5], Wv[6], j, ny, Ky2);
+                const double dudy = mr_g2<IN>(Wu[2], Wu[3], u0, Wu[5], Wu[6], j, ny, Ky2);
+                const double dvdx = mr_g2<IN>(vm2, vm1, v0, vp1, vp2, i, nx, K.x2);
+                double e1 = e1i, e2 = e2i, e3 = e3i;
+                if (A.visc && sol) {
+                    e1 = e1 + A.eta_s * dudx;
+                    e2 = e2 + A.eta_s * dvdy;
+                    e3 = e3 + A.eta_s * 0.5 * (dudy + dvdx);
+                }
+                const double h = hs, omh = 1 - h;
+                oxx = h * (2 * A.mu_f * dudx) + omh * e1;
+                oyy = h * (2 * A.mu_f * dvdy) + omh * e2;
+                oxy = h * (A.mu_f * (dudy + dvdx)) + omh * e3;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { Sx[q] = Sx[q + 1]; Sm[q] = Sm[q + 1]; Sy[q] = Sy[q + 1]; Hw[q] = Hw[q + 1]; }
+            Sx[4] = oxx; Sm[4] = oxy; Sy[4] = oyy; Hw[4] = hs;
+        }
+        // 3. the RHS of row j = r - 4: stress rows j-2 .. j+2 at S[0..4], W rows j-2 .. j+2
+        //    at indices 0 .. 4
+        const int j = r - 4;
+        if (j < y0 || j >= y1) continue;
+        const bool out = col_ok && lane >= 2 && lane < 2 + MR_OUT && i < nx;
+        const long c = (long)j * nx + i;
+        // grad p operands (the same expressions as k_mom_stage)
+        double pc = 0.0, pxp = 0.0, pxm = 0.0, pyp = 0.0, pym = 0.0, px2 = 0.0, py2 = 0.0;
+        double x0v = 0.0, y0v = 0.0, x1v = 0.0, y1v = 0.0;
+        if (out) {
+            const bool exd = i == 0 || i == nx - 1, eyd = j == 0 || j == ny - 1;
+            const long sx = i == nx - 1 ? -1 : 1, sy = j == ny - 1 ? -(long)nx : (long)nx;
+            pc = A.p[c];
+            pxp = A.p[c + sx]; pxm = !exd ? A.p[c - 1] : 0.0;
+            pyp = A.p[c + sy]; pym = !eyd ? A.p[c - nx] : 0.0;
+            if (!IN) {
+                if (i == 0) px2 = A.p[c + 2]; else if (i == nx - 1) px2 = A.p[c - 2];
+                if (j == 0) py2 = A.p[c + 2L * nx]; else if (j == ny - 1) py2 = A.p[c - 2L * nx];
+            }
+            if (S3) {
+                x0v = (A.k1u[c] + 2 * A.k2u[c]) + 2 * A.kpu[c];
+                y0v = (A.k1v[c] + 2 * A.k2v[c]) + 2 * A.kpv[c];
+                x1v = A.u[c]; y1v = A.v[c];
+            }
+        }
+        const double gx0 = Sx[2], gm0 = Sm[2], gy0 = Sy[2];
+        const double gxp = mr_next(gx0), gxm = mr_prev(gx0), gmp = mr_next(gm0), gmm = mr_prev(gm0);
+        double gxp2 = 0.0, gxm2 = 0.0, gmp2 = 0.0, gmm2 = 0.0;
+        if (!IN) { gxp2 = mr_next(gxp); gxm2 = mr_prev(gxm); gmp2 = mr_next(gmp); gmm2 = mr_prev(gmm); }
+        const double u0 = Wu[2], v0 = Wv[2];
+        const double up1 = mr_next(u0), um1 = mr_prev(u0), vp1 = mr_next(v0), vm1 = mr_prev(v0);
+        const double up2 = mr_next(up1), um2 = mr_prev(um1), vp2 = mr_next(vp1), vm2 = mr_prev(vm1);
+        if (!out) continue;
+        const double divx = mr_g2<IN>(gxm2, gxm, gx0, gxp, gxp2, i, nx, K.x2) +
+                            mr_g2<IN>(Sm[0], Sm[1], gm0, Sm[3], Sm[4], j, ny, Ky2);
+        const double divy = mr_g2<IN>(gmm2, gmm, gm0, gmp, gmp2, i, nx, K.x2) +
+                            mr_g2<IN>(Sy[0], Sy[1], gy0, Sy[3], Sy[4], j, ny, Ky2);
+        const double uc = u0, vc = v0;
+        const double uadv = -uc * mr_u3<IN>(um2, um1, u0, up1, up2, i, nx, uc, K.x6, K.x1) -
+                            vc * mr_u3<IN>(Wu[0], Wu[1], u0, Wu[3], Wu[4], j, ny, vc, Ky6, Ky1);
+        const double vadv = -uc * mr_u3<IN>(vm2, vm1, v0, vp1, vp2, i, nx, uc, K.x6, K.x1) -
+                            vc * mr_u3<IN>(Wv[0], Wv[1], v0, Wv[3], Wv[4], j, ny, vc, Ky6, Ky1);
+        double dpx, dpy;
+        if (IN) {
+            dpx = divk(pxp - pxm, K.x2);
+            dpy = divk(pyp - pym, Ky2);
+        } else {
+            if (i == 0) dpx = divk(-3 * pc + 4 * pxp - px2, K.x2);
+            else if (i == nx - 1) dpx = divk(3 * pc - 4 * pxp + px2, K.x2);
+            else dpx = divk(pxp - pxm, K.x2);
+            if (j == 0) dpy = divk(-3 * pc + 4 * pyp - py2, Ky2);
+            else if (j == ny - 1) dpy = divk(3 * pc - 4 * pyp + py2, Ky2);
+            else dpy = divk(pyp - pym, Ky2);
+        }
+        const double h = Hw[2];
+        double k1, k2;
+        if (K.den_const) {
+            const double nu = divx + 0.0 - dpx, nv = divy + 0.0 - dpy;
+            k1 = uadv + divk(h == h ? nu : h, K.den);
+            k2 = vadv + divk(h == h ? nv : h, K.den);
+        } else {
+            const double den = ((1 - h) * A.rho_s + h * A.rho_f) + 1e-12;
+            k1 = uadv + (divx + 0.0 - dpx) / den;
+            k2 = vadv + (divy + 0.0 - dpy) / den;
+        }
+        if (!S3) {
+            A.ku[c] = k1; A.kv[c] = k2;
+        } else {
+            A.outu[c] = x1v + dt6 * (x0v + k1);
+            A.outv[c] = y1v + dt6 * (y0v + k2);
+        }
+    }
+}
+
+// one row-streaming stage launch (mode 3) over rows [ws.jb, ws.je); fluid: row flags
+static int mom_rows(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const double *u,
+                    const double *v, const double *p, const double *sxx, const double *sxy,
+                    const double *syy, const MomWork &W, double *u_new, double *v_new,
+                    RowWin ws, const unsigned char *fluid) {
+    const int nx = ctx->nx, ny = ctx->ny;
+    double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
+    MrArgs A{};
+    A.u = u; A.v = v; A.kpu = s ? ku[s - 1] : u; A.kpv = s ? kv[s - 1] : v; A.p = p;
+    A.sxx = sxx; A.sxy = sxy; A.syy = syy; A.H = W.H; A.solid = W.solid; A.fluid = fluid;
+    A.k1u = W.k1u; A.k1v = W.k1v; A.k2u = W.k2u; A.k2v = W.k2v;
+    A.ku = s < 3 ? ku[s] : nullptr; A.kv = s < 3 ? kv[s] : nullptr; A.outu = u_new; A.outv = v_new;
+    A.dtp = W.dtp;
+    A.coef = s == 0 ? 0.0 : s == 3 ? P->dt : 0.5 * P->dt; A.dt6 = P->dt / 6.0;
+    A.lid = P->lid; A.mu_f = P->mu_f; A.eta_s = P->eta_s; A.rho_s = P->rho_s; A.rho_f = P->rho_f;
+    A.stage = s; A.bc = P->bc_kind; A.visc = P->eta_s > 0.0; A.ny = ny; A.nx = nx;
+    A.tiles_x = (nx + MS_TX - 1) / MS_TX;
+    A.nstrips = (nx + MR_OUT - 1) / MR_OUT;
+    A.nchunks = (ws.je - ws.jb + MR_H - 1) / MR_H;
+    A.rw = ws;
+    A.K = mom_div(P->dx, P->dy, P->rho_s, P->rho_f);
+    const long waves = (long)A.nstrips * A.nchunks;
+    if (waves <= 0) return RMT_OK;
+    const unsigned blocks = grid1d(waves, 4);
+    auto launch = [&](auto kin, auto kedge) {
+        kin<<<blocks, 256, 0, ctx->stream>>>(A);
+        kedge<<<blocks, 256, 0, ctx->stream>>>(A);
+    };
+    const bool sq = P->dx == P->dy, s3 = s == 3;
+    if (sq && s3) launch(k_mom_rows<true, true, true>, k_mom_rows<false, true, true>);
+    else if (sq) launch(k_mom_rows<true, true, false>, k_mom_rows<false, true, false>);
+    else if (s3) launch(k_mom_rows<true, false, true>, k_mom_rows<false, false, true>);
+    else launch(k_mom_rows<true, false, false>, k_mom_rows<false, false, false>);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
 // ------------------------------------------------------------ temporally blocked RK4 --
 // The four stages of one TX x TY output tile in one workgroup.  Stage s needs stage s-1 two
 // cells out (upwind3 / grad2 of the blended stress), so on the tile plus an 8-cell halo the
@@ -797,6 +1083,7 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
     const bool unfused = g_mom_mode == 2;
     const bool blocked = g_mom_mode == 1 && P->bc_kind != RMT_BC_PERIODIC;
+    const bool rowstream = g_mom_mode == 3;
     const int tiles_x = (nx + MS_TX - 1) / MS_TX;
     if (blocked) {
         Rk4Args A = rk4_args(P, u, v, p, sxx, sxy, syy, W, u_new, v_new, ny, nx);
@@ -816,11 +1103,15 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
         if (!W.fluid_rows_ready)
             k_fluid_rows<<<grid1d(nw, 4), 256, 0, ctx->stream>>>(phi, thr, nx, tiles_x, w0.lo,
                                                                   w0.hi, fluid_rows);
-        k_fluid_win<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(fluid_rows, tiles_x, w0.lo, w0.hi,
-                                                               fluid_rows + nw);
+        if (!rowstream)
+            k_fluid_win<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(fluid_rows, tiles_x, w0.lo,
+                                                                   w0.hi, fluid_rows + nw);
         RMT_LAUNCHED();
     }
-    for (int s = 0; s < 4 && !unfused && !blocked; ++s) {
+    for (int s = 0; s < 4 && rowstream; ++s)
+        RMT_TRY(mom_rows(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, grow(2 * (3 - s)),
+                         fluid_rows));
+    for (int s = 0; s < 4 && !unfused && !blocked && !rowstream; ++s) {
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
@@ -891,7 +1182,7 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
 using namespace rmt;
 
 extern "C" int rmt_momentum_set_mode(int mode) {
-    RMT_CHECK(mode >= 0 && mode <= 2, RMT_EINVAL, "momentum mode must be 0 .. 2");
+    RMT_CHECK(mode >= 0 && mode <= 3, RMT_EINVAL, "momentum mode must be 0 .. 3");
     rmt::g_mom_mode = mode;
     return RMT_OK;
 }

@@ -7,8 +7,10 @@
 #   bench          20-step bench line (no CPU baseline)
 #   benchpar       the same with RMT_EXTRAP_PARALLEL=1
 #   kt / ktpar     rocprofv3 kernel trace + stats of the 20-step bench (exact / parallel)
+#   env:K=V        export K=V for the following steps
+#   out:SUB        write the following steps' logs under OUT/SUB
 set -o pipefail
-O=gpurun_out/${1:?out}; shift; mkdir -p "$O"; export TMPDIR=/tmp
+BASE=gpurun_out/${1:?out}; O=$BASE; shift; mkdir -p "$O"; export TMPDIR=/tmp
 PYT="python -u -m pytest -v --timeout 240 --timeout-method thread"
 for s in "$@"; do
     echo "== $s $(date +%T)"
@@ -36,7 +38,7 @@ for s in "$@"; do
             cut -d, -f1-4 "$f" | head -16 ;;
         pmc|pmcpar)   # counter passes (one group each) over a short bench, stage / SL / DCT / px kernels
             [ "$s" = pmcpar ] && export RMT_EXTRAP_PARALLEL=1
-            RX="k_mom_stage|k_sim_sl|k_dct1|k_px_|k_divergence_rc|k_project_correct|k_mom_prep|k_transpose"
+            RX="k_mom_stage|k_mom_rows|k_sim_sl|k_dct1|k_px_|k_divergence_rc|k_project_correct|k_mom_prep|k_transpose"
             timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
                 SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES --kernel-include-regex "$RX" \
                 --kernel-trace -T -f csv -d "$O/${s}_sq" -o sq -- python3 bench.py --steps 2 --warmup 1 \
@@ -50,6 +52,8 @@ for s in "$@"; do
                 > "$O/${s}_write.log" 2>&1 || exit 1
             unset RMT_EXTRAP_PARALLEL
             echo "pmc passes done" ;;
+        out:*) O=$BASE/${s#out:}; mkdir -p "$O" ;;
+        env:*) export "${s#env:}"; echo "exported ${s#env:}" ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
