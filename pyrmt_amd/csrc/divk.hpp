@@ -89,4 +89,45 @@ __host__ __device__ __forceinline__ double divk(double x, const DivK &K) {
     return std::copysign(q, x);   // x = -0 with yl < 0: RN(x*yl) = +0 makes q0 = +0
 }
 
+// ---- unchecked form, certified per batch (the stencil kernels' interior paths) ----------
+// divk_nc(x, K) is divk without its per-call range test: equal to x / K.d whenever x is in the
+// certified range (or +-0) and K.rspan != 0.  A kernel certifies its numerators in bulk, not
+// one by one, with the grain argument:
+//   every double y with 2^-800 <= |y| is a multiple of 2^-852 (its ulp is), and so is 0.  A
+//   sum, difference or small-integer multiple of such values is exact or rounds onto a grid
+//   of spacing >= 2^-852 (results below 2^-800 are exact: they fit in 53 bits of 2^-852),
+//   so it is again a multiple of 2^-852: zero, or at least 2^-852 > 2^-900 in magnitude.
+//   With |y| < 2^990 and at most 16 such terms, |sum| < 2^994 < 2^1000.
+// So a numerator formed by additions / small-integer scalings (exact factors 2, 3, 4, 6) of
+// stored values that all passed DivNote (|y| in [2^-800, 2^990) or 0, finite) lies in the
+// certified range; a numerator of any other form (a sum of quotients, ...) is noted itself.
+// A failed note sends the work item (tile phase, cell) to the checked divk: bit-identical
+// either way, the note only picks which one runs.
+__host__ __device__ __forceinline__ double divk_nc(double x, const DivK &K) {
+    const double q0 = std::fma(x, K.yh, x * K.yl);
+    const double t = std::fma(q0, K.d, -x);
+    return std::copysign(std::fma(-t, K.yh, q0), x);
+}
+
+__host__ __device__ __forceinline__ int divk_frexp_exp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_frexp_exp(x);   // 0 for +-0 (and for inf / NaN: the lt test below)
+#else
+    int e = 0;
+    if (std::isfinite(x)) (void)std::frexp(x, &e);
+    return e;
+#endif
+}
+
+// running certificate of the values noted: |y| in [2^-800, 2^990) or y = +-0, none NaN / inf
+struct DivNote {
+    int emin = 0;      // min frexp exponent (|y| >= 2^-800 <=> e >= -799; 0 for y = 0)
+    bool lt = true;    // every |y| < 2^990 (false for inf, NaN)
+    __host__ __device__ __forceinline__ void note(double y) {
+        emin = std::min(emin, divk_frexp_exp(y));
+        lt = lt && std::fabs(y) < 0x1p990;
+    }
+    __host__ __device__ __forceinline__ bool ok() const { return emin >= -799 && lt; }
+};
+
 }  // namespace rmt

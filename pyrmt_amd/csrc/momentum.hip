@@ -167,18 +167,24 @@ __device__ __forceinline__ int xcd_tile(int b, int nb) {
 // interior-tile stencils (IN): the centred branch of grad2 / upwind3 only; upwind3's
 // two numerators are both formed and the one its velocity sign picks is divided (one
 // division, no divergent branch) -- each the expression of rmt_internal.hpp, operand for operand
-template <bool IN>
+// CHK = false: divk_nc on numerators certified in bulk (DivNote, divk.hpp)
+template <bool CHK>
+__device__ __forceinline__ double dk(double x, const DivK &K) {
+    if constexpr (CHK) return divk(x, K);
+    else return divk_nc(x, K);
+}
+template <bool IN, bool CHK = true>
 __device__ __forceinline__ double g2(const double *f, long s, int k, int n, const DivK &K2) {
-    if constexpr (IN) return divk(f[s] - f[-s], K2);
+    if constexpr (IN) return dk<CHK>(f[s] - f[-s], K2);
     else return grad2k(f, s, k, n, K2);
 }
-template <bool IN>
+template <bool IN, bool CHK = true>
 __device__ __forceinline__ double u3(const double *f, long s, int k, int n, double vel,
                                      const DivK &K6, const DivK &K1) {
     if constexpr (IN) {
         const double a = 2 * f[s] + 3 * f[0] - 6 * f[-s] + f[-2 * s];
         const double b = -f[2 * s] + 6 * f[s] - 3 * f[0] - 2 * f[-s];
-        return divk(vel > 0 ? a : b, K6);
+        return dk<CHK>(vel > 0 ? a : b, K6);
     } else {
         return upwind3k(f, s, k, n, vel, K6, K1);
     }
@@ -191,6 +197,7 @@ __device__ __forceinline__ double u3(const double *f, long s, int k, int n, doub
 struct MomDiv {
     DivK x2, y2, x6, y6, x1, y1, den;
     int den_const;
+    int nc;   // every divisor certified (rspan != 0): the unchecked interior path may run
 };
 static MomDiv mom_div(double dx, double dy, double rho_s, double rho_f) {
     MomDiv m;
@@ -201,6 +208,8 @@ static MomDiv mom_div(double dx, double dy, double rho_s, double rho_f) {
     m.den_const = rho_s == rho_f && rho_s > 0.0 && std::isnormal(rho_s) &&
                   std::frexp(rho_s, &e) == 0.5;
     m.den = divk_make(rho_s + 1e-12);
+    m.nc = m.x2.rspan && m.y2.rspan && m.x6.rspan && m.y6.rspan && m.x1.rspan && m.y1.rspan &&
+           (!m.den_const || m.den.rspan);
     return m;
 }
 
@@ -220,7 +229,8 @@ __device__ __forceinline__ void ms_tile(
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
     const unsigned char *__restrict__ fluid_tiles, const MomDiv &K, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
-    double (&gx)[MS_GY][MS_GX], double (&gm)[MS_GY][MS_GX], double (&gy)[MS_GY][MS_GX]) {
+    double (&gx)[MS_GY][MS_GX], double (&gm)[MS_GY][MS_GX], double (&gy)[MS_GY][MS_GX],
+    int (&wfl)[2][MS_T / 64]) {
     const DivK &Ky2 = SQ ? K.x2 : K.y2, &Ky6 = SQ ? K.x6 : K.y6, &Ky1 = SQ ? K.x1 : K.y1;
     // pure-fluid tile (k_fluid_rows / k_fluid_win): every cell the blended stress is formed
     // on has phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not
@@ -286,19 +296,43 @@ __device__ __forceinline__ void ms_tile(
         pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !eyd ? p[c - nx] : 0.0;
         hh[it] = fluid ? 1.0 : H[c];
     }
+    // Interior tiles divide unchecked (divk_nc) when every stored operand of a phase passed
+    // its DivNote: the stage velocity (phase 1) certifies phase 2's numerators and phase 3's
+    // upwind ones, the blended stress (phase 2) phase 3's divergence; the pressure and the
+    // density-division numerators are noted per cell.  Any failed note (per wave, gathered
+    // through wfl) sends the rest of the tile -- or the one cell -- to the checked divk.
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    const int wv = threadIdx.x >> 6;
     // 1. stage velocity (functions.py:714), BC applied
+    {
+        DivNote nt;
 #pragma unroll
-    for (int it = 0; it < MS_NU; ++it) {
-        const int q = threadIdx.x + it * MS_T;
-        if (q >= MS_UX * MS_UY) break;
-        const double ru = stage == 0 ? a[it] : a[it] + coef * ka[it];
-        const double rv = stage == 0 ? b[it] : b[it] + coef * kb[it];
-        (&su[0][0])[q] = !ok1[it] ? 0.0 : uc[it] ? uval[it] : ru;
-        (&sv[0][0])[q] = !ok1[it] ? 0.0 : vc[it] ? 0.0 : rv;
+        for (int it = 0; it < MS_NU; ++it) {
+            const int q = threadIdx.x + it * MS_T;
+            if (q >= MS_UX * MS_UY) break;
+            const double ru = stage == 0 ? a[it] : a[it] + coef * ka[it];
+            const double rv = stage == 0 ? b[it] : b[it] + coef * kb[it];
+            const double su_ = !ok1[it] ? 0.0 : uc[it] ? uval[it] : ru;
+            const double sv_ = !ok1[it] ? 0.0 : vc[it] ? 0.0 : rv;
+            (&su[0][0])[q] = su_;
+            (&sv[0][0])[q] = sv_;
+            if constexpr (IN) { nt.note(su_); nt.note(sv_); }
+        }
+        if constexpr (IN) {
+            const bool bad = __ballot(!nt.ok()) != 0;
+            if (lane0) wfl[0][wv] = bad;
+        }
     }
     __syncthreads();
+    bool chk = !IN || !K.nc;
+    if constexpr (IN) {
+#pragma unroll
+        for (int w = 0; w < MS_T / 64; ++w) chk = chk || wfl[0][w];
+    }
     // 2. blended stress (functions.py:717-735, 906-921)
-    {
+    auto phase2 = [&](auto ctag) {
+        constexpr bool CHK = decltype(ctag)::value;
+        DivNote nt;
 #pragma unroll
         for (int it = 0; it < MS_NG; ++it) {
             const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
@@ -307,8 +341,8 @@ __device__ __forceinline__ void ms_tile(
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
             if (ok2[it]) {
                 const double *pu = &su[ry + 1][rx + 1], *pv = &sv[ry + 1][rx + 1];
-                const double dudx = g2<IN>(pu, 1, i, nx, K.x2), dvdy = g2<IN>(pv, MS_UX, j, ny, Ky2);
-                const double dudy = g2<IN>(pu, MS_UX, j, ny, Ky2), dvdx = g2<IN>(pv, 1, i, nx, K.x2);
+                const double dudx = g2<IN, CHK>(pu, 1, i, nx, K.x2), dvdy = g2<IN, CHK>(pv, MS_UX, j, ny, Ky2);
+                const double dudy = g2<IN, CHK>(pu, MS_UX, j, ny, Ky2), dvdx = g2<IN, CHK>(pv, 1, i, nx, K.x2);
                 double e1 = ex[it], e2 = ey[it], e3 = exy[it];
                 if (visc && sol[it]) {
                     e1 = e1 + eta_s * dudx;
@@ -321,9 +355,26 @@ __device__ __forceinline__ void ms_tile(
                 oxy = h * (mu_f * (dudy + dvdx)) + omh * e3;
             }
             (&gx[0][0])[q] = oxx; (&gm[0][0])[q] = oxy; (&gy[0][0])[q] = oyy;
+            if constexpr (!CHK) { nt.note(oxx); nt.note(oxy); nt.note(oyy); }
         }
+        if constexpr (!CHK) {
+            const bool bad = __ballot(!nt.ok()) != 0;
+            if (lane0) wfl[1][wv] = bad;
+        }
+    };
+    if constexpr (IN) {
+        if (chk) phase2(std::true_type{});
+        else phase2(std::false_type{});
+    } else {
+        phase2(std::true_type{});
     }
     __syncthreads();
+    if constexpr (IN) {
+        if (!chk) {
+#pragma unroll
+            for (int w = 0; w < MS_T / 64; ++w) chk = chk || wfl[1][w];
+        }
+    }
     // 3. RHS and RK4 accumulation (functions.py:923-944, 743-758); stage 3 forms
     // acc = (k1 + 2 k2) + 2 k3 from the three k planes (loaded here: registers)
     {
@@ -339,27 +390,28 @@ __device__ __forceinline__ void ms_tile(
                 x1[it] = u[c]; y1[it] = v[c];
             }
         }
-#pragma unroll
-        for (int it = 0; it < MS_NO; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+        // one output cell: (k1, k2); with CHK = false, *nt notes its own numerators
+        auto cell = [&](auto ctag, int it, int ry, int rx, DivNote *nt) {
+            constexpr bool CHK = decltype(ctag)::value;
             const int j = j0 + ry, i = i0 + rx;
-            if (!ok[it]) continue;
             const long c = (long)j * nx + i;
-            const double divx = g2<IN>(&gx[ry + 2][rx + 2], 1, i, nx, K.x2) +
-                                g2<IN>(&gm[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
-            const double divy = g2<IN>(&gm[ry + 2][rx + 2], 1, i, nx, K.x2) +
-                                g2<IN>(&gy[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
+            const double divx = g2<IN, CHK>(&gx[ry + 2][rx + 2], 1, i, nx, K.x2) +
+                                g2<IN, CHK>(&gm[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
+            const double divy = g2<IN, CHK>(&gm[ry + 2][rx + 2], 1, i, nx, K.x2) +
+                                g2<IN, CHK>(&gy[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
             const double *pu = &su[ry + 3][rx + 3], *pv = &sv[ry + 3][rx + 3];
             const double uc = *pu, vc = *pv;
-            const double uadv = -uc * u3<IN>(pu, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * u3<IN>(pu, MS_UX, j, ny, vc, Ky6, Ky1);
-            const double vadv = -uc * u3<IN>(pv, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * u3<IN>(pv, MS_UX, j, ny, vc, Ky6, Ky1);
+            const double uadv = -uc * u3<IN, CHK>(pu, 1, i, nx, uc, K.x6, K.x1) -
+                                vc * u3<IN, CHK>(pu, MS_UX, j, ny, vc, Ky6, Ky1);
+            const double vadv = -uc * u3<IN, CHK>(pv, 1, i, nx, uc, K.x6, K.x1) -
+                                vc * u3<IN, CHK>(pv, MS_UX, j, ny, vc, Ky6, Ky1);
             // grad2 of p with the operands loaded above (same expressions as grad2)
             double dpx, dpy;
             if (IN) {
-                dpx = divk(pxp[it] - pxm[it], K.x2);
-                dpy = divk(pyp[it] - pym[it], Ky2);
+                const double gxn = pxp[it] - pxm[it], gyn = pyp[it] - pym[it];
+                if constexpr (!CHK) { nt->note(gxn); nt->note(gyn); }
+                dpx = dk<CHK>(gxn, K.x2);
+                dpy = dk<CHK>(gyn, Ky2);
             } else {
             if (i == 0) dpx = divk(-3 * pc[it] + 4 * pxp[it] - p[c + 2], K.x2);
             else if (i == nx - 1) dpx = divk(3 * pc[it] - 4 * pxp[it] + p[c - 2], K.x2);
@@ -372,13 +424,35 @@ __device__ __forceinline__ void ms_tile(
             double k1, k2;
             if (K.den_const) {   // uniform: (1 - h) rho + h rho == rho (MomDiv)
                 const double nu = divx + 0.0 - dpx, nv = divy + 0.0 - dpy;
-                k1 = uadv + divk(h == h ? nu : h, K.den);
-                k2 = vadv + divk(h == h ? nv : h, K.den);
+                const double fu = h == h ? nu : h, fv = h == h ? nv : h;
+                if constexpr (!CHK) { nt->note(fu); nt->note(fv); }
+                k1 = uadv + dk<CHK>(fu, K.den);
+                k2 = vadv + dk<CHK>(fv, K.den);
             } else {
                 const double den = ((1 - h) * rho_s + h * rho_f) + 1e-12;
                 k1 = uadv + (divx + 0.0 - dpx) / den;
                 k2 = vadv + (divy + 0.0 - dpy) / den;
             }
+            return make_double2(k1, k2);
+        };
+#pragma unroll
+        for (int it = 0; it < MS_NO; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+            if (!ok[it]) continue;
+            const long c = (long)(j0 + ry) * nx + i0 + rx;
+            double2 kk;
+            if constexpr (IN) {
+                if (chk) {
+                    kk = cell(std::true_type{}, it, ry, rx, nullptr);
+                } else {
+                    DivNote nt;
+                    kk = cell(std::false_type{}, it, ry, rx, &nt);
+                    if (__builtin_expect(!nt.ok(), 0)) kk = cell(std::true_type{}, it, ry, rx, nullptr);
+                }
+            } else {
+                kk = cell(std::true_type{}, it, ry, rx, nullptr);
+            }
+            const double k1 = kk.x, k2 = kk.y;
             if (stage < 3) {
                 ku[c] = k1; kv[c] = k2;
             } else {
@@ -413,6 +487,7 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
         dt6 = dt / 6.0;
     }
     __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
+    __shared__ int wfl[2][MS_T / 64];   // per-wave failed DivNote flags of phases 1 and 2
     // tlist: the listed tiles only (momentum_fixup); otherwise every tile of rows [jb, je)
     if (tlist && (int)blockIdx.x >= (tcount ? *tcount : ntiles)) return;
     const int tile = tlist ? tlist[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
@@ -422,7 +497,7 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 && j0 - 3 >= max(rw.lo, 2) &&
                           j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
     if (interior != IN) return;
-    ms_tile<IN, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy);
+    ms_tile<IN, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
 }
 
 // per row j of [jlo, jhi) (out row j - jlo) and 64-column tile tx: all of phi[j][64 tx - 2 .. 64 tx + 66) (the

@@ -418,3 +418,48 @@ def test_momentum_modes_bitwise(gpu, shape, bc):
         gpu.momentum_mode(0)
     for o in outs[1:]:
         _eq(o[0], outs[0][0]); _eq(o[1], outs[0][1])
+
+
+def _bits(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64)).view(np.int64)
+
+
+@pytest.mark.parametrize("case", ["tiny", "tiny_band", "nan", "inf", "negzero"])
+def test_momentum_uncertified_operands(gpu, case):
+    """The stage kernel's interior tiles divide unchecked only on operands their DivNotes
+    certify (divk.hpp); the cases here fail the notes in a whole tile (values below 2^-800),
+    in a band of cells, or through one NaN / inf, and must fall back to the checked division:
+    every mode bit-identical to the unfused passes (mode 2), signs of zero included."""
+    ny, nx = 257, 300
+    rng = np.random.default_rng(11)
+    X, Y, dx, dy = gpu.create_grid(nx, ny, 1.0, 1.0)
+    u = rng.standard_normal((ny, nx)) * 0.1
+    v = rng.standard_normal((ny, nx)) * 0.1
+    p = rng.standard_normal((ny, nx))
+    if case == "tiny":
+        u *= 2.0 ** -830; v *= 2.0 ** -830; p *= 2.0 ** -830
+    elif case == "tiny_band":
+        u[100:120] *= 2.0 ** -1000; p[:, 140:150] *= 2.0 ** -1010
+    elif case == "nan":
+        u[130, 150] = np.nan
+    elif case == "inf":
+        v[70, 200] = np.inf
+    elif case == "negzero":
+        u[:, :] = -0.0; v[:, :] = 0.0; p[:, :] = -0.0
+    X1 = X + 1e-3 * rng.standard_normal((ny, nx))
+    X2 = Y + 1e-3 * rng.standard_normal((ny, nx))
+    phi = np.sqrt((X - 0.5) ** 2 + (Y - 0.45) ** 2) - 0.2
+    outs = []
+    try:
+        for mode in (2, 0, 1, 3):
+            gpu.momentum_mode(mode)
+            outs.append(gpu.momentum_step_rk4(u, v, p, X1, X2, gpu.NoSlipLid(1.0), 0.7, 0.3, 0.05,
+                                              dx, dy, 2e-3, 1.0, 1.0, phi, 0.01, 2 * dx,
+                                              stress_band=True, detg_clamp=3.0))
+    finally:
+        gpu.momentum_mode(0)
+    for o in outs[1:]:
+        for k in (0, 1):
+            a, b = _bits(o[k]), _bits(outs[0][k])
+            same = (a == b) | (np.isnan(np.asarray(o[k])) & np.isnan(np.asarray(outs[0][k])))
+            assert same.all(), (case, k, np.argwhere(~same)[:5])

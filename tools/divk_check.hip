@@ -119,9 +119,44 @@ int main(int argc, char **argv) {
                              0x1.fffffffffffffp-901, 0x1p1000, 0x1.fffffffffffffp999, 1e308,
                              INFINITY, -INFINITY, NAN, 1.0, d, -d, 3 * d, d / 3};
         for (double x : sp) check(x, false);
+        // (4) divk_nc on numerators the kernels certify in bulk (divk.hpp, DivNote): sums and
+        // small-integer combinations of noted values, including cancelling pairs near 2^-800
+        long nnc = 0;
+        auto stored = [&]() {
+            const int r = (int)(rng() % 8);
+            if (r == 0) return (rng() & 1) ? 0.0 : -0.0;
+            int ex = r == 1 ? -799 + (int)(rng() % 4) : r == 2 ? 986 + (int)(rng() % 4)
+                                                           : (int)(rng() % 1789) - 799;
+            const double m = 0.5 + (double)(rng() >> 12) * 0x1p-53;   // [0.5, 1)
+            return std::ldexp((rng() & 1) ? -m : m, ex);
+        };
+        for (int i = 0; i < 300000 && K.rspan; ++i) {   // rspan 0: divk_nc is never used
+            double a = stored(), b = stored(), c = stored(), e4 = stored();
+            if (i & 1) b = std::nextafter(a, (rng() & 1) ? INFINITY : -INFINITY);   // cancel
+            rmt::DivNote nt;
+            nt.note(a); nt.note(b); nt.note(c); nt.note(e4);
+            if (!nt.ok()) continue;
+            const double nums[3] = {a - b, 2 * a + 3 * b - 6 * c + e4, -a + 6 * b - 3 * c - 2 * e4};
+            for (double x : nums) {
+                const double q = rmt::divk_nc(x, K), r = x / d;
+                ++nnc;
+                if (bits(q) != bits(r)) {
+                    if (bad < 5) printf("  NC MISMATCH d=%a x=%a nc=%a ieee=%a\n", d, x, q, r);
+                    ++bad;
+                }
+            }
+        }
+        {   // the notes reject what they must
+            rmt::DivNote t1, t2, t3, t4, t5;
+            t1.note(0x1p-801); t2.note(0x1p990); t3.note(NAN); t4.note(-INFINITY); t5.note(0x1p-1074);
+            if (t1.ok() || t2.ok() || t3.ok() || t4.ok() || t5.ok()) { printf("  DivNote accepts out of range\n"); ++bad; }
+            rmt::DivNote t6;
+            t6.note(0.0); t6.note(-0.0); t6.note(0x1p-800); t6.note(-0x1.fffffffffffffp989);
+            if (!t6.ok()) { printf("  DivNote rejects the range's edges\n"); ++bad; }
+        }
         printf("d=%.17g (%a) D=%.17g fast=%d: %ld operands, %ld mismatches; hard cases %ld, "
-               "single-reciprocal Markstein wrong on %ld, x*RN(1/d) on %ld of them\n",
-               d, d, D, K.rspan != 0, n, bad, nhard, nbad, nmul);
+               "single-reciprocal Markstein wrong on %ld, x*RN(1/d) on %ld of them; %ld certified "
+               "numerators unchecked\n", d, d, D, K.rspan != 0, n, bad, nhard, nbad, nmul, nnc);
         total_bad += bad;
     }
     printf("%s\n", total_bad ? "FAIL" : "OK: divk == IEEE division on every operand");
