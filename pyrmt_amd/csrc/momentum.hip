@@ -41,10 +41,11 @@ __global__ void __launch_bounds__(256) k_mom_prep_tiles(
     double *__restrict__ syy, double *__restrict__ J, double *__restrict__ H,
     double *__restrict__ rho, unsigned char *__restrict__ solid, const int *__restrict__ tiles,
     const int *__restrict__ count, int tiles_x, int jlo, int jhi) {
-    if ((int)blockIdx.x >= *count) return;
-    const int t = tiles[blockIdx.x];
-    const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
+    const int cnt = *count;
+    for (int b = blockIdx.x; b < cnt; b += gridDim.x)   // list_grid launch
     for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
+        const int t = tiles[b];
+        const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
         const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
         if (j >= ny || i >= nx || j < jlo || j >= jhi) continue;   // rows [jlo, jhi) only
         const long c = (long)j * nx + i;
@@ -500,6 +501,45 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     ms_tile<IN, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
 }
 
+// The listed tiles (momentum_fixup), interior and edge alike, in one launch of at most
+// LIST_BLOCKS workgroups looping over the list: a fix-up list holds a few hundred tiles, so
+// one round of workgroups covers it and the stage costs one tile's latency, not two launches'.
+template <bool SQ>
+__global__ void __launch_bounds__(MS_T, 2) k_mom_stage_list(
+    const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
+    const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
+    const double *__restrict__ sxx, const double *__restrict__ sxy,
+    const double *__restrict__ syy, const double *__restrict__ H,
+    const unsigned char *__restrict__ solid, int visc, double mu_f, double eta_s, double rho_s,
+    double rho_f, const double *__restrict__ p, double dt6, double dx, double dy, int ny, int nx,
+    int tiles_x, int ntiles, double *__restrict__ ku, double *__restrict__ kv,
+    const double *__restrict__ ainu, const double *__restrict__ ainv, double *__restrict__ accu,
+    double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
+    const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
+    int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
+    const unsigned char *__restrict__ fluid_tiles, MomDiv K) {
+    __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
+    __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
+    __shared__ int wfl[2][MS_T / 64];
+    if (dtp) {
+        const double dt = *dtp;
+        coef = stage == 0 ? 0.0 : stage == 3 ? dt : 0.5 * dt;
+        dt6 = dt / 6.0;
+    }
+    const int cnt = tcount ? *tcount : ntiles;
+    for (int b = blockIdx.x; b < cnt; b += gridDim.x) {
+        const int tile = tlist[b];
+        const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
+        const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 &&
+                              j0 - 3 >= max(rw.lo, 2) && j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
+        if (interior)
+            ms_tile<true, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
+        else
+            ms_tile<false, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
+        __syncthreads();   // the next tile's phase 1 overwrites su / sv
+    }
+}
+
 // per row j of [jlo, jhi) (out row j - jlo) and 64-column tile tx: all of phi[j][64 tx - 2 .. 64 tx + 66) (the
 // columns a stage tile's blended stress is formed on) > thr = max(w_t, w_cut, 0).  One wave
 // per (row, tile); NaN phi is not fluid.
@@ -596,8 +636,13 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
         W.solid, P->eta_s > 0.0, P->mu_f, P->eta_s, P->rho_s, P->rho_f, p, dt6, P->dx, P->dy, ny, \
         nx, tiles_x, NT, s < 3 ? ku[s] : nullptr, s < 3 ? kv[s] : nullptr, W.k1u, W.k1v, nullptr, \
         nullptr, u_new, v_new, ws, TL, TC, W.dtp, olo, ohi, W.k2u, W.k2v, fluid_rows, K
-    kin<<<ntiles, MS_T, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
-    if (enb > 0) kedge<<<enb, MS_T, 0, ctx->stream>>>(MS_ARGS(elist, ecount, enb));
+    if (tlist) {
+        auto kl = sq ? k_mom_stage_list<true> : k_mom_stage_list<false>;
+        kl<<<list_grid(ntiles), MS_T, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
+    } else {
+        kin<<<ntiles, MS_T, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
+        if (enb > 0) kedge<<<enb, MS_T, 0, ctx->stream>>>(MS_ARGS(elist, ecount, enb));
+    }
 #undef MS_ARGS
     RMT_LAUNCHED();
     return RMT_OK;
@@ -1230,7 +1275,7 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
     // the rows momentum_rk4 computes for this window: prep on w0 +- 7, stage s on w0 +- 2(3-s)
     const RowWin w0 = win ? *win : RowWin{0, ny, 0, ny};
     auto grow = [&](int m) { return std::pair<int, int>{std::max(w0.jb - m, 0), std::min(w0.je + m, ny)}; };
-    k_mom_prep_tiles<<<max_tiles, 256, 0, ctx->stream>>>(
+    k_mom_prep_tiles<<<list_grid(max_tiles), 256, 0, ctx->stream>>>(
         X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
         P->rho_f, sxx, sxy, syy, J, W.H, nullptr, W.solid, tiles, count, tiles_x, grow(7).first,
         grow(7).second);

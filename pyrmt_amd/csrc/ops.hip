@@ -420,16 +420,18 @@ __global__ void __launch_bounds__(256) k_divergence_tiles(
     int ny, int nx, RcDiv K, double *__restrict__ divU, double rho, double dt,
     const double *__restrict__ dtp, const int *__restrict__ tiles,
     const int *__restrict__ count, int tiles_x) {
-    if ((int)blockIdx.x >= *count) return;
     if (dtp) dt = *dtp;
     const double d_f = dt / rho;   // as the host's dt / rho
-    const int t = tiles[blockIdx.x];
-    const int i0 = (t % tiles_x) * MOM_TX - 1, j0 = (t / tiles_x) * MOM_TY - 1;
+    const int cnt = *count;
     constexpr int TW = MOM_TX + 2, TH = MOM_TY + 2;
-    for (int e = threadIdx.x; e < TW * TH; e += blockDim.x) {
-        const int j = j0 + e / TW, i = i0 + e % TW;
-        if (j >= 0 && j < ny && i >= 0 && i < nx)
-            div_rc_cell(a, b, p, ny, nx, d_f, K, divU, rho, dt, j, i);
+    for (int bk = blockIdx.x; bk < cnt; bk += gridDim.x) {   // list_grid launch
+        const int t = tiles[bk];
+        const int i0 = (t % tiles_x) * MOM_TX - 1, j0 = (t / tiles_x) * MOM_TY - 1;
+        for (int e = threadIdx.x; e < TW * TH; e += blockDim.x) {
+            const int j = j0 + e / TW, i = i0 + e % TW;
+            if (j >= 0 && j < ny && i >= 0 && i < nx)
+                div_rc_cell(a, b, p, ny, nx, d_f, K, divU, rho, dt, j, i);
+        }
     }
 }
 __global__ void k_divergence_central(const double *__restrict__ a, const double *__restrict__ b,
@@ -826,7 +828,7 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
     RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
     double *rhs = ctx->scratch, *pc = rhs + n;
     if (tiles)   // the rhs of the other cells of the marked rows is still in scratch
-        k_divergence_tiles<<<max_tiles, 256, 0, ctx->stream>>>(
+        k_divergence_tiles<<<list_grid(max_tiles), 256, 0, ctx->stream>>>(
             a_star, b_star, p_prev, ctx->ny, ctx->nx, rc_div(dx, dy), rhs, rho, dt, dtp, tiles, tcount,
             (ctx->nx + MOM_TX - 1) / MOM_TX);
     else

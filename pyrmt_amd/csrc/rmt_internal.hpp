@@ -16,6 +16,14 @@
 
 namespace rmt {
 
+// Workgroups of a launch over a device-side tile list (count on the device): kernels loop
+// b = blockIdx.x, b + gridDim.x, ... < *count; a fix-up list is a few hundred tiles, and a
+// launch of max_tiles mostly-empty workgroups costs its dispatch.
+constexpr int LIST_BLOCKS = 1024;
+inline unsigned list_grid(long max_tiles) {
+    return (unsigned)std::max(1L, std::min<long>(max_tiles, LIST_BLOCKS));
+}
+
 // NaN-propagating max (a NaN operand wins; fmax would drop it)
 __host__ __device__ __forceinline__ double nanmax(double a, double b) {
     return (a != a || b != b) ? (a + b) : (a > b ? a : b);

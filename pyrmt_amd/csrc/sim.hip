@@ -303,10 +303,11 @@ __global__ void __launch_bounds__(256) k_phi_tiles(const double *__restrict__ X1
                                                    const int *__restrict__ tiles,
                                                    const int *__restrict__ count, int tiles_x,
                                                    unsigned long long *__restrict__ nbits) {
-    if ((int)blockIdx.x >= *count) return;
-    const int t = tiles[blockIdx.x];
-    const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
+    const int cnt = *count;
+    for (int b = blockIdx.x; b < cnt; b += gridDim.x)   // list_grid launch
     for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
+        const int t = tiles[b];
+        const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
         const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
         bool known = false;
         if (j < ny && i < nx) {
@@ -371,10 +372,11 @@ __global__ void __launch_bounds__(256) k_dt_part(const double *__restrict__ part
 // (u*, v* at j-1 .. j+1) the tile re-run can change
 __global__ void k_mark_rows(const int *__restrict__ tiles, const int *__restrict__ count,
                             int tiles_x, int ny, unsigned char *__restrict__ rowmark) {
-    if ((int)blockIdx.x >= *count) return;
-    const int j0 = (tiles[blockIdx.x] / tiles_x) * MOM_TY - 1;
-    const int j = j0 + (int)threadIdx.x;
-    if (threadIdx.x < MOM_TY + 2 && j >= 0 && j < ny) rowmark[j] = 1;
+    const int cnt = *count;
+    for (int b = blockIdx.x; b < cnt; b += gridDim.x) {   // list_grid launch
+        const int j = (tiles[b] / tiles_x) * MOM_TY - 1 + (int)threadIdx.x;
+        if (threadIdx.x < MOM_TY + 2 && j >= 0 && j < ny) rowmark[j] = 1;
+    }
 }
 // completes a ring record after k_diag_p2 wrote its diagnostics: max |u|^2, dt, flags
 __global__ void k_ring_put(const double *__restrict__ sc, const int *__restrict__ flag,
@@ -868,7 +870,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 RMT_TRY(fs);
                 if (S->split_proj) {
                     RMT_HIP(hipMemsetAsync(S->rowmark, 0, ny, S->st2));
-                    k_mark_rows<<<S->max_tiles, 64, 0, S->st2>>>(
+                    k_mark_rows<<<list_grid(S->max_tiles), 64, 0, S->st2>>>(
                         S->tiles, S->tcount, (nx + MOM_TX - 1) / MOM_TX, ny, S->rowmark);
                     RMT_LAUNCHED();
                 }
@@ -923,7 +925,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // 4 + 5 on the tiles the extrapolation can reach
             RMT_HIP(hipStreamWaitEvent(st, S->e_mom, 0));
             const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
-            k_phi_tiles<<<S->max_tiles, 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
+            k_phi_tiles<<<list_grid(S->max_tiles), 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
                                                        S->phi, S->X1, S->X2, S->tiles, S->tcount,
                                                        tiles_x, nb);
             RMT_LAUNCHED();
