@@ -244,58 +244,99 @@ __device__ __forceinline__ void ms_tile(
     bool ok1[MS_NU], uc[MS_NU], vc[MS_NU];
     double uval[MS_NU];
     double ex[MS_NG], ey[MS_NG], exy[MS_NG], hh2[MS_NG];
-    bool sol[MS_NG], ok2[MS_NG];
+    int sol[MS_NG];   // the solid byte, tested where phase 2 uses it (not at the load)
+    bool ok2[MS_NG];
     double pc[MS_NO], pxm[MS_NO], pxp[MS_NO], pym[MS_NO], pyp[MS_NO], hh[MS_NO];
     bool ok[MS_NO];
-    {
+    if constexpr (IN) {
+        // interior tile: every operand cell lies in the grid and the resident rows, every BC
+        // kind is the identity there; addresses are a uniform tile base + a 32-bit offset
+        const long b1 = (long)(j0 - 3) * nx + (i0 - 3), b2 = b1 + nx + 1, b3 = b2 + 2L * nx + 2;
+        const double *u1 = u + b1, *v1 = v + b1, *ku1 = kpu + b1, *kv1 = kpv + b1;
 #pragma unroll
         for (int it = 0; it < MS_NU; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q % MS_UX;
-            const int j = j0 - 3 + ry, i = i0 - 3 + rx;
-            ok1[it] = q < MS_UX * MS_UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
-            long cu, cv;
-            if constexpr (IN) {   // interior cell: every BC kind is the identity there
-                uc[it] = false; vc[it] = false; uval[it] = 0.0;
-                cu = cv = ok1[it] ? (long)j * nx + i : (long)rw.lo * nx;
-            } else {
-                const BCSrc s = bc_source(bc, lid, ok1[it] ? j : 1, ok1[it] ? i : 1, ny, nx);
-                uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
-                cu = ok1[it] ? s.u_src : (long)rw.lo * nx; cv = ok1[it] ? s.v_src : (long)rw.lo * nx;
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q - ry * MS_UX;
+            ok1[it] = q < MS_UX * MS_UY;
+            const int o = ok1[it] ? ry * nx + rx : 0;
+            uc[it] = false; vc[it] = false; uval[it] = 0.0;
+            a[it] = u1[o]; b[it] = v1[o];
+            ka[it] = stage ? ku1[o] : 0.0; kb[it] = stage ? kv1[o] : 0.0;
+        }
+        // a pure-fluid tile reads every operand from its first output cell (j0, i0) instead,
+        // which prep wrote (an output row) and which is fluid (0, 0, 0, H = 1, not solid):
+        // one cached line, and no branch, so no load result is consumed before the barrier
+        const double *sxx2 = sxx + b2, *syy2 = syy + b2, *sxy2 = sxy + b2, *H2 = H + b2;
+        const unsigned char *sol2 = solid + b2;
+        const int ofl = 2 * nx + 2;   // (j0, i0) from the stress region's corner
+#pragma unroll
+        for (int it = 0; it < MS_NG; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q - ry * MS_GX;
+            ok2[it] = q < MS_GX * MS_GY;
+            const int o = fluid ? ofl : ok2[it] ? ry * nx + rx : 0;
+            ex[it] = sxx2[o]; ey[it] = syy2[o]; exy[it] = sxy2[o]; hh2[it] = H2[o];
+            sol[it] = sol2[o];
+        }
+        const double *p3 = p + b3, *H3 = H + b3;
+#pragma unroll
+        for (int it = 0; it < MS_NO; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q - ry * MS_TX;
+            ok[it] = q < MS_TX * MS_TY && j0 + ry >= olo && j0 + ry < ohi;   // output rows
+            const int o = ok[it] ? ry * nx + rx : 0;
+            pc[it] = p3[o]; pxp[it] = p3[o + 1]; pxm[it] = p3[o - 1];
+            pyp[it] = p3[o + nx]; pym[it] = p3[o - nx];
+            hh[it] = H3[fluid ? 0 : o];
+        }
+    } else {
+    {
+    #pragma unroll
+            for (int it = 0; it < MS_NU; ++it) {
+                const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q % MS_UX;
+                const int j = j0 - 3 + ry, i = i0 - 3 + rx;
+                ok1[it] = q < MS_UX * MS_UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
+                long cu, cv;
+                if constexpr (IN) {   // interior cell: every BC kind is the identity there
+                    uc[it] = false; vc[it] = false; uval[it] = 0.0;
+                    cu = cv = ok1[it] ? (long)j * nx + i : (long)rw.lo * nx;
+                } else {
+                    const BCSrc s = bc_source(bc, lid, ok1[it] ? j : 1, ok1[it] ? i : 1, ny, nx);
+                    uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
+                    cu = ok1[it] ? s.u_src : (long)rw.lo * nx; cv = ok1[it] ? s.v_src : (long)rw.lo * nx;
+                }
+                a[it] = u[cu]; b[it] = v[cv];
+                ka[it] = stage ? kpu[cu] : 0.0; kb[it] = stage ? kpv[cv] : 0.0;
             }
-            a[it] = u[cu]; b[it] = v[cv];
-            ka[it] = stage ? kpu[cu] : 0.0; kb[it] = stage ? kpv[cv] : 0.0;
         }
-    }
-    // phase-2 operands: the elastic stress, H and the solid mask on the tile + 2 halo
-#pragma unroll
-    for (int it = 0; it < MS_NG; ++it) {
-        const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
-        const int j = j0 - 2 + ry, i = i0 - 2 + rx;
-        ok2[it] = q < MS_GX * MS_GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
-        const long c = ok2[it] ? (long)j * nx + i : (long)rw.lo * nx;
-        if (fluid) {
-            ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh2[it] = 1.0; sol[it] = false;
-        } else {
-            ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh2[it] = H[c];
-            sol[it] = solid[c] != 0;
+        // phase-2 operands: the elastic stress, H and the solid mask on the tile + 2 halo
+    #pragma unroll
+        for (int it = 0; it < MS_NG; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
+            const int j = j0 - 2 + ry, i = i0 - 2 + rx;
+            ok2[it] = q < MS_GX * MS_GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
+            const long c = ok2[it] ? (long)j * nx + i : (long)rw.lo * nx;
+            if (fluid) {
+                ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh2[it] = 1.0; sol[it] = 0;
+            } else {
+                ex[it] = sxx[c]; ey[it] = syy[c]; exy[it] = sxy[c]; hh2[it] = H[c];
+                sol[it] = solid[c];
+            }
         }
-    }
-    // phase-3 operands on the output cells
-#pragma unroll
-    for (int it = 0; it < MS_NO; ++it) {
-        const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
-        const int j = j0 + ry, i = i0 + rx;
-        ok[it] = q < MS_TX * MS_TY && j >= olo && j < ohi && i < nx;   // output rows
-        const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
-        // grad2(p) operands (functions.py:941): centred inside, one-sided at the edges
-        // (inside: c+1 / c-1; i == 0: c+1; i == nx-1: c-1 as the "+s" operand; the "-s"
-        // operand only inside) -- every index stays in the grid
-        const bool exd = i == 0 || i == nx - 1, eyd = j == 0 || j == ny - 1;
-        const long sx = i == nx - 1 ? -1 : 1, sy = j == ny - 1 ? -(long)nx : (long)nx;
-        pc[it] = p[c];
-        pxp[it] = ok[it] ? p[c + sx] : 0.0; pxm[it] = ok[it] && !exd ? p[c - 1] : 0.0;
-        pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !eyd ? p[c - nx] : 0.0;
-        hh[it] = fluid ? 1.0 : H[c];
+        // phase-3 operands on the output cells
+    #pragma unroll
+        for (int it = 0; it < MS_NO; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+            const int j = j0 + ry, i = i0 + rx;
+            ok[it] = q < MS_TX * MS_TY && j >= olo && j < ohi && i < nx;   // output rows
+            const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
+            // grad2(p) operands (functions.py:941): centred inside, one-sided at the edges
+            // (inside: c+1 / c-1; i == 0: c+1; i == nx-1: c-1 as the "+s" operand; the "-s"
+            // operand only inside) -- every index stays in the grid
+            const bool exd = i == 0 || i == nx - 1, eyd = j == 0 || j == ny - 1;
+            const long sx = i == nx - 1 ? -1 : 1, sy = j == ny - 1 ? -(long)nx : (long)nx;
+            pc[it] = p[c];
+            pxp[it] = ok[it] ? p[c + sx] : 0.0; pxm[it] = ok[it] && !exd ? p[c - 1] : 0.0;
+            pyp[it] = ok[it] ? p[c + sy] : 0.0; pym[it] = ok[it] && !eyd ? p[c - nx] : 0.0;
+            hh[it] = fluid ? 1.0 : H[c];
+        }
     }
     // Interior tiles divide unchecked (divk_nc) when every stored operand of a phase passed
     // its DivNote: the stage velocity (phase 1) certifies phase 2's numerators and phase 3's
@@ -345,7 +386,7 @@ __device__ __forceinline__ void ms_tile(
                 const double dudx = g2<IN, CHK>(pu, 1, i, nx, K.x2), dvdy = g2<IN, CHK>(pv, MS_UX, j, ny, Ky2);
                 const double dudy = g2<IN, CHK>(pu, MS_UX, j, ny, Ky2), dvdx = g2<IN, CHK>(pv, 1, i, nx, K.x2);
                 double e1 = ex[it], e2 = ey[it], e3 = exy[it];
-                if (visc && sol[it]) {
+                if (visc && sol[it] != 0) {
                     e1 = e1 + eta_s * dudx;
                     e2 = e2 + eta_s * dvdy;
                     e3 = e3 + eta_s * 0.5 * (dudy + dvdx);

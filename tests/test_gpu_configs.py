@@ -78,6 +78,31 @@ def test_config4_fused_step_N4096_vs_oracle(gpu, fast_oracle):
     assert max(eu, ev) <= 1e-15 and ep <= 1e-12   # measured 9e-17, 6e-17, 1.9e-14
 
 
+def test_config4_N4096_20_steps(gpu, fast_oracle):
+    """The bench workload, 20 fused steps against the oracle: the per-step centroid at the
+    north-star bar, minJ / maxJ within twice the reference's own noise floor at this size
+    (1-ulp weight nudges of the oracle move them by up to 3.1e-4 / 6.1e-4 in 30 steps and the
+    centroid by 4.8e-7: tools/noise_floor.py, profiles/r03/noise/lid_n4096.json)."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    N, S = 4096, 20
+    ref = fast_oracle.SoftDisc(N, "lid")
+    rec = [ref.step() for _ in range(S)]
+    sim = soft_disc_in_lid_driven(N)
+    sim.step(S)
+    d = sim.diagnostics()
+    keys = ("t", "cx", "cy", "minJ", "maxJ")
+    want = np.array([[r[k] for k in keys] for r in rec])
+    got = np.stack([d[k] for k in keys], axis=1)
+    rel = np.abs(got - want) / np.abs(want)
+    print(f"\n[config4 N=4096 x{S}] max rel: t {rel[:, 0].max():.3g} cx {rel[:, 1].max():.3g} "
+          f"cy {rel[:, 2].max():.3g} minJ {rel[:, 3].max():.3g} maxJ {rel[:, 4].max():.3g}; "
+          f"|dX1| {_maxdiff(sim.get('X1'), ref.X1):.3g} |du| {_maxdiff(sim.get('u'), ref.a):.3g}")
+    np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=1e-12)
+    np.testing.assert_allclose(got[:, 1:3], want[:, 1:3], rtol=1e-6)     # north star
+    np.testing.assert_allclose(got[:, 3], want[:, 3], rtol=7e-4)
+    np.testing.assert_allclose(got[:, 4], want[:, 4], rtol=1.3e-3)
+
+
 def test_config2_N256_1000_steps(gpu, fast_oracle):
     """soft_disc_in_lid_driven N=256 (semi-Lagrangian): the per-step centroid / J trajectory
     (soft_disc_in_lid_driven.py:233) over 1000 steps."""
