@@ -216,7 +216,7 @@ static MomDiv mom_div(double dx, double dy, double rho_s, double rho_f) {
 
 // one stage tile (k_mom_stage); IN: an interior tile (see the kernel); SQ: dx == dy (the
 // y divisors are the x ones: fewer live scalar registers)
-template <bool IN, bool SQ>
+template <bool IN, bool SQ, bool S3>
 __device__ __forceinline__ void ms_tile(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
@@ -345,6 +345,8 @@ __device__ __forceinline__ void ms_tile(
     // through wfl) sends the rest of the tile -- or the one cell -- to the checked divk.
     const bool lane0 = (threadIdx.x & 63) == 0;
     const int wv = threadIdx.x >> 6;
+    double s3a[MS_NO], s3b[MS_NO], s3c[MS_NO], s3d[MS_NO], s3e[MS_NO], s3f[MS_NO];
+    double x1[MS_NO], y1[MS_NO];
     // 1. stage velocity (functions.py:714), BC applied
     {
         DivNote nt;
@@ -410,6 +412,18 @@ __device__ __forceinline__ void ms_tile(
     } else {
         phase2(std::true_type{});
     }
+    if constexpr (S3) {
+        // the last stage's k planes and u, v at the output cells, issued here (phase 2's
+        // operands are dead) so that they arrive during phase 3's LDS reads
+#pragma unroll
+        for (int it = 0; it < MS_NO; ++it) {
+            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q - ry * MS_TX;
+            const long c = ok[it] ? (long)(j0 + ry) * nx + i0 + rx : (long)rw.lo * nx;
+            s3a[it] = ainu[c]; s3b[it] = k2u[c]; s3c[it] = kpu[c];
+            s3d[it] = ainv[c]; s3e[it] = k2v[c]; s3f[it] = kpv[c];
+            x1[it] = u[c]; y1[it] = v[c];
+        }
+    }
     __syncthreads();
     if constexpr (IN) {
         if (!chk) {
@@ -420,16 +434,14 @@ __device__ __forceinline__ void ms_tile(
     // 3. RHS and RK4 accumulation (functions.py:923-944, 743-758); stage 3 forms
     // acc = (k1 + 2 k2) + 2 k3 from the three k planes (loaded here: registers)
     {
-        double x0[MS_NO], y0[MS_NO], x1[MS_NO], y1[MS_NO];
+        double x0[MS_NO], y0[MS_NO];
 #pragma unroll
         for (int it = 0; it < MS_NO; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
-            const long c = ok[it] ? (long)(j0 + ry) * nx + i0 + rx : (long)rw.lo * nx;
-            x0[it] = 0.0; y0[it] = 0.0; x1[it] = 0.0; y1[it] = 0.0;
-            if (stage == 3 && ok[it]) {
-                x0[it] = (ainu[c] + 2 * k2u[c]) + 2 * kpu[c];
-                y0[it] = (ainv[c] + 2 * k2v[c]) + 2 * kpv[c];
-                x1[it] = u[c]; y1[it] = v[c];
+            x0[it] = 0.0; y0[it] = 0.0;
+            if constexpr (S3) {   // formed here (pinned): 4 registers live through the cells, not 8
+                x0[it] = (s3a[it] + 2 * s3b[it]) + 2 * s3c[it];
+                y0[it] = (s3d[it] + 2 * s3e[it]) + 2 * s3f[it];
+                asm volatile("" : "+v"(x0[it]), "+v"(y0[it]));
             }
         }
         // one output cell: (k1, k2); with CHK = false, *nt notes its own numerators
@@ -495,7 +507,7 @@ __device__ __forceinline__ void ms_tile(
                 kk = cell(std::true_type{}, it, ry, rx, nullptr);
             }
             const double k1 = kk.x, k2 = kk.y;
-            if (stage < 3) {
+            if constexpr (!S3) {
                 ku[c] = k1; kv[c] = k2;
             } else {
                 outu[c] = x1[it] + dt6 * (x0[it] + k1);
@@ -508,7 +520,7 @@ __device__ __forceinline__ void ms_tile(
 // IN: the interior tiles only (the others return), !IN: the others (a host-built list of the
 // tiles a full launch does not cover, or the fix-up list).  Two kernels instead of a branch:
 // the interior body alone fits its registers (no scalar spills).
-template <bool IN, bool SQ>
+template <bool IN, bool SQ, bool S3>
 __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
@@ -539,7 +551,7 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 && j0 - 3 >= max(rw.lo, 2) &&
                           j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
     if (interior != IN) return;
-    ms_tile<IN, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
+    ms_tile<IN, SQ, S3>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
 }
 
 // The listed tiles (momentum_fixup), interior and edge alike, in one launch of at most
@@ -573,10 +585,13 @@ __global__ void __launch_bounds__(MS_T, 2) k_mom_stage_list(
         const int i0 = (tile % tiles_x) * MS_TX, j0 = rw.jb + (tile / tiles_x) * MS_TY;
         const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 &&
                               j0 - 3 >= max(rw.lo, 2) && j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
-        if (interior)
-            ms_tile<true, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
-        else
-            ms_tile<false, SQ>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
+#define MS_TILE(I, S) ms_tile<I, SQ, S>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl)
+        if (interior) {
+            if (stage == 3) MS_TILE(true, true); else MS_TILE(true, false);
+        } else {
+            if (stage == 3) MS_TILE(false, true); else MS_TILE(false, false);
+        }
+#undef MS_TILE
         __syncthreads();   // the next tile's phase 1 overwrites su / sv
     }
 }
@@ -663,8 +678,11 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
     double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
     const double *kpu = s ? ku[s - 1] : u, *kpv = s ? kv[s - 1] : v;
     const bool sq = P->dx == P->dy;
-    auto kin = sq ? k_mom_stage<true, true> : k_mom_stage<true, false>;
-    auto kedge = sq ? k_mom_stage<false, true> : k_mom_stage<false, false>;
+    const bool s3 = s == 3;
+    auto kin = sq ? (s3 ? k_mom_stage<true, true, true> : k_mom_stage<true, true, false>)
+                  : (s3 ? k_mom_stage<true, false, true> : k_mom_stage<true, false, false>);
+    auto kedge = sq ? (s3 ? k_mom_stage<false, true, true> : k_mom_stage<false, true, false>)
+                    : (s3 ? k_mom_stage<false, false, true> : k_mom_stage<false, false, false>);
     const MomDiv K = mom_div(P->dx, P->dy, P->rho_s, P->rho_f);
     // the tiles a full launch's interior kernel skips (host list, per row window)
     const int *elist = tlist, *ecount = tcount;

@@ -99,8 +99,12 @@ def test_config4_N4096_20_steps(gpu, fast_oracle):
           f"|dX1| {_maxdiff(sim.get('X1'), ref.X1):.3g} |du| {_maxdiff(sim.get('u'), ref.a):.3g}")
     np.testing.assert_allclose(got[:, 0], want[:, 0], rtol=1e-12)
     np.testing.assert_allclose(got[:, 1:3], want[:, 1:3], rtol=1e-6)     # north star
-    np.testing.assert_allclose(got[:, 3], want[:, 3], rtol=7e-4)
+    np.testing.assert_allclose(got[:, 3], want[:, 3], rtol=7e-4)         # noise floor x 2
     np.testing.assert_allclose(got[:, 4], want[:, 4], rtol=1.3e-3)
+    # achieved (MI355X): the map bit-exact after 20 steps, centroid 1.7e-15, J identical
+    np.testing.assert_allclose(got[:, 1:3], want[:, 1:3], rtol=1e-12)
+    np.testing.assert_allclose(got[:, 3:], want[:, 3:], rtol=1e-10)
+    assert _maxdiff(sim.get("X1"), ref.X1) <= 1e-13 and _maxdiff(sim.get("X2"), ref.X2) <= 1e-13
 
 
 def test_config2_N256_1000_steps(gpu, fast_oracle):
