@@ -20,11 +20,12 @@ constexpr int EX_DCAP = 8192;       // fix-up dirty-list capacity
 // ctl words (int): fallback flag, abort flag, accepted count, and 64-bit arena cursor
 // EXC_ANY / EXC_NOOP: k_ex_none's proof that no target can be accepted (both paths skip)
 // EXC_CMIN / EXC_CMAX: column range of the targets; EXC_NPART + p: fits in chain part p
+constexpr int CH_MAXP = 4;          // chain parts (workgroups), split by target column
 enum { EXC_FALLBACK = 0, EXC_ABORT = 1, EXC_FILLED = 2, EXC_ARENA = 4, EXC_REJ = 8,
        EXC_BASE = 8 + EX_MAXL, EXC_ANY = 8 + 2 * EX_MAXL, EXC_NOOP = EXC_ANY + 1,
        EXC_CMIN = EXC_ANY + 2, EXC_CMAX = EXC_ANY + 3, EXC_NPART = EXC_ANY + 4,
-       EXC_WORDS = 8 + 2 * EX_MAXL + 16 };
-constexpr int CH_MAXP = 4;          // chain parts (workgroups), split by target column
+       EXC_WSTART = EXC_NPART + CH_MAXP + 1,                // + p * CH_W + w: wave w's first
+       EXC_WORDS = EXC_WSTART + CH_MAXP * CH_W + 8 };       // ordinal in part p
 constexpr int PX_K = 64;            // parallel mode: fits per segment
 constexpr int PX_F = 64;            // frontier capacity (more: the segment is solved serially)
 constexpr int PX_S = 81;            // window sources per fit
@@ -47,6 +48,9 @@ struct ExWs {
     // meta bit 63 marks a fit read by another part)
     unsigned char *part;                      // MAXT
     int *loc, *inv, *gtag;                    // MAXT each
+    // wave assignment: rkey[x] = L * ny + j of chain index x; wnext[base_p + l] = the next
+    // ordinal of part p that ordinal l's wave runs (row runs: k_ex_runs)
+    int *rkey, *wnext;                        // MAXT each
     double *gval;                             // 2 * MAXT
     int2 *crit;                               // MAXT by global slot: the fit's latest source
                                               // in chain order {ring tag, or -1 when it

@@ -598,6 +598,7 @@ __global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, in
         const int x = ws.cbase[(long)L * ny + j] +
                       (id - ws.ctl[EXC_BASE + L] - ws.rowoff[(long)L * (ny + 1) + j]);
         ws.chain_of[id] = x;
+        ws.rkey[x] = L * ny + j;
         ws.part[x] = (unsigned char)ch_part_of(ws.ctl, (int)(ws.tcell[id] % nx));
         const long long r = ws.recoff[id];
         ws.rec_by_chain[x] = r;
@@ -662,6 +663,56 @@ __device__ __forceinline__ int ch_base(const int *ctl, int p) {
     return b;
 }
 
+// Wave assignment of part blockIdx.x.  Round robin (runs = 0): ordinal l on wave l % CH_W.
+// Row runs (runs = 1): the maximal runs of consecutive ordinals of one row and layer go to
+// one wave each, runs dealt round robin -- a fit's left neighbour (the critical source of
+// about half the chain's links) is then its own wave's previous fit, already in the ring when
+// the fit starts, instead of a hand-off from another wave noticed by polling.  Every wave's
+// sequence still increases, so the chain stays deadlock-free.  One block per part.
+__global__ void __launch_bounds__(1024) k_ex_runs(ExWs ws, int runs) {
+    __shared__ int sc[1024];
+    if (ws.ctl[EXC_FALLBACK]) return;
+    const int p = blockIdx.x, t = threadIdx.x;
+    if (p >= ws.ctl[EXC_NPART + CH_MAXP]) return;
+    const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
+    int *wst = ws.ctl + EXC_WSTART + p * CH_W;
+    if (!runs) {
+        for (int l = t; l < np; l += 1024) ws.wnext[base + l] = l + CH_W;
+        if (t < CH_W) wst[t] = min(t, np);
+        return;
+    }
+    const int per = (np + 1023) / 1024, a = min(np, t * per), b = min(np, a + per);
+    auto start = [&](int l) {
+        return l == 0 || ws.rkey[ws.inv[base + l]] != ws.rkey[ws.inv[base + l - 1]];
+    };
+    int cnt = 0;
+    for (int l = a; l < b; ++l) cnt += start(l);
+    sc[t] = cnt;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = t >= d ? sc[t - d] : 0;
+        __syncthreads();
+        sc[t] += v;
+        __syncthreads();
+    }
+    const int nruns = sc[1023];
+    // run r starts at ordinal rs(r): dmark (free after the fix-up passes) holds the starts
+    int *rs = ws.dmark + base;
+    int r = sc[t] - cnt;
+    for (int l = a; l < b; ++l)
+        if (start(l)) rs[r++] = l;
+    __threadfence_block();
+    __syncthreads();
+    r = sc[t] - cnt;   // runs started before a
+    for (int l = a; l < b; ++l) {
+        if (start(l)) ++r;          // l's run is r - 1
+        const int rr = r - 1;
+        const bool last = l + 1 >= np || start(l + 1);
+        ws.wnext[base + l] = !last ? l + 1 : rr + CH_W < nruns ? rs[rr + CH_W] : np;
+    }
+    if (t < CH_W) wst[t] = t < nruns ? rs[t] : np;
+}
+
 // record sources: fit ids -> ring tags within the fit's part (the ring needs every source
 // < CH_R/2 back), or -(global slot + 1) for a source in the other part (marked for the HBM
 // hand-off); header word 23 <- (ordinal, record) of the next accepted fit of the same chain
@@ -701,8 +752,8 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
         }
     }
     if (ws.crit) ws.crit[base + l] = crit;
-    int ln = l + CH_W;
-    while (ln < np && ws.rec_by_chain[ws.inv[base + ln]] < 0) ln += CH_W;
+    int ln = ws.wnext[base + l];
+    while (ln < np && ws.rec_by_chain[ws.inv[base + ln]] < 0) ln = ws.wnext[base + ln];
     const long long rn = ln < np ? ws.rec_by_chain[ws.inv[base + ln]] : 0;   // (size64 << 32) | off64
     const unsigned r32 = (unsigned)(rn & 0xffffffffLL) | ((unsigned)(rn >> 32) << 25);
     rec[23] = __longlong_as_double(((long long)ln << 32) | r32);
@@ -1153,10 +1204,11 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
     const int part = blockIdx.x, base = ch_base(ctl, part);
     const int total = ctl[EXC_NPART + part];
     double *B = buf[wv];
-    // this wave's first accepted fit; every record names the wave's next one (k_ex_relink)
-    int x = wv;
+    // this wave's first accepted fit (k_ex_runs); every record names the wave's next one
+    // (k_ex_relink)
+    int x = ctl[EXC_WSTART + part * CH_W + wv];
     long long r0 = -1;
-    while (x < total && (r0 = C.ws.rec_by_chain[C.ws.inv[base + x]]) < 0) x += CH_W;
+    while (x < total && (r0 = C.ws.rec_by_chain[C.ws.inv[base + x]]) < 0) x = C.ws.wnext[base + x];
     unsigned r = (unsigned)(r0 & 0xffffffffLL) | (unsigned)((r0 >> 32) << 25);
     double2 d0, d1, d2, d3, d4;
     if (x < total) CH_LOAD(r);
@@ -1229,6 +1281,9 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     const unsigned idb = grid1d(ws.maxt, 256);
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
     k_ex_local<<<1, 1024, 0, st>>>(ws, ML);
+    // RMT_CH_RUNS=0: round-robin wave assignment instead of row runs
+    static const int runs = getenv("RMT_CH_RUNS") ? atoi(getenv("RMT_CH_RUNS")) != 0 : 1;
+    k_ex_runs<<<nparts, 1024, 0, st>>>(ws, runs);
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
     RMT_LAUNCHED();
     return RMT_OK;
