@@ -664,11 +664,12 @@ __device__ __forceinline__ int ch_base(const int *ctl, int p) {
 }
 
 // Wave assignment of part blockIdx.x.  Round robin (runs = 0): ordinal l on wave l % CH_W.
-// Row runs (runs = 1): the maximal runs of consecutive ordinals of one row and layer go to
-// one wave each, runs dealt round robin -- a fit's left neighbour (the critical source of
-// about half the chain's links) is then its own wave's previous fit, already in the ring when
-// the fit starts, instead of a hand-off from another wave noticed by polling.  Every wave's
-// sequence still increases, so the chain stays deadlock-free.  One block per part.
+// Row runs (runs = 1, RMT_CH_RUNS): the maximal runs of consecutive ordinals of one row and
+// layer go to one wave each, runs dealt round robin -- a fit's left neighbour (the critical
+// source of about half the chain's links) is then its own wave's previous fit, with no
+// hand-off to notice.  Measured slower (4.32 vs 3.0 ms at N=4096): the fit's record staging,
+// products and prefix fold, which overlap the predecessor's wait under round robin, become
+// serial.  Every wave's sequence increases either way (deadlock-free).  One block per part.
 __global__ void __launch_bounds__(1024) k_ex_runs(ExWs ws, int runs) {
     __shared__ int sc[1024];
     if (ws.ctl[EXC_FALLBACK]) return;
@@ -1281,8 +1282,9 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     const unsigned idb = grid1d(ws.maxt, 256);
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
     k_ex_local<<<1, 1024, 0, st>>>(ws, ML);
-    // RMT_CH_RUNS=0: round-robin wave assignment instead of row runs
-    static const int runs = getenv("RMT_CH_RUNS") ? atoi(getenv("RMT_CH_RUNS")) != 0 : 1;
+    // RMT_CH_RUNS=1: row-run wave assignment (measured slower: chain 4.32 vs 3.0 ms at
+    // N=4096 -- a fit's own set-up and prefix fold no longer overlap its predecessor's wait)
+    static const int runs = getenv("RMT_CH_RUNS") ? atoi(getenv("RMT_CH_RUNS")) != 0 : 0;
     k_ex_runs<<<nparts, 1024, 0, st>>>(ws, runs);
     k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
     RMT_LAUNCHED();
