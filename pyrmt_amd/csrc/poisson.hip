@@ -434,6 +434,56 @@ __device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__r
     }
 }
 
+// The same Stockham pass with the radix, Ns and length known at compile time (the n = 4096
+// plan, M = 4095 = 5 7 9 13): constant index math, no pass switch, the same arithmetic in the
+// same order as fft_pass (bit-identical results)
+template <int R, int NS, int NT, int M>
+__device__ __forceinline__ void fft_pass_k(double2 *z, const double2 *__restrict__ tw) {
+    constexpr int NB = M / R, BPT = (NB + NT - 1) / NT;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    double2 v[BPT][R];
+    int o[BPT];
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+        const int j = tid + b * NT;
+        if (j < NB) {
+            const int g = j / NS, k = j - g * NS;
+            o[b] = g * NS * R + k;
+            double2 w[R - 1];
+            if constexpr (NS > 1) {
+#pragma unroll
+                for (int r = 1; r < R; ++r) w[r - 1] = tw[(r - 1) * NS + k];
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[b][r] = z[j + r * NB];
+            if constexpr (NS > 1) {
+#pragma unroll
+                for (int r = 1; r < R; ++r) v[b][r] = cmul(v[b][r], w[r - 1]);
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < BPT; ++b) {
+        const int j = tid + b * NT;
+        if (j < NB) {
+            dft<R>(v[b]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) z[o[b] + r * NS] = v[b][r];
+        }
+    }
+    __syncthreads();
+}
+// factor(4095)'s plan: radices 5, 7, 9, 13 (ascending), twiddle offsets 0, 4, 34, 314
+template <int NT>
+__device__ __forceinline__ void fft_4095(double2 *z, const double2 *__restrict__ W) {
+    fft_pass_k<5, 1, NT, 4095>(z, W);
+    fft_pass_k<7, 5, NT, 4095>(z, W + 4);
+    fft_pass_k<9, 35, NT, 4095>(z, W + 34);
+    fft_pass_k<13, 315, NT, 4095>(z, W + 314);
+}
+
 // DCT-I of one real row per workgroup.  The even extension e (length M = 2N, N = n - 1) is
 // real, so its length-M DFT -- the unnormalised DCT-I -- comes from ONE length-N complex FFT
 // of z_m = e_{2m} + i e_{2m+1} (the packed-real FFT): with Z = FFT_N(z), Z_N = Z_0 and
@@ -468,7 +518,7 @@ __device__ __forceinline__ void put_row_even(double *d, int N, const double *__r
     }
 }
 
-template <bool SOLVE, int BIG>
+template <bool SOLVE, int BIG, int PLAN = 0>
 __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double *__restrict__ src,
                                                       double *__restrict__ dst, int rows, int n,
                                                       const double2 *__restrict__ W,
@@ -482,7 +532,8 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
     constexpr int PP = (K1_MAXN / 2 + NT - 1) / NT;   // (k, N - k) pairs per thread, N < K1_MAXN
     extern __shared__ double2 z[];
     __shared__ double red[256];
-    const int N = n - 1, r = blockIdx.x;
+    // PLAN 1: n = 4096 (compile-time passes, fft_4095)
+    const int N = PLAN == 1 ? 4095 : n - 1, r = blockIdx.x;
     double *d = (double *)z;
     const double2 *Wq0 = W + (N - 1);   // after the N - 1 pass twiddles: W^k, k = 0 .. N
     put_row_even<NT>(d, N, src + (long)r * n);
@@ -491,7 +542,8 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
 #pragma unroll 1
     for (int it = 0; it < (SOLVE ? 2 : 1); ++it) {
         __syncthreads();
-        fft_lds<BIG, NT, K1_MAXN>(z, N, rd, W);
+        if constexpr (PLAN == 1) fft_4095<NT>(z, W);
+        else fft_lds<BIG, NT, K1_MAXN>(z, N, rd, W);
         // opaque per iteration: keeps the twiddle / eigenvalue loads below from being hoisted
         // above the FFT (they would hold ~40 registers across it)
         const double2 *Wq = Wq0;
@@ -613,8 +665,9 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     RMT_CHECK(!rowmark || (!solve && !rs), RMT_EINVAL, "dct_pass: row marks on a plain row pass");
     static bool attr = false;
     if (!attr) {
-        const void *fs[4] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
-                             (const void *)k_dct1<false, 1>, (const void *)k_dct1<true, 1>};
+        const void *fs[6] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
+                             (const void *)k_dct1<false, 1>, (const void *)k_dct1<true, 1>,
+                             (const void *)k_dct1<false, 0, 1>, (const void *)k_dct1<true, 0, 1>};
         for (auto f : fs)
             RMT_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)FFT_LDS_MAX));
@@ -628,7 +681,15 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     const size_t lds = (size_t)(n - 1) * sizeof(double2);
     const unsigned g = (unsigned)nrows;   // one row per workgroup
     hipStream_t st = ctx->stream;
-    if (solve) {
+    // RMT_DCT_GENERIC=1: the runtime-plan kernel for n = 4096 too
+    static const bool generic = getenv("RMT_DCT_GENERIC") && atoi(getenv("RMT_DCT_GENERIC"));
+    const bool k4095 = n == 4096 && !P->big && !generic && np == 4 && rad[0] == 5 &&
+                       rad[1] == 7 && rad[2] == 9 && rad[3] == 13;   // fft_4095's plan
+    if (k4095 && solve)
+        k_dct1<true, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
+    else if (k4095)
+        k_dct1<false, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark);
+    else if (solve) {
         if (P->big) k_dct1<true, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
         else k_dct1<true, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
     } else {
