@@ -359,6 +359,19 @@ int rmt_slab_project_unrows(rmt_slab *slab);             /* then: allgather scal
 int rmt_slab_sub_mean(rmt_slab *slab, int which, const double *roots_dev);  /* 0 p_c, 1 p */
 int rmt_slab_project_correct(rmt_slab *slab, double dt); /* after halo(p_c); then roots   */
 int rmt_slab_finish(rmt_slab *slab);                     /* then: allgather scal          */
+/* Device-dt step (no host round trip inside the step; distributed.py's asynchronous path):
+ * with on != 0 every phase reads dt from the slab's device scalar instead of its dt argument.
+ * rmt_slab_next_dt: after the scalar allgather (G x 16 doubles, device), record
+ * {dt, max|u|^2, the gathered blocks} into ring_slot (nullable, 2 + 16 G doubles) and set the
+ * next dt from the gathered max|u|^2 -- the host's expression, NaN-propagating max.
+ * rmt_slab_rim_pack + rmt_slab_rim_cap: the rim allgather moves a fixed `cap` entries per slab
+ * (flag 8 in the scalar block's flags when a slab's rim is larger; the host raises);
+ * rmt_slab_extrapolate_dev reads the counts from the gathered scalar blocks. */
+int rmt_slab_set_device_dt(rmt_slab *slab, int on);
+int rmt_slab_next_dt(rmt_slab *slab, const double *gathered_scal, int G, double *ring_slot);
+int rmt_slab_rim_cap(rmt_slab *slab, long long cap);
+int rmt_slab_extrapolate_dev(rmt_slab *slab, const double *gathered, const double *gathered_scal,
+                             long long cap);
 
 /* ---- MAC path (config 5): pyRMT/mac.py operators on an N x N cell grid -----------
  * ctx created for (N, N) cells; u is (N, N+1) x-faces, v (N+1, N) y-faces, p / phi (N, N). */

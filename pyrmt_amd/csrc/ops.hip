@@ -538,20 +538,22 @@ __global__ void k_div_scalar(const double *__restrict__ x, long n, double s,
 }
 // Row-window launches for the slab-decomposed step (global cell indices, rows [jb, je))
 int divergence_rc_rows(rmt_ctx *ctx, const double *a, const double *b, const double *p,
-                       double d_f, double dx, double dy, double *divU, int jb, int je) {
+                       double d_f, double dx, double dy, double *divU, int jb, int je,
+                       double rho, double dt, const double *dtp) {
     if (je > jb)
         k_divergence_rc<<<rows_grid(ctx->nx, jb, je), 256, 0, ctx->stream>>>(
-            a, b, p, ctx->ny, ctx->nx, d_f, rc_div(dx, dy), divU, jb, je);
+            a, b, p, ctx->ny, ctx->nx, d_f, rc_div(dx, dy), divU, jb, je, rho, dt, dtp);
     RMT_LAUNCHED();
     return RMT_OK;
 }
 int project_correct_rows(rmt_ctx *ctx, const double *a_s, const double *b_s, const double *pc,
                          const double *p_prev, double dx, double dy, double dt_rho, int bc,
-                         double lid, double *a, double *b, double *p, int jb, int je) {
+                         double lid, double *a, double *b, double *p, int jb, int je,
+                         const double *dtp, double rho) {
     if (je > jb)
         k_project_correct<<<rows_grid(ctx->nx, jb, je), 256, 0, ctx->stream>>>(
             a_s, b_s, pc, p_prev, ctx->ny, ctx->nx, divk_make(2 * dx), divk_make(2 * dy), dt_rho, bc, lid, a, b, p, jb, je,
-            nullptr, 1.0);
+            nullptr, 1.0, dtp, rho);
     RMT_LAUNCHED();
     return RMT_OK;
 }

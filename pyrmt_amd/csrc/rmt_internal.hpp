@@ -524,11 +524,15 @@ int sub_mean_rows(rmt_ctx *ctx, double *x, int ny, int nx);
 // of the reference sees the true domain edge.  A single-domain call is {0, ny, 0, ny}.
 struct RowWin { int jb, je, lo, hi; };
 
+// rho > 0: divU = (rho * div) / dt, the projection's rhs (dt = *dtp when dtp is given)
 int divergence_rc_rows(rmt_ctx *ctx, const double *a, const double *b, const double *p,
-                       double d_f, double dx, double dy, double *divU, int jb, int je);
+                       double d_f, double dx, double dy, double *divU, int jb, int je,
+                       double rho = 0.0, double dt = 1.0, const double *dtp = nullptr);
+// dtp (nullable): dt_rho = *dtp / rho on the device
 int project_correct_rows(rmt_ctx *ctx, const double *a_s, const double *b_s, const double *pc,
                          const double *p_prev, double dx, double dy, double dt_rho, int bc,
-                         double lid, double *a, double *b, double *p, int jb, int je);
+                         double lid, double *a, double *b, double *p, int jb, int je,
+                         const double *dtp = nullptr, double rho = 1.0);
 
 // sim.hip: the fused step's diagnostic partials (centroid sums, J range, energies) over rows
 // [jb, je); part holds DIAG_PART doubles, out receives 10
@@ -668,7 +672,8 @@ int slab_rim_pack(rmt_ctx *ctx, const unsigned long long *bits, int ny, int nx, 
 int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *counts, int G,
                          long long cap, double *X1d, double *X2d, const unsigned long long *bits,
                          double dx, double dy, int layers, int *exflags, double *X1n,
-                         double *X2n, long c_lo, long c_hi);
+                         double *X2n, long c_lo, long c_hi,
+                         const double *gs = nullptr);
 int slab_cols(rmt_ctx *ctx, bool pack, double *Y, int rows, int nx, const int *csplits, int G,
               double *A);
 

@@ -43,8 +43,9 @@ using rmt::u64;
 namespace rmt {
 constexpr int SLAB_MAXG = 64;
 enum { SC_M2 = 0, SC_DIAG = 1, SC_FLAGS = 11, SC_COUNT = 12, SC_ROOT = 13, SC_FIT = 14,
-       SC_M2RES = 15, SC_N = 16, SC_M2OWN = 16 /* device-only, past the exported block */ };
-enum { FL_NONFINITE = 1, FL_HALO = 2, FL_EXABORT = 4 };
+       SC_M2RES = 15, SC_N = 16, SC_M2OWN = 16 /* device-only, past the exported block */,
+       SC_DT = 20, SC_M2G = 21 /* device dt: this step's dt and the max |u|^2 it came from */ };
+enum { FL_NONFINITE = 1, FL_HALO = 2, FL_EXABORT = 4, FL_RIMCAP = 8 };
 struct Splits { int v[SLAB_MAXG + 1]; };
 struct Counts { long long c[SLAB_MAXG]; };
 }  // namespace rmt
@@ -76,6 +77,9 @@ struct rmt_slab {
     hipEvent_t e_chain = nullptr, e_mom = nullptr;
     int *tiles = nullptr, *tcount = nullptr, max_tiles = 0;
     double dt_cur = 0;
+    // device dt (rmt_slab_set_device_dt): the step's kernels read dt from *dtp instead of the
+    // host argument, and the rim counts come from the gathered scalars (rmt_slab_extrapolate_dev)
+    const double *dtp = nullptr;
     bool spec = false;     // a speculative momentum is in flight for this step
     bool interior = false; // rmt_slab_advect_interior ran for this step
     double *gv(double *q) const { return q - (long)lo * NX; }   // global-index view
@@ -91,9 +95,10 @@ __global__ void k_slab_sl(const double *__restrict__ X1, const double *__restric
                           int nx, double dt, DivK Kx, DivK Ky, double x0, double y0, double R,
                           double *__restrict__ X1n, double *__restrict__ X2n,
                           double *__restrict__ phi_pre, int *flags, int jb, int je, int lo,
-                          int hi, const double *m2) {
+                          int hi, const double *m2, const double *__restrict__ dtp) {
     // grid (ceil(nx / 256), je - jb); the block skip of sl_zero_block (rmt_internal.hpp) with
     // m2 bounding the velocities of the resident rows
+    if (dtp) dt = *dtp;
     const int j = jb + blockIdx.y, i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
     const bool zero = sl_skip_ok(m2, dt, fmin(Kx.d, Ky.d)) &&
                       sl_zero_block(X1, X2, ny, nx, j, i0, 256, lo, hi);
@@ -217,12 +222,18 @@ __global__ void __launch_bounds__(256) k_rim_emit(const u64 *__restrict__ rimw,
         base += __shfl(inc, 63);
     }
 }
+// gathered rim counts: on the host (cn) or in the gathered scalar blocks (gs, G x SC_N: the
+// device-dt path, counts capped at cap -- an overflow is flagged by k_rim_cap)
+__device__ __forceinline__ long rim_count(const Counts &cn, const double *gs, int k, long cap) {
+    return gs ? min((long)gs[(long)k * SC_N + SC_COUNT], cap) : cn.c[k];
+}
 __global__ void k_rim_unpack(const double *__restrict__ g, Counts cn, int G, long cap,
-                             double *__restrict__ X1d, double *__restrict__ X2d) {
+                             double *__restrict__ X1d, double *__restrict__ X2d,
+                             const double *__restrict__ gs) {
     const long q = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (q >= G * cap) return;
     const int k = (int)(q / cap);
-    if (q - k * cap >= cn.c[k]) return;
+    if (q - k * cap >= rim_count(cn, gs, k, cap)) return;
     const long c = (long)g[3 * q];
     X1d[c] = g[3 * q + 1];
     X2d[c] = g[3 * q + 2];
@@ -230,11 +241,11 @@ __global__ void k_rim_unpack(const double *__restrict__ g, Counts cn, int G, lon
 __global__ void k_rim_writeback(const double *__restrict__ g, Counts cn, int G, long cap,
                                 const double *__restrict__ X1d, const double *__restrict__ X2d,
                                 double *__restrict__ X1n, double *__restrict__ X2n, long c_lo,
-                                long c_hi) {
+                                long c_hi, const double *__restrict__ gs) {
     const long q = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (q >= G * cap) return;
     const int k = (int)(q / cap);
-    if (q - k * cap >= cn.c[k]) return;
+    if (q - k * cap >= rim_count(cn, gs, k, cap)) return;
     const long c = (long)g[3 * q];
     if (c < c_lo || c >= c_hi) return;
     X1n[c] = X1d[c];
@@ -275,12 +286,33 @@ __global__ void __launch_bounds__(256) k_slab_phi_tiles(const double *__restrict
     }
 }
 
-// ------------------------------------------------------------------ projection --
-// rhs = rho * divU / dt (k_scale_copy then k_div_scalar in ops.hip: the same two roundings)
-__global__ void k_slab_rhs(double *__restrict__ x, long n, double rho, double dt) {
-    const long k = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    if (k < n) x[k] = (rho * x[k]) / dt;
+// ------------------------------------------------------------------ device dt --
+// ring (nullable) <- {this step's dt, the max |u|^2 it came from, the gathered scalar blocks};
+// then the next dt from the gathered max |u|^2 (NaN-propagating, as numpy's max), with the
+// host's expression (distributed.py: min(dt_const, cfl dx / (sqrt(m2) + 1e-6)); Python's
+// min(dt_const, nan) is dt_const, as fmin)
+__global__ void k_slab_dt(const double *__restrict__ gs, int G, double dt_const, double cfl,
+                          double dx, double *__restrict__ scal, double *__restrict__ ring) {
+    if (threadIdx.x != 0) {
+        if (ring)
+            for (int q = threadIdx.x - 1; q < G * SC_N; q += blockDim.x - 1) ring[2 + q] = gs[q];
+        return;
+    }
+    if (ring) { ring[0] = scal[SC_DT]; ring[1] = scal[SC_M2G]; }
+    double m2 = gs[SC_M2];
+    for (int k = 1; k < G; ++k) {
+        const double x = gs[(long)k * SC_N + SC_M2];
+        if (x > m2 || x != x) m2 = x;
+    }
+    scal[SC_M2G] = m2;
+    scal[SC_DT] = fmin(dt_const, cfl * dx / (sqrt(m2) + 1e-6));
 }
+// the rim allgather moves `cap` entries per slab: a larger count is flagged (the host raises)
+__global__ void k_rim_cap(const double *__restrict__ scal, long cap, int *__restrict__ flags) {
+    if (scal[SC_COUNT] > (double)cap) atomicOr(flags, FL_RIMCAP);
+}
+
+// ------------------------------------------------------------------ projection --
 // owned rows x NX  <->  per-destination column blocks (rows x nc_m at offset rows * c0_m)
 template <bool PACK>
 __global__ void k_cols(double *__restrict__ Y, int rows, int nx, Splits cs, int G,
@@ -318,7 +350,7 @@ int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, c
     if (je <= jb) return RMT_OK;
     k_slab_sl<<<dim3((nx + 255) / 256, je - jb), 256, 0, ctx->stream>>>(
         X1, X2, a, b, xs, ys, ny, nx, dt, divk_make(dx), divk_make(dy), x0, y0, R, X1n, X2n, phi_pre, flags, jb, je,
-        lo, hi, dev_m2);
+        lo, hi, dev_m2, nullptr);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -351,21 +383,21 @@ int rim_words(rmt_ctx *ctx, const u64 *bits, int ny, int nx, int W, u64 *rimw, i
 int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *counts, int G,
                          long long cap, double *X1d, double *X2d, const u64 *bits, double dx,
                          double dy, int layers, int *exflags, double *X1n, double *X2n,
-                         long c_lo, long c_hi) {
+                         long c_lo, long c_hi, const double *gs) {
     Counts cn{};
-    for (int k = 0; k < G; ++k) {
+    for (int k = 0; k < G && !gs; ++k) {
         RMT_CHECK(counts[k] >= 0 && counts[k] <= cap, RMT_EINVAL, "slab: rim count > cap");
         cn.c[k] = counts[k];
     }
     const long tot = (long)G * cap;
     if (tot > 0) {
-        k_rim_unpack<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, G, cap, X1d, X2d);
+        k_rim_unpack<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, G, cap, X1d, X2d, gs);
         RMT_LAUNCHED();
     }
     RMT_TRY(extrapolate(ctx, X1d, X2d, nullptr, dx, dy, layers, X1d, X2d, exflags, bits));
     if (tot > 0) {
         k_rim_writeback<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, G, cap, X1d, X2d,
-                                                                   X1n, X2n, c_lo, c_hi);
+                                                                   X1n, X2n, c_lo, c_hi, gs);
         RMT_LAUNCHED();
     }
     return RMT_OK;
@@ -502,6 +534,27 @@ int rmt_slab_buffer(rmt_slab *S, int id, void **ptr) {
     return RMT_OK;
 }
 
+int rmt_slab_set_device_dt(rmt_slab *S, int on) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    S->dtp = on ? S->scal + SC_DT : nullptr;
+    return RMT_OK;
+}
+
+int rmt_slab_next_dt(rmt_slab *S, const double *gathered_scal, int G, double *ring_slot) {
+    RMT_CHECK(S && gathered_scal && G == S->G, RMT_EINVAL, "rmt_slab_next_dt: bad argument");
+    k_slab_dt<<<1, 256, 0, S->ctx->stream>>>(gathered_scal, G, S->dt_const, S->P.cfl, S->P.dx,
+                                             S->scal, ring_slot);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+int rmt_slab_rim_cap(rmt_slab *S, long long cap) {
+    RMT_CHECK(S && cap >= 0, RMT_EINVAL, "rmt_slab_rim_cap: bad argument");
+    k_rim_cap<<<1, 1, 0, S->ctx->stream>>>(S->scal, (long)cap, S->flags);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
 int rmt_slab_begin(rmt_slab *S) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
     const long o = (long)(S->r0 - S->lo) * S->NX, n = (long)(S->r1 - S->r0) * S->NX;
@@ -531,7 +584,7 @@ int rmt_slab_advect_interior(rmt_slab *S, double dt) {
         k_slab_sl<<<dim3((NX + 255) / 256, ie - ib), 256, 0, ctx->stream>>>(
             S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt,
             divk_make(P.dx), divk_make(P.dy), P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
-            S->flags, ib, ie, S->r0, S->r1, S->scal + SC_M2OWN);
+            S->flags, ib, ie, S->r0, S->r1, S->scal + SC_M2OWN, S->dtp);
         RMT_LAUNCHED();
     }
     return RMT_OK;
@@ -546,7 +599,7 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
     // next step
     const bool in = S->interior;
     S->interior = false;
-    RMT_CHECK(!in || dt == S->dt_cur, RMT_EINVAL, "slab advect: dt differs");
+    RMT_CHECK(!in || S->dtp || dt == S->dt_cur, RMT_EINVAL, "slab advect: dt differs");
     S->dt_cur = dt;
     if (!in) RMT_HIP(hipMemsetAsync(S->flags, 0, 8 * sizeof(int), ctx->stream));
     // max |u|^2 over the resident rows: bounds every velocity sample of the backtraces
@@ -560,7 +613,7 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
         k_slab_sl<<<dim3((NX + 255) / 256, b - a), 256, 0, ctx->stream>>>(
             S->gv(S->X1), S->gv(S->X2), S->gv(S->u), S->gv(S->v), S->xs, S->ys, S->NY, NX, dt,
             divk_make(P.dx), divk_make(P.dy), P.x0, P.y0, P.R, S->gv(S->X1n), S->gv(S->X2n), S->gv(S->phi_pre),
-            S->flags, a, b, S->lo, S->hi, S->scal + SC_M2RES);
+            S->flags, a, b, S->lo, S->hi, S->scal + SC_M2RES, S->dtp);
         RMT_LAUNCHED();
     }
     k_slab_bits<<<dim3((NX + 255) / 256, S->r1 - S->r0), 256, 0, ctx->stream>>>(
@@ -575,9 +628,21 @@ int rmt_slab_rim_pack(rmt_slab *S) {
                          S->gv(S->X1n), S->gv(S->X2n), S->rim, S->scal + SC_COUNT);
 }
 
+static int slab_extrapolate(rmt_slab *S, const double *gathered, const long long *counts,
+                            long long cap, const double *gs);
 int rmt_slab_extrapolate(rmt_slab *S, const double *gathered, const long long *counts,
                          long long cap) {
     RMT_CHECK(S && counts && (gathered || cap == 0), RMT_EINVAL, "null argument");
+    return slab_extrapolate(S, gathered, counts, cap, nullptr);
+}
+int rmt_slab_extrapolate_dev(rmt_slab *S, const double *gathered, const double *gathered_scal,
+                             long long cap) {
+    RMT_CHECK(S && gathered_scal && (gathered || cap == 0), RMT_EINVAL, "null argument");
+    return slab_extrapolate(S, gathered, nullptr, cap, gathered_scal);
+}
+}  // extern "C"
+static int slab_extrapolate(rmt_slab *S, const double *gathered, const long long *counts,
+                            long long cap, const double *gs) {
     rmt_ctx *ctx = S->ctx;
     const rmt_sim_params &P = S->P;
     static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
@@ -586,7 +651,7 @@ int rmt_slab_extrapolate(rmt_slab *S, const double *gathered, const long long *c
     if (S->spec) ctx->ev_chain = S->e_chain;
     const int es = slab_rim_extrapolate(ctx, gathered, counts, S->G, cap, S->X1d, S->X2d, S->bits,
                                         P.dx, P.dy, P.layers, S->flags + 4, S->gv(S->X1n),
-                                        S->gv(S->X2n), (long)S->lo * S->NX, (long)S->hi * S->NX);
+                                        S->gv(S->X2n), (long)S->lo * S->NX, (long)S->hi * S->NX, gs);
     ctx->ev_chain = nullptr;
     if (es != RMT_OK) { S->spec = false; return es; }
     if (!S->spec) {
@@ -611,11 +676,13 @@ int rmt_slab_extrapolate(rmt_slab *S, const double *gathered, const long long *c
     RMT_HIP(hipEventRecord(S->e_mom, S->st2));
     return extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount);
 }
+extern "C" {
 
 int rmt_slab_momentum(rmt_slab *S, double dt) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
     if (S->spec) {
-        RMT_CHECK(dt == S->dt_cur, RMT_EINVAL, "slab momentum: dt differs from the advection's");
+        RMT_CHECK(S->dtp || dt == S->dt_cur, RMT_EINVAL,
+                  "slab momentum: dt differs from the advection's");
         S->spec = false;
         rmt_ctx *ctx = S->ctx;
         const rmt_sim_params &P = S->P;
@@ -641,6 +708,7 @@ static int slab_momentum_pass(rmt_slab *S, double dt, bool fixup) {
     M.detg_clamp = P.detg_clamp;
     const long nl = (long)(S->hi - S->lo) * S->NX, off = (long)S->lo * S->NX;
     MomWork W = mom_work(S->mw - off, nl, S->solid - off, S->flags + 1);
+    W.dtp = S->dtp;
     const RowWin win{std::max(0, S->r0 - 1), std::min(S->NY, S->r1 + 1), S->lo, S->hi};
     if (fixup)
         return momentum_fixup(S->ctx, &M, S->gv(S->u), S->gv(S->v), S->gv(S->p), S->gv(S->X1),
@@ -662,10 +730,10 @@ int rmt_slab_project_rows(rmt_slab *S, double dt) {
     const int rows = S->r1 - S->r0;
     const long no = (long)rows * S->NX;
     double *rhs = S->gv(S->rhs) + (long)S->r0 * S->NX;   // owned rows of the rhs plane
+    // rhs = (rho * div) / dt in the divergence kernel (the same two roundings as the scale and
+    // divide passes of ops.hip)
     RMT_TRY(divergence_rc_rows(ctx, S->gv(S->us), S->gv(S->vs), S->gv(S->p), dt / rho, P.dx, P.dy,
-                               S->gv(S->rhs), S->r0, S->r1));
-    k_slab_rhs<<<grid1d(no, 256), 256, 0, ctx->stream>>>(rhs, no, rho, dt);
-    RMT_LAUNCHED();
+                               S->gv(S->rhs), S->r0, S->r1, rho, dt, S->dtp));
     RMT_TRY(dct_pass(ctx, false, 0, rhs, S->Y, rows, 0, 1.0));
     k_cols<true><<<grid1d(no, 256), 256, 0, ctx->stream>>>(S->Y, rows, S->NX, S->cs, S->G, S->A);
     RMT_LAUNCHED();
@@ -712,7 +780,7 @@ int rmt_slab_project_correct(rmt_slab *S, double dt) {
     const rmt_sim_params &P = S->P;
     RMT_TRY(project_correct_rows(S->ctx, S->gv(S->us), S->gv(S->vs), S->gv(S->pc), S->gv(S->p),
                                  P.dx, P.dy, dt / P.rho_f, P.bc_kind, P.lid, S->gv(S->u),
-                                 S->gv(S->v), S->gv(S->p), S->r0, S->r1));
+                                 S->gv(S->v), S->gv(S->p), S->r0, S->r1, S->dtp, P.rho_f));
     return rowtree_root(S->ctx, S->gv(S->p) + (long)S->r0 * S->NX, S->r1 - S->r0, S->NX,
                         S->scal + SC_ROOT);
 }

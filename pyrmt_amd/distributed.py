@@ -21,6 +21,7 @@ small allgathers of row-tree roots and per-slab scalars (the means and diagnosti
 """
 import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -327,6 +328,12 @@ class DistributedSim:
         self.m2 = None
         self.records = []
         self._counts = (ctypes.c_longlong * self.G)()
+        # the asynchronous step (no host round trip inside a step): device dt, a fixed rim
+        # capacity per slab, the per-step scalars into a device ring read every sync_every
+        self.sync_every = 32
+        self._dev_dt = False          # the slabs' device dt holds this step's dt
+        self._rim_cap = None          # rim entries moved per slab (set from the first count)
+        self._min_owned = min(self.rsplits[k + 1] - self.rsplits[k] for k in range(self.G)) * N
 
     # -------------------------------------------------------------- state in / out --
     def set_state(self, **fields):
@@ -384,11 +391,19 @@ class DistributedSim:
             ev.append(e)
 
     def step(self, nsteps=1, t_end=math.inf):
+        """nsteps steps (stopping at t_end).  With no t_end and no profiling the steps run
+        asynchronously (_step_async: bit-identical, no host round trip inside a step);
+        RMT_SLAB_SYNC=1 forces the synchronous path."""
         self.ctx.bind()
         comm, S = self.comm, self.slabs
         if self.m2 is None:
             self._call("rmt_slab_begin")
             self.m2 = float(self._scalars()[:, SC_M2].max())
+            self._dev_dt = False
+        if (math.isinf(t_end) and t_end > 0 and not getattr(self, "_prof", False)
+                and not int(os.environ.get("RMT_SLAB_SYNC", "0"))):
+            return self._step_async(nsteps)
+        self._set_dev_dt(False)
         for _ in range(nsteps):
             if not (self.t < t_end):
                 break
@@ -446,6 +461,88 @@ class DistributedSim:
                 self._ms["extrap_chain_kernel"] += ms2[1]
                 self._nprof += 1
 
+    def _set_dev_dt(self, on):
+        for s in self.slabs:
+            L.check(s.lib.rmt_slab_set_device_dt(s.h, int(bool(on))), "rmt_slab_set_device_dt")
+        if not on:
+            self._dev_dt = False
+
+    def _step_async(self, nsteps):
+        """The step of step() with dt computed on the device (rmt_slab_next_dt: the host's
+        expression on the allgathered max |u|^2), the rim allgathered at a fixed capacity
+        (rmt_slab_rim_cap flags an overflow, raised at the next read-back) with the counts
+        read on the device (rmt_slab_extrapolate_dev), and each step's dt and scalar blocks
+        recorded in a device ring that the host reads every sync_every steps."""
+        torch, comm, S, G = self.torch, self.comm, self.slabs, self.G
+        self._set_dev_dt(True)
+        if not self._dev_dt:
+            gs = comm.allgather([s.view("scal") for s in S])[0]
+            for s in S:
+                L.check(s.lib.rmt_slab_next_dt(s.h, gs.data_ptr(), G, None), "rmt_slab_next_dt")
+            self._dev_dt = True
+        width = 2 + G * SC_N
+        ring = torch.empty((self.sync_every, width), dtype=torch.float64,
+                           device=S[0].view("scal").device)
+        keep, slot = [], 0
+
+        def flush():
+            nonlocal slot, keep
+            if not slot:
+                return
+            rows = ring[:slot].cpu().numpy()
+            slot, keep = 0, []
+            for r in rows:
+                sc = r[2:].reshape(G, SC_N)
+                if int(np.bitwise_or.reduce(sc[:, SC_FLAGS].astype(np.int64))) & 8:
+                    raise L.RMTError(f"slab step: the rim exceeded its allgather capacity "
+                                     f"({self._rim_cap} entries per slab)")
+                self.t += float(r[0])
+                self._record(sc, float(r[0]), float(r[1]))
+                self._rim_cap = max(self._rim_cap, _rim_capacity(sc[:, SC_COUNT].max()))
+
+        for _ in range(nsteps):
+            h = comm.halo_start(S, ("u", "v", "p", "X1", "X2"), HALO)
+            self._call("rmt_slab_advect_interior", 0.0)
+            comm.halo_finish(h)
+            self._call("rmt_slab_advect", 0.0)
+            comm.allgather_rows(S, "bits")
+            self._call("rmt_slab_rim_pack")
+            if self._rim_cap is None:   # once: the capacity from the first rim (host read)
+                self._rim_cap = _rim_capacity(self._scalars()[:, SC_COUNT].max())
+            # never more than the smallest slab owns (equal on every rank: the global splits)
+            cap = min(self._rim_cap, self._min_owned)
+            for s in S:
+                L.check(s.lib.rmt_slab_rim_cap(s.h, cap), "rmt_slab_rim_cap")
+            gs = comm.allgather([s.view("scal") for s in S])[0]
+            rims = comm.allgather([s.view("rim").reshape(-1)[:max(cap, 1) * 3] for s in S])
+            for s, g in zip(S, rims):
+                L.check(s.lib.rmt_slab_extrapolate_dev(s.h, g.data_ptr(), gs.data_ptr(), cap),
+                        "rmt_slab_extrapolate_dev")
+            self._call("rmt_slab_momentum", 0.0)
+            self._call("rmt_slab_project_rows", 0.0)
+            sp = [s.a2a_splits() for s in S]
+            comm.all_to_all([s.view("A") for s in S], [s.view("B") for s in S],
+                            [x[0] for x in sp], [x[1] for x in sp])
+            self._call("rmt_slab_project_cols")
+            comm.all_to_all([s.view("B") for s in S], [s.view("A") for s in S],
+                            [x[1] for x in sp], [x[0] for x in sp])
+            self._call("rmt_slab_project_unrows")
+            self._sub_mean(0)
+            comm.halo(S, ("pc",), 2)
+            self._call("rmt_slab_project_correct", 0.0)
+            self._sub_mean(1)
+            self._call("rmt_slab_finish")
+            gs2 = comm.allgather([s.view("scal") for s in S])[0]
+            for k, s in enumerate(S):
+                L.check(s.lib.rmt_slab_next_dt(s.h, gs2.data_ptr(), G,
+                                               ring[slot].data_ptr() if k == 0 else None),
+                        "rmt_slab_next_dt")
+            keep += [gs, gs2]   # (librmt runs on torch's current stream: stream-ordered reuse)
+            slot += 1
+            if slot == self.sync_every:
+                flush()
+        flush()
+
     def _sub_mean(self, which):
         roots = self.comm.allgather([s.view("scal")[SC_ROOT:SC_ROOT + 1] for s in self.slabs])
         for s, r in zip(self.slabs, roots):
@@ -472,6 +569,12 @@ class DistributedSim:
     def diagnostics(self):
         keys = self.records[0].keys() if self.records else ()
         return {k: np.array([r[k] for r in self.records]) for k in keys}
+
+
+def _rim_capacity(count):
+    """Rim entries moved per slab by the asynchronous step: 1.5x the largest slab rim seen,
+    rounded up to 4096 (a slab's rim grows by a few cells per step)."""
+    return int(-(-int(1.5 * float(count) + 4096) // 4096) * 4096)
 
 
 def soft_disc_in_lid_driven(N, comm):
