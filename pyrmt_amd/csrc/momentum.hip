@@ -33,6 +33,47 @@ __global__ void k_mom_prep(const double *__restrict__ X1, const double *__restri
     solid[c] = pc <= 0.0;
 }
 
+// k_mom_prep on rows [jb, je) of a grid with nx % 64 == 0, by 64-column row segments.  Where
+// every phi of a segment exceeds max(w_t, w_cut, 0) (its fluid flag frows, row flo first, on
+// the same phi) the outputs are the constants (0, 0, 0, J = 1, H = 1, not solid); if the
+// planes already hold them (pconst: the last write of the segment was such a pass) it is
+// skipped.  A wave takes PS_SEGS consecutive segments: lane l < PS_SEGS reads segment l's
+// two flags, the wave then runs the segments to be written one after the other (64 lanes =
+// 64 cells; few per wave, so that the serial chain of segment latencies stays short).  Same
+// per-cell arithmetic as k_mom_prep (no rho plane).
+constexpr int PS_SEGS = 8;
+__global__ void __launch_bounds__(256) k_mom_prep_seg(
+    const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ phi,
+    int ny, int nx, double dx, double dy, double mu_s, double kappa, double w_cut, double clamp,
+    double w_t, double *__restrict__ sxx, double *__restrict__ sxy, double *__restrict__ syy,
+    double *__restrict__ J, double *__restrict__ H, unsigned char *__restrict__ solid, int jb,
+    int je, const unsigned char *__restrict__ frows, int flo, unsigned char *__restrict__ pconst) {
+    const int lane = threadIdx.x & 63, tiles_x = nx >> 6;
+    const long s1 = (long)je * tiles_x;
+    const long g0 = (long)jb * tiles_x + (long)PS_SEGS * (blockIdx.x * 4L + (threadIdx.x >> 6));
+    if (g0 >= s1) return;
+    const long sl = g0 + lane;
+    bool need = false;
+    if (lane < PS_SEGS && sl < s1) {
+        const bool f = frows[sl - (long)flo * tiles_x] != 0;
+        need = !(f && pconst[sl]);
+        pconst[sl] = f;   // the planes hold the constants after this pass iff f
+    }
+    for (unsigned long long m = __ballot(need); m; m &= m - 1) {
+        const long seg = g0 + __builtin_ctzll(m);
+        const int j = (int)(seg / tiles_x), tx = (int)(seg - (long)j * tiles_x);
+        const int i = 64 * tx + lane;
+        const long c = (long)j * nx + i;
+        Stress st{0.0, 0.0, 0.0, 1.0};
+        if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1)
+            solid_stress_cell(X1, X2, phi, c, nx, dx, dy, mu_s, kappa, w_cut, clamp, false, st);
+        sxx[c] = st.sxx; sxy[c] = st.sxy; syy[c] = st.syy; J[c] = st.J;
+        const double pc = phi[c];
+        H[c] = heaviside(pc, w_t);
+        solid[c] = pc <= 0.0;
+    }
+}
+
 // k_mom_prep over the listed 64 x 16 tiles (momentum_fixup)
 __global__ void __launch_bounds__(256) k_mom_prep_tiles(
     const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ phi,
@@ -40,7 +81,8 @@ __global__ void __launch_bounds__(256) k_mom_prep_tiles(
     double w_t, double rho_s, double rho_f, double *__restrict__ sxx, double *__restrict__ sxy,
     double *__restrict__ syy, double *__restrict__ J, double *__restrict__ H,
     double *__restrict__ rho, unsigned char *__restrict__ solid, const int *__restrict__ tiles,
-    const int *__restrict__ count, int tiles_x, int jlo, int jhi) {
+    const int *__restrict__ count, int tiles_x, int jlo, int jhi,
+    unsigned char *__restrict__ pconst) {
     const int cnt = *count;
     for (int b = blockIdx.x; b < cnt; b += gridDim.x)   // list_grid launch
     for (int q = threadIdx.x; q < MOM_TX * MOM_TY; q += 256) {
@@ -49,6 +91,8 @@ __global__ void __launch_bounds__(256) k_mom_prep_tiles(
         const int j = j0 + q / MOM_TX, i = i0 + q % MOM_TX;
         if (j >= ny || i >= nx || j < jlo || j >= jhi) continue;   // rows [jlo, jhi) only
         const long c = (long)j * nx + i;
+        // k_mom_prep's skip flags: these segments now hold this pass's values
+        if (pconst && q % MOM_TX == 0) pconst[c >> 6] = 0;
         Stress s{0.0, 0.0, 0.0, 1.0};
         if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1)
             solid_stress_cell(X1, X2, phi, c, nx, dx, dy, mu_s, kappa, w_cut, clamp, false, s);
@@ -154,11 +198,7 @@ __global__ void k_stage_rhs(const double *__restrict__ us, const double *__restr
 // point the one-sided edge stencils of grad2 / upwind3 reach.  Tiles are dealt so that the
 // blocks of one XCD take a contiguous band of tile rows (shared halos stay in that XCD's L2).
 constexpr int MS_TX = 64, MS_TY = 16, MS_T = 512;
-constexpr int MS_UX = MS_TX + 6, MS_UY = MS_TY + 6;
-constexpr int MS_GX = MS_TX + 4, MS_GY = MS_TY + 4;
-constexpr int MS_NU = (MS_UX * MS_UY + MS_T - 1) / MS_T;   // per-thread items, phase 1
-constexpr int MS_NG = (MS_GX * MS_GY + MS_T - 1) / MS_T;   // phase 2
-constexpr int MS_NO = (MS_TX * MS_TY + MS_T - 1) / MS_T;   // phase 3
+constexpr int MS_TI = 512;   // threads of the full-grid interior kernel
 
 __device__ __forceinline__ int xcd_tile(int b, int nb) {
     const int per = nb / 8;
@@ -214,9 +254,28 @@ static MomDiv mom_div(double dx, double dy, double rho_s, double rho_f) {
     return m;
 }
 
+// Tile geometry per kind.  An edge tile (!IN) stages the BC'd stage velocity on the tile + 3
+// and the blended stress on the tile + 2: every point the one-sided edge stencils of grad2 /
+// upwind3 reach.  An interior tile takes only the centred stencils: grad2 of the stress reaches
+// +-1 and upwind3 of the velocity +-2, so it stages the stress on the tile + 1 (formed from
+// the velocity at +-1 of it) and the velocity on the tile + 2 -- 12 % fewer phase-1 and 13 %
+// fewer phase-2 cells, same per-cell arithmetic.
+template <bool IN, int T = MS_T>
+struct MsGeo {
+    static constexpr int HU = IN ? 2 : 3, HG = IN ? 1 : 2;
+    static constexpr int UX = MS_TX + 2 * HU, UY = MS_TY + 2 * HU;
+    static constexpr int GX = MS_TX + 2 * HG, GY = MS_TY + 2 * HG;
+    static constexpr int NU = (UX * UY + T - 1) / T;   // per-thread items, phase 1
+    static constexpr int NG = (GX * GY + T - 1) / T;   // phase 2
+    static constexpr int NO = (MS_TX * MS_TY + T - 1) / T;   // phase 3 (output cells)
+};
+constexpr int MS_LDS_U = MsGeo<false>::UX * MsGeo<false>::UY;   // LDS doubles per plane
+constexpr int MS_LDS_G = MsGeo<false>::GX * MsGeo<false>::GY;
+
 // one stage tile (k_mom_stage); IN: an interior tile (see the kernel); SQ: dx == dy (the
-// y divisors are the x ones: fewer live scalar registers)
-template <bool IN, bool SQ, bool S3>
+// y divisors are the x ones: fewer live scalar registers).  su, sv: MsGeo<IN>::UY x UX;
+// gx, gm, gy: GY x GX (LDS, row-major)
+template <bool IN, bool SQ, bool S3, int T = MS_T, bool DC = false>
 __device__ __forceinline__ void ms_tile(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
@@ -229,89 +288,79 @@ __device__ __forceinline__ void ms_tile(
     double *__restrict__ accv, double *__restrict__ outu, double *__restrict__ outv, RowWin rw,
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
-    const unsigned char *__restrict__ fluid_tiles, const MomDiv &K, int i0, int j0, double (&su)[MS_UY][MS_UX], double (&sv)[MS_UY][MS_UX],
-    double (&gx)[MS_GY][MS_GX], double (&gm)[MS_GY][MS_GX], double (&gy)[MS_GY][MS_GX],
-    int (&wfl)[2][MS_T / 64]) {
+    const unsigned char *__restrict__ fluid_tiles, const MomDiv &K, int i0, int j0,
+    double *__restrict__ su, double *__restrict__ sv, double *__restrict__ gx,
+    double *__restrict__ gm, double *__restrict__ gy, int (&wfl)[2][T / 64]) {
+    using G = MsGeo<IN, T>;
+    constexpr int HU = G::HU, HG = G::HG, UX = G::UX, UY = G::UY, GX = G::GX, GY = G::GY;
+    constexpr int NU = G::NU, NG = G::NG, NO = G::NO;
     const DivK &Ky2 = SQ ? K.x2 : K.y2, &Ky6 = SQ ? K.x6 : K.y6, &Ky1 = SQ ? K.x1 : K.y1;
     // pure-fluid tile (k_fluid_rows / k_fluid_win): every cell the blended stress is formed
     // on has phi > max(w_t, w_cut, 0), so H = 1, the elastic stress is 0 and the cell is not
-    // solid exactly -- those constants replace the loads of sxx, sxy, syy, H and solid below
-    // (the arithmetic is unchanged).  One uniform flag per tile.
+    // solid exactly -- those constants replace the loads of sxx, sxy, syy, H and solid below,
+    // and the blend h a + (1 - h) e = 1 a + 0 0 is formed as a + 0.0 (the same value, bit for
+    // bit: 1 a = a, 0 0 = +0).  One uniform flag per tile.
     const bool fluid = fluid_tiles && fluid_tiles[(long)(j0 - rw.lo) * tiles_x + i0 / MS_TX];
     // every global load of the three phases is issued first (one exposed latency per tile),
     // then the LDS phases run
-    double a[MS_NU], b[MS_NU], ka[MS_NU], kb[MS_NU];
-    bool ok1[MS_NU], uc[MS_NU], vc[MS_NU];
-    double uval[MS_NU];
-    double ex[MS_NG], ey[MS_NG], exy[MS_NG], hh2[MS_NG];
-    int sol[MS_NG];   // the solid byte, tested where phase 2 uses it (not at the load)
-    bool ok2[MS_NG];
-    double pc[MS_NO], pxm[MS_NO], pxp[MS_NO], pym[MS_NO], pyp[MS_NO], hh[MS_NO];
-    bool ok[MS_NO];
+    double a[NU], b[NU], ka[NU], kb[NU];
+    bool ok1[NU], uc[NU], vc[NU];
+    double uval[NU];
+    double ex[NG], ey[NG], exy[NG], hh2[NG];
+    int sol[NG];   // the solid byte, tested where phase 2 uses it (not at the load)
+    bool ok2[NG];
+    double pc[NO], pxm[NO], pxp[NO], pym[NO], pyp[NO], hh[NO];
+    bool ok[NO];
     if constexpr (IN) {
         // interior tile: every operand cell lies in the grid and the resident rows, every BC
         // kind is the identity there; addresses are a uniform tile base + a 32-bit offset
-        const long b1 = (long)(j0 - 3) * nx + (i0 - 3), b2 = b1 + nx + 1, b3 = b2 + 2L * nx + 2;
+        const long b1 = (long)(j0 - HU) * nx + (i0 - HU), b3 = (long)j0 * nx + i0;
         const double *u1 = u + b1, *v1 = v + b1, *ku1 = kpu + b1, *kv1 = kpv + b1;
 #pragma unroll
-        for (int it = 0; it < MS_NU; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q - ry * MS_UX;
-            ok1[it] = q < MS_UX * MS_UY;
+        for (int it = 0; it < NU; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / UX, rx = q - ry * UX;
+            ok1[it] = q < UX * UY;
             const int o = ok1[it] ? ry * nx + rx : 0;
             uc[it] = false; vc[it] = false; uval[it] = 0.0;
             a[it] = u1[o]; b[it] = v1[o];
             ka[it] = stage ? ku1[o] : 0.0; kb[it] = stage ? kv1[o] : 0.0;
         }
-        // a pure-fluid tile reads every operand from its first output cell (j0, i0) instead,
-        // which prep wrote (an output row) and which is fluid (0, 0, 0, H = 1, not solid):
-        // one cached line, and no branch, so no load result is consumed before the barrier
-        const double *sxx2 = sxx + b2, *syy2 = syy + b2, *sxy2 = sxy + b2, *H2 = H + b2;
-        const unsigned char *sol2 = solid + b2;
-        const int ofl = 2 * nx + 2;   // (j0, i0) from the stress region's corner
+        (void)b3;
 #pragma unroll
-        for (int it = 0; it < MS_NG; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q - ry * MS_GX;
-            ok2[it] = q < MS_GX * MS_GY;
-            const int o = fluid ? ofl : ok2[it] ? ry * nx + rx : 0;
-            ex[it] = sxx2[o]; ey[it] = syy2[o]; exy[it] = sxy2[o]; hh2[it] = H2[o];
-            sol[it] = sol2[o];
-        }
-        const double *p3 = p + b3, *H3 = H + b3;
-#pragma unroll
-        for (int it = 0; it < MS_NO; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q - ry * MS_TX;
+        for (int it = 0; it < NO; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / MS_TX;
             ok[it] = q < MS_TX * MS_TY && j0 + ry >= olo && j0 + ry < ohi;   // output rows
-            const int o = ok[it] ? ry * nx + rx : 0;
-            pc[it] = p3[o]; pxp[it] = p3[o + 1]; pxm[it] = p3[o - 1];
-            pyp[it] = p3[o + nx]; pym[it] = p3[o - nx];
-            hh[it] = H3[fluid ? 0 : o];
+            pc[it] = 0.0;   // (the one-sided edge stencils only)
+        }
+        // a pure-fluid tile loads no phase-2 operand (the constants above); the others issue
+        // theirs after phase 1 (interior tiles run at 6 waves per SIMD: the phase-1 operands'
+        // registers are reused)
+#pragma unroll
+        for (int it = 0; it < NG; ++it) {
+            ok2[it] = threadIdx.x + it * T < GX * GY;
+            ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh2[it] = 1.0; sol[it] = 0;
         }
     } else {
     {
     #pragma unroll
-            for (int it = 0; it < MS_NU; ++it) {
-                const int q = threadIdx.x + it * MS_T, ry = q / MS_UX, rx = q % MS_UX;
-                const int j = j0 - 3 + ry, i = i0 - 3 + rx;
-                ok1[it] = q < MS_UX * MS_UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
+            for (int it = 0; it < NU; ++it) {
+                const int q = threadIdx.x + it * T, ry = q / UX, rx = q % UX;
+                const int j = j0 - HU + ry, i = i0 - HU + rx;
+                ok1[it] = q < UX * UY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
                 long cu, cv;
-                if constexpr (IN) {   // interior cell: every BC kind is the identity there
-                    uc[it] = false; vc[it] = false; uval[it] = 0.0;
-                    cu = cv = ok1[it] ? (long)j * nx + i : (long)rw.lo * nx;
-                } else {
-                    const BCSrc s = bc_source(bc, lid, ok1[it] ? j : 1, ok1[it] ? i : 1, ny, nx);
-                    uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
-                    cu = ok1[it] ? s.u_src : (long)rw.lo * nx; cv = ok1[it] ? s.v_src : (long)rw.lo * nx;
-                }
+                const BCSrc s = bc_source(bc, lid, ok1[it] ? j : 1, ok1[it] ? i : 1, ny, nx);
+                uc[it] = s.u_const; vc[it] = s.v_const; uval[it] = s.u_val;
+                cu = ok1[it] ? s.u_src : (long)rw.lo * nx; cv = ok1[it] ? s.v_src : (long)rw.lo * nx;
                 a[it] = u[cu]; b[it] = v[cv];
                 ka[it] = stage ? kpu[cu] : 0.0; kb[it] = stage ? kpv[cv] : 0.0;
             }
         }
         // phase-2 operands: the elastic stress, H and the solid mask on the tile + 2 halo
     #pragma unroll
-        for (int it = 0; it < MS_NG; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
-            const int j = j0 - 2 + ry, i = i0 - 2 + rx;
-            ok2[it] = q < MS_GX * MS_GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
+        for (int it = 0; it < NG; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / GX, rx = q % GX;
+            const int j = j0 - HG + ry, i = i0 - HG + rx;
+            ok2[it] = q < GX * GY && j >= rw.lo && j < rw.hi && i >= 0 && i < nx;
             const long c = ok2[it] ? (long)j * nx + i : (long)rw.lo * nx;
             if (fluid) {
                 ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh2[it] = 1.0; sol[it] = 0;
@@ -322,8 +371,8 @@ __device__ __forceinline__ void ms_tile(
         }
         // phase-3 operands on the output cells
     #pragma unroll
-        for (int it = 0; it < MS_NO; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+        for (int it = 0; it < NO; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / MS_TX, rx = q % MS_TX;
             const int j = j0 + ry, i = i0 + rx;
             ok[it] = q < MS_TX * MS_TY && j >= olo && j < ohi && i < nx;   // output rows
             const long c = ok[it] ? (long)j * nx + i : (long)rw.lo * nx;
@@ -345,21 +394,21 @@ __device__ __forceinline__ void ms_tile(
     // through wfl) sends the rest of the tile -- or the one cell -- to the checked divk.
     const bool lane0 = (threadIdx.x & 63) == 0;
     const int wv = threadIdx.x >> 6;
-    double s3a[MS_NO], s3b[MS_NO], s3c[MS_NO], s3d[MS_NO], s3e[MS_NO], s3f[MS_NO];
-    double x1[MS_NO], y1[MS_NO];
+    double s3a[NO], s3b[NO], s3c[NO], s3d[NO], s3e[NO], s3f[NO];
+    double x1[NO], y1[NO];
     // 1. stage velocity (functions.py:714), BC applied
     {
         DivNote nt;
 #pragma unroll
-        for (int it = 0; it < MS_NU; ++it) {
-            const int q = threadIdx.x + it * MS_T;
-            if (q >= MS_UX * MS_UY) break;
+        for (int it = 0; it < NU; ++it) {
+            const int q = threadIdx.x + it * T;
+            if (q >= UX * UY) break;
             const double ru = stage == 0 ? a[it] : a[it] + coef * ka[it];
             const double rv = stage == 0 ? b[it] : b[it] + coef * kb[it];
             const double su_ = !ok1[it] ? 0.0 : uc[it] ? uval[it] : ru;
             const double sv_ = !ok1[it] ? 0.0 : vc[it] ? 0.0 : rv;
-            (&su[0][0])[q] = su_;
-            (&sv[0][0])[q] = sv_;
+            su[q] = su_;
+            sv[q] = sv_;
             if constexpr (IN) { nt.note(su_); nt.note(sv_); }
         }
         if constexpr (IN) {
@@ -367,38 +416,59 @@ __device__ __forceinline__ void ms_tile(
             if (lane0) wfl[0][wv] = bad;
         }
     }
+    if constexpr (IN) {
+        if (!fluid) {
+            const long b2 = (long)(j0 - HG) * nx + (i0 - HG);
+            const double *sxx2 = sxx + b2, *syy2 = syy + b2, *sxy2 = sxy + b2, *H2 = H + b2;
+            const unsigned char *sol2 = solid + b2;
+#pragma unroll
+            for (int it = 0; it < NG; ++it) {
+                const int q = threadIdx.x + it * T, ry = q / GX, rx = q - ry * GX;
+                const int o = ok2[it] ? ry * nx + rx : 0;
+                ex[it] = sxx2[o]; ey[it] = syy2[o]; exy[it] = sxy2[o]; hh2[it] = H2[o];
+                sol[it] = sol2[o];
+            }
+        }
+    }
     __syncthreads();
     bool chk = !IN || !K.nc;
     if constexpr (IN) {
 #pragma unroll
-        for (int w = 0; w < MS_T / 64; ++w) chk = chk || wfl[0][w];
+        for (int w = 0; w < T / 64; ++w) chk = chk || wfl[0][w];
     }
-    // 2. blended stress (functions.py:717-735, 906-921)
-    auto phase2 = [&](auto ctag) {
-        constexpr bool CHK = decltype(ctag)::value;
+    // 2. blended stress (functions.py:717-735, 906-921); stress cell (ry, rx) is the velocity
+    // cell (ry + 1, rx + 1) (HU - HG = 1 for both kinds)
+    auto phase2 = [&](auto ctag, auto ftag) {
+        constexpr bool CHK = decltype(ctag)::value, FL = decltype(ftag)::value;
         DivNote nt;
 #pragma unroll
-        for (int it = 0; it < MS_NG; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_GX, rx = q % MS_GX;
-            if (q >= MS_GX * MS_GY) break;
-            const int j = j0 - 2 + ry, i = i0 - 2 + rx;
+        for (int it = 0; it < NG; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / GX, rx = q % GX;
+            if (q >= GX * GY) break;
+            const int j = j0 - HG + ry, i = i0 - HG + rx;
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
             if (ok2[it]) {
-                const double *pu = &su[ry + 1][rx + 1], *pv = &sv[ry + 1][rx + 1];
-                const double dudx = g2<IN, CHK>(pu, 1, i, nx, K.x2), dvdy = g2<IN, CHK>(pv, MS_UX, j, ny, Ky2);
-                const double dudy = g2<IN, CHK>(pu, MS_UX, j, ny, Ky2), dvdx = g2<IN, CHK>(pv, 1, i, nx, K.x2);
-                double e1 = ex[it], e2 = ey[it], e3 = exy[it];
-                if (visc && sol[it] != 0) {
-                    e1 = e1 + eta_s * dudx;
-                    e2 = e2 + eta_s * dvdy;
-                    e3 = e3 + eta_s * 0.5 * (dudy + dvdx);
+                const double *pu = su + (ry + 1) * UX + rx + 1, *pv = sv + (ry + 1) * UX + rx + 1;
+                const double dudx = g2<IN, CHK>(pu, 1, i, nx, K.x2), dvdy = g2<IN, CHK>(pv, UX, j, ny, Ky2);
+                const double dudy = g2<IN, CHK>(pu, UX, j, ny, Ky2), dvdx = g2<IN, CHK>(pv, 1, i, nx, K.x2);
+                if constexpr (FL) {   // h = 1, e = 0, not solid (see above)
+                    oxx = 2 * mu_f * dudx + 0.0;
+                    oyy = 2 * mu_f * dvdy + 0.0;
+                    oxy = mu_f * (dudy + dvdx) + 0.0;
+                } else {
+                    double e1 = ex[it], e2 = ey[it], e3 = exy[it];
+                    if (visc && sol[it] != 0) {
+                        e1 = e1 + eta_s * dudx;
+                        e2 = e2 + eta_s * dvdy;
+                        e3 = e3 + eta_s * 0.5 * (dudy + dvdx);
+                    }
+                    const double h = hh2[it], omh = 1 - h;
+                    oxx = h * (2 * mu_f * dudx) + omh * e1;
+                    oyy = h * (2 * mu_f * dvdy) + omh * e2;
+                    oxy = h * (mu_f * (dudy + dvdx)) + omh * e3;
                 }
-                const double h = hh2[it], omh = 1 - h;
-                oxx = h * (2 * mu_f * dudx) + omh * e1;
-                oyy = h * (2 * mu_f * dvdy) + omh * e2;
-                oxy = h * (mu_f * (dudy + dvdx)) + omh * e3;
             }
-            (&gx[0][0])[q] = oxx; (&gm[0][0])[q] = oxy; (&gy[0][0])[q] = oyy;
+            gx[q] = oxx; gm[q] = oxy; gy[q] = oyy;
             if constexpr (!CHK) { nt.note(oxx); nt.note(oxy); nt.note(oyy); }
         }
         if constexpr (!CHK) {
@@ -407,17 +477,22 @@ __device__ __forceinline__ void ms_tile(
         }
     };
     if constexpr (IN) {
-        if (chk) phase2(std::true_type{});
-        else phase2(std::false_type{});
+        if (fluid) {
+            if (chk) phase2(std::true_type{}, std::true_type{});
+            else phase2(std::false_type{}, std::true_type{});
+        } else {
+            if (chk) phase2(std::true_type{}, std::false_type{});
+            else phase2(std::false_type{}, std::false_type{});
+        }
     } else {
-        phase2(std::true_type{});
+        phase2(std::true_type{}, std::false_type{});
     }
     if constexpr (S3) {
         // the last stage's k planes and u, v at the output cells, issued here (phase 2's
         // operands are dead) so that they arrive during phase 3's LDS reads
 #pragma unroll
-        for (int it = 0; it < MS_NO; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q - ry * MS_TX;
+        for (int it = 0; it < NO; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / MS_TX, rx = q - ry * MS_TX;
             const long c = ok[it] ? (long)(j0 + ry) * nx + i0 + rx : (long)rw.lo * nx;
             s3a[it] = ainu[c]; s3b[it] = k2u[c]; s3c[it] = kpu[c];
             s3d[it] = ainv[c]; s3e[it] = k2v[c]; s3f[it] = kpv[c];
@@ -428,15 +503,28 @@ __device__ __forceinline__ void ms_tile(
     if constexpr (IN) {
         if (!chk) {
 #pragma unroll
-            for (int w = 0; w < MS_T / 64; ++w) chk = chk || wfl[1][w];
+            for (int w = 0; w < T / 64; ++w) chk = chk || wfl[1][w];
+        }
+    }
+    if constexpr (IN) {
+        // the pressure operands and H at the output cells: loaded here, not held through
+        // phases 1 and 2 (register pressure; the other waves hide the latency)
+        const double *p3 = p + (long)j0 * nx + i0, *H3 = H + (long)j0 * nx + i0;
+#pragma unroll
+        for (int it = 0; it < NO; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / MS_TX, rx = q - ry * MS_TX;
+            const int o = ok[it] ? ry * nx + rx : 0;
+            pxp[it] = p3[o + 1]; pxm[it] = p3[o - 1];
+            pyp[it] = p3[o + nx]; pym[it] = p3[o - nx];
+            hh[it] = fluid ? 1.0 : H3[o];
         }
     }
     // 3. RHS and RK4 accumulation (functions.py:923-944, 743-758); stage 3 forms
     // acc = (k1 + 2 k2) + 2 k3 from the three k planes (loaded here: registers)
     {
-        double x0[MS_NO], y0[MS_NO];
+        double x0[NO], y0[NO];
 #pragma unroll
-        for (int it = 0; it < MS_NO; ++it) {
+        for (int it = 0; it < NO; ++it) {
             x0[it] = 0.0; y0[it] = 0.0;
             if constexpr (S3) {   // formed here (pinned): 4 registers live through the cells, not 8
                 x0[it] = (s3a[it] + 2 * s3b[it]) + 2 * s3c[it];
@@ -449,16 +537,17 @@ __device__ __forceinline__ void ms_tile(
             constexpr bool CHK = decltype(ctag)::value;
             const int j = j0 + ry, i = i0 + rx;
             const long c = (long)j * nx + i;
-            const double divx = g2<IN, CHK>(&gx[ry + 2][rx + 2], 1, i, nx, K.x2) +
-                                g2<IN, CHK>(&gm[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
-            const double divy = g2<IN, CHK>(&gm[ry + 2][rx + 2], 1, i, nx, K.x2) +
-                                g2<IN, CHK>(&gy[ry + 2][rx + 2], MS_GX, j, ny, Ky2);
-            const double *pu = &su[ry + 3][rx + 3], *pv = &sv[ry + 3][rx + 3];
+            const int gq = (ry + HG) * GX + rx + HG, uq = (ry + HU) * UX + rx + HU;
+            const double divx = g2<IN, CHK>(gx + gq, 1, i, nx, K.x2) +
+                                g2<IN, CHK>(gm + gq, GX, j, ny, Ky2);
+            const double divy = g2<IN, CHK>(gm + gq, 1, i, nx, K.x2) +
+                                g2<IN, CHK>(gy + gq, GX, j, ny, Ky2);
+            const double *pu = su + uq, *pv = sv + uq;
             const double uc = *pu, vc = *pv;
             const double uadv = -uc * u3<IN, CHK>(pu, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * u3<IN, CHK>(pu, MS_UX, j, ny, vc, Ky6, Ky1);
+                                vc * u3<IN, CHK>(pu, UX, j, ny, vc, Ky6, Ky1);
             const double vadv = -uc * u3<IN, CHK>(pv, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * u3<IN, CHK>(pv, MS_UX, j, ny, vc, Ky6, Ky1);
+                                vc * u3<IN, CHK>(pv, UX, j, ny, vc, Ky6, Ky1);
             // grad2 of p with the operands loaded above (same expressions as grad2)
             double dpx, dpy;
             if (IN) {
@@ -476,7 +565,7 @@ __device__ __forceinline__ void ms_tile(
             }
             const double h = hh[it];
             double k1, k2;
-            if (K.den_const) {   // uniform: (1 - h) rho + h rho == rho (MomDiv)
+            if (DC || K.den_const) {   // uniform: (1 - h) rho + h rho == rho (MomDiv)
                 const double nu = divx + 0.0 - dpx, nv = divy + 0.0 - dpy;
                 const double fu = h == h ? nu : h, fv = h == h ? nv : h;
                 if constexpr (!CHK) { nt->note(fu); nt->note(fv); }
@@ -490,8 +579,8 @@ __device__ __forceinline__ void ms_tile(
             return make_double2(k1, k2);
         };
 #pragma unroll
-        for (int it = 0; it < MS_NO; ++it) {
-            const int q = threadIdx.x + it * MS_T, ry = q / MS_TX, rx = q % MS_TX;
+        for (int it = 0; it < NO; ++it) {
+            const int q = threadIdx.x + it * T, ry = q / MS_TX, rx = q % MS_TX;
             if (!ok[it]) continue;
             const long c = (long)(j0 + ry) * nx + i0 + rx;
             double2 kk;
@@ -513,15 +602,21 @@ __device__ __forceinline__ void ms_tile(
                 outu[c] = x1[it] + dt6 * (x0[it] + k1);
                 outv[c] = y1[it] + dt6 * (y0[it] + k2);
             }
+            // one cell's LDS reads in flight at a time (hoisting the next cell's ~26 reads
+            // above this one's arithmetic doubled the live registers)
+            if constexpr (IN) __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
 
 // IN: the interior tiles only (the others return), !IN: the others (a host-built list of the
 // tiles a full launch does not cover, or the fix-up list).  Two kernels instead of a branch:
-// the interior body alone fits its registers (no scalar spills).
-template <bool IN, bool SQ, bool S3>
-__global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
+// the interior body alone fits its registers (no scalar spills), and its LDS is the smaller
+// interior geometry.
+// DC: K.den_const known on the host (drops the IEEE density division's registers: the
+// interior stages 0-2 then run 6 waves per SIMD, LDS 50 KB per block)
+template <bool IN, bool SQ, bool S3, bool DC>
+__global__ void __launch_bounds__(IN ? MS_TI : MS_T, IN && DC && !S3 ? 6 : 4) k_mom_stage(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
     const double *__restrict__ sxx, const double *__restrict__ sxy,
@@ -534,14 +629,16 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
     const unsigned char *__restrict__ fluid_tiles, MomDiv K) {
-    __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
+    constexpr int T = IN ? MS_TI : MS_T;
+    using G = MsGeo<IN, T>;
+    __shared__ double su[G::UX * G::UY], sv[G::UX * G::UY];
     if (dtp) {   // the same roundings as mom_stage's host constants
         const double dt = *dtp;
         coef = stage == 0 ? 0.0 : stage == 3 ? dt : 0.5 * dt;
         dt6 = dt / 6.0;
     }
-    __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
-    __shared__ int wfl[2][MS_T / 64];   // per-wave failed DivNote flags of phases 1 and 2
+    __shared__ double gx[G::GX * G::GY], gm[G::GX * G::GY], gy[G::GX * G::GY];
+    __shared__ int wfl[2][T / 64];   // per-wave failed DivNote flags of phases 1 and 2
     // tlist: the listed tiles only (momentum_fixup); otherwise every tile of rows [jb, je)
     if (tlist && (int)blockIdx.x >= (tcount ? *tcount : ntiles)) return;
     const int tile = tlist ? tlist[blockIdx.x] : xcd_tile(blockIdx.x, ntiles);
@@ -551,7 +648,7 @@ __global__ void __launch_bounds__(MS_T, 4) k_mom_stage(
     const bool interior = i0 - 3 >= 2 && i0 + MS_TX + 3 <= nx - 2 && j0 - 3 >= max(rw.lo, 2) &&
                           j0 + MS_TY + 3 <= min(rw.hi, ny - 2);
     if (interior != IN) return;
-    ms_tile<IN, SQ, S3>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
+    ms_tile<IN, SQ, S3, T, DC>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
 }
 
 // The listed tiles (momentum_fixup), interior and edge alike, in one launch of at most
@@ -571,8 +668,8 @@ __global__ void __launch_bounds__(MS_T, 2) k_mom_stage_list(
     const int *__restrict__ tlist, const int *__restrict__ tcount, const double *__restrict__ dtp,
     int olo, int ohi, const double *__restrict__ k2u, const double *__restrict__ k2v,
     const unsigned char *__restrict__ fluid_tiles, MomDiv K) {
-    __shared__ double su[MS_UY][MS_UX], sv[MS_UY][MS_UX];
-    __shared__ double gx[MS_GY][MS_GX], gm[MS_GY][MS_GX], gy[MS_GY][MS_GX];
+    __shared__ double su[MS_LDS_U], sv[MS_LDS_U];
+    __shared__ double gx[MS_LDS_G], gm[MS_LDS_G], gy[MS_LDS_G];
     __shared__ int wfl[2][MS_T / 64];
     if (dtp) {
         const double dt = *dtp;
@@ -679,11 +776,14 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
     const double *kpu = s ? ku[s - 1] : u, *kpv = s ? kv[s - 1] : v;
     const bool sq = P->dx == P->dy;
     const bool s3 = s == 3;
-    auto kin = sq ? (s3 ? k_mom_stage<true, true, true> : k_mom_stage<true, true, false>)
-                  : (s3 ? k_mom_stage<true, false, true> : k_mom_stage<true, false, false>);
-    auto kedge = sq ? (s3 ? k_mom_stage<false, true, true> : k_mom_stage<false, true, false>)
-                    : (s3 ? k_mom_stage<false, false, true> : k_mom_stage<false, false, false>);
     const MomDiv K = mom_div(P->dx, P->dy, P->rho_s, P->rho_f);
+    const bool dc = K.den_const;
+    auto kin = dc ? (sq ? (s3 ? k_mom_stage<true, true, true, true> : k_mom_stage<true, true, false, true>)
+                        : (s3 ? k_mom_stage<true, false, true, true> : k_mom_stage<true, false, false, true>))
+                  : (sq ? (s3 ? k_mom_stage<true, true, true, false> : k_mom_stage<true, true, false, false>)
+                        : (s3 ? k_mom_stage<true, false, true, false> : k_mom_stage<true, false, false, false>));
+    auto kedge = sq ? (s3 ? k_mom_stage<false, true, true, false> : k_mom_stage<false, true, false, false>)
+                    : (s3 ? k_mom_stage<false, false, true, false> : k_mom_stage<false, false, false, false>);
     // the tiles a full launch's interior kernel skips (host list, per row window)
     const int *elist = tlist, *ecount = tcount;
     int enb = ntiles;
@@ -699,7 +799,7 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
         auto kl = sq ? k_mom_stage_list<true> : k_mom_stage_list<false>;
         kl<<<list_grid(ntiles), MS_T, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
     } else {
-        kin<<<ntiles, MS_T, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
+        kin<<<ntiles, MS_TI, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
         if (enb > 0) kedge<<<enb, MS_T, 0, ctx->stream>>>(MS_ARGS(elist, ecount, enb));
     }
 #undef MS_ARGS
@@ -994,7 +1094,7 @@ static int mom_rows(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const dou
 }
 
 // ------------------------------------------------------------ temporally blocked RK4 --
-// The four stages of one TX x TY output tile in one workgroup.  Stage s needs stage s-1 two
+// The four stages of one MS_TX x MS_TY output tile in one workgroup.  Stage s needs stage s-1 two
 // cells out (upwind3 / grad2 of the blended stress), so on the tile plus an 8-cell halo the
 // stage velocity lives in LDS on halo 2(3-s)+2, the blended stress on 2(3-s)+1 and k is formed
 // on 2(3-s); the per-cell inputs (u, v, elastic stress, H, grad p) and the RK4 accumulators
@@ -1013,18 +1113,18 @@ struct Rk4Args {
     MomDiv K;
 };
 constexpr int RK_HL = 8;
-template <int TX, int TY>
-constexpr int rk4_lds() { return 5 * (TX + 2 * RK_HL) * (TY + 2 * RK_HL) * (int)sizeof(double); }
+template <int MS_TX, int MS_TY>
+constexpr int rk4_lds() { return 5 * (MS_TX + 2 * RK_HL) * (MS_TY + 2 * RK_HL) * (int)sizeof(double); }
 
-template <int TX, int TY, int NT>
+template <int MS_TX, int MS_TY, int NT>
 __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
-    constexpr int HL = RK_HL, RX = TX + 2 * HL, RY = TY + 2 * HL, NR = RX * RY;
+    constexpr int HL = RK_HL, RX = MS_TX + 2 * HL, RY = MS_TY + 2 * HL, NR = RX * RY;
     constexpr int NQ = (NR + NT - 1) / NT;
     extern __shared__ double rk_lds[];
     double *U = rk_lds, *V = U + NR, *GX = V + NR, *GM = GX + NR, *GY = GM + NR;
     if (A.tlist && (int)blockIdx.x >= *A.tcount) return;
     const int tile = A.tlist ? A.tlist[blockIdx.x] : xcd_tile(blockIdx.x, A.ntiles);
-    const int ri = (tile % A.tiles_x) * TX - HL, rj = A.rw.jb + (tile / A.tiles_x) * TY - HL;
+    const int ri = (tile % A.tiles_x) * MS_TX - HL, rj = A.rw.jb + (tile / A.tiles_x) * MS_TY - HL;
     const int nx = A.nx, ny = A.ny;
     const MomDiv &K = A.K;
     const double dt = A.dtp ? *A.dtp : A.dt;
@@ -1054,7 +1154,7 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
             u0[m] = A.u[c]; v0[m] = A.v[c];
             ex[m] = A.sxx[c]; ey[m] = A.syy[c]; exy[m] = A.sxy[c]; hh[m] = A.H[c];
             solm |= (unsigned)(A.solid[c] != 0) << m;
-            const bool k0 = ok && ly >= HL - 6 && ly < HL + TY + 6 && lx >= HL - 6 && lx < HL + TX + 6;
+            const bool k0 = ok && ly >= HL - 6 && ly < HL + MS_TY + 6 && lx >= HL - 6 && lx < HL + MS_TX + 6;
             dpx[m] = k0 ? grad2k(A.p + c, 1, i, nx, K.x2) : 0.0;
             dpy[m] = k0 ? grad2k(A.p + c, nx, j, ny, K.y2) : 0.0;
             au[m] = 0.0; av[m] = 0.0;
@@ -1075,7 +1175,7 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
 #pragma unroll
         for (int m = 0; m < NQ; ++m) {
             const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-            if (q >= NR || ly < HL - hg || ly >= HL + TY + hg || lx < HL - hg || lx >= HL + TX + hg)
+            if (q >= NR || ly < HL - hg || ly >= HL + MS_TY + hg || lx < HL - hg || lx >= HL + MS_TX + hg)
                 continue;
             const int j = rj + ly, i = ri + lx;
             double oxx = 0.0, oxy = 0.0, oyy = 0.0;
@@ -1103,8 +1203,8 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
         for (int m = 0; m < NQ; ++m) {
             ru[m] = 0.0; rv[m] = 0.0;
             const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + TY + hk ||
-                lx < HL - hk || lx >= HL + TX + hk)
+            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + MS_TY + hk ||
+                lx < HL - hk || lx >= HL + MS_TX + hk)
                 continue;
             const int j = rj + ly, i = ri + lx;
             if (st == 3 && (j < A.olo || j >= A.ohi)) continue;
@@ -1137,7 +1237,7 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
                 ru[m] = u0[m] + cf * k1; rv[m] = v0[m] + cf * k2;
             } else {
                 const long c = (long)j * nx + i;
-                if (ly >= HL && ly < HL + TY && lx >= HL && lx < HL + TX) {
+                if (ly >= HL && ly < HL + MS_TY && lx >= HL && lx < HL + MS_TX) {
                     A.outu[c] = u0[m] + dt6 * (au[m] + k1);
                     A.outv[c] = v0[m] + dt6 * (av[m] + k2);
                 }
@@ -1149,8 +1249,8 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
 #pragma unroll
         for (int m = 0; m < NQ; ++m) {
             const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + TY + hk ||
-                lx < HL - hk || lx >= HL + TX + hk)
+            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + MS_TY + hk ||
+                lx < HL - hk || lx >= HL + MS_TX + hk)
                 continue;
             const int j = rj + ly, i = ri + lx;
             const bool edge = i == 0 || i == nx - 1 || j == 0 || j == ny - 1;
@@ -1162,8 +1262,8 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
 #pragma unroll
             for (int m = 0; m < NQ; ++m) {
                 const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-                if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + TY + hk ||
-                    lx < HL - hk || lx >= HL + TX + hk)
+                if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + MS_TY + hk ||
+                    lx < HL - hk || lx >= HL + MS_TX + hk)
                     continue;
                 const int j = rj + ly, i = ri + lx;
                 if (!(i == 0 || i == nx - 1 || j == 0 || j == ny - 1)) continue;
@@ -1181,16 +1281,16 @@ __global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
     }
 }
 
-template <int TX, int TY, int NT>
+template <int MS_TX, int MS_TY, int NT>
 static int launch_rk4(rmt_ctx *ctx, const Rk4Args &A, int nblocks) {
     static bool attr = false;
     if (!attr) {
-        RMT_HIP(hipFuncSetAttribute((const void *)k_mom_rk4<TX, TY, NT>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, rk4_lds<TX, TY>()));
+        RMT_HIP(hipFuncSetAttribute((const void *)k_mom_rk4<MS_TX, MS_TY, NT>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, rk4_lds<MS_TX, MS_TY>()));
         attr = true;
     }
     if (nblocks <= 0) return RMT_OK;
-    k_mom_rk4<TX, TY, NT><<<nblocks, NT, rk4_lds<TX, TY>(), ctx->stream>>>(A);
+    k_mom_rk4<MS_TX, MS_TY, NT><<<nblocks, NT, rk4_lds<MS_TX, MS_TY>(), ctx->stream>>>(A);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -1249,9 +1349,22 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
               "momentum window: resident rows must cover the RK4 halo (9 rows)");
     double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
     const RowWin wp = grow(7);
-    k_mom_prep<<<grid1d((long)(wp.je - wp.jb) * nx, 256), 256, 0, ctx->stream>>>(
-        X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
-        P->rho_f, sxx, sxy, syy, J, W.H, g_mom_mode == 2 ? W.rho : nullptr, W.solid, wp.jb, wp.je);
+    // skip the pure-fluid segments whose planes already hold the constants: needs the fluid
+    // flags before the prep (written by the phi producer) and 64-column segments
+    const bool pskip = W.prep_const && W.fluid_rows_ready && nx % 64 == 0 && MS_TX == 64 &&
+                       g_mom_mode != 2;
+    if (pskip) {
+        const long nseg = (long)(wp.je - wp.jb) * (nx / 64);
+        k_mom_prep_seg<<<(unsigned)((nseg + 4 * PS_SEGS - 1) / (4 * PS_SEGS)), 256, 0, ctx->stream>>>(
+            X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t,
+            sxx, sxy, syy, J, W.H, W.solid, wp.jb, wp.je, fluid_rows_buf(W, w0.lo, nx), w0.lo,
+            W.prep_const);
+    } else {
+        k_mom_prep<<<grid1d((long)(wp.je - wp.jb) * nx, 256), 256, 0, ctx->stream>>>(
+            X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
+            P->rho_f, sxx, sxy, syy, J, W.H, g_mom_mode == 2 ? W.rho : nullptr, W.solid, wp.jb,
+            wp.je);
+    }
     RMT_LAUNCHED();
     // visc = eta_s > 0 and any(solid): cells with no solid contribute nothing anyway, so
     // the per-cell solid test reproduces the reference's np.any guard.
@@ -1337,7 +1450,7 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
     k_mom_prep_tiles<<<list_grid(max_tiles), 256, 0, ctx->stream>>>(
         X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
         P->rho_f, sxx, sxy, syy, J, W.H, nullptr, W.solid, tiles, count, tiles_x, grow(7).first,
-        grow(7).second);
+        grow(7).second, nx % 64 == 0 ? W.prep_const : nullptr);
     RMT_LAUNCHED();
     const RowWin all{0, ny, w0.lo, w0.hi};
     if (g_mom_mode == 1 && P->bc_kind != RMT_BC_PERIODIC) {

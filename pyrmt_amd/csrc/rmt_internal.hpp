@@ -562,6 +562,10 @@ struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + 
     // the pure-fluid row flags (k_fluid_rows' output, at fluid_rows_buf) were already written
     // by the producer of phi (the fused step's k_phi_rebuild): momentum_rk4 skips that pass
     bool fluid_rows_ready = false;
+    // per 64-column row segment (nx % 64 == 0), persistent across steps: the last write of the
+    // prep planes there was a pure-fluid segment's constants, so k_mom_prep may skip it while
+    // it stays pure fluid (null: prep every cell)
+    unsigned char *prep_const = nullptr;
 };
 inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
     return MomWork{w,          w + n,      w + 2 * n,  w + 3 * n,  w + 4 * n,  w + 5 * n,

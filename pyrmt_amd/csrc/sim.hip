@@ -66,6 +66,8 @@ struct rmt_sim {
     // double-buffered with kbits, valid from the second step of a call on
     unsigned long long *kbits_next = nullptr;
     bool bits_ready = false;
+    // k_mom_prep's per-segment skip flags (MomWork::prep_const), cleared at each call's start
+    unsigned char *pconst = nullptr;
     int *segs = nullptr;     // rim row segments (k_rim_segments): ny * ceil(nx / 256) + count
     unsigned long long *m2acc = nullptr;   // k_dt_part's atomic max + block counter (zeroed)
     bool prof = false;
@@ -587,6 +589,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     S->segs = (int *)(S->kbits_next + (size_t)ny * Wn);
     S->m2acc = (unsigned long long *)(S->segs + (((size_t)ny * ((nx + 255) / 256) + 3) & ~(size_t)1));
     RMT_HIP(hipMemsetAsync(S->m2acc, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    if (nx % 64 == 0) RMT_HIP(hipMalloc(&S->pconst, (size_t)ny * (nx / 64)));
     if (S->st2) {
         RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_proj, hipEventDisableTiming));
@@ -607,6 +610,7 @@ int rmt_sim_destroy(rmt_sim *S) {
     if (!S) return RMT_OK;
     (void)hipFree(S->block);
     if (S->m2part) (void)hipFree(S->m2part);
+    if (S->pconst) (void)hipFree(S->pconst);
     if (S->tiles) (void)hipFree(S->tiles);
     if (S->e_sl) (void)hipEventDestroy(S->e_sl);
     if (S->e_mom) (void)hipEventDestroy(S->e_mom);
@@ -738,6 +742,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         return RMT_OK;
     };
     S->bits_ready = false;   // the caller may have changed the map between calls
+    // ... or the prep planes: the first prep of a call writes every segment
+    if (S->pconst) RMT_HIP(hipMemsetAsync(S->pconst, 0, (size_t)ny * (nx / 64), st));
     // the next step's rim words and extrapolation geometry, prepared on the second stream
     // beside this step's projection (they depend on the known plane alone)
     static const bool geo_env = !(getenv("RMT_EARLY_GEOMETRY") && !atoi(getenv("RMT_EARLY_GEOMETRY")));
@@ -781,6 +787,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         M.detg_clamp = P.detg_clamp;
         MomWork W = mom_work(S->mw, n, S->mbytes, S->flag + 1);
         W.dtp = dtp;
+        W.prep_const = S->pconst;
         // the extrapolation chain occupies one CU for milliseconds; everything it does not
         // feed runs beside it: the momentum of every cell, from the pre-extrapolation map, on
         // a second stream, re-run afterwards on the tiles within reach of a target
@@ -956,9 +963,16 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                    S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,
                                    S->max_tiles));
         } else {
-            // 4. phi from the advected + extrapolated map
-            k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R, S->phi,
-                                              S->X1, S->X2, nb);
+            // 4. phi from the advected + extrapolated map (and the momentum's pure-fluid flags)
+            if (fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 && MOM_TX == 64) {
+                k_phi_rebuild_fluid<<<g, 256, 0, st>>>(
+                    S->X1n, S->X2n, n, nx, (nx + 63) / 64, P.x0, P.y0, P.R, S->phi, S->X1,
+                    S->X2, nb, fluid_threshold(&M), fluid_rows_buf(W, 0, nx));
+                W.fluid_rows_ready = true;
+            } else {
+                k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R,
+                                                  S->phi, S->X1, S->X2, nb);
+            }
             RMT_LAUNCHED();
             if (par && async && geo_env && nb && P.layers > 0 && S->st2 && it + 1 < nsteps) {
                 // the next step's extrapolation geometry (known plane nb) beside this step's

@@ -1,13 +1,15 @@
 """Print one steady-state step of a rocprofv3 kernel trace: every dispatch between two
-consecutive k_ex_chain launches, with queue, start/end (us, relative to the first chain's
-end) and duration.  usage: python tools/step_window.py TRACE.csv [STEP_INDEX]"""
+consecutive launches of the key kernel (default k_ex_chain; k_dt_part for the parallel
+extrapolation mode), with queue, start/end (us, relative to the first key launch's end) and
+duration.  usage: python tools/step_window.py TRACE.csv [STEP_INDEX [KEY]]"""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 30
-ch = [i for i, r in enumerate(rows) if r['Kernel_Name'] == 'k_ex_chain']
+key = sys.argv[3] if len(sys.argv) > 3 else 'k_ex_chain'
+ch = [i for i, r in enumerate(rows) if r['Kernel_Name'] == key]
 i0, i1 = ch[k], ch[k + 1]
 t0 = int(rows[i0]['End_Timestamp'])
 busy = {}
