@@ -827,6 +827,10 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
     return RMT_OK;
 }
 
+const int *extrap_status(rmt_ctx *ctx, int max_layers) {
+    return extrap_layout(ctx->bytes, ctx->ny, ctx->nx, max_layers, nullptr, ctx->ex_par).status;
+}
+
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
                 double dy, int max_layers, double *X1o, double *X2o, int *dev_status,
                 const u64 *kin) {

@@ -104,6 +104,72 @@ __global__ void __launch_bounds__(256) k_mom_prep_tiles(
     }
 }
 
+// k_phi_tiles + k_mom_prep_tiles in one pass over the listed 64 x 16 tiles (the fused step's
+// fix-up): phi on the tile + 1 from X1n, X2n into LDS, the tile's X1, X2, phi and known-plane
+// words written, then the prep of every tile cell of rows [jlo, jhi) with phi from LDS and the
+// map from X1n, X2n.  Equal to the two kernels: outside the listed tiles X1n == X1 and phi is
+// the speculative rebuild of the same X1n (the chain writes targets only, all inside listed
+// tiles); inside, X1 <- X1n.  One thread per tile cell.
+__global__ void __launch_bounds__(MOM_TX * MOM_TY) k_phi_prep_tiles(
+    const double *__restrict__ X1n, const double *__restrict__ X2n, double x0, double y0,
+    double R, unsigned long long *__restrict__ nbits, int ny, int nx, double dx, double dy,
+    double mu_s, double kappa, double w_cut, double clamp, double w_t,
+    double *__restrict__ X1, double *__restrict__ X2, double *__restrict__ phi,
+    double *__restrict__ sxx, double *__restrict__ sxy, double *__restrict__ syy,
+    double *__restrict__ J, double *__restrict__ H, unsigned char *__restrict__ solid,
+    const int *__restrict__ tiles, const int *__restrict__ count, int tiles_x, int jlo, int jhi,
+    unsigned char *__restrict__ pconst, const int *__restrict__ st_src, int *__restrict__ st_dst) {
+    constexpr int PX = MOM_TX + 2, PY = MOM_TY + 2;
+    __shared__ double ph[PY * PX];
+    // the extrapolation's status words into the step's flags (a D2D copy's launch saved)
+    if (st_src && blockIdx.x == 0 && threadIdx.x < 2) st_dst[threadIdx.x] = st_src[threadIdx.x];
+    const int cnt = *count;
+    const int q = threadIdx.x, ry = q / MOM_TX, rx = q % MOM_TX;
+    for (int b = blockIdx.x; b < cnt; b += gridDim.x) {   // list_grid launch
+        const int t = tiles[b];
+        const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY;
+        for (int h = q; h < PX * PY; h += MOM_TX * MOM_TY) {
+            const int hy = h / PX, hx = h % PX, j = j0 - 1 + hy, i = i0 - 1 + hx;
+            double v = 0.0;
+            if (j >= 0 && j < ny && i >= 0 && i < nx) {
+                const long c = (long)j * nx + i;
+                const double a = X1n[c], bb = X2n[c];
+                v = disc_phi(a, bb, x0, y0, R);
+                if (hy >= 1 && hy <= MOM_TY && hx >= 1 && hx <= MOM_TX) {
+                    X1[c] = a; X2[c] = bb; phi[c] = v;
+                }
+            }
+            ph[h] = v;
+        }
+        const int j = j0 + ry, i = i0 + rx;
+        const bool in = j < ny && i < nx;
+        const double *pc = ph + (ry + 1) * PX + rx + 1;   // written by other threads: after the barrier
+        __syncthreads();
+        if (nbits) {   // a wave is one 64-cell word of row j (tile columns are word-aligned)
+            const unsigned long long w = __ballot(in && *pc < 0);
+            if (rx == 0 && j < ny) nbits[(long)j * (nx >> 6) + (i0 >> 6)] = w;
+        }
+        if (in && j >= jlo && j < jhi) {
+            const long c = (long)j * nx + i;
+            Stress st{0.0, 0.0, 0.0, 1.0};
+            if (j >= 1 && j < ny - 1 && i >= 1 && i < nx - 1) {
+                const long off[5] = {c, c - 1, c + 1, c - nx, c + nx};
+                const int lo[5] = {0, -1, 1, -PX, PX};
+                solid_stress_acc([&](int o) { return X1n[off[o]]; },
+                                 [&](int o) { return X2n[off[o]]; },
+                                 [&](int o) { return pc[lo[o]]; }, dx, dy, mu_s, kappa, w_cut,
+                                 clamp, false, st);
+            }
+            sxx[c] = st.sxx; sxy[c] = st.sxy; syy[c] = st.syy; J[c] = st.J;
+            const double p0 = *pc;
+            H[c] = heaviside(p0, w_t);
+            solid[c] = p0 <= 0.0;
+            if (pconst && rx == 0) pconst[c >> 6] = 0;
+        }
+        __syncthreads();   // the next tile's phi overwrites ph
+    }
+}
+
 // Stage pass, three per-cell kernels (round-1 structure: simple and verifiable).
 // 1. k_stage_vel: BC'd stage velocity us = BC(u + coef k_prev)   (functions.py:714)
 // 2. k_stage_sigma: blended stress H sigma_f + (1-H)(sigma_el + solid viscous)
@@ -1314,6 +1380,7 @@ static Rk4Args rk4_args(const rmt_momentum_params *P, const double *u, const dou
 // RMT_MOM_MODE=<mode> (benchmarking) or RMT_MOM_UNFUSED=1 (mode 2)
 static int g_mom_mode = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED")) ? 2 :
                         getenv("RMT_MOM_MODE") ? atoi(getenv("RMT_MOM_MODE")) : 0;
+int momentum_mode() { return g_mom_mode; }
 constexpr int RK_TX = 48, RK_TY = 32, RK_T = 768;   // full pass: region 64 x 48 (one row a wave)
 
 // Final BC (functions.py:760) on the boundary cells of rows [jb, je) only: the bottom / top
@@ -1435,11 +1502,28 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     return RMT_OK;
 }
 
+int fixup_phi_prep(rmt_ctx *ctx, const rmt_momentum_params *P, const MomWork &W,
+                   const double *X1n, const double *X2n, double x0, double y0, double R,
+                   double *X1, double *X2, double *phi, unsigned long long *nbits, double *sxx,
+                   double *sxy, double *syy, double *J, const int *tiles, const int *count,
+                   int max_tiles, const int *st_src, int *st_dst) {
+    const int ny = ctx->ny, nx = ctx->nx;
+    RMT_CHECK(nx % 64 == 0 && g_mom_mode != 2, RMT_EINVAL,
+              "fixup_phi_prep: nx % 64 == 0 and the fused momentum modes only");
+    const double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
+    k_phi_prep_tiles<<<list_grid(max_tiles), MOM_TX * MOM_TY, 0, ctx->stream>>>(
+        X1n, X2n, x0, y0, R, nbits, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp,
+        P->w_t, X1, X2, phi, sxx, sxy, syy, J, W.H, W.solid, tiles, count, nx / MOM_TX, 0, ny,
+        W.prep_const, st_src, st_dst);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
 int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                    const double *p, const double *X1, const double *X2, const double *phi,
                    double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
                    const MomWork &W, const int *tiles, const int *count, int max_tiles,
-                   const RowWin *win) {
+                   const RowWin *win, bool skip_prep) {
     const int ny = ctx->ny, nx = ctx->nx;
     static_assert(MOM_TX == MS_TX && MOM_TY == MS_TY, "fixup tiles are the stage tiles");
     const double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
@@ -1447,11 +1531,13 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
     // the rows momentum_rk4 computes for this window: prep on w0 +- 7, stage s on w0 +- 2(3-s)
     const RowWin w0 = win ? *win : RowWin{0, ny, 0, ny};
     auto grow = [&](int m) { return std::pair<int, int>{std::max(w0.jb - m, 0), std::min(w0.je + m, ny)}; };
-    k_mom_prep_tiles<<<list_grid(max_tiles), 256, 0, ctx->stream>>>(
-        X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
-        P->rho_f, sxx, sxy, syy, J, W.H, nullptr, W.solid, tiles, count, tiles_x, grow(7).first,
-        grow(7).second, nx % 64 == 0 ? W.prep_const : nullptr);
-    RMT_LAUNCHED();
+    if (!skip_prep) {
+        k_mom_prep_tiles<<<list_grid(max_tiles), 256, 0, ctx->stream>>>(
+            X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t, P->rho_s,
+            P->rho_f, sxx, sxy, syy, J, W.H, nullptr, W.solid, tiles, count, tiles_x,
+            grow(7).first, grow(7).second, nx % 64 == 0 ? W.prep_const : nullptr);
+        RMT_LAUNCHED();
+    }
     const RowWin all{0, ny, w0.lo, w0.hi};
     if (g_mom_mode == 1 && P->bc_kind != RMT_BC_PERIODIC) {
         Rk4Args A = rk4_args(P, u, v, p, sxx, sxy, syy, W, u_new, v_new, ny, nx);

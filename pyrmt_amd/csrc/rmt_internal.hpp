@@ -303,7 +303,6 @@ __device__ __forceinline__ double heaviside(double v, double w_t) {
     return h;
 }
 
-// functions.py:545-658 solid_cauchy_stress at interior cell c (neighbour offsets 1, nx).
 // output.py:41-134 strain-energy density at one cell (4-cell edge-padded central grads).
 __device__ __forceinline__ double se_density(const double *__restrict__ X1,
                                              const double *__restrict__ X2, long c, int j, int i,
@@ -322,31 +321,31 @@ __device__ __forceinline__ double se_density(const double *__restrict__ X1,
 }
 
 struct Stress { double sxx, sxy, syy, J; };
-__device__ __forceinline__ bool solid_stress_cell(const double *__restrict__ X1,
-                                                  const double *__restrict__ X2,
-                                                  const double *__restrict__ phi, long c,
-                                                  long nx, double dx, double dy, double mu_s,
-                                                  double kappa, double w_cut, double clamp,
-                                                  bool iso, Stress &out) {
+// The cell arithmetic of functions.py:545-658 on accessors: X1(o), X2(o), PH(o) give the
+// value at the neighbour o of the cell (o: 0 = c, 1 = left, 2 = right, 3 = down, 4 = up), so
+// that a kernel can take phi from LDS and the map from any plane -- one arithmetic for all.
+template <class F1, class F2, class FP>
+__device__ __forceinline__ bool solid_stress_acc(F1 X1, F2 X2, FP PH, double dx, double dy,
+                                                 double mu_s, double kappa, double w_cut,
+                                                 double clamp, bool iso, Stress &out) {
     out = {0.0, 0.0, 0.0, 1.0};
-    double pc = phi[c];
+    double pc = PH(0);
     bool in_band = w_cut > 0.0 ? (pc < w_cut) : (pc <= 0.0);
     if (!in_band) return false;
     const double inv_2dx = 1.0 / (2.0 * dx), inv_2dy = 1.0 / (2.0 * dy);
-    long l = c - 1, r = c + 1, d = c - nx, u = c + nx;
     double g11, g21, g12, g22;
     if (w_cut > 0.0) {
-        g11 = (X1[r] - X1[l]) * inv_2dx; g21 = (X2[r] - X2[l]) * inv_2dx;
-        g12 = (X1[u] - X1[d]) * inv_2dy; g22 = (X2[u] - X2[d]) * inv_2dy;
+        g11 = (X1(2) - X1(1)) * inv_2dx; g21 = (X2(2) - X2(1)) * inv_2dx;
+        g12 = (X1(4) - X1(3)) * inv_2dy; g22 = (X2(4) - X2(3)) * inv_2dy;
     } else {
-        bool lf = phi[l] > 0.0, rf = phi[r] > 0.0;
-        if (lf && !rf) { g11 = (X1[r] - X1[c]) / dx; g21 = (X2[r] - X2[c]) / dx; }
-        else if (rf && !lf) { g11 = (X1[c] - X1[l]) / dx; g21 = (X2[c] - X2[l]) / dx; }
-        else { g11 = (X1[r] - X1[l]) * inv_2dx; g21 = (X2[r] - X2[l]) * inv_2dx; }
-        bool bf = phi[d] > 0.0, tf = phi[u] > 0.0;
-        if (bf && !tf) { g12 = (X1[u] - X1[c]) / dy; g22 = (X2[u] - X2[c]) / dy; }
-        else if (tf && !bf) { g12 = (X1[c] - X1[d]) / dy; g22 = (X2[c] - X2[d]) / dy; }
-        else { g12 = (X1[u] - X1[d]) * inv_2dy; g22 = (X2[u] - X2[d]) * inv_2dy; }
+        bool lf = PH(1) > 0.0, rf = PH(2) > 0.0;
+        if (lf && !rf) { g11 = (X1(2) - X1(0)) / dx; g21 = (X2(2) - X2(0)) / dx; }
+        else if (rf && !lf) { g11 = (X1(0) - X1(1)) / dx; g21 = (X2(0) - X2(1)) / dx; }
+        else { g11 = (X1(2) - X1(1)) * inv_2dx; g21 = (X2(2) - X2(1)) * inv_2dx; }
+        bool bf = PH(3) > 0.0, tf = PH(4) > 0.0;
+        if (bf && !tf) { g12 = (X1(4) - X1(0)) / dy; g22 = (X2(4) - X2(0)) / dy; }
+        else if (tf && !bf) { g12 = (X1(0) - X1(3)) / dy; g22 = (X2(0) - X2(3)) / dy; }
+        else { g12 = (X1(4) - X1(3)) * inv_2dy; g22 = (X2(4) - X2(3)) * inv_2dy; }
     }
     double detG = g11 * g22 - g12 * g21;
     if (fabs(detG) < 1e-10) return false;
@@ -365,6 +364,18 @@ __device__ __forceinline__ bool solid_stress_cell(const double *__restrict__ X1,
         out = {mu_s * b11 + vol, mu_s * b12, mu_s * b22 + vol, jv};
     }
     return true;
+}
+// functions.py:545-658 solid_cauchy_stress at interior cell c of the planes (offsets 1, nx)
+__device__ __forceinline__ bool solid_stress_cell(const double *__restrict__ X1,
+                                                  const double *__restrict__ X2,
+                                                  const double *__restrict__ phi, long c,
+                                                  long nx, double dx, double dy, double mu_s,
+                                                  double kappa, double w_cut, double clamp,
+                                                  bool iso, Stress &out) {
+    const long off[5] = {c, c - 1, c + 1, c - nx, c + nx};
+    return solid_stress_acc([&](int o) { return X1[off[o]]; }, [&](int o) { return X2[off[o]]; },
+                            [&](int o) { return phi[off[o]]; }, dx, dy, mu_s, kappa, w_cut,
+                            clamp, iso, out);
 }
 
 // functions.py:256-318 WENO5 reconstructions (Jiang-Shu, eps 1e-6; x**2 as x*x like Numba).
@@ -589,11 +600,21 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
 // re-run prep + the 4 stages on the 64 x 16 tiles listed in tiles[0 .. *count) (device) after
 // a speculative momentum_rk4 whose inputs changed only inside them (sim.hip overlap)
 constexpr int MOM_TX = 64, MOM_TY = 16;
+int momentum_mode();   // rmt_momentum_set_mode / RMT_MOM_MODE
+// skip_prep: the caller ran fixup_phi_prep on the same tiles
 int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                    const double *p, const double *X1, const double *X2, const double *phi,
                    double *u_new, double *v_new, double *sxx, double *sxy, double *syy, double *J,
                    const MomWork &W, const int *tiles, const int *count, int max_tiles,
-                   const RowWin *win = nullptr);
+                   const RowWin *win = nullptr, bool skip_prep = false);
+// the fused step's level-set rebuild on the fix-up tiles and momentum_fixup's prep in one
+// kernel (k_phi_prep_tiles; single domain, nx % 64 == 0): X1, X2 <- X1n, X2n, phi =
+// disc_phi(X1n, X2n), the next step's known-plane words (nbits, nullable), then the prep planes
+int fixup_phi_prep(rmt_ctx *ctx, const rmt_momentum_params *P, const MomWork &W,
+                   const double *X1n, const double *X2n, double x0, double y0, double R,
+                   double *X1, double *X2, double *phi, unsigned long long *nbits, double *sxx,
+                   double *sxy, double *syy, double *J, const int *tiles, const int *count,
+                   int max_tiles, const int *st_src = nullptr, int *st_dst = nullptr);
 
 // ---------------------------------------------------------------------- poisson --
 // dev_root: nullptr -> p = solve - mean (functions.py:1119); else p = the raw solve and
@@ -641,6 +662,8 @@ int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *
 int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi,
                     double dx, double dy, int max_layers, double *X1o, double *X2o,
                     const unsigned long long *kin);
+// the extrapolation's device status words {fitted, aborted} (valid until the next geometry)
+const int *extrap_status(rmt_ctx *ctx, int max_layers);
 int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
                   int *dev_status);
 size_t extrap_workspace(int ny, int nx, int max_layers, bool px = false);   // ctx->bytes used

@@ -381,12 +381,14 @@ __global__ void k_mark_rows(const int *__restrict__ tiles, const int *__restrict
     }
 }
 // completes a ring record after k_diag_p2 wrote its diagnostics: max |u|^2, dt, flags
-__global__ void k_ring_put(const double *__restrict__ sc, const int *__restrict__ flag,
+// and clears the non-finite flag for the next step (in place of a memset launch)
+__global__ void k_ring_put(const double *__restrict__ sc, int *__restrict__ flag,
                            double *__restrict__ e) {
     if (threadIdx.x == 0) {
         e[DIAG_VALS] = sc[0];
         e[DIAG_VALS + 1] = sc[1];
         for (int k = 0; k < 4; ++k) e[DIAG_VALS + 2 + k] = flag ? (double)flag[k] : 0.0;
+        if (flag) flag[0] = 0;
     }
 }
 
@@ -797,10 +799,12 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // runs in order (its geometry still beside the previous step's projection)
         const bool par = extrap_par_enabled();
         const bool overlap = solid && S->st2 && !no_overlap && !par;
+        bool fixprep = false;   // the fused fix-up prep (set where the extrapolation runs)
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
             // 2. advect the reference map with the pre-advection level set and mask
-            RMT_HIP(hipMemsetAsync(S->flag, 0, sizeof(int), st));
+            // (on the asynchronous path the previous step's k_ring_put cleared it)
+            if (!(async && it > 0)) RMT_HIP(hipMemsetAsync(S->flag, 0, sizeof(int), st));
             if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && overlap && S->e_bits) {
                 // known plane -> rim words -> the rim's advection here; the rest on the second
                 // stream, beside the extrapolation (which reads rim cells only)
@@ -859,10 +863,15 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // starts at the chain's launch) predicts the chain's latest sources
             ctx->ex_pred1 = S->X1; ctx->ex_pred2 = S->X2;
             if (geo_ready && !overlap) RMT_HIP(hipStreamWaitEvent(st, S->e_geo, 0));
+            // with the fused fix-up prep (below) the status words are copied by its kernel
+            static const bool fp_env = !(getenv("RMT_FUSED_FIXPREP") && !atoi(getenv("RMT_FUSED_FIXPREP")));
+            fixprep = overlap && fp_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 &&
+                      momentum_mode() != 2 && P.layers > 0;
+            int *dstat = fixprep ? nullptr : S->flag + 2;
             const int es = geo_ready && P.layers > 0
-                               ? extrap_finish(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->flag + 2)
+                               ? extrap_finish(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, dstat)
                                : extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
-                                             S->X1n, S->X2n, S->flag + 2, kb ? S->kbits : nullptr);
+                                             S->X1n, S->X2n, dstat, kb ? S->kbits : nullptr);
             geo_ready = false;
             ctx->ex_pred1 = ctx->ex_pred2 = nullptr;
             ctx->ev_chain = nullptr;
@@ -932,14 +941,25 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // 4 + 5 on the tiles the extrapolation can reach
             RMT_HIP(hipStreamWaitEvent(st, S->e_mom, 0));
             const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
-            k_phi_tiles<<<list_grid(S->max_tiles), 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
-                                                       S->phi, S->X1, S->X2, S->tiles, S->tcount,
-                                                       tiles_x, nb);
-            RMT_LAUNCHED();
+            // phi on the tiles and the momentum's prep there in one kernel (RMT_FUSED_FIXPREP,
+            // default on where nx % 64 == 0), which also copies the extrapolation's status
+            if (fixprep) {
+                RMT_TRY(fixup_phi_prep(ctx, &M, W, S->X1n, S->X2n, P.x0, P.y0, P.R, S->X1, S->X2,
+                                       S->phi, nb, S->sxx, S->sxy, S->syy, S->J, S->tiles,
+                                       S->tcount, S->max_tiles, extrap_status(ctx, P.layers),
+                                       S->flag + 2));
+            } else {
+                k_phi_tiles<<<list_grid(S->max_tiles), 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
+                                                           S->phi, S->X1, S->X2, S->tiles, S->tcount,
+                                                           tiles_x, nb);
+                RMT_LAUNCHED();
+            }
             if (async && geo_env && nb && P.layers > 0 && it + 1 < nsteps) {
-                // the next step's known plane is final (k_phi_tiles): its rim words, rim
+                // the next step's known plane is final (the phi kernel above): its rim words, rim
                 // segments and extrapolation geometry on the second stream, beside the rest of
-                // this step (nothing there uses them or the extrapolation workspace)
+                // this step (nothing there uses them or the extrapolation workspace).  Issued
+                // before the fix-up stages: after them its few-block kernels would share the CUs
+                // with the projection's FFT passes (measured: the step no faster)
                 RMT_HIP(hipEventRecord(S->e_kb, st));
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_kb, 0));
                 const long nseg = (long)ny * ((nx + 255) / 256);
@@ -961,7 +981,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             }
             RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
                                    S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,
-                                   S->max_tiles));
+                                   S->max_tiles, nullptr, fixprep));
         } else {
             // 4. phi from the advected + extrapolated map (and the momentum's pure-fluid flags)
             if (fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 && MOM_TX == 64) {

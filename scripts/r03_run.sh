@@ -5,6 +5,7 @@
 #   par            tests/test_gpu_extrap_par.py
 #   t:EXPR         pytest -m gpu -k EXPR
 #   bench          20-step bench line (no CPU baseline)
+#   bench100       three 100-step bench lines (ms/step each)
 #   benchpar       the same with RMT_EXTRAP_PARALLEL=1
 #   kt / ktpar     rocprofv3 kernel trace + stats of the 20-step bench (exact / parallel)
 #   env:K=V        export K=V for the following steps
@@ -27,6 +28,11 @@ for s in "$@"; do
         bench) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/bench.log" 2>&1 \
                    || { tail -20 "$O/bench.log"; exit 1; }
                tail -1 "$O/bench.log" | cut -c1-400 ;;
+        bench100) for k in 1 2 3; do
+                      timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline > "$O/bench100_$k.log" 2>&1 \
+                          || { tail -20 "$O/bench100_$k.log"; exit 1; }
+                      tail -1 "$O/bench100_$k.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('bench100', round(d['ms_per_step'], 4))"
+                  done ;;
         benchpar) RMT_EXTRAP_PARALLEL=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/benchpar.log" 2>&1 \
                    || { tail -20 "$O/benchpar.log"; exit 1; }
                tail -1 "$O/benchpar.log" | cut -c1-400 ;;
