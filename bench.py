@@ -29,10 +29,10 @@ RK4_ALG_BYTES_PER_CELL = 7 * 8
 STEP_ALG_BYTES_PER_CELL = 208  # the whole step
 # HBM bytes per launch and per step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
 # bench (scripts/gpu.sh pmc -> tools/pmc_traffic.py; FETCH x2 per the gfx950 calibration)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc_traffic_n4096.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_n4096.json")
 # fp64 VALU counts of the same kernel and the measured FMA peak (scripts/pmc_f64.sh ->
 # tools/f64_roof.py): k_mom_stage is VALU-issue-bound, not HBM-bound
-F64_ROOF = os.path.join(ROOT, "profiles", "r02", "f64_roof_n4096.json")
+F64_ROOF = os.path.join(ROOT, "profiles", "r03", "f64_roof_n4096.json")
 # dependent fits on the critical path of the bench-state extrapolation at N=4096 (per-fit
 # trace of the chain kernel, tools/chain_trace.py; profiles/r02/chain_trace/)
 CHAIN_DEPTH_4096 = 3257

@@ -40,9 +40,9 @@ for s in "$@"; do
             f=$(find "$O/kt" -name "*kernel_stats.csv" | head -1); cp "$f" "$O/kernel_stats.csv"
             cut -d, -f1-4 "$f" | head -16 ;;
         pmc) timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T -f csv -d "$O/pf" -o fetch -- \
-                 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmc_fetch.log" 2>&1 || exit 1
+                 python3 bench.py --steps 6 --warmup 1 --no-cpu-baseline > "$O/pmc_fetch.log" 2>&1 || exit 1
              timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T -f csv -d "$O/pw" -o write -- \
-                 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmc_write.log" 2>&1 || exit 1
+                 python3 bench.py --steps 6 --warmup 1 --no-cpu-baseline > "$O/pmc_write.log" 2>&1 || exit 1
              echo "pmc done" ;;
         chainprof) RMT_EX_PROFILE=1 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 \
                        --no-cpu-baseline > "$O/chainprof.log" 2>&1 || { tail -20 "$O/chainprof.log"; exit 1; }

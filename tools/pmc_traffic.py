@@ -3,8 +3,8 @@
 
 FETCH_SIZE is doubled (gfx950 counts 128-B requests at 64 B: MI355X_MICROARCH.md section HBM;
 calibrated on librmt's own 8-B/lane pattern in round 1, profiles/r01/hbm_traffic_n4096.md),
-WRITE_SIZE is taken as is.  Per step: the dispatches from the second k_dt launch (the first
-kernel of a step after its max|u| reduction) to the end, divided by the steps they cover.
+WRITE_SIZE is taken as is.  Per step: the dispatches from the second step boundary (a k_dt or
+k_dt_part launch: the first kernel of every step) to the end, divided by the steps they cover.
 
     python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [git-rev]
 """
@@ -60,12 +60,17 @@ def main():
         per_launch[n] = [a + b for a, b in zip(fseq[n], wseq.get(n, []))]
     # per step, from the fetch pass's dispatch order
     order = sorted(fe)
-    starts = [d for d in order if fe[d][0] == "k_dt"]
+    starts = [d for d in order if fe[d][0] in ("k_dt", "k_dt_part")]
+    nsteps = len(starts) - 1
     step = {}
     for label, per, scale in (("fetch", fe, 2.0), ("write", wr, 1.0)):
         if len(starts) >= 2:
-            tot = sum(v for d, (n, v) in per.items() if d >= starts[1]) * scale * 1024.0
-            step[label] = tot / (len(starts) - 1)
+            # the write pass is a separate run: its dispatch ids are paired by order, so the
+            # boundary is the fetch pass's boundary index in sorted order
+            ids = sorted(per)
+            b = ids[order.index(starts[1])] if len(ids) == len(order) else starts[1]
+            tot = sum(v for d, (n, v) in per.items() if d >= b) * scale * 1024.0
+            step[label] = tot / nsteps
     res = {"git_rev": rev, "units": "bytes", "fetch_correction": 2.0,
            "kernels": {n: {"launches": c, "fetch_per_launch": f / max(c, 1),
                            "write_per_launch": w / max(c, 1),
@@ -77,7 +82,7 @@ def main():
                        for n, (c, f, w) in sorted(kern.items(), key=lambda kv: -(kv[1][1] + kv[1][2]))},
            "per_step": {"fetch": step.get("fetch"), "write": step.get("write"),
                         "total": (step["fetch"] + step["write"]) if step else None,
-                        "steps": len(starts) - 1}}
+                        "steps": nsteps}}
     json.dump(res, open(out, "w"), indent=1)
     print(f"per step: {res['per_step']}")
     for n, k in list(res["kernels"].items())[:12]:
