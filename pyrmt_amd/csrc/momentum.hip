@@ -391,20 +391,36 @@ __device__ __forceinline__ void ms_tile(
             a[it] = u1[o]; b[it] = v1[o];
             ka[it] = stage ? ku1[o] : 0.0; kb[it] = stage ? kv1[o] : 0.0;
         }
-        (void)b3;
+        // a pure-fluid tile loads no phase-2 operand (the constants of H = 1, not solid)
+        const long b2 = (long)(j0 - HG) * nx + (i0 - HG);
+        if (!fluid) {
+            const double *sxx2 = sxx + b2, *syy2 = syy + b2, *sxy2 = sxy + b2, *H2 = H + b2;
+            const unsigned char *sol2 = solid + b2;
+#pragma unroll
+            for (int it = 0; it < NG; ++it) {
+                const int q = threadIdx.x + it * T, ry = q / GX, rx = q - ry * GX;
+                ok2[it] = q < GX * GY;
+                const int o = ok2[it] ? ry * nx + rx : 0;
+                ex[it] = sxx2[o]; ey[it] = syy2[o]; exy[it] = sxy2[o]; hh2[it] = H2[o];
+                sol[it] = sol2[o];
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < NG; ++it) {
+                ok2[it] = threadIdx.x + it * T < GX * GY;
+                ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh2[it] = 1.0; sol[it] = 0;
+            }
+        }
+        const double *p3 = p + b3, *H3 = H + b3;
 #pragma unroll
         for (int it = 0; it < NO; ++it) {
-            const int q = threadIdx.x + it * T, ry = q / MS_TX;
+            const int q = threadIdx.x + it * T, ry = q / MS_TX, rx = q - ry * MS_TX;
             ok[it] = q < MS_TX * MS_TY && j0 + ry >= olo && j0 + ry < ohi;   // output rows
+            const int o = ok[it] ? ry * nx + rx : 0;
             pc[it] = 0.0;   // (the one-sided edge stencils only)
-        }
-        // a pure-fluid tile loads no phase-2 operand (the constants above); the others issue
-        // theirs after phase 1 (interior tiles run at 6 waves per SIMD: the phase-1 operands'
-        // registers are reused)
-#pragma unroll
-        for (int it = 0; it < NG; ++it) {
-            ok2[it] = threadIdx.x + it * T < GX * GY;
-            ex[it] = 0.0; ey[it] = 0.0; exy[it] = 0.0; hh2[it] = 1.0; sol[it] = 0;
+            pxp[it] = p3[o + 1]; pxm[it] = p3[o - 1];
+            pyp[it] = p3[o + nx]; pym[it] = p3[o - nx];
+            hh[it] = fluid ? 1.0 : H3[o];
         }
     } else {
     {
@@ -482,20 +498,6 @@ __device__ __forceinline__ void ms_tile(
             if (lane0) wfl[0][wv] = bad;
         }
     }
-    if constexpr (IN) {
-        if (!fluid) {
-            const long b2 = (long)(j0 - HG) * nx + (i0 - HG);
-            const double *sxx2 = sxx + b2, *syy2 = syy + b2, *sxy2 = sxy + b2, *H2 = H + b2;
-            const unsigned char *sol2 = solid + b2;
-#pragma unroll
-            for (int it = 0; it < NG; ++it) {
-                const int q = threadIdx.x + it * T, ry = q / GX, rx = q - ry * GX;
-                const int o = ok2[it] ? ry * nx + rx : 0;
-                ex[it] = sxx2[o]; ey[it] = syy2[o]; exy[it] = sxy2[o]; hh2[it] = H2[o];
-                sol[it] = sol2[o];
-            }
-        }
-    }
     __syncthreads();
     bool chk = !IN || !K.nc;
     if constexpr (IN) {
@@ -570,19 +572,6 @@ __device__ __forceinline__ void ms_tile(
         if (!chk) {
 #pragma unroll
             for (int w = 0; w < T / 64; ++w) chk = chk || wfl[1][w];
-        }
-    }
-    if constexpr (IN) {
-        // the pressure operands and H at the output cells: loaded here, not held through
-        // phases 1 and 2 (register pressure; the other waves hide the latency)
-        const double *p3 = p + (long)j0 * nx + i0, *H3 = H + (long)j0 * nx + i0;
-#pragma unroll
-        for (int it = 0; it < NO; ++it) {
-            const int q = threadIdx.x + it * T, ry = q / MS_TX, rx = q - ry * MS_TX;
-            const int o = ok[it] ? ry * nx + rx : 0;
-            pxp[it] = p3[o + 1]; pxm[it] = p3[o - 1];
-            pyp[it] = p3[o + nx]; pym[it] = p3[o - nx];
-            hh[it] = fluid ? 1.0 : H3[o];
         }
     }
     // 3. RHS and RK4 accumulation (functions.py:923-944, 743-758); stage 3 forms
@@ -682,7 +671,7 @@ __device__ __forceinline__ void ms_tile(
 // DC: K.den_const known on the host (drops the IEEE density division's registers: the
 // interior stages 0-2 then run 6 waves per SIMD, LDS 50 KB per block)
 template <bool IN, bool SQ, bool S3, bool DC>
-__global__ void __launch_bounds__(IN ? MS_TI : MS_T, IN && DC && !S3 ? 6 : 4) k_mom_stage(
+__global__ void __launch_bounds__(IN ? MS_TI : MS_T, 4) k_mom_stage(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
     const double *__restrict__ sxx, const double *__restrict__ sxy,
@@ -720,6 +709,11 @@ __global__ void __launch_bounds__(IN ? MS_TI : MS_T, IN && DC && !S3 ? 6 : 4) k_
 // The listed tiles (momentum_fixup), interior and edge alike, in one launch of at most
 // LIST_BLOCKS workgroups looping over the list: a fix-up list holds a few hundred tiles, so
 // one round of workgroups covers it and the stage costs one tile's latency, not two launches'.
+// The listed tiles (momentum_fixup), interior and edge alike, in one launch of at most
+// LIST_BLOCKS workgroups looping over the list: a fix-up list holds a few hundred tiles, so
+// one round of workgroups covers it and the stage costs one tile's latency, not two launches'.
+// (A kernel per kind of tile -- the interior one at two workgroups per CU -- measured slower:
+// 27-32 us per interior launch plus ~9 us for the edge launch, against 21-25 us.)
 template <bool SQ>
 __global__ void __launch_bounds__(MS_T, 2) k_mom_stage_list(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
