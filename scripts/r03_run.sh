@@ -6,6 +6,8 @@
 #   t:EXPR         pytest -m gpu -k EXPR
 #   bench          20-step bench line (no CPU baseline)
 #   bench100       three 100-step bench lines (ms/step each)
+#   smoke          __graft_entry__.smoke()
+#   benchfull      the default bench line (the driver's command: CPU baselines included)
 #   benchpar       the same with RMT_EXTRAP_PARALLEL=1
 #   kt / ktpar     rocprofv3 kernel trace + stats of the 20-step bench (exact / parallel)
 #   env:K=V        export K=V for the following steps
@@ -28,6 +30,12 @@ for s in "$@"; do
         bench) timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/bench.log" 2>&1 \
                    || { tail -20 "$O/bench.log"; exit 1; }
                tail -1 "$O/bench.log" | cut -c1-400 ;;
+        smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+                   || { tail -20 "$O/smoke.log"; exit 1; }
+               tail -1 "$O/smoke.log" ;;
+        benchfull) timeout -k 10 900 python -u bench.py > "$O/benchfull.log" 2>&1 \
+                   || { tail -20 "$O/benchfull.log"; exit 1; }
+               tail -1 "$O/benchfull.log" | cut -c1-300 ;;
         bench100) for k in 1 2 3; do
                       timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline > "$O/bench100_$k.log" 2>&1 \
                           || { tail -20 "$O/bench100_$k.log"; exit 1; }
