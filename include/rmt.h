@@ -370,6 +370,17 @@ int rmt_slab_finish(rmt_slab *slab);                     /* then: allgather scal
 int rmt_slab_set_device_dt(rmt_slab *slab, int on);
 int rmt_slab_next_dt(rmt_slab *slab, const double *gathered_scal, int G, double *ring_slot);
 int rmt_slab_rim_cap(rmt_slab *slab, long long cap);
+/* The next step's extrapolation geometry beside this step's projection (as rmt_sim_step's
+ * early geometry): after rmt_slab_momentum, rmt_slab_next_bits writes the owned rows of the
+ * next known plane into buffer 13 (bits_next); the caller allgathers its rows; then
+ * rmt_slab_geometry runs the value-independent extrapolation passes on the slab's second
+ * stream, and the next step's rmt_slab_advect / rmt_slab_extrapolate* use them (no bits
+ * allgather, no geometry on the critical path).  rmt_slab_drop_geometry forgets it (a step
+ * that will not run).  Replaces the geometry half of extrapolate_reference_map
+ * (functions.py:78-99: targets, acceptance, weights depend on the known set only). */
+int rmt_slab_next_bits(rmt_slab *slab);
+int rmt_slab_geometry(rmt_slab *slab);
+int rmt_slab_drop_geometry(rmt_slab *slab);
 int rmt_slab_extrapolate_dev(rmt_slab *slab, const double *gathered, const double *gathered_scal,
                              long long cap);
 

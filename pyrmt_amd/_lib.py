@@ -144,6 +144,9 @@ SIGNATURES = {
     "rmt_slab_set_device_dt": (_I, [_P, _I]),
     "rmt_slab_next_dt": (_I, [_P, _P, _I, _P]),
     "rmt_slab_rim_cap": (_I, [_P, ctypes.c_longlong]),
+    "rmt_slab_next_bits": (_I, [_P]),
+    "rmt_slab_geometry": (_I, [_P]),
+    "rmt_slab_drop_geometry": (_I, [_P]),
     "rmt_slab_extrapolate_dev": (_I, [_P, _P, _P, ctypes.c_longlong]),
     # MAC slabs (distributed.py MacDistributedSim)
     "rmt_mac_slab_create": (_I, [_P, ctypes.POINTER(rmt_mac_params), _I, _I, ctypes.POINTER(_I),

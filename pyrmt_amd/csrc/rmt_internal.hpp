@@ -700,7 +700,7 @@ int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *
                          long long cap, double *X1d, double *X2d, const unsigned long long *bits,
                          double dx, double dy, int layers, int *exflags, double *X1n,
                          double *X2n, long c_lo, long c_hi,
-                         const double *gs = nullptr);
+                         const double *gs = nullptr, hipEvent_t geo = nullptr);
 int slab_cols(rmt_ctx *ctx, bool pack, double *Y, int rows, int nx, const int *csplits, int G,
               double *A);
 

@@ -82,6 +82,15 @@ struct rmt_slab {
     const double *dtp = nullptr;
     bool spec = false;     // a speculative momentum is in flight for this step
     bool interior = false; // rmt_slab_advect_interior ran for this step
+    // the next step's extrapolation geometry beside this step's projection (as rmt_sim_step):
+    // the next known plane (bits_next: owned rows from phi after the fix-up, then allgathered)
+    // and the geometry on st2 into this slab's own extrapolation workspace (ws; slabs sharing
+    // a context must not share it while geometries run beside other slabs' chains)
+    u64 *bits_next = nullptr;
+    unsigned char *ws = nullptr;
+    size_t ws_len = 0;
+    hipEvent_t e_bits = nullptr, e_geo = nullptr;
+    bool geo_ready = false;
     double *gv(double *q) const { return q - (long)lo * NX; }   // global-index view
 };
 
@@ -342,6 +351,22 @@ static int check_splits(const int *s, int G, int n, int minsz, bool even) {
 }
 
 
+// this slab's extrapolation workspace as the context's byte scratch for the scope (written
+// back: ensure_bytes may reallocate it)
+struct SlabWs {
+    rmt_slab *S;
+    unsigned char *b;
+    size_t l;
+    explicit SlabWs(rmt_slab *s) : S(s), b(s->ctx->bytes), l(s->ctx->bytes_len) {
+        if (S->ws) { S->ctx->bytes = S->ws; S->ctx->bytes_len = S->ws_len; }
+    }
+    ~SlabWs() {
+        if (!S->ws) return;
+        S->ws = S->ctx->bytes; S->ws_len = S->ctx->bytes_len;
+        S->ctx->bytes = b; S->ctx->bytes_len = l;
+    }
+};
+
 // ------------------------------------------- shared with the MAC slabs (mac.hip) --
 int slab_sl(rmt_ctx *ctx, const double *X1, const double *X2, const double *a, const double *b,
             const double *xs, const double *ys, int ny, int nx, double dt, double dx, double dy,
@@ -383,7 +408,7 @@ int rim_words(rmt_ctx *ctx, const u64 *bits, int ny, int nx, int W, u64 *rimw, i
 int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *counts, int G,
                          long long cap, double *X1d, double *X2d, const u64 *bits, double dx,
                          double dy, int layers, int *exflags, double *X1n, double *X2n,
-                         long c_lo, long c_hi, const double *gs) {
+                         long c_lo, long c_hi, const double *gs, hipEvent_t geo) {
     Counts cn{};
     for (int k = 0; k < G && !gs; ++k) {
         RMT_CHECK(counts[k] >= 0 && counts[k] <= cap, RMT_EINVAL, "slab: rim count > cap");
@@ -394,7 +419,12 @@ int slab_rim_extrapolate(rmt_ctx *ctx, const double *gathered, const long long *
         k_rim_unpack<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, G, cap, X1d, X2d, gs);
         RMT_LAUNCHED();
     }
-    RMT_TRY(extrapolate(ctx, X1d, X2d, nullptr, dx, dy, layers, X1d, X2d, exflags, bits));
+    if (geo && layers > 0) {   // the geometry ran beside the previous step's projection
+        RMT_HIP(hipStreamWaitEvent(ctx->stream, geo, 0));
+        RMT_TRY(extrap_finish(ctx, dx, dy, layers, X1d, X2d, exflags));
+    } else {
+        RMT_TRY(extrapolate(ctx, X1d, X2d, nullptr, dx, dy, layers, X1d, X2d, exflags, bits));
+    }
     if (tot > 0) {
         k_rim_writeback<<<grid1d(tot, 256), 256, 0, ctx->stream>>>(gathered, cn, G, cap, X1d, X2d,
                                                                    X1n, X2n, c_lo, c_hi, gs);
@@ -499,6 +529,11 @@ int rmt_slab_create(rmt_ctx *ctx, const rmt_sim_params *prm, int G, int rank,
         S->max_tiles = ((S->NX + MOM_TX - 1) / MOM_TX) * ((S->NY + MOM_TY - 1) / MOM_TY);
         RMT_HIP(hipMalloc(&S->tiles, (S->max_tiles + 64) * sizeof(int)));
         S->tcount = S->tiles + S->max_tiles;
+        RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_geo, hipEventDisableTiming));
+        RMT_HIP(hipMalloc(&S->bits_next, (size_t)S->NY * W * sizeof(u64)));
+        S->ws_len = extrap_workspace(S->NY, S->NX, prm->layers, extrap_par_enabled());
+        RMT_HIP(hipMalloc(&S->ws, S->ws_len));
     }
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
@@ -512,6 +547,10 @@ int rmt_slab_destroy(rmt_slab *S) {
     if (S->tiles) (void)hipFree(S->tiles);
     if (S->e_chain) (void)hipEventDestroy(S->e_chain);
     if (S->e_mom) (void)hipEventDestroy(S->e_mom);
+    if (S->e_bits) (void)hipEventDestroy(S->e_bits);
+    if (S->e_geo) (void)hipEventDestroy(S->e_geo);
+    if (S->bits_next) (void)hipFree(S->bits_next);
+    if (S->ws) (void)hipFree(S->ws);
     if (S->st2) (void)hipStreamDestroy(S->st2);
     delete S;
     return RMT_OK;
@@ -528,7 +567,8 @@ int rmt_slab_info(rmt_slab *S, int *ints8, double *dt_const) {
 int rmt_slab_buffer(rmt_slab *S, int id, void **ptr) {
     RMT_CHECK(S && ptr, RMT_EINVAL, "null argument");
     void *b[] = {S->u, S->v, S->p, S->X1, S->X2, S->phi, S->J, S->pc, S->bits, S->rim,
-                 S->A, S->B, S->scal};
+                 S->A, S->B, S->scal, S->bits_next};
+    RMT_CHECK(id != 13 || S->bits_next, RMT_ENOTSUP, "slab: no early-geometry buffers");
     RMT_CHECK(id >= 0 && id < (int)(sizeof(b) / sizeof(b[0])), RMT_EINVAL, "unknown buffer id");
     *ptr = b[id];
     return RMT_OK;
@@ -616,9 +656,57 @@ int rmt_slab_advect(rmt_slab *S, double dt) {
             S->flags, a, b, S->lo, S->hi, S->scal + SC_M2RES, S->dtp);
         RMT_LAUNCHED();
     }
+    if (S->geo_ready) {
+        // the whole known plane was gathered with the geometry (rmt_slab_geometry): the
+        // owned rows equal k_slab_bits of this phi_pre (the same disc_phi of the same map)
+        RMT_HIP(hipMemcpyAsync(S->bits, S->bits_next, (size_t)S->NY * S->W * sizeof(u64),
+                               hipMemcpyDeviceToDevice, ctx->stream));
+        return RMT_OK;
+    }
     k_slab_bits<<<dim3((NX + 255) / 256, S->r1 - S->r0), 256, 0, ctx->stream>>>(
         S->gv(S->phi_pre), NX, S->W, S->bits, S->r0);
     RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+// the next step's known plane, owned rows (after rmt_slab_momentum: phi is final)
+int rmt_slab_next_bits(rmt_slab *S) {
+    RMT_CHECK(S && S->bits_next, RMT_ENOTSUP, "slab: no early-geometry buffers");
+    k_slab_bits<<<dim3((S->NX + 255) / 256, S->r1 - S->r0), 256, 0, S->ctx->stream>>>(
+        S->gv(S->phi), S->NX, S->W, S->bits_next, S->r0);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
+
+// the next step's extrapolation geometry from the gathered bits_next, on the second stream
+// beside the rest of this step; the next rmt_slab_advect / extrapolate use it
+int rmt_slab_geometry(rmt_slab *S) {
+    RMT_CHECK(S && S->bits_next && S->st2, RMT_ENOTSUP, "slab: no early-geometry buffers");
+    rmt_ctx *ctx = S->ctx;
+    const rmt_sim_params &P = S->P;
+    S->geo_ready = false;
+    if (P.layers <= 0) return RMT_OK;
+    RMT_HIP(hipEventRecord(S->e_bits, ctx->stream));
+    RMT_HIP(hipStreamWaitEvent(S->st2, S->e_bits, 0));
+    hipStream_t st = ctx->stream;
+    ctx->stream = S->st2;
+    int gs;
+    {
+        SlabWs ws(S);
+        gs = extrap_geometry(ctx, S->X1d, S->X2d, nullptr, P.dx, P.dy, P.layers, S->X1d, S->X2d,
+                             S->bits_next);
+    }
+    ctx->stream = st;
+    RMT_TRY(gs);
+    RMT_HIP(hipEventRecord(S->e_geo, S->st2));
+    S->geo_ready = true;
+    return RMT_OK;
+}
+
+// forget a geometry prepared for a step that will not run (the state may change in between)
+int rmt_slab_drop_geometry(rmt_slab *S) {
+    RMT_CHECK(S, RMT_EINVAL, "null slab");
+    S->geo_ready = false;
     return RMT_OK;
 }
 
@@ -649,9 +737,16 @@ static int slab_extrapolate(rmt_slab *S, const double *gathered, const long long
     S->spec = S->st2 && !no_overlap;
     const int jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
     if (S->spec) ctx->ev_chain = S->e_chain;
-    const int es = slab_rim_extrapolate(ctx, gathered, counts, S->G, cap, S->X1d, S->X2d, S->bits,
-                                        P.dx, P.dy, P.layers, S->flags + 4, S->gv(S->X1n),
-                                        S->gv(S->X2n), (long)S->lo * S->NX, (long)S->hi * S->NX, gs);
+    const bool geo = S->geo_ready;
+    S->geo_ready = false;
+    int es;
+    {
+        SlabWs ws(S);
+        es = slab_rim_extrapolate(ctx, gathered, counts, S->G, cap, S->X1d, S->X2d, S->bits,
+                                  P.dx, P.dy, P.layers, S->flags + 4, S->gv(S->X1n),
+                                  S->gv(S->X2n), (long)S->lo * S->NX, (long)S->hi * S->NX, gs,
+                                  geo ? S->e_geo : nullptr);
+    }
     ctx->ev_chain = nullptr;
     if (es != RMT_OK) { S->spec = false; return es; }
     if (!S->spec) {
@@ -674,6 +769,7 @@ static int slab_extrapolate(rmt_slab *S, const double *gathered, const long long
     ctx->stream = st;
     RMT_TRY(ms);
     RMT_HIP(hipEventRecord(S->e_mom, S->st2));
+    SlabWs ws(S);   // the tiles come from this step's extrapolation workspace
     return extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount);
 }
 extern "C" {

@@ -33,6 +33,7 @@ HALO = 12           # RMT_SLAB_HALO
 SC_N = 16           # scalar block: [0] max|u|^2, [1..10] diag partials, [11] flags,
 SC_M2, SC_DIAG, SC_FLAGS, SC_COUNT, SC_ROOT, SC_FIT = 0, 1, 11, 12, 13, 14
 BUF = {"u": 0, "v": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5, "J": 6, "pc": 7, "bits": 8,
+       "bits_next": 13,
        "rim": 9, "A": 10, "B": 11, "scal": 12}
 
 
@@ -273,10 +274,11 @@ class Slab:
             torch = F._torch()
             nl, no = self.hi - self.lo, self.r1 - self.r0
             nc = self.c1 - self.c0
-            shape = {"bits": (self.NY, self.W), "rim": (no * self.NX, 3), "A": (no * self.NX,),
+            shape = {"bits": (self.NY, self.W), "bits_next": (self.NY, self.W),
+                     "rim": (no * self.NX, 3), "A": (no * self.NX,),
                      "B": (self.NY * nc,), "scal": (SC_N,)}.get(name, (nl, self.NX))
             t = _wrap_device(torch, self._ptr(BUF[name]), shape)
-            if name == "bits":
+            if name in ("bits", "bits_next"):
                 t = t.view(torch.int64)
             self._views[name] = t
         return self._views[name]
@@ -334,6 +336,10 @@ class DistributedSim:
         self._dev_dt = False          # the slabs' device dt holds this step's dt
         self._rim_cap = None          # rim entries moved per slab (set from the first count)
         self._min_owned = min(self.rsplits[k + 1] - self.rsplits[k] for k in range(self.G)) * N
+        # the next step's extrapolation geometry beside the projection (layers 1 .. 12: the
+        # slabs have their second stream)
+        self._early_geo = (1 <= layers <= 12 and
+                           int(os.environ.get("RMT_SLAB_EARLY_GEO", "1")) != 0)
 
     # -------------------------------------------------------------- state in / out --
     def set_state(self, **fields):
@@ -404,7 +410,8 @@ class DistributedSim:
                 and not int(os.environ.get("RMT_SLAB_SYNC", "0"))):
             return self._step_async(nsteps)
         self._set_dev_dt(False)
-        for _ in range(nsteps):
+        geo = False
+        for k in range(nsteps):
             if not (self.t < t_end):
                 break
             ev = []
@@ -421,7 +428,9 @@ class DistributedSim:
             # advection + exact extrapolation (band replicated on every slab)
             self._call("rmt_slab_advect", dt)
             self._mark(ev)
-            comm.allgather_rows(S, "bits")
+            if not geo:   # else the plane was gathered with the early geometry
+                comm.allgather_rows(S, "bits")
+            geo = False
             self._call("rmt_slab_rim_pack")
             counts = [int(c) for c in self._scalars()[:, SC_COUNT]]
             gathered, cap = comm.allgather_padded([s.view("rim") for s in S], counts, 3)
@@ -431,8 +440,10 @@ class DistributedSim:
                 L.check(s.lib.rmt_slab_extrapolate(s.h, g.data_ptr(), self._counts, cap),
                         "rmt_slab_extrapolate")
             self._mark(ev)
-            # momentum, projection
+            # momentum (then the next step's geometry beside the projection), projection
             self._call("rmt_slab_momentum", dt)
+            if k + 1 < nsteps and self.t + dt < t_end:
+                geo = self._early_geometry()
             self._mark(ev)
             self._call("rmt_slab_project_rows", dt)
             sp = [s.a2a_splits() for s in S]
@@ -460,6 +471,18 @@ class DistributedSim:
                 self._ms["rk4_stage_kernels"] += ms2[0]
                 self._ms["extrap_chain_kernel"] += ms2[1]
                 self._nprof += 1
+        self._call("rmt_slab_drop_geometry")
+
+    def _early_geometry(self):
+        """The next step's known plane (owned rows of phi after the fix-up), allgathered, and
+        its extrapolation geometry on each slab's second stream beside the projection
+        (rmt_sim_step's early geometry; RMT_SLAB_EARLY_GEO=0 turns it off)."""
+        if not self._early_geo:
+            return False
+        self._call("rmt_slab_next_bits")
+        self.comm.allgather_rows(self.slabs, "bits_next")
+        self._call("rmt_slab_geometry")
+        return True
 
     def _set_dev_dt(self, on):
         for s in self.slabs:
@@ -500,12 +523,15 @@ class DistributedSim:
                 self._record(sc, float(r[0]), float(r[1]))
                 self._rim_cap = max(self._rim_cap, _rim_capacity(sc[:, SC_COUNT].max()))
 
-        for _ in range(nsteps):
+        geo = False
+        for k in range(nsteps):
             h = comm.halo_start(S, ("u", "v", "p", "X1", "X2"), HALO)
             self._call("rmt_slab_advect_interior", 0.0)
             comm.halo_finish(h)
             self._call("rmt_slab_advect", 0.0)
-            comm.allgather_rows(S, "bits")
+            if not geo:   # else the plane was gathered with the early geometry
+                comm.allgather_rows(S, "bits")
+            geo = False
             self._call("rmt_slab_rim_pack")
             if self._rim_cap is None:   # once: the capacity from the first rim (host read)
                 self._rim_cap = _rim_capacity(self._scalars()[:, SC_COUNT].max())
@@ -519,6 +545,8 @@ class DistributedSim:
                 L.check(s.lib.rmt_slab_extrapolate_dev(s.h, g.data_ptr(), gs.data_ptr(), cap),
                         "rmt_slab_extrapolate_dev")
             self._call("rmt_slab_momentum", 0.0)
+            if k + 1 < nsteps:
+                geo = self._early_geometry()
             self._call("rmt_slab_project_rows", 0.0)
             sp = [s.a2a_splits() for s in S]
             comm.all_to_all([s.view("A") for s in S], [s.view("B") for s in S],
@@ -541,6 +569,7 @@ class DistributedSim:
             slot += 1
             if slot == self.sync_every:
                 flush()
+        self._call("rmt_slab_drop_geometry")
         flush()
 
     def _sub_mean(self, which):
