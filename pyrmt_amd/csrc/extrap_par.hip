@@ -301,8 +301,11 @@ __global__ void __launch_bounds__(64) k_px_seg(ExWs ws, int ML) {
 // packed block of segment g (doubles): [0] nF, [1] nL, [2] kind (0 packed, 1 serial, 2 too
 // large: k_px_comb reads M and d from their own arrays), [3] lo, [4] n, [8, 72) frontier ids,
 // [72, 136) live rows, [136, 264) d of the live rows (k_px_d), [264, PX_PB) M of the live
-// rows, column-major: M[r_k][c] at 264 + c nL + k
-constexpr int PXB_F = 8, PXB_R = 72, PXB_D = 136, PXB_M = 264;
+// rows at a fixed stride: M[r_k][c] at 264 + c PXB_S + k (nF <= PXB_C, nL <= PXB_S; larger
+// segments are kind 2).  Fixed addresses let k_px_comb read a whole block in one LDS round
+// trip, before its header is known.
+constexpr int PXB_F = 8, PXB_R = 72, PXB_D = 136, PXB_M = 264, PXB_S = 20, PXB_C = 24;
+static_assert(PXB_M + PXB_C * PXB_S <= PX_PB, "packed block");
 __global__ void __launch_bounds__(64) k_px_pack(ExWs ws, int ML) {
     if (ws.ctl[EXC_FALLBACK]) return;
     const int g = blockIdx.x, lane = threadIdx.x;
@@ -318,7 +321,7 @@ __global__ void __launch_bounds__(64) k_px_pack(ExWs ws, int ML) {
     const bool lv = !serial && lane < n && ws.live[lo + lane];
     const u64 lm = __ballot(lv);
     const int nL = __popcll(lm);
-    const int kind = serial ? 1 : (PXB_M + nF * nL > PX_PB ? 2 : 0);
+    const int kind = serial ? 1 : (nF > PXB_C || nL > PXB_S ? 2 : 0);
     if (lane == 0) { B[0] = nF; B[1] = nL; B[2] = kind; B[3] = lo; B[4] = n; }
     if (serial) return;
     if (lane < nF) B[PXB_F + lane] = ws.sF[(long)g * PX_F + lane];
@@ -327,7 +330,7 @@ __global__ void __launch_bounds__(64) k_px_pack(ExWs ws, int ML) {
     if (kind != 0) return;
     const double *MT = ws.sMT + (long)g * PX_F * PX_K;
     for (int c = 0; c < nF; ++c)
-        if (lv) B[PXB_M + c * nL + k] = MT[c * PX_K + lane];
+        if (lv) B[PXB_M + c * PXB_S + k] = MT[c * PX_K + lane];
 }
 
 // ------------------------------------------------------------------ values ---------
@@ -457,27 +460,49 @@ __global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
         }
         return;
     }
+    static_assert(PXB_C == PX_FR, "the consumer holds a packed block's M in registers");
+    const int ml = lane < PXB_S ? lane : 0;
     for (int gi = 0; gi < ns; ++gi) {   // consumer (wave 0)
         const int slot = gi % PX_NS, g = s0 + gi;
-        long spin = 0;
-        while (ready[slot] != gi)
-            if (++spin > SPIN) { if (lane == 0) atomicExch(ws.status + 1, 1); return; }
         const double *B = slots + (size_t)slot * PX_PB;
-        const int nF = (int)B[0], nL = (int)B[1], kind = (int)B[2], lo = (int)B[3], n = (int)B[4];
+        // the ready flag, then the whole block at fixed addresses, in one LDS round trip (a
+        // wave's LDS operations execute in order: if the flag read sees gi, the reads after it
+        // see the producer's block); read again after a wait if the producer was not done
+        int rd;
+        double h0, h1, h2, h3, h4, sd, rdd;
+        double2 xd;
+        double m[PX_FR];
+        auto read_block = [&]() {
+            rd = ready[slot];
+            asm volatile("" ::: "memory");
+            h0 = B[0]; h1 = B[1]; h2 = B[2]; h3 = B[3]; h4 = B[4];
+            sd = B[PXB_F + lane]; rdd = B[PXB_R + lane];
+            xd = make_double2(B[PXB_D + 2 * lane], B[PXB_D + 2 * lane + 1]);
+#pragma unroll
+            for (int c = 0; c < PX_FR; ++c) m[c] = B[PXB_M + c * PXB_S + ml];
+        };
+        read_block();
+        if (rd != gi) {
+            long spin = 0;
+            while (ready[slot] != gi)
+                if (++spin > SPIN) { if (lane == 0) atomicExch(ws.status + 1, 1); return; }
+            read_block();
+        }
+        const int nF = (int)h0, nL = (int)h1, kind = (int)h2, lo = (int)h3, n = (int)h4;
         if (kind == 1) {
             // serial segment, fit by fit: x_t = c_t + sum over same-layer sources beta x_s
             for (int r = 0; r < n; ++r) {
                 const int t = lo + r, nst = ws.pns[t], nd = ws.pnd[t];
-                int s = 0;
+                int sr = 0;
                 double b = 0.0, a1 = 0.0, a2 = 0.0;
                 if (lane < nd) {
-                    s = -ws.pkey[(long)t * PX_S + nst + lane] - 1;
+                    sr = -ws.pkey[(long)t * PX_S + nst + lane] - 1;
                     b = ws.pbeta[(long)t * PX_S + nst + lane];
                 }
-                const bool far = lane < nd && t - s > PX_RING;
+                const bool far = lane < nd && t - sr > PX_RING;
                 if (__ballot(far)) __threadfence();
                 if (lane < nd) {
-                    const double2 v = far ? px_far(&ws.pval[s]) : ring[s & (PX_RING - 1)];
+                    const double2 v = far ? px_far(&ws.pval[sr]) : ring[sr & (PX_RING - 1)];
                     a1 = b * v.x; a2 = b * v.y;
                 }
                 a1 = px_wsum(a1); a2 = px_wsum(a2);
@@ -491,40 +516,28 @@ __global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
                 }
             }
         } else if (nL > 0) {
-            // every LDS read of the segment is issued before the first use: the frontier ids,
-            // then (independent of each other) the ring values, the live rows, their d and up
-            // to PX_FR columns of M; the FMAs then run back to back in px_row's order
-            const int s = lane < nF ? (int)B[PXB_F + lane] : lo;
-            const int r = lane < nL ? (int)B[PXB_R + lane] : 0;
-            double2 x = make_double2(0.0, 0.0);
-            double m[PX_FR];
-            if (kind == 0) {
-                if (lane < nL) x = make_double2(B[PXB_D + 2 * lane], B[PXB_D + 2 * lane + 1]);
-#pragma unroll
-                for (int c = 0; c < PX_FR; ++c)
-                    m[c] = (c < nF && lane < nL) ? B[PXB_M + c * nL + lane] : 0.0;
-            }
+            // the frontier's values: the one read that waits on earlier segments
+            const int sf = lane < nF ? (int)sd : lo;
+            const int r = lane < nL ? (int)rdd : 0;
             double f1 = 0.0, f2 = 0.0;
             {
-                const bool far = lane < nF && lo - s > PX_RING;
+                const bool far = lane < nF && lo - sf > PX_RING;
                 if (__ballot(far)) __threadfence();
                 if (lane < nF) {
-                    const double2 v = far ? px_far(&ws.pval[s]) : ring[s & (PX_RING - 1)];
+                    const double2 v = far ? px_far(&ws.pval[sf]) : ring[sf & (PX_RING - 1)];
                     f1 = v.x; f2 = v.y;
                 }
             }
-            if (kind == 0) {
+            double2 x;
+            if (kind == 0) {   // the FMAs back to back in px_row's order
+                x = lane < nL ? xd : make_double2(0.0, 0.0);
 #pragma unroll
                 for (int c = 0; c < PX_FR; ++c) {
                     if (c < nF) {
-                        x.x += m[c] * px_rl(f1, c);
-                        x.y += m[c] * px_rl(f2, c);
+                        const double mc = lane < nL ? m[c] : 0.0;
+                        x.x += mc * px_rl(f1, c);
+                        x.y += mc * px_rl(f2, c);
                     }
-                }
-                for (int c = PX_FR; c < nF; ++c) {   // a wide frontier: the rest from LDS
-                    const double mc = lane < nL ? B[PXB_M + c * nL + lane] : 0.0;
-                    x.x += mc * px_rl(f1, c);
-                    x.y += mc * px_rl(f2, c);
                 }
             } else {   // block too small for this segment's M: its own arrays (same order)
                 x = px_row(ws.sMT + (long)g * PX_F * PX_K, nF, ws.sd[(long)g * PX_K + r], f1, f2,
@@ -535,7 +548,7 @@ __global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
                 ws.pval[lo + r] = x;
             }
         }
-        // every read of the slot is issued: hand it back (LDS operations stay in order)
+        // every read of the slot is done: hand it back (LDS operations stay in order)
         if (lane == 0) freeg[slot] = gi + PX_NS;
     }
 }
