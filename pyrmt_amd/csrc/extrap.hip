@@ -811,6 +811,9 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
     if (chain) RMT_TRY(extrap_chain_run(ctx, ws, X1o, X2o, max_layers));
     if (par) {
         if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
+        // the caller's work beside the extrapolation may start now (its combine pass is one
+        // workgroup, as the chain)
+        if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, ctx->stream));
         RMT_TRY(extrap_par_values(ctx, ws, X1o, X2o, max_layers));
         if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
     }
@@ -823,7 +826,7 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
     if (dev_status)
         RMT_HIP(hipMemcpyAsync(dev_status, ws.status, 2 * sizeof(int), hipMemcpyDeviceToDevice,
                                ctx->stream));
-    if (ctx->ev_chain && !chain) RMT_HIP(hipEventRecord(ctx->ev_chain, ctx->stream));
+    if (ctx->ev_chain && !chain && !par) RMT_HIP(hipEventRecord(ctx->ev_chain, ctx->stream));
     return RMT_OK;
 }
 

@@ -795,10 +795,12 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // a second stream, re-run afterwards on the tiles within reach of a target
         static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
         static const bool side_tail = !(getenv("RMT_SIDE_TAIL") && !atoi(getenv("RMT_SIDE_TAIL")));
-        // the parallel extrapolation takes ~0.2 ms: nothing to hide it behind, so the step
-        // runs in order (its geometry still beside the previous step's projection)
+        // the parallel extrapolation: its values pass (~0.5 ms at N=4096, mostly the
+        // one-workgroup combine) runs beside the speculative momentum too (RMT_PAR_OVERLAP=0:
+        // in order, the momentum after it)
         const bool par = extrap_par_enabled();
-        const bool overlap = solid && S->st2 && !no_overlap && !par;
+        static const bool par_ov = !(getenv("RMT_PAR_OVERLAP") && !atoi(getenv("RMT_PAR_OVERLAP")));
+        const bool overlap = solid && S->st2 && !no_overlap && (!par || par_ov);
         bool fixprep = false;   // the fused fix-up prep (set where the extrapolation runs)
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
