@@ -195,6 +195,9 @@ def lib():
             raise ImportError(
                 f"librmt.so not found at {LIB_PATH}: build it first "
                 "(python -c 'import __graft_entry__ as g; g.build()')")
+        # torch first: librmt's libamdhip64 dependency then binds to the HIP runtime torch
+        # loaded (loaded the other way round, torch's device calls found no device)
+        import torch  # noqa: F401
         h = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(h, name)

@@ -143,12 +143,14 @@ __global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, 
     for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int j = jb + blockIdx.x * 4 + wv;
-    if (j < 1 || j > ny - 2 || j >= je) return;
     double (*t)[96] = tb[wv];
     auto K = [&](int jj, int w) -> u64 {
         return (jj < 0 || jj >= ny || w < 0 || w >= W) ? 0 : kbits[(long)jj * W + w];
     };
+    // a wave per row, rows strided over the grid (a grid smaller than the rows stops every
+    // wave soon after the first fit is found)
+    for (int j = jb + blockIdx.x * 4 + wv; j < je && j <= ny - 2; j += gridDim.x * 4) {
+    if (j < 1) continue;
     for (int wb = 0; wb < W; wb += 64) {
         if (__hip_atomic_load(ctl + EXC_ANY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
         u64 mine = 0;
@@ -212,6 +214,7 @@ __global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, 
                 }
             }
         }
+    }
     }
 }
 __global__ void k_ex_none_fin(int *ctl) {
@@ -746,8 +749,10 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
         }
         // exact shortcut: no target can be accepted -> identity (k_ex_none)
         const double r = 4 * std::sqrt(dx * dx + dy * dy);
-        k_ex_none<<<grid1d(ny, 4), 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, dx, dy, r * r,
-                                                           ws.ctl, 0, ny);
+        // 64 workgroups: the disc's first rim rows end the search (this runs beside the
+        // critical path when sim.hip prepares the next step's geometry early)
+        k_ex_none<<<std::min<unsigned>(grid1d(ny, 4), 64), 256, 0, ctx->stream>>>(
+            ws.kbits, ny, nx, W, dx, dy, r * r, ws.ctl, 0, ny);
         k_ex_none_fin<<<1, 1, 0, ctx->stream>>>(ws.ctl);
         RMT_LAUNCHED();
         if (par) {
@@ -780,7 +785,13 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
     ExSweep A{X1o, X2o, ws.kbits, ws.cbits, ws.Kold, ws.rowcand, ws.jrange, ny, nx, W,
               max_layers, dx, dy, ws.status, ctl};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
-    if (!prof) {
+    const bool defer = chain && ctx->ex_sweep_defer && ctx->ev_chain;
+    RMT_CHECK(!defer || !dev_status, RMT_EINVAL,
+              "extrap_finish: a deferred sweep leaves the status to the caller");
+    if (defer) {
+        // the caller's extrap_sweep, beside the chain (both exit at once unless their path
+        // is the one the chain prep chose)
+    } else if (!prof) {
         k_ex_sweep<false><<<1, EXW * 64, 0, ctx->stream>>>(A, nullptr);
         RMT_LAUNCHED();
     } else {
@@ -827,6 +838,19 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
         RMT_HIP(hipMemcpyAsync(dev_status, ws.status, 2 * sizeof(int), hipMemcpyDeviceToDevice,
                                ctx->stream));
     if (ctx->ev_chain && !chain && !par) RMT_HIP(hipEventRecord(ctx->ev_chain, ctx->stream));
+    return RMT_OK;
+}
+
+int extrap_sweep(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
+                 hipStream_t s) {
+    const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
+    RMT_CHECK(ctx->ex_chain && !ctx->ex_par && ctx->ex_layers == max_layers, RMT_EINVAL,
+              "extrap_sweep: follows an exact-chain extrap_finish of the same layers");
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
+    ExSweep A{X1o, X2o, ws.kbits, ws.cbits, ws.Kold, ws.rowcand, ws.jrange, ny, nx, W,
+              max_layers, dx, dy, ws.status, ws.ctl};
+    k_ex_sweep<false><<<1, EXW * 64, 0, s>>>(A, nullptr);
+    RMT_LAUNCHED();
     return RMT_OK;
 }
 

@@ -91,6 +91,10 @@ struct rmt_ctx {
     // chain's prediction of each fit's latest source (extrap_chain.hip, fast fold); null:
     // the input map
     const double *ex_pred1 = nullptr, *ex_pred2 = nullptr;
+    // optional (sim.hip overlap): extrap_finish leaves the fallback sweep (an early exit unless
+    // a chain capacity limit tripped) to the caller, who runs extrap_sweep on another stream
+    // after ev_chain, beside the chain instead of ahead of it
+    bool ex_sweep_defer = false;
     // momentum.hip: the stage tiles a full launch's interior kernel skips, per row window
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
     EdgeTiles edge[8];
@@ -666,6 +670,10 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
 const int *extrap_status(rmt_ctx *ctx, int max_layers);
 int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
                   int *dev_status);
+// the fallback sweep of the last extrap_finish on stream s (ctx->ex_sweep_defer), ordered after
+// that call's ev_chain; the map and the status words are final once it completes
+int extrap_sweep(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
+                 hipStream_t s);
 size_t extrap_workspace(int ny, int nx, int max_layers, bool px = false);   // ctx->bytes used
 void imex_destroy(rmt_ctx *ctx);   // imex.hip: the context's DST plans
 // the parallel extrapolation mode (extrap_par.hip; rmt_extrap_set_parallel or the environment

@@ -335,13 +335,20 @@ __global__ void k_dt(const double *m2, double dt_const, double cfl, double dx, d
 // max, exact in any order): DTP_BLOCKS blocks fold their share and merge with a 64-bit atomic
 // max on the bit patterns (values are +0.0 .. +inf or NaN, which orders them as doubles with
 // every NaN on top); the last block writes sc[0] = max |u|^2, sc[1] = dt and re-arms acc.
+// With e, block 0 first completes the previous step's ring record (k_ring_put's work, one
+// launch fewer between the projection and the next chain): it reads sc before its atomic
+// ticket, so before the last block overwrites sc.
 constexpr int DTP_BLOCKS = 64;
+__device__ __forceinline__ void ring_record(const double *sc, int *flag, double *e);
 __global__ void __launch_bounds__(256) k_dt_part(const double *__restrict__ part, int np,
                                                  double dt_const, double cfl, double dx,
                                                  double *__restrict__ sc,
-                                                 unsigned long long *__restrict__ acc) {
+                                                 unsigned long long *__restrict__ acc,
+                                                 int *__restrict__ flag = nullptr,
+                                                 double *__restrict__ e = nullptr) {
     __shared__ double s[256];
     __shared__ bool last;
+    if (e && blockIdx.x == 0 && threadIdx.x == 0) ring_record(sc, flag, e);
     double m = 0.0;
     for (int k = blockIdx.x * 256 + threadIdx.x; k < np; k += DTP_BLOCKS * 256) {
         const double y = part[k];
@@ -382,14 +389,15 @@ __global__ void k_mark_rows(const int *__restrict__ tiles, const int *__restrict
 }
 // completes a ring record after k_diag_p2 wrote its diagnostics: max |u|^2, dt, flags
 // and clears the non-finite flag for the next step (in place of a memset launch)
+__device__ __forceinline__ void ring_record(const double *sc, int *flag, double *e) {
+    e[DIAG_VALS] = sc[0];
+    e[DIAG_VALS + 1] = sc[1];
+    for (int k = 0; k < 4; ++k) e[DIAG_VALS + 2 + k] = flag ? (double)flag[k] : 0.0;
+    if (flag) flag[0] = 0;
+}
 __global__ void k_ring_put(const double *__restrict__ sc, int *__restrict__ flag,
                            double *__restrict__ e) {
-    if (threadIdx.x == 0) {
-        e[DIAG_VALS] = sc[0];
-        e[DIAG_VALS + 1] = sc[1];
-        for (int k = 0; k < 4; ++k) e[DIAG_VALS + 2 + k] = flag ? (double)flag[k] : 0.0;
-        if (flag) flag[0] = 0;
-    }
+    if (threadIdx.x == 0) ring_record(sc, flag, e);
 }
 
 struct DiagArgs {
@@ -726,8 +734,16 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         tail = false;
         return RMT_OK;
     };
+    // the last step's ring record, completed by the next step's k_dt_part (or here)
+    double *ring_e = nullptr;
+    int *const ring_flag = P.shape != RMT_SHAPE_NONE ? S->flag : nullptr;
     auto flush = [&]() -> int {
         RMT_TRY(join());
+        if (ring_e) {
+            k_ring_put<<<1, 64, 0, st>>>(sc, ring_flag, ring_e);
+            RMT_LAUNCHED();
+            ring_e = nullptr;
+        }
         if (!slot) return RMT_OK;
         std::vector<double> h((size_t)slot * RING_VALS);
         RMT_HIP(hipMemcpyAsync(h.data(), S->ring, h.size() * sizeof(double),
@@ -764,9 +780,12 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         double hv[2] = {0.0, 0.0}, dt = NAN;
         if (async && it > 0) {
             k_dt_part<<<DTP_BLOCKS, 256, 0, st>>>(S->m2part, S->m2n, S->dt_const, P.cfl, P.dx,
-                                                  sc, S->m2acc);
+                                                  sc, S->m2acc, ring_e ? ring_flag : nullptr,
+                                                  ring_e);
             RMT_LAUNCHED();
+            ring_e = nullptr;
         } else {
+            RMT_CHECK(!ring_e, RMT_EINVAL, "sim: ring record pending on a synchronous step");
             RMT_TRY(reduce_maxsq2_nan(ctx, S->u, S->v, n, sc));
             k_dt<<<1, 1, 0, st>>>(sc, S->dt_const, P.cfl, P.dx, sc + 1);
             RMT_LAUNCHED();
@@ -805,7 +824,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
             // 2. advect the reference map with the pre-advection level set and mask
-            // (on the asynchronous path the previous step's k_ring_put cleared it)
+            // (on the asynchronous path the previous step's ring record -- k_dt_part or k_ring_put --
+            // cleared it)
             if (!(async && it > 0)) RMT_HIP(hipMemsetAsync(S->flag, 0, sizeof(int), st));
             if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && overlap && S->e_bits) {
                 // known plane -> rim words -> the rim's advection here; the rest on the second
@@ -825,7 +845,6 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     k_rim_segments<<<grid1d(nseg, 256), 256, 0, st>>>(S->rimw, ny, nx, S->segs,
                                                                        scount);
                 }
-                RMT_HIP(hipEventRecord(S->e_bits, st));
                 k_sim_sl_rim<<<4096, 256, 0, st>>>(   // ~one rim segment per block
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.x0, P.y0,
                     P.R, S->X1n, S->X2n, S->flag, sc, dtp, S->rimw, S->segs, scount);
@@ -870,6 +889,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             fixprep = overlap && fp_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 &&
                       momentum_mode() != 2 && P.layers > 0;
             int *dstat = fixprep ? nullptr : S->flag + 2;
+            // with the fused fix-up prep the fallback sweep runs on the second stream beside the
+            // chain (the fix-up joins that stream before it reads the map or the status)
+            ctx->ex_sweep_defer = fixprep;
             const int es = geo_ready && P.layers > 0
                                ? extrap_finish(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, dstat)
                                : extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
@@ -877,9 +899,12 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             geo_ready = false;
             ctx->ex_pred1 = ctx->ex_pred2 = nullptr;
             ctx->ev_chain = nullptr;
+            ctx->ex_sweep_defer = false;
             RMT_TRY(es);
             if (overlap) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
+                if (fixprep && ctx->ex_chain && !ctx->ex_par)
+                    RMT_TRY(extrap_sweep(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->st2));
                 RMT_TRY(emit_tail());   // the previous step's tail, beside the chain
                 // the fix-up tiles and the rows they reach depend on the known plane only
                 ctx->stream = S->st2;
@@ -962,23 +987,24 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 // this step (nothing there uses them or the extrapolation workspace).  Issued
                 // before the fix-up stages: after them its few-block kernels would share the CUs
                 // with the projection's FFT passes (measured: the step no faster)
+                hipStream_t sg = S->st2;
                 RMT_HIP(hipEventRecord(S->e_kb, st));
-                RMT_HIP(hipStreamWaitEvent(S->st2, S->e_kb, 0));
+                RMT_HIP(hipStreamWaitEvent(sg, S->e_kb, 0));
                 const long nseg = (long)ny * ((nx + 255) / 256);
                 int *scount = S->segs + nseg;
-                ctx->stream = S->st2;
+                ctx->stream = sg;
                 int gs = rim_words(ctx, nb, ny, nx, (nx + 63) / 64, S->rimw, S->rimcnt);
                 if (gs == RMT_OK)
-                    gs = hipMemsetAsync(scount, 0, sizeof(int), S->st2) ? RMT_EDEVICE : RMT_OK;
+                    gs = hipMemsetAsync(scount, 0, sizeof(int), sg) ? RMT_EDEVICE : RMT_OK;
                 if (gs == RMT_OK) {
-                    k_rim_segments<<<grid1d(nseg, 256), 256, 0, S->st2>>>(S->rimw, ny, nx,
-                                                                           S->segs, scount);
+                    k_rim_segments<<<grid1d(nseg, 256), 256, 0, sg>>>(S->rimw, ny, nx,
+                                                                       S->segs, scount);
                     gs = extrap_geometry(ctx, S->X1n, S->X2n, nullptr, P.dx, P.dy, P.layers,
                                          S->X1n, S->X2n, nb);
                 }
                 ctx->stream = st;
                 RMT_TRY(gs);
-                RMT_HIP(hipEventRecord(S->e_geo, S->st2));
+                RMT_HIP(hipEventRecord(S->e_geo, sg));
                 geo_ready = true;
             }
             RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
@@ -1045,8 +1071,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_HIP(hipEventRecord(S->e_proj, st));
             pend_e = e;
             pending = true;
-            k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
-            RMT_LAUNCHED();
+            ring_e = e;
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
             if (++slot == S->sync_every) RMT_TRY(flush());
             continue;
@@ -1055,8 +1080,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (async) {
             double *e = S->ring + (size_t)slot * RING_VALS;
             k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, e);
-            k_ring_put<<<1, 64, 0, st>>>(sc, solid ? S->flag : nullptr, e);
             RMT_LAUNCHED();
+            ring_e = e;
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
             if (++slot == S->sync_every) RMT_TRY(flush());
             continue;

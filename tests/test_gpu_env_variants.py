@@ -12,6 +12,9 @@ projection (LDS DCT plan: 255 = 3 5 17) and with it the early transpose are on.
   RMT_CH_PARTS=1          the chain in one workgroup
   RMT_CH_VARIANT=35       the chain's residue fast fold (sim.hip / extrap_chain.hip ch_fast)
   RMT_FUSED_FLUID=0       the momentum's pure-fluid flags from their own pass over phi
+  TEST_EX_MODE=2          (this file's child) the extrapolation's forced fallback sweep, which
+                          the fused step runs on its second stream beside the chain
+  RMT_FUSED_FIXPREP=0     the fix-up's phi and momentum prep in two kernels (the sweep in order)
 """
 import os
 import subprocess
@@ -28,7 +31,11 @@ CHILD = r"""
 import sys
 import numpy as np
 sys.path.insert(0, sys.argv[1])
+import os
 from pyrmt_amd.simulation import soft_disc_in_lid_driven
+from pyrmt_amd.functions import extrapolation_mode
+if os.environ.get("TEST_EX_MODE"):
+    extrapolation_mode(int(os.environ["TEST_EX_MODE"]))
 s = soft_disc_in_lid_driven(256)
 s.step(12)
 out = {f: s.get(f) for f in %r}
@@ -56,6 +63,8 @@ def default_run(tmp_path_factory, gpu):
     {"RMT_SIM_HIPRIO": "0"}, {"RMT_EARLY_TRANSPOSE": "0"}, {"RMT_EARLY_GEOMETRY": "0"},
     {"RMT_SIDE_TAIL": "0"}, {"RMT_NO_OVERLAP": "1"}, {"RMT_SIM_SYNC": "1"},
     {"RMT_CH_PARTS": "1"}, {"RMT_CH_VARIANT": "35"}, {"RMT_FUSED_FLUID": "0"},
+    {"TEST_EX_MODE": "2"}, {"TEST_EX_MODE": "2", "RMT_FUSED_FIXPREP": "0"},
+    {"RMT_FUSED_FIXPREP": "0"},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(tmp_path, default_run, env):
     got = _run(tmp_path, "variant", env)
