@@ -134,7 +134,10 @@ def main():
     backend = os.environ.get("RMT_DIST_BACKEND", "nccl")
     dev = local % torch.cuda.device_count() if backend == "gloo" else local
     torch.cuda.set_device(dev)
-    if ws > 1:
+    # RMT_BENCH_DIST=1: the multi-rank path (process group, TorchComm slabs, barriers, MAX
+    # over ranks) even at one rank -- the driver's N>1 code path rehearsed on one GPU
+    md = ws > 1 or os.environ.get("RMT_BENCH_DIST") == "1"
+    if md:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
@@ -142,7 +145,7 @@ def main():
     import sys
     sys.path.insert(0, ROOT)
     N = args.n
-    if ws > 1:
+    if md:
         from pyrmt_amd import distributed as D
         sim = D.soft_disc_in_lid_driven(N, D.TorchComm())
     else:
@@ -152,16 +155,16 @@ def main():
     torch.cuda.synchronize()
 
     def timed(k):
-        if ws > 1:
+        if md:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sim.step(k)
         torch.cuda.synchronize()
-        if ws > 1:
+        if md:
             dist.barrier()
         el = time.perf_counter() - t0
-        if ws > 1:
+        if md:
             t = torch.tensor([el], device="cuda", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -181,17 +184,17 @@ def main():
     if rank == 0:
         cells = N * N * args.steps          # one problem (strong scaling when ws > 1)
         value = cells / elapsed
-        traffic, step_traffic, pmc_rev = _pmc(N, ws)
+        traffic, step_traffic, pmc_rev = _pmc(N, 2 if md else 1)
         rk_ms, rk_intervals = ph["rk4_stage_kernels"]
-        rk_launches = rk_intervals if ws == 1 else 4 * rk_intervals
+        rk_launches = rk_intervals if not md else 4 * rk_intervals
         per_launch_s = rk_ms / 1e3 / rk_launches
         # achieved: SURVEY 8(d)'s algorithmic bytes of the stress + RK4 pass (7 planes per cell
         # for the 4 stage launches) spread over the launches, / the HIP-event launch time;
         # a slab's cell-updates are its owned rows (the recomputed halo rows are overhead)
-        own = N * N if ws == 1 else (sim.slabs[0].r1 - sim.slabs[0].r0) * N
+        own = N * N if not md else (sim.slabs[0].r1 - sim.slabs[0].r0) * N
         alg_per_launch = RK4_ALG_BYTES_PER_CELL * own / 4
         achieved = alg_per_launch / per_launch_s / 1e9
-        ex_ms, ex_calls = ph["extrap_sweep_kernel" if ws == 1 else "extrap_chain_kernel"]
+        ex_ms, ex_calls = ph["extrap_sweep_kernel" if not md else "extrap_chain_kernel"]
         out = {
             "metric": "cell-updates/s (full RMT step) at N=4096; achieved HBM GB/s vs peak",
             "value": value, "unit": "cell-updates/s", "n_gpus": ws, "steps": args.steps,
@@ -201,7 +204,8 @@ def main():
             "dtype": "f64", "data": "synthetic (driver initial condition: disc at rest, lid U=1)",
             "config": {"workload": f"soft_disc_in_lid_driven N={N} semilagrangian "
                                    "(configs 2/4 loop body)", "grid": N,
-                       "parallelism": f"slab{ws} (row slabs, RCCL)" if ws > 1 else "single-gpu"},
+                       "parallelism": (f"slab{ws} (row slabs, {'RCCL' if backend == 'nccl' else backend})"
+                                       if md else "single-gpu")},
             # the dominant HBM-bound kernel: the fused RK4 stage (4 launches per step)
             "roofline": {"bound": "hbm", "kernel": "k_mom_stage (fused RK4 stage, 4 launches/step)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -210,7 +214,7 @@ def main():
                          "launch_ms": per_launch_s * 1e3,
                          "alg_bytes_per_launch": alg_per_launch},
             # ... whose own bound is the fp64 VALU issue rate (SQ counters)
-            "compute_roofline": _f64_roof(N, ws, per_launch_s),
+            "compute_roofline": _f64_roof(N, 2 if md else 1, per_launch_s),
             # the dominant kernel by time is not HBM-bound: the exact raster-order extrapolation
             # chain runs on one workgroup, bounded by its dependency depth
             "latency_bound": {"kernel": "k_ex_chain (exact serial-order extrapolation chain)",
@@ -229,7 +233,7 @@ def main():
         if not args.no_cpu_baseline and ws == 1:
             out["cpu_baseline"] = cpu_baseline(N, args.cpu_steps)
         print(json.dumps(out), flush=True)
-    if ws > 1:
+    if md:
         dist.destroy_process_group()
 
 

@@ -104,6 +104,33 @@ def test_slab_step_two_processes_gloo(gpu):
 
 
 @pytest.mark.gpu
+def test_slab_step_rccl_one_rank(gpu):
+    """The TorchComm path over RCCL (backend "nccl": device tensors, no host staging) at one
+    rank -- the one-GPU box cannot place two RCCL ranks on one device -- against the fused
+    step."""
+    out = _torchrun(1, "dist_step.py", 256, 4, "nccl", timeout=300)
+    assert "dist_step ok" in out
+
+
+@pytest.mark.gpu
+def test_bench_multi_rank_path_rccl(gpu):
+    """bench.py's N>1 code path (process group with device_id, TorchComm slabs, barriers, MAX
+    over ranks) at one rank over RCCL (RMT_BENCH_DIST=1): one JSON line with the slab
+    parallelism."""
+    import json
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--grid", "256", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    e = dict(os.environ, OMP_NUM_THREADS="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+             RMT_BENCH_DIST="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=e)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["config"]["parallelism"] == "slab1 (row slabs, RCCL)"
+    assert line["value"] > 0 and line["steps"] == 3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_config4_slab_step_N4096(gpu, G):
     """Config 4 (soft_disc_in_lid_driven N=4096, 2->4->8 slabs) at its own size: G virtual
