@@ -1318,9 +1318,9 @@ int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     const double r = 4 * std::sqrt(dx * dx + dy * dy);
     ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r, 0};
     const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
-    k_ex_vals<<<gblocks, 256, 0, ctx->stream>>>(A, ML, ctx->ex_pred1 ? ctx->ex_pred1 : X1o,
-                                                ctx->ex_pred2 ? ctx->ex_pred2 : X2o);
-    RMT_LAUNCHED();
+    RMT_HIP(launch_done(k_ex_vals, dim3(gblocks), dim3(256), 0, ctx->stream,
+                        ctx->ev_chain_vals ? ctx->ev_chain : nullptr, A, ML,
+                        ctx->ex_pred1 ? ctx->ex_pred1 : X1o, ctx->ex_pred2 ? ctx->ex_pred2 : X2o));
     return RMT_OK;
 }
 
@@ -1330,7 +1330,7 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
     static const int nparts = getenv("RMT_CH_PARTS") ? std::min(CH_MAXP, std::max(1,
                                   atoi(getenv("RMT_CH_PARTS")))) : 2;
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
-    if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
+    if (ctx->ev_chain && !ctx->ev_chain_vals) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status, nullptr};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
     const int var = ch_variant();

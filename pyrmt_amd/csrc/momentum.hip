@@ -1500,16 +1500,16 @@ int fixup_phi_prep(rmt_ctx *ctx, const rmt_momentum_params *P, const MomWork &W,
                    const double *X1n, const double *X2n, double x0, double y0, double R,
                    double *X1, double *X2, double *phi, unsigned long long *nbits, double *sxx,
                    double *sxy, double *syy, double *J, const int *tiles, const int *count,
-                   int max_tiles, const int *st_src, int *st_dst) {
+                   int max_tiles, const int *st_src, int *st_dst, hipEvent_t done) {
     const int ny = ctx->ny, nx = ctx->nx;
     RMT_CHECK(nx % 64 == 0 && g_mom_mode != 2, RMT_EINVAL,
               "fixup_phi_prep: nx % 64 == 0 and the fused momentum modes only");
     const double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
-    k_phi_prep_tiles<<<list_grid(max_tiles), MOM_TX * MOM_TY, 0, ctx->stream>>>(
-        X1n, X2n, x0, y0, R, nbits, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp,
-        P->w_t, X1, X2, phi, sxx, sxy, syy, J, W.H, W.solid, tiles, count, nx / MOM_TX, 0, ny,
-        W.prep_const, st_src, st_dst);
-    RMT_LAUNCHED();
+    RMT_HIP(launch_done(k_phi_prep_tiles, dim3(list_grid(max_tiles)), dim3(MOM_TX * MOM_TY), 0,
+                        ctx->stream, done, X1n, X2n, x0, y0, R, nbits, ny, nx, P->dx, P->dy,
+                        P->mu_s, P->kappa, w_cut, clamp, P->w_t, X1, X2, phi, sxx, sxy, syy, J,
+                        W.H, W.solid, tiles, count, nx / MOM_TX, 0, ny, W.prep_const, st_src,
+                        st_dst));
     return RMT_OK;
 }
 

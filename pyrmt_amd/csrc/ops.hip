@@ -12,6 +12,10 @@
 namespace rmt {
 static thread_local std::string g_err;
 void set_error(const std::string &m) { g_err = m; }
+bool ext_events() {
+    static const bool on = !(getenv("RMT_EXT_EVENTS") && !atoi(getenv("RMT_EXT_EVENTS")));
+    return on;
+}
 
 int ensure_scratch(rmt_ctx *ctx, size_t bytes) {
     if (ctx->scratch_bytes >= bytes) return RMT_OK;
@@ -863,14 +867,16 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,
-                      double *m2part, bool sub_mean, const unsigned char *early_marks) {
+                      double *m2part, bool sub_mean, const unsigned char *early_marks,
+                      hipEvent_t done) {
     const long n = (long)ctx->ny * ctx->nx;
     double *pc = ctx->scratch + n, *root = ctx->red + RED_BLOCKS + 17;
     RMT_TRY(dct_solve_after_rows(ctx, pc, root, early_marks));
-    k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
-        a_star, b_star, pc, p_prev, ctx->ny, ctx->nx, divk_make(2 * dx), divk_make(2 * dy), dt / rho, bc_kind, lid, a, b, p, 0,
-        ctx->ny, root, (double)n, dtp, rho, m2part);
-    RMT_LAUNCHED();
+    RMT_CHECK(!done || !sub_mean, RMT_EINVAL, "projection_finish: done tracks the last kernel");
+    RMT_HIP(launch_done(k_project_correct, rows_grid(ctx->nx, 0, ctx->ny), dim3(256), 0,
+                        ctx->stream, done, a_star, b_star, (const double *)pc, p_prev, ctx->ny,
+                        ctx->nx, divk_make(2 * dx), divk_make(2 * dy), dt / rho, bc_kind, lid, a,
+                        b, p, 0, ctx->ny, (const double *)root, (double)n, dtp, rho, m2part));
     return sub_mean ? sub_mean_rows(ctx, p, ctx->ny, ctx->nx) : RMT_OK;
 }
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,

@@ -6,6 +6,7 @@
 // wherever no transcendental function or FFT is involved.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <rocfft/rocfft.h>
 #include <algorithm>
 #include <cmath>
@@ -95,6 +96,9 @@ struct rmt_ctx {
     // a chain capacity limit tripped) to the caller, who runs extrap_sweep on another stream
     // after ev_chain, beside the chain instead of ahead of it
     bool ex_sweep_defer = false;
+    // optional (sim.hip overlap, with ex_sweep_defer): ev_chain tracks the completion of the
+    // values pass right before the chain (launch_done) instead of a record of its own
+    bool ev_chain_vals = false;
     // momentum.hip: the stage tiles a full launch's interior kernel skips, per row window
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
     EdgeTiles edge[8];
@@ -108,6 +112,24 @@ namespace rmt {
 int ensure_scratch(rmt_ctx *ctx, size_t bytes);    // >= bytes of double scratch
 int ensure_bytes(rmt_ctx *ctx, size_t bytes);      // >= bytes of byte scratch
 inline unsigned grid1d(long n, int block) { return (unsigned)((n + block - 1) / block); }
+
+// A launch whose completion also completes `done` (hipExtLaunchKernel's stop event tracks the
+// kernel itself: no marker packet between it and the stream's next launch -- an event record
+// there costs the in-order stream ~6-8 us of command-processor time).  RMT_EXT_EVENTS=0: the
+// launch, then a plain record.  done null: a plain launch.
+bool ext_events();
+template <typename... Formals, typename... Actuals>
+inline hipError_t launch_done(void (*k)(Formals...), dim3 g, dim3 b, uint32_t lds,
+                              hipStream_t s, hipEvent_t done, Actuals... a) {
+    if (done && ext_events()) {
+        hipExtLaunchKernelGGL(k, g, b, lds, s, nullptr, done, 0, a...);
+        return hipGetLastError();
+    }
+    hipExtLaunchKernelGGL(k, g, b, lds, s, nullptr, nullptr, 0, a...);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    return e;
+}
 
 // ------------------------------------------------------------- device arithmetic --
 // utils.py:4-25: second-order gradient along a line of length n (stride s) at index k;
@@ -527,7 +549,7 @@ int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, 
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,
                       double *m2part, bool sub_mean = true,
-                      const unsigned char *early_marks = nullptr);
+                      const unsigned char *early_marks = nullptr, hipEvent_t done = nullptr);
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                    double dy, const double *dtp, double rho, int bc_kind, double lid,
                    const double *p_prev, double *a, double *b, double *p, double *m2part);
@@ -618,7 +640,8 @@ int fixup_phi_prep(rmt_ctx *ctx, const rmt_momentum_params *P, const MomWork &W,
                    const double *X1n, const double *X2n, double x0, double y0, double R,
                    double *X1, double *X2, double *phi, unsigned long long *nbits, double *sxx,
                    double *sxy, double *syy, double *J, const int *tiles, const int *count,
-                   int max_tiles, const int *st_src = nullptr, int *st_dst = nullptr);
+                   int max_tiles, const int *st_src = nullptr, int *st_dst = nullptr,
+                   hipEvent_t done = nullptr);
 
 // ---------------------------------------------------------------------- poisson --
 // dev_root: nullptr -> p = solve - mean (functions.py:1119); else p = the raw solve and

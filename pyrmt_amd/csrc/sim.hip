@@ -892,6 +892,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // with the fused fix-up prep the fallback sweep runs on the second stream beside the
             // chain (the fix-up joins that stream before it reads the map or the status)
             ctx->ex_sweep_defer = fixprep;
+            ctx->ev_chain_vals = fixprep;   // ev_chain completes with the values pass
             const int es = geo_ready && P.layers > 0
                                ? extrap_finish(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, dstat)
                                : extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
@@ -900,6 +901,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             ctx->ex_pred1 = ctx->ex_pred2 = nullptr;
             ctx->ev_chain = nullptr;
             ctx->ex_sweep_defer = false;
+            ctx->ev_chain_vals = false;
             RMT_TRY(es);
             if (overlap) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
@@ -964,31 +966,39 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_HIP(hipEventRecord(S->pev[2], st));
             RMT_HIP(hipEventRecord(S->pev[3], st));
         }
+        // one join of the second stream instead of two (RMT_MERGED_JOIN, default on; not in
+        // the parallel mode, whose values pass ends long before that stream's row passes):
+        // e_rows, after the speculative momentum AND the projection's rows, here -- beside the
+        // ~3 ms chain both are done -- and no second wait before the projection
+        static const bool mj_env = !(getenv("RMT_MERGED_JOIN") && !atoi(getenv("RMT_MERGED_JOIN")));
+        const bool mjoin = overlap && mj_env && !par;
         if (overlap) {
             // 4 + 5 on the tiles the extrapolation can reach
-            RMT_HIP(hipStreamWaitEvent(st, S->e_mom, 0));
+            RMT_HIP(hipStreamWaitEvent(st, mjoin ? S->e_rows : S->e_mom, 0));
             const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;
             // phi on the tiles and the momentum's prep there in one kernel (RMT_FUSED_FIXPREP,
             // default on where nx % 64 == 0), which also copies the extrapolation's status
+            // the next step's geometry below starts once the known plane is final (e_kb)
+            const bool geo_next = async && geo_env && nb && P.layers > 0 && it + 1 < nsteps;
             if (fixprep) {
                 RMT_TRY(fixup_phi_prep(ctx, &M, W, S->X1n, S->X2n, P.x0, P.y0, P.R, S->X1, S->X2,
                                        S->phi, nb, S->sxx, S->sxy, S->syy, S->J, S->tiles,
                                        S->tcount, S->max_tiles, extrap_status(ctx, P.layers),
-                                       S->flag + 2));
+                                       S->flag + 2, geo_next ? S->e_kb : nullptr));
             } else {
                 k_phi_tiles<<<list_grid(S->max_tiles), 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
                                                            S->phi, S->X1, S->X2, S->tiles, S->tcount,
                                                            tiles_x, nb);
                 RMT_LAUNCHED();
             }
-            if (async && geo_env && nb && P.layers > 0 && it + 1 < nsteps) {
+            if (geo_next) {
                 // the next step's known plane is final (the phi kernel above): its rim words, rim
                 // segments and extrapolation geometry on the second stream, beside the rest of
                 // this step (nothing there uses them or the extrapolation workspace).  Issued
                 // before the fix-up stages: after them its few-block kernels would share the CUs
                 // with the projection's FFT passes (measured: the step no faster)
                 hipStream_t sg = S->st2;
-                RMT_HIP(hipEventRecord(S->e_kb, st));
+                if (!fixprep) RMT_HIP(hipEventRecord(S->e_kb, st));   // (else: with the prep)
                 RMT_HIP(hipStreamWaitEvent(sg, S->e_kb, 0));
                 const long nseg = (long)ny * ((nx + 255) / 256);
                 int *scount = S->segs + nseg;
@@ -1044,13 +1054,15 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (overlap && S->split_proj) {
             // redo the rhs on the fix-up tiles (+1 cell) and the row DCT of the rows they
             // reach, then the column pass and the rest
-            RMT_HIP(hipStreamWaitEvent(st, S->e_rows, 0));
+            if (!mjoin) RMT_HIP(hipStreamWaitEvent(st, S->e_rows, 0));
             RMT_TRY(projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
                                     S->rowmark, S->tiles, S->tcount, S->max_tiles));
+            // on the side-tail path e_proj completes with the velocity correction
             RMT_TRY(projection_finish(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, P.bc_kind,
                                       P.lid, S->p, S->u, S->v, S->p,
                                       async ? S->m2part : nullptr, !(async && side_tail),
-                                      early_t ? S->rowmark : nullptr));
+                                      early_t ? S->rowmark : nullptr,
+                                      async && side_tail ? S->e_proj : nullptr));
             early_t = false;
         } else if (async)
             RMT_TRY(projection_dev(ctx, S->us, S->vs, P.dx, P.dy, dtp, P.rho_f, P.bc_kind, P.lid,
@@ -1068,8 +1080,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // step's chain reads p or writes what they read (that stream's next work -- the
             // speculative phi, momentum -- is queued behind them)
             double *e = S->ring + (size_t)slot * RING_VALS;
-            RMT_HIP(hipEventRecord(S->e_proj, st));
-            pend_e = e;
+            pend_e = e;   // (e_proj: with the velocity correction, projection_finish)
             pending = true;
             ring_e = e;
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }

@@ -15,6 +15,10 @@ projection (LDS DCT plan: 255 = 3 5 17) and with it the early transpose are on.
   TEST_EX_MODE=2          (this file's child) the extrapolation's forced fallback sweep, which
                           the fused step runs on its second stream beside the chain
   RMT_FUSED_FIXPREP=0     the fix-up's phi and momentum prep in two kernels (the sweep in order)
+  RMT_EXT_EVENTS=0        the cross-stream events recorded after their kernels instead of
+                          completing with them (hipExtLaunchKernel)
+  RMT_MERGED_JOIN=0       the second stream joined twice (after its momentum, before the
+                          projection) instead of once after its row passes
 """
 import os
 import subprocess
@@ -64,7 +68,8 @@ def default_run(tmp_path_factory, gpu):
     {"RMT_SIDE_TAIL": "0"}, {"RMT_NO_OVERLAP": "1"}, {"RMT_SIM_SYNC": "1"},
     {"RMT_CH_PARTS": "1"}, {"RMT_CH_VARIANT": "35"}, {"RMT_FUSED_FLUID": "0"},
     {"TEST_EX_MODE": "2"}, {"TEST_EX_MODE": "2", "RMT_FUSED_FIXPREP": "0"},
-    {"RMT_FUSED_FIXPREP": "0"},
+    {"RMT_FUSED_FIXPREP": "0"}, {"RMT_EXT_EVENTS": "0"},
+    {"RMT_MERGED_JOIN": "0"},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(tmp_path, default_run, env):
     got = _run(tmp_path, "variant", env)
