@@ -294,6 +294,15 @@ int rmt_sim_field(rmt_sim *sim, int field, double **dev_ptr);
  * sync_every = 1, or a finite t_end, they are the failing step's).  The call returns once the
  * last step has finished on the stream. */
 int rmt_sim_step(rmt_sim *sim, int nsteps, double t_end);
+/* Carry (off by default): with on != 0, a call's last step also prepares what the next
+ * step needs from the final state alone (the extrapolation geometry of its known plane, the
+ * prep planes' constant-segment marks, max |u|^2 from the projection), and the next
+ * rmt_sim_step starts from it -- its first step then costs what every later step costs.
+ * The caller promises to call rmt_sim_invalidate after writing any field between calls; any
+ * other use of the context's workspace between calls ends the carry by itself.  Results
+ * are bit-identical either way. */
+int rmt_sim_set_carry(rmt_sim *sim, int on);
+int rmt_sim_invalidate(rmt_sim *sim);
 /* Phase timers (HIP events on the context stream, accumulated over steps while on):
  * ms[0] dt reduction, [1] advection, [2] extrapolation, [3] momentum (prep + 4 stages +
  * BC), [4] projection, [5] diagnostics, [6] the four RK4 stage kernels alone,

@@ -116,6 +116,8 @@ SIGNATURES = {
     "rmt_sim_step": (_I, [_P, _I, _D]),
     "rmt_sim_diagnostics": (_I, [_P, ctypes.POINTER(rmt_diag), _I, ctypes.POINTER(_I)]),
     "rmt_sim_set_profiling": (_I, [_P, _I]),
+    "rmt_sim_set_carry": (_I, [_P, _I]),
+    "rmt_sim_invalidate": (_I, [_P]),
     "rmt_sim_phase_times": (_I, [_P, ctypes.POINTER(_D), ctypes.POINTER(_L)]),
     # periodic branch
     "rmt_divergence_periodic": (_I, [_P, _P, _P, _D, _D, _P]),

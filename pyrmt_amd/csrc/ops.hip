@@ -26,6 +26,7 @@ int ensure_scratch(rmt_ctx *ctx, size_t bytes) {
     return RMT_OK;
 }
 int ensure_bytes(rmt_ctx *ctx, size_t bytes) {
+    ++ctx->bytes_gen;   // (rmt_sim's carried geometry lives there: any other user ends it)
     if (ctx->bytes_len >= bytes) return RMT_OK;
     if (ctx->bytes) RMT_HIP(hipFree(ctx->bytes));
     ctx->bytes = nullptr; ctx->bytes_len = 0;

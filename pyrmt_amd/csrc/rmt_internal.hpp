@@ -75,6 +75,7 @@ struct rmt_ctx {
     int rsum_len = 0;
     unsigned char *bytes = nullptr;
     size_t bytes_len = 0;
+    unsigned long bytes_gen = 0;   // bumped by every ensure_bytes (a user of the workspace)
     rmt::DctPlan *dct = nullptr;
     rmt::Dct2Plan *dct2 = nullptr;
     rmt::PerPlan *per = nullptr;

@@ -72,6 +72,11 @@ struct rmt_sim {
     unsigned long long *m2acc = nullptr;   // k_dt_part's atomic max + block counter (zeroed)
     bool prof = false;
     int sync_every = rmt::RING_N;   // rmt_sim_set_sync_every
+    // rmt_sim_set_carry: a call's last step also prepares the next step's geometry (and its
+    // projection's max |u|^2 partials stay valid), and the next call starts from them unless
+    // rmt_sim_invalidate or another user of the context's workspace came in between
+    bool carry_on = false, carry_valid = false, m2_valid = false;
+    unsigned long carry_gen = 0;
     hipEvent_t pev[7] = {};
     double ms[8] = {};
     long calls[8] = {};
@@ -759,9 +764,16 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         }
         return RMT_OK;
     };
-    S->bits_ready = false;   // the caller may have changed the map between calls
-    // ... or the prep planes: the first prep of a call writes every segment
-    if (S->pconst) RMT_HIP(hipMemsetAsync(S->pconst, 0, (size_t)ny * (nx / 64), st));
+    // a carried state (rmt_sim_set_carry): this call's first step uses the geometry, known
+    // plane, prep planes and max |u|^2 partials the previous call's last step left
+    const bool carry = S->carry_on && S->carry_valid && S->carry_gen == ctx->bytes_gen;
+    const bool m2_ok = carry && S->m2_valid;
+    S->carry_valid = false;
+    if (!carry) {
+        S->bits_ready = false;   // the caller may have changed the map between calls
+        // ... or the prep planes: the first prep of a call writes every segment
+        if (S->pconst) RMT_HIP(hipMemsetAsync(S->pconst, 0, (size_t)ny * (nx / 64), st));
+    }
     // the next step's rim words and extrapolation geometry, prepared on the second stream
     // beside this step's projection (they depend on the known plane alone)
     static const bool geo_env = !(getenv("RMT_EARLY_GEOMETRY") && !atoi(getenv("RMT_EARLY_GEOMETRY")));
@@ -771,14 +783,15 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     bool early_t = false;
     // k_phi_rebuild writes the momentum's pure-fluid flags (RMT_FUSED_FLUID, default on)
     static const bool fluid_env = !(getenv("RMT_FUSED_FLUID") && !atoi(getenv("RMT_FUSED_FLUID")));
-    bool geo_ready = false;
+    bool geo_ready = carry;
+    bool m2_last = false;   // the last step's projection wrote the max |u|^2 partials
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end)) break;
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[0], st));
         // 1. dt (compute_timestep + the drivers' clip to t_end); NaN-propagating max so it
         // also bounds the velocities for the SL block skip
         double hv[2] = {0.0, 0.0}, dt = NAN;
-        if (async && it > 0) {
+        if (async && (it > 0 || m2_ok)) {
             k_dt_part<<<DTP_BLOCKS, 256, 0, st>>>(S->m2part, S->m2n, S->dt_const, P.cfl, P.dx,
                                                   sc, S->m2acc, ring_e ? ring_flag : nullptr,
                                                   ring_e);
@@ -979,7 +992,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // phi on the tiles and the momentum's prep there in one kernel (RMT_FUSED_FIXPREP,
             // default on where nx % 64 == 0), which also copies the extrapolation's status
             // the next step's geometry below starts once the known plane is final (e_kb)
-            const bool geo_next = async && geo_env && nb && P.layers > 0 && it + 1 < nsteps;
+            const bool geo_next = async && geo_env && nb && P.layers > 0 &&
+                                  (it + 1 < nsteps || S->carry_on);
             if (fixprep) {
                 RMT_TRY(fixup_phi_prep(ctx, &M, W, S->X1n, S->X2n, P.x0, P.y0, P.R, S->X1, S->X2,
                                        S->phi, nb, S->sxx, S->sxy, S->syy, S->J, S->tiles,
@@ -1071,6 +1085,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_TRY(rmt_pressure_projection(ctx, S->us, S->vs, P.dx, P.dy, dt, P.rho_f,
                                             P.bc_kind, P.lid, S->p, S->u, S->v, S->p));
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[5], st));
+        m2_last = async;
         // 7. diagnostics (running them beside the projection on the second stream measured
         // no gain: both are HBM-bound)
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
@@ -1121,7 +1136,27 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
         RMT_TRY(sim_record(S, dv, hv[0], dt, fl));
     }
-    return flush();
+    // the geometry prepared for a next call is joined here: nothing of this call stays in
+    // flight on the second stream (the caller may reuse the context's workspace)
+    if (geo_ready) RMT_HIP(hipStreamWaitEvent(st, S->e_geo, 0));
+    RMT_TRY(flush());
+    S->carry_valid = S->carry_on && geo_ready;
+    S->m2_valid = m2_last;
+    S->carry_gen = ctx->bytes_gen;
+    return RMT_OK;
+}
+
+int rmt_sim_set_carry(rmt_sim *S, int on) {
+    RMT_CHECK(S, RMT_EINVAL, "null sim");
+    S->carry_on = on != 0;
+    S->carry_valid = false;
+    return RMT_OK;
+}
+
+int rmt_sim_invalidate(rmt_sim *S) {
+    RMT_CHECK(S, RMT_EINVAL, "null sim");
+    S->carry_valid = false;
+    return RMT_OK;
 }
 
 int rmt_sim_set_sync_every(rmt_sim *S, int k) {

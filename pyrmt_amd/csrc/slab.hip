@@ -358,6 +358,7 @@ struct SlabWs {
     unsigned char *b;
     size_t l;
     explicit SlabWs(rmt_slab *s) : S(s), b(s->ctx->bytes), l(s->ctx->bytes_len) {
+        ++S->ctx->bytes_gen;
         if (S->ws) { S->ctx->bytes = S->ws; S->ctx->bytes_len = S->ws_len; }
     }
     ~SlabWs() {

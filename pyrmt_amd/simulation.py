@@ -55,6 +55,9 @@ class Simulation:
                 "rmt_sim_create")
         self.h = h
         self._views = {}
+        # carry the last step's prepared state into the next step() call (rmt_sim_set_carry);
+        # every write path below (field views, set_field) invalidates it
+        L.check(L.lib().rmt_sim_set_carry(self.h, 1), "rmt_sim_set_carry")
 
     def __del__(self):
         try:
@@ -62,8 +65,7 @@ class Simulation:
         except Exception:
             pass
 
-    def field(self, name):
-        """A torch CUDA view (no copy) of a state field: u/a, v/b, p, X1, X2, phi, J."""
+    def _view(self, name):
         fid = FIELDS[name]
         if fid not in self._views:
             ptr = ctypes.c_void_p()
@@ -71,13 +73,25 @@ class Simulation:
             self._views[fid] = _wrap_device(self.torch, ptr.value, (self.N, self.N))
         return self._views[fid]
 
+    def field(self, name):
+        """A torch CUDA view (no copy) of a state field: u/a, v/b, p, X1, X2, phi, J.  The
+        caller may write through it before the next step(); a view kept across step() calls
+        and written later needs invalidate() first."""
+        self.invalidate()
+        return self._view(name)
+
+    def invalidate(self):
+        """The state was changed from outside: the next step() recomputes everything it
+        derives from it (rmt_sim_invalidate)."""
+        L.check(L.lib().rmt_sim_invalidate(self.h), "rmt_sim_invalidate")
+
     def set_field(self, name, value):
         t = self.field(name)
         t.copy_(self.torch.as_tensor(np.ascontiguousarray(value, dtype=np.float64)).to(t.device))
 
     def get(self, name):
         self.torch.cuda.synchronize()
-        return self.field(name).cpu().numpy()
+        return self._view(name).cpu().numpy()
 
     def step(self, nsteps=1, t_end=math.inf):
         self.ctx.bind()

@@ -33,3 +33,49 @@ def test_async_step_reports_nonfinite_velocity(gpu):
     with pytest.raises(FloatingPointError):
         s.step(4)
     assert len(s.diagnostics()["t"]) == 3    # the failing step is not recorded
+
+
+def _carry_off(sim):
+    from pyrmt_amd import _lib as L
+    L.check(L.lib().rmt_sim_set_carry(sim.h, 0), "rmt_sim_set_carry")
+
+
+def _same(a, b):
+    da, db = a.diagnostics(), b.diagnostics()
+    for k in da:
+        np.testing.assert_array_equal(da[k], db[k], err_msg=k)
+    for f in ("u", "v", "p", "X1", "X2", "phi", "J"):
+        np.testing.assert_array_equal(a.get(f), b.get(f), err_msg=f)
+
+
+def test_carry_across_calls_bitwise(gpu):
+    """rmt_sim_set_carry (the Python Simulation's default): a call's first step starts from
+    the geometry, known plane and max |u|^2 partials the previous call's last step left --
+    four calls of 3 steps == the same four calls without the carry == one call of 12."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    a, b, c = (soft_disc_in_lid_driven(256) for _ in range(3))
+    _carry_off(b)
+    for s in (a, b):           # one sim after the other: they share the size's context, and
+        for _ in range(4):     # another sim's step on it would end the carry (by design)
+            s.step(3)
+    c.step(12)
+    _same(a, b)
+    _same(a, c)
+
+
+def test_carry_invalidated_by_writes_and_workspace_reuse(gpu):
+    """A field written between calls (set_field: rmt_sim_invalidate) and another user of the
+    context's workspace between calls (an extrapolation on the same-size context) both end
+    the carry: results equal the no-carry run's."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    from pyrmt_amd import functions as F
+    a, b = soft_disc_in_lid_driven(256), soft_disc_in_lid_driven(256)
+    _carry_off(b)
+    for s in (a, b):
+        s.step(4)
+        s.set_field("u", 0.5 * s.get("u"))
+        s.step(4)
+        X1, X2, phi = s.get("X1"), s.get("X2"), s.get("phi")
+        F.extrapolate_reference_map(X1, X2, phi, 1.0 / 255, 1.0 / 255, 3)
+        s.step(4)
+    _same(a, b)
