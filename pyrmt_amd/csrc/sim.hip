@@ -716,12 +716,18 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     // not crowd the next step's rim advection and record values either.
     bool tail = false, pending = false;
     double *pend_e = nullptr;
-    auto emit_tail = [&]() -> int {
+    // after_sl: the second stream already waits for this step's e_sl, recorded on the main
+    // stream after the tail's projection -- no event of its own (a record right after the
+    // velocity correction cost the critical path ~5 us); else one recorded now
+    auto emit_tail = [&](bool after_sl) -> int {
         if (!pending) return RMT_OK;
         pending = false;
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
                    P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s, P.mu_s, P.kappa, 0, ny};
-        RMT_HIP(hipStreamWaitEvent(S->st2, S->e_proj, 0));
+        if (!after_sl) {
+            RMT_HIP(hipEventRecord(S->e_proj, st));
+            RMT_HIP(hipStreamWaitEvent(S->st2, S->e_proj, 0));
+        }
         ctx->stream = S->st2;
         const int ts = sub_mean_rows(ctx, S->p, ny, nx);
         ctx->stream = st;
@@ -734,7 +740,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         return RMT_OK;
     };
     auto join = [&]() -> int {
-        RMT_TRY(emit_tail());
+        RMT_TRY(emit_tail(false));
         if (tail) RMT_HIP(hipStreamWaitEvent(st, S->e_tail, 0));
         tail = false;
         return RMT_OK;
@@ -920,7 +926,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
                 if (fixprep && ctx->ex_chain && !ctx->ex_par)
                     RMT_TRY(extrap_sweep(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->st2));
-                RMT_TRY(emit_tail());   // the previous step's tail, beside the chain
+                // the previous step's tail, beside the chain (e_sl, recorded by this step's
+                // extrapolation when it has layers, follows that step's projection)
+                RMT_TRY(emit_tail(P.layers > 0));
                 // the fix-up tiles and the rows they reach depend on the known plane only
                 ctx->stream = S->st2;
                 const int fs = extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount);
@@ -1071,12 +1079,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             if (!mjoin) RMT_HIP(hipStreamWaitEvent(st, S->e_rows, 0));
             RMT_TRY(projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
                                     S->rowmark, S->tiles, S->tcount, S->max_tiles));
-            // on the side-tail path e_proj completes with the velocity correction
             RMT_TRY(projection_finish(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, P.bc_kind,
                                       P.lid, S->p, S->u, S->v, S->p,
                                       async ? S->m2part : nullptr, !(async && side_tail),
-                                      early_t ? S->rowmark : nullptr,
-                                      async && side_tail ? S->e_proj : nullptr));
+                                      early_t ? S->rowmark : nullptr));
             early_t = false;
         } else if (async)
             RMT_TRY(projection_dev(ctx, S->us, S->vs, P.dx, P.dy, dtp, P.rho_f, P.bc_kind, P.lid,
@@ -1095,7 +1101,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // step's chain reads p or writes what they read (that stream's next work -- the
             // speculative phi, momentum -- is queued behind them)
             double *e = S->ring + (size_t)slot * RING_VALS;
-            pend_e = e;   // (e_proj: with the velocity correction, projection_finish)
+            pend_e = e;
             pending = true;
             ring_e = e;
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
