@@ -718,46 +718,64 @@ __global__ void __launch_bounds__(1024) k_ex_runs(ExWs ws, int runs) {
 // < CH_R/2 back), or -(global slot + 1) for a source in the other part (marked for the HBM
 // hand-off); header word 23 <- (ordinal, record) of the next accepted fit of the same chain
 // wave of the part
+// One wave per fit, lanes over its dynamic sources (the per-source lookups are independent
+// dependent-load chains: a thread per fit walked them serially, ~90 us at N=4096).
 __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
     if (ws.ctl[EXC_FALLBACK]) return;
-    const int id = blockIdx.x * 256 + threadIdx.x, total = ws.ctl[EXC_BASE + ML];
-    if (id >= total) return;
-    const long long r = ws.recoff[id];
-    if (r < 0) return;
-    double *rec = (double *)(ws.arena + ((r & 0xffffffffLL) << 6));
-    // meta bit 63 (set here by the readers in other parts): publish to HBM as well
-    const long long meta = __double_as_longlong(rec[1]);
-    const int nd = (int)((meta >> 32) & 0x7fffffff);
-    int2 *dyn = (int2 *)(rec + CH_HDR);   // entry d at int2 index 2d: (k, src)
-    const int x = ws.chain_of[id], p = ws.part[x], l = ws.loc[x];
-    const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
-    int2 crit = make_int2(-1, -1);   // the latest source in chain order (k_ex_chain fast fold)
-    int xmax = -1;
-    for (int d = 0; d < nd; ++d) {
-        const int xs = ws.chain_of[dyn[4 * d].y];
-        if (ws.crit && xs > xmax) {   // (variant 35 only: ws.crit is null otherwise)
-            xmax = xs;
-            crit = make_int2(ws.part[xs] == p ? ws.loc[xs] : -1, (int)ws.tcell[dyn[4 * d].y]);
+    const int lane = threadIdx.x & 63, total = ws.ctl[EXC_BASE + ML];
+    for (int id = blockIdx.x * 4 + (int)(threadIdx.x >> 6); id < total; id += gridDim.x * 4) {
+        const long long r = ws.recoff[id];
+        if (r < 0) continue;
+        double *rec = (double *)(ws.arena + ((r & 0xffffffffLL) << 6));
+        // meta bit 63 (set here by the readers in other parts): publish to HBM as well
+        const long long meta = __double_as_longlong(rec[1]);
+        const int nd = (int)((meta >> 32) & 0x7fffffff);
+        int2 *dyn = (int2 *)(rec + CH_HDR);   // entry d at int2 index 2d: (k, src)
+        const int x = ws.chain_of[id], p = ws.part[x], l = ws.loc[x];
+        const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
+        int2 crit = make_int2(-1, -1);   // the latest source in chain order (fast fold)
+        int xmax = -1;
+        for (int d = lane; d < nd; d += 64) {
+            const int src = dyn[4 * d].y;
+            const int xs = ws.chain_of[src];
+            if (ws.crit && xs > xmax) {   // (variant 35 only: ws.crit is null otherwise)
+                xmax = xs;
+                crit = make_int2(ws.part[xs] == p ? ws.loc[xs] : -1, (int)ws.tcell[src]);
+            }
+            if (xs >= x) { ws.ctl[EXC_ABORT] = 1; atomicExch(ws.status + 1, 1); }   // a bug
+            if (ws.part[xs] == p) {
+                const int ls = ws.loc[xs];
+                dyn[4 * d].y = ls;
+                if (l - ls >= CH_R / 2) ws.ctl[EXC_FALLBACK] = 1;
+            } else {
+                const int g = ch_base(ws.ctl, ws.part[xs]) + ws.loc[xs];
+                dyn[4 * d].y = -(g + 1);
+                const long long rs = ws.rec_by_chain[xs];
+                double *srec = (double *)(ws.arena + ((rs & 0xffffffffLL) << 6));
+                atomicOr((unsigned long long *)&srec[1], 1ull << 63);
+            }
         }
-        if (xs >= x) { ws.ctl[EXC_ABORT] = 1; atomicExch(ws.status + 1, 1); }   // a bug
-        if (ws.part[xs] == p) {
-            const int ls = ws.loc[xs];
-            dyn[4 * d].y = ls;
-            if (l - ls >= CH_R / 2) ws.ctl[EXC_FALLBACK] = 1;
-        } else {
-            const int g = ch_base(ws.ctl, ws.part[xs]) + ws.loc[xs];
-            dyn[4 * d].y = -(g + 1);
-            const long long rs = ws.rec_by_chain[xs];
-            double *srec = (double *)(ws.arena + ((rs & 0xffffffffLL) << 6));
-            atomicOr((unsigned long long *)&srec[1], 1ull << 63);
+        if (ws.crit) {
+            // the source with the largest chain index (sources are distinct fits)
+            int m = xmax;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+            const unsigned long long who = __ballot(m >= 0 && xmax == m);
+            int2 c = make_int2(-1, -1);
+            if (who) {
+                const int src_l = __ffsll((long long)who) - 1;
+                c = make_int2(__shfl(crit.x, src_l), __shfl(crit.y, src_l));
+            }
+            if (lane == 0) ws.crit[base + l] = c;
+        }
+        if (lane == 0) {
+            int ln = ws.wnext[base + l];
+            while (ln < np && ws.rec_by_chain[ws.inv[base + ln]] < 0) ln = ws.wnext[base + ln];
+            const long long rn = ln < np ? ws.rec_by_chain[ws.inv[base + ln]] : 0;   // (size64 << 32) | off64
+            const unsigned r32 = (unsigned)(rn & 0xffffffffLL) | ((unsigned)(rn >> 32) << 25);
+            rec[23] = __longlong_as_double(((long long)ln << 32) | r32);
         }
     }
-    if (ws.crit) ws.crit[base + l] = crit;
-    int ln = ws.wnext[base + l];
-    while (ln < np && ws.rec_by_chain[ws.inv[base + ln]] < 0) ln = ws.wnext[base + ln];
-    const long long rn = ln < np ? ws.rec_by_chain[ws.inv[base + ln]] : 0;   // (size64 << 32) | off64
-    const unsigned r32 = (unsigned)(rn & 0xffffffffLL) | ((unsigned)(rn >> 32) << 25);
-    rec[23] = __longlong_as_double(((long long)ln << 32) | r32);
 }
 
 // ------------------------------------------------------------------ 3. the chain ---
@@ -1286,7 +1304,7 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     // N=4096 -- a fit's own set-up and prefix fold no longer overlap its predecessor's wait)
     static const int runs = getenv("RMT_CH_RUNS") ? atoi(getenv("RMT_CH_RUNS")) != 0 : 0;
     k_ex_runs<<<nparts, 1024, 0, st>>>(ws, runs);
-    k_ex_relink<<<idb, 256, 0, st>>>(ws, ML);
+    k_ex_relink<<<std::min<unsigned>(grid1d(ws.maxt, 4), 2048), 256, 0, st>>>(ws, ML);
     RMT_LAUNCHED();
     return RMT_OK;
 }
