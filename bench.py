@@ -2,6 +2,14 @@
 physics) on MI355X: cell-updates/s at N=4096 (BASELINE.json metric).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--no-cpu-baseline]
+                  [--config 4|2|3|5]
+
+--config names a BASELINE.json configuration (default 4, the one the metric is quoted on):
+  2  soft_disc_in_lid_driven N=256 semilagrangian        (208 B/cell)
+  3  disc_in_taylor_green N=1024 WENO5 + SSP-RK3          (224 B/cell)
+  4  soft_disc_in_lid_driven N=4096 semilagrangian       (208 B/cell)
+  5  mac_multi_disc_lid N=8192, 3 discs (seed 3)          (280 B/cell)
+Configs 2/3/5 are single-GPU lines for the per-config roofline (the driver's line is config 4).
 
 A step is one loop body of benchmarks/soft_disc_in_lid_driven.py:206-235 (timestep,
 reference-map advection, narrow-band extrapolation, level-set rebuild, RK4 momentum,
@@ -27,6 +35,13 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # (reads u, v, p, X1, X2; writes u*, v*) = 7 planes x 8 B per cell for one RK4 pass.
 RK4_ALG_BYTES_PER_CELL = 7 * 8
 STEP_ALG_BYTES_PER_CELL = 208  # the whole step
+# per BASELINE config: (grid, algorithmic bytes per cell-update of the whole step, workload)
+CONFIGS = {
+    2: (256, 208, "soft_disc_in_lid_driven N=256 semilagrangian (config 2)"),
+    3: (1024, 224, "disc_in_taylor_green N=1024 weno5 + SSP-RK3 (config 3)"),
+    4: (4096, 208, "soft_disc_in_lid_driven N=4096 semilagrangian (configs 2/4 loop body)"),
+    5: (8192, 280, "mac_multi_disc_lid N=8192, 3 discs, seed 3 (config 5)"),
+}
 # HBM bytes per launch and per step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
 # bench (scripts/gpu.sh pmc -> tools/pmc_traffic.py; FETCH x2 per the gfx950 calibration)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_n4096.json")
@@ -116,8 +131,77 @@ def cpu_baseline(n, steps):
                       f"{out['all_cores']['s_per_step']:.1f} s/step) on {_cpu_model()}"}
 
 
+def cpu_baseline_cfg(cfg, n):
+    """Configs 3 and 5: the oracle on a bounded sample of the same loop (config 5's N=8192 MAC
+    step takes ~90 s in the oracle: the sample is one step at N=2048, per cell-update)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    cores = min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 16)
+    O.set_threads(cores)
+    O.set_all_cores(True)
+    if cfg == 3:
+        sim, m, steps, rec = O.SoftDisc(n, "tg", "weno5"), n, 2, {"energies": True}
+    else:
+        from oracle import mac_oracle as M
+        m = 2048
+        sim, steps, rec = M.MacMultiDisc(m), 1, {}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sim.step(**rec)
+    dt = time.perf_counter() - t0
+    O.set_all_cores(False)
+    return {"value": m * m * steps / dt, "unit": "cell-updates/s", "cores": cores, "kind": "port",
+            "cpu": _cpu_model(),
+            "sample": f"{steps} step(s) of the config-{cfg} loop at N={m} (oracle, all-cores "
+                      f"OpenMP, {dt / steps:.1f} s/step) on {_cpu_model()}"}
+
+
+def main_config(args, cfg):
+    """One single-GPU line for BASELINE config 2, 3 or 5 (step roofline on the config's own
+    algorithmic bytes; the phase / kernel breakdown comes from rocprofv3 of this command)."""
+    import sys
+    import torch
+    sys.path.insert(0, ROOT)
+    N, alg, work = CONFIGS[cfg]
+    if cfg == 5:
+        from pyrmt_amd.mac import MacMultiDisc
+        sim = MacMultiDisc(N, n_discs=3, seed=3)
+    elif cfg == 3:
+        from pyrmt_amd.simulation import disc_in_taylor_green
+        sim = disc_in_taylor_green(N, "weno5")
+    else:
+        from pyrmt_amd.simulation import soft_disc_in_lid_driven
+        sim = soft_disc_in_lid_driven(N)
+    sim.step(args.warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sim.step(args.steps)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    d = sim.diagnostics()
+    assert np.all(np.isfinite(np.asarray(d["cx"]))), "non-finite state"
+    value = N * N * args.steps / el
+    gbs = value * alg / 1e9
+    out = {"metric": "cell-updates/s (full RMT step) at N=4096; achieved HBM GB/s vs peak",
+           "value": value, "unit": "cell-updates/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": "synthetic (the driver's own initial condition)",
+           "config": {"workload": work, "grid": N, "baseline_config": cfg,
+                      "parallelism": "single-gpu"},
+           "roofline": {"bound": "hbm", "kernel": "whole step (every kernel of the loop body)",
+                        "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                        "alg_bytes_per_cell": alg}}
+    if not args.no_cpu_baseline and cfg in (3, 5):
+        out["cpu_baseline"] = cpu_baseline_cfg(cfg, N)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
@@ -125,6 +209,10 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.config != 4:
+        if args.gpus != 1 or int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            raise SystemExit("--config 2/3/5: single-GPU lines (the multi-GPU line is config 4)")
+        return main_config(args, args.config)
 
     ws, rank, local = _dist()
     import torch

@@ -218,6 +218,7 @@ extern "C" {
 
 int rmt_divergence_2d_interior(rmt_ctx *ctx, const double *u, const double *v, double dx,
                                double dy, int pad, double *div) {
+    RMT_CHECK(ctx && u && v && div, RMT_EINVAL, "null argument");
     RMT_CHECK(pad >= 1, RMT_EINVAL, "divergence_2d_interior: pad >= 1");
     const long n = (long)ctx->ny * ctx->nx;
     k_div_interior<<<grid1d(n, 256), 256, 0, ctx->stream>>>(u, v, ctx->ny, ctx->nx,

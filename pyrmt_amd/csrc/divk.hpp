@@ -11,7 +11,11 @@
 //     q1 = RN(q0 - t*yh)              (fma)
 // Claim: q1 = RN(x/d) for every x with 2^-900 <= |x| < 2^1000, and for x = +-0 (|q1| = 0;
 // the sign is copied from x, as x/d has it for d > 0), provided d > 0 is normal and its
-// significand D = d / 2^e_d satisfies D < 2 - 2^-50 (checked on the host; D = 1 is exact).
+// significand D = d / 2^e_d satisfies D < 2 - 2^-50 (checked on the host; D = 1 is exact)
+// and its exponent e_d lies in [-20, 60] (DIVK_ED_MIN .. DIVK_ED_MAX): then for every
+// certified x the quotient x/d stays normal and finite (|x/d| < 2^1000 / 2^-20 = 2^1020 and
+// > 2^-900 / 2^61 = 2^-961) and x*yl (~ 2^-54 x/d >= 2^-1015) does not underflow, which the
+// sketch below assumes.  Other divisors take IEEE division (rspan = 0).
 // Proof sketch (z = x/d, z in [2^f, 2^(f+1)), u = ulp(z) = 2^(f-52)):
 //   * |x*(yh+yl) - z| <= 2^-106 z and |RN(x*yl) - x*yl| <= 2^-106 z, so q0 = RN(z(1+eta))
 //     with |eta| <= 2^-105(1+2^-50): |q0 - z| <= u/2 + 2^-52 u < u, so q0 is a faithful
@@ -45,6 +49,7 @@ struct DivK {
 // 2^-900 and 2^1000 as high words of |x| (exponent field in bits 20..30)
 constexpr unsigned DIVK_HI_LO = (unsigned)(1023 - 900) << 20;
 constexpr unsigned DIVK_HI_HI = (unsigned)(1023 + 1000) << 20;
+constexpr int DIVK_ED_MIN = -20, DIVK_ED_MAX = 60;   // certified divisor exponents
 
 __host__ __device__ inline DivK divk_make(double d) {
     DivK k{d, 0.0, 0.0, 0u};
@@ -52,6 +57,7 @@ __host__ __device__ inline DivK divk_make(double d) {
     int e;
     const double D = 2.0 * std::frexp(d, &e);            // significand in [1, 2)
     if (!(D < 2.0 - 0x1p-50)) return k;
+    if (e - 1 < DIVK_ED_MIN || e - 1 > DIVK_ED_MAX) return k;   // quotients may leave the normal range
     k.yh = 1.0 / d;
     const double r = std::fma(-d, k.yh, 1.0);             // 1 - d*yh, exact
     k.yl = r / d;                                         // RN(r / d) = RN(1/d - yh)

@@ -229,9 +229,13 @@ __global__ void k_ex_none_fin(int *ctl) {
 __global__ void __launch_bounds__(256) k_fix_tiles(const u64 *__restrict__ kbits, int ny, int nx,
                                                    int W, int reach, int margin, int tiles_x,
                                                    int ntiles, int *__restrict__ list,
-                                                   int *__restrict__ count) {
+                                                   int *__restrict__ count, int all) {
     const int lane = threadIdx.x & 63, t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= ntiles) return;
+    if (all) {   // (RMT_FIX_ALL: a test of the tile-list kernels on every tile kind)
+        if (lane == 0) list[atomicAdd(count, 1)] = t;
+        return;
+    }
     const int i0 = (t % tiles_x) * MOM_TX, j0 = (t / tiles_x) * MOM_TY, w0 = i0 >> 6;
     auto cols = [&](int ww, int a, int b) -> u64 {   // bits of word ww for columns [a, b)
         if (ww < 0 || ww >= W) return 0;
@@ -621,6 +625,11 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A, long long *gpr
 }
 
 static int g_ex_mode = 0;   // rmt_extrap_set_mode
+// bumped by every change of the extrapolation's configuration (rmt_extrap_set_mode,
+// rmt_extrap_set_parallel): state an rmt_sim carries across calls was prepared for the old one
+static unsigned long g_ex_cfg_gen = 0;
+unsigned long extrap_config_gen() { return g_ex_cfg_gen; }
+void extrap_config_changed() { ++g_ex_cfg_gen; }
 
 // byte workspace: both paths' bit planes, the chain path's tables and its record arena
 ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bool px) {
@@ -892,6 +901,7 @@ extern "C" int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, con
 
 extern "C" int rmt_extrap_set_mode(int mode) {
     RMT_CHECK(mode >= 0 && mode <= 3, RMT_EINVAL, "extrapolation mode must be 0 .. 3");
+    if (rmt::g_ex_mode != mode) rmt::extrap_config_changed();
     rmt::g_ex_mode = mode;
     return RMT_OK;
 }
@@ -902,9 +912,14 @@ int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *c
     const int tiles_x = (nx + MOM_TX - 1) / MOM_TX, ntiles = tiles_x * ((ny + MOM_TY - 1) / MOM_TY);
     RMT_CHECK(margin + max_layers <= 24 && margin >= 0, RMT_EINVAL, "fix-tile reach");
     const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
+    // RMT_FIX_ALL=1 (tests only): list every tile.  The fix-up then re-runs phi, the prep and
+    // the four stages on the whole grid from the same inputs: bit-identical to the default if
+    // the tile-list kernels are right on interior, edge and domain-boundary tiles alike
+    static const int all = getenv("RMT_FIX_ALL") ? atoi(getenv("RMT_FIX_ALL")) != 0 : 0;
     RMT_HIP(hipMemsetAsync(count, 0, sizeof(int), ctx->stream));
     k_fix_tiles<<<grid1d(ntiles, 4), 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, margin + max_layers,
-                                                             margin, tiles_x, ntiles, list, count);
+                                                             margin, tiles_x, ntiles, list, count,
+                                                             all);
     RMT_LAUNCHED();
     return RMT_OK;
 }

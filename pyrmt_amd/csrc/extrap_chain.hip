@@ -38,6 +38,7 @@
 namespace rmt {
 
 constexpr int EXS = 82;   // term-buffer row stride of the geometry fold (16-B aligned rows)
+constexpr long long CH_CRIT = 1LL << 16;   // dyn entry term field: the fit's latest local source
 
 __device__ __forceinline__ u64 ld_l2(const u64 *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -734,10 +735,11 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
         const int x = ws.chain_of[id], p = ws.part[x], l = ws.loc[x];
         const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
         int2 crit = make_int2(-1, -1);   // the latest source in chain order (fast fold)
-        int xmax = -1;
+        int xmax = -1, lmax = -1, dmax = -1;   // the latest local source: its ordinal, entry
         for (int d = lane; d < nd; d += 64) {
             const int src = dyn[4 * d].y;
             const int xs = ws.chain_of[src];
+            dyn[4 * d].x &= 0xffff;
             if (ws.crit && xs > xmax) {   // (variant 35 only: ws.crit is null otherwise)
                 xmax = xs;
                 crit = make_int2(ws.part[xs] == p ? ws.loc[xs] : -1, (int)ws.tcell[src]);
@@ -746,6 +748,7 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
             if (ws.part[xs] == p) {
                 const int ls = ws.loc[xs];
                 dyn[4 * d].y = ls;
+                if (ls > lmax) { lmax = ls; dmax = d; }
                 if (l - ls >= CH_R / 2) ws.ctl[EXC_FALLBACK] = 1;
             } else {
                 const int g = ch_base(ws.ctl, ws.part[xs]) + ws.loc[xs];
@@ -754,6 +757,13 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
                 double *srec = (double *)(ws.arena + ((rs & 0xffffffffLL) << 6));
                 atomicOr((unsigned long long *)&srec[1], 1ull << 63);
             }
+        }
+        {
+            // mark the latest local source (ordinals of distinct fits differ)
+            int m = lmax;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+            if (m >= 0 && lmax == m) dyn[4 * dmax].x |= (int)CH_CRIT;
         }
         if (ws.crit) {
             // the source with the largest chain index (sources are distinct fits)
@@ -1078,7 +1088,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     if (has) {
         const double2 q0 = ((const double2 *)dyn)[2 * lane], q1 = ((const double2 *)dyn)[2 * lane + 1];
         const long long kk = __double_as_longlong(q0.x);
-        e = make_int2((int)(kk & 0xffffffff), (int)(kk >> 32));
+        e = make_int2((int)(kk & 0xffff), (int)(kk >> 32));
         cf[0] = q0.y; cf[1] = q1.x; cf[2] = q1.y;
     }
     bool done = !has;   // product written
@@ -1205,6 +1215,241 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     return true;
 }
 
+// fold row[a .. b) into acc in order; reads run 8 terms ahead of the adds (LDS reads past b
+// read unused words of the wave's buffer and are never added).  Fully unrolled over the
+// longest row: straight-line code keeps the compiler's LDS wait counts exact (a loop's back
+// edge makes it wait for every read in flight once per trip)
+#define CH_S(acc, row, n, r, k)                                                \
+    if ((k) >= (n)) break;                                                     \
+    acc += r[(k) & 7];                                                         \
+    r[(k) & 7] = (row)[(k) + 8];                                               \
+    __builtin_amdgcn_sched_barrier(0);
+#define CH_S8(acc, row, n, r, b)                                                       \
+    CH_S(acc, row, n, r, b) CH_S(acc, row, n, r, b + 1) CH_S(acc, row, n, r, b + 2)    \
+    CH_S(acc, row, n, r, b + 3) CH_S(acc, row, n, r, b + 4) CH_S(acc, row, n, r, b + 5) \
+    CH_S(acc, row, n, r, b + 6) CH_S(acc, row, n, r, b + 7)
+#define CH_TAIL(acc, row, n, r)                                                        \
+    do {                                                                               \
+        CH_S8(acc, row, n, r, 0) CH_S8(acc, row, n, r, 8) CH_S8(acc, row, n, r, 16)    \
+        CH_S8(acc, row, n, r, 24) CH_S8(acc, row, n, r, 32) CH_S8(acc, row, n, r, 40)  \
+        CH_S8(acc, row, n, r, 48) CH_S8(acc, row, n, r, 56) CH_S8(acc, row, n, r, 64)  \
+        CH_S8(acc, row, n, r, 72) CH_S8(acc, row, n, r, 80)                            \
+    } while (0)
+static_assert(CH_TVS <= 88, "CH_TAIL unrolls 88 terms");
+__device__ __forceinline__ double ch_fold_rng(double acc, const double *row, int a, int b) {
+    if (a >= b) return acc;
+    row += a;
+    double r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = row[k];
+    CH_TAIL(acc, row, b - a, r);
+    return acc;
+}
+
+// The lean fit (VAR bit 6).  The fit's latest local source in chain order (marked CH_CRIT by
+// k_ex_relink) is the one its predecessor link hands over; everything else is done before it
+// arrives: the other sources' products (written to the staged record's term rows as they
+// arrive), the fold of the terms before the critical one's window position kc, and the
+// first reads of the terms after it.  The critical value is polled with one broadcast LDS
+// read of its tag and value (issued back to back: a wave's LDS operations are performed in
+// order, and the producer writes the value before the tag), its product is added in
+// registers -- never written to LDS -- and the terms after kc follow: the reference's order,
+// the same operations.
+template <bool PROF, int VAR>
+__device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val, int *tag,
+                                        int *cur, int &wm, double &o_out, long &c_out,
+                                        long long *pr, long long &tl, int *gtag, double *gval,
+                                        int gslot, long long *trace = nullptr, int base = 0) {
+    long long tr_start = 0, tr_ready = 0;
+    int tr_crit = -1;
+    long spins = 0;
+    while (x - CH_R / 2 >= wm) {
+        int m = 0x7fffffff;
+        for (int k = 0; k < CH_W; ++k)
+            m = min(m, __hip_atomic_load(&cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        wm = m;
+        if (x - CH_R / 2 >= wm) {
+            if (++spins > CH_SPIN_LIMIT) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    CH_STAMP(1);
+    if constexpr (PROF) tr_start = __builtin_amdgcn_s_memrealtime();
+    const long long meta = __double_as_longlong(B[1]);
+    const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
+    const int nd = __builtin_amdgcn_readfirstlane((int)((meta >> 32) & 0x7fffffff));
+    const bool pub = __builtin_amdgcn_readfirstlane((int)((unsigned long long)meta >> 63)) != 0;
+    if (npad > CH_TVS || nd > 64 || npad < 0 || nd < 0) return false;   // bug guard
+    const double *dyn = B + CH_HDR;
+    double *tv = B + CH_HDR + 4 * nd;
+    auto U = [&](int k) {
+        const double v = B[k];
+        return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                                __builtin_amdgcn_readfirstlane(__double2loint(v)));
+    };
+    const double x0 = U(2), y0 = U(3), M0 = U(4), M1 = U(5), M2 = U(6), M3 = U(7), M4 = U(8);
+    const double M5 = U(9), M6 = U(10), M7 = U(11), M8 = U(12), C0 = U(13), C1 = U(14);
+    const double C2 = U(15), inv_det = U(16);
+    double acc = 0.0;
+    if (lane < 6) acc = B[17 + lane];
+    const bool has = lane < nd;
+    int2 e = make_int2(0, -1);
+    bool crit = false;
+    double cf[3] = {0.0, 0.0, 0.0};
+    if (has) {
+        const double2 q0 = ((const double2 *)dyn)[2 * lane], q1 = ((const double2 *)dyn)[2 * lane + 1];
+        const long long kk = __double_as_longlong(q0.x);
+        crit = (kk & CH_CRIT) != 0;
+        e = make_int2((int)(kk & 0xffff), (int)(kk >> 32));
+        cf[0] = q0.y; cf[1] = q1.x; cf[2] = q1.y;
+    }
+    const int slot = e.y & (CH_R - 1);
+    // the other part's sources (rare) first, through HBM
+    const bool far = has && e.y < 0;
+    bool done = !has || crit;
+    if (__ballot(far)) {
+        long sp = 0;
+        double2 v = make_double2(0.0, 0.0);
+        for (;;) {
+            if (far && !done && ch_probe(e.y, tag, val, gtag, gval, v)) {
+#pragma unroll
+                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+                done = true;
+            }
+            if (__ballot(far && !done) == 0) break;
+            if (++sp > CH_SPIN_LIMIT) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        // a use of the probe's registers on this path only: no probe load is left pending past
+        // here (else the critical poll below would wait on vmcnt -- the record prefetch too)
+        asm volatile("" ::"v"(v.x), "v"(v.y));
+    }
+    // the critical source: its term position, slot, tag and coefficients (uniform)
+    const u64 cm = __ballot(crit);
+    const int cl = cm ? __builtin_ctzll(cm) : 0;
+    const int kc = cm ? __builtin_amdgcn_readlane(e.x, cl) : npad;
+    const int eyc = __builtin_amdgcn_readlane(e.y, cl);
+    const int slc = eyc & (CH_R - 1);
+    const int m3 = lane % 3;
+    const double cfc = rlf(m3 == 0 ? cf[0] : (m3 == 1 ? cf[1] : cf[2]), cl);
+    // pass 1: products of the other sources already published
+    {
+        const bool ready = !done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
+        asm volatile("" ::: "memory");
+        if (ready) {
+            const double2 v = val[slot];
+#pragma unroll
+            for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+            done = true;
+        }
+    }
+    // fold up to the first missing term (or kc), then wait for the other sources
+    u64 pend = __ballot(!done);
+    int kmiss = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : kc;
+    if (kmiss > kc) kmiss = kc;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane < 6) acc = ch_fold_rng(acc, tv + lane * npad, 0, kmiss);
+    CH_STAMP(3);
+    if (pend) {
+        long sp = 0;
+        __builtin_amdgcn_s_setprio(0);
+        for (;;) {
+            if (!done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
+                asm volatile("" ::: "memory");
+                const double2 v = val[slot];
+#pragma unroll
+                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
+                done = true;
+            }
+            if (__ballot(!done) == 0) break;
+            if (++sp > CH_SPIN_LIMIT) return false;
+            __builtin_amdgcn_s_sleep(0);
+        }
+        __builtin_amdgcn_s_setprio(3);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (lane < 6) acc = ch_fold_rng(acc, tv + lane * npad, kmiss, kc);
+    if (cm) {
+        // first reads of the terms after kc, then the critical value
+        const double *row = tv + lane * npad + kc + 1;
+        const int nt = npad - kc - 1;
+        double r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = row[k];
+        double2 vc;
+        long sp = 0;
+        // the tag and the value read back to back in one LDS round trip (relaxed atomic
+        // loads: a plain value load would be sunk out of the loop)
+        const unsigned long long *vq = (const unsigned long long *)&val[slc];
+        for (;;) {
+            const int tg = __hip_atomic_load(&tag[slc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("" ::: "memory");             // the tag read is issued first
+            __builtin_amdgcn_sched_barrier(0);
+            vc.x = __longlong_as_double((long long)__hip_atomic_load(vq, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_WORKGROUP));
+            vc.y = __longlong_as_double((long long)__hip_atomic_load(vq + 1, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (__builtin_amdgcn_readfirstlane(tg) == eyc) break;
+            if (++sp > CH_SPIN_LIMIT) return false;
+        }
+        if constexpr (PROF) {
+            if (sp) tr_crit = eyc;
+            pr[7] += sp;
+            CH_STAMP(2);
+            tr_ready = __builtin_amdgcn_s_memrealtime();
+        }
+        if (lane < 6) {
+            acc += cfc * (lane < 3 ? vc.x : vc.y);
+            CH_TAIL(acc, row, nt, r);
+        }
+    }
+    if constexpr (PROF) asm volatile("" : "+v"(acc));
+    CH_STAMP(4);
+    double bb1 = dpp_shl(acc, 1), bb2 = dpp_shl(acc, 2);
+    if constexpr (PROF) asm volatile("" : "+v"(bb1), "+v"(bb2));
+    CH_STAMP(8);
+    if (lane == 0 || lane == 3) {
+        const double b0 = acc, b1 = bb1, b2 = bb2;
+        const double xs = (b0 * C0 - M1 * (b1 * M8 - M5 * b2) + M2 * (b1 * M7 - M4 * b2)) * inv_det;
+        const double ys = (M0 * (b1 * M8 - M5 * b2) - b0 * C1 + M2 * (M3 * b2 - b1 * M6)) * inv_det;
+        const double zs = (M0 * (M4 * b2 - b1 * M7) - M1 * (M3 * b2 - b1 * M6) + b0 * C2) * inv_det;
+        double o = xs + ys * x0 + zs * y0;
+        if constexpr (PROF) asm volatile("" : "+v"(o));
+        CH_STAMP(9);
+        ((double *)&val[x & (CH_R - 1)])[lane == 0 ? 0 : 1] = o;
+        if (pub) gval[2 * gslot + (lane == 0 ? 0 : 1)] = o;
+        o_out = o;
+    }
+    asm volatile("" ::: "memory");
+    if (lane == 0)
+        __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (pub) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0)
+            __hip_atomic_store(&gtag[gslot], gslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    CH_STAMP(10);
+    __builtin_amdgcn_s_setprio(1);
+    c_out = __double_as_longlong(B[0]);
+    if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    CH_STAMP(5);
+    if constexpr (PROF) {
+        if (trace && lane == 0) {
+            const long long tp = __builtin_amdgcn_s_memrealtime();
+            long long *t = trace + 6L * gslot;
+            t[0] = tr_start; t[1] = tr_ready ? tr_ready : tr_start; t[2] = tp;
+            t[3] = tr_crit >= 0 ? base + tr_crit : -1;
+            t[4] = threadIdx.x >> 6; t[5] = c_out;
+        }
+    }
+    return true;
+}
+
 template <bool PROF, int VAR>
 __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *gprof) {
     __shared__ double2 val[CH_R];
@@ -1253,8 +1498,14 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         if (x2 <= x) { ok = false; break; }   // bug guard: the wave's sequence must advance
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
-        if (!ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag, C.ws.gval,
-                               base + x, C.trace, base, C.ws.crit, C.ws.pred)) { ok = false; break; }
+        bool fit_ok;
+        if constexpr ((VAR & 64) != 0)
+            fit_ok = ch_fit4<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag,
+                                        C.ws.gval, base + x, C.trace, base);
+        else
+            fit_ok = ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag,
+                                       C.ws.gval, base + x, C.trace, base, C.ws.crit, C.ws.pred);
+        if (!fit_ok) { ok = false; break; }
         x = x2; r = r2;
     }
     if constexpr (PROF)
@@ -1358,6 +1609,10 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
             case 1: k_ex_chain<false, 1><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 2: k_ex_chain<false, 2><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
             case 35: k_ex_chain<false, 35><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
+            case 67:
+                if (nparts == 1) k_ex_chain<false, 83><<<1, CH_W * 64, 0, st>>>(C, nullptr);
+                else k_ex_chain<false, 67><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
+                break;
             default:
                 if (nparts == 1) k_ex_chain<false, 19><<<1, CH_W * 64, 0, st>>>(C, nullptr);
                 else k_ex_chain<false, 3><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
@@ -1381,7 +1636,8 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
             C.trace = dtr;
         }
         RMT_HIP(hipEventRecord(e0, st));
-        k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
+        if (var == 67) k_ex_chain<true, 67><<<nparts, CH_W * 64, 0, st>>>(C, gp);
+        else k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, st));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));

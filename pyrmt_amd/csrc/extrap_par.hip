@@ -615,6 +615,7 @@ int extrap_par_values(rmt_ctx *ctx, const ExWs &ws, double *X1o, double *X2o, in
 }  // namespace rmt
 
 extern "C" int rmt_extrap_set_parallel(int on) {
+    if ((on ? 1 : 0) != (rmt::extrap_par_enabled() ? 1 : 0)) rmt::extrap_config_changed();
     rmt::g_par = on ? 1 : 0;
     return RMT_OK;
 }

@@ -668,6 +668,7 @@ __global__ void k_divk_selftest(const double *__restrict__ x, long n, DivK K,
 }
 int rmt_selftest_divk(rmt_ctx *ctx, const double *x, long n, double d, double *q,
                       double *q_ieee) {
+    RMT_CHECK(ctx && (n == 0 || (x && q && q_ieee)), RMT_EINVAL, "null argument");
     RMT_CHECK(n >= 0, RMT_EINVAL, "rmt_selftest_divk: n < 0");
     if (n) k_divk_selftest<<<grid1d(n, 256), 256, 0, ctx->stream>>>(x, n, divk_make(d), q, q_ieee);
     RMT_LAUNCHED();

@@ -704,6 +704,9 @@ void imex_destroy(rmt_ctx *ctx);   // imex.hip: the context's DST plans
 // variable RMT_EXTRAP_PARALLEL=1): the fits solved as one sparse triangular system by
 // segments instead of the exact raster-order chain -- not bit-exact, see extrap_par.hip
 bool extrap_par_enabled();
+// generation of the extrapolation's configuration (mode, parallel switch): bumped on a change
+unsigned long extrap_config_gen();
+void extrap_config_changed();
 // the exact no-op test of extrapolate() (k_ex_none) on rows [jb, je) of a whole known plane:
 // ctl[EXC_ANY] (extrap.hpp; zeroed by the caller) set iff a first-layer target there fits
 int extrap_none_rows(rmt_ctx *ctx, const unsigned long long *kbits, int ny, int nx, double dx,

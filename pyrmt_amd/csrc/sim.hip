@@ -76,7 +76,7 @@ struct rmt_sim {
     // projection's max |u|^2 partials stay valid), and the next call starts from them unless
     // rmt_sim_invalidate or another user of the context's workspace came in between
     bool carry_on = false, carry_valid = false, m2_valid = false;
-    unsigned long carry_gen = 0;
+    unsigned long carry_gen = 0, carry_cfg = 0;   // workspace / extrapolation config generations
     hipEvent_t pev[7] = {};
     double ms[8] = {};
     long calls[8] = {};
@@ -772,7 +772,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     };
     // a carried state (rmt_sim_set_carry): this call's first step uses the geometry, known
     // plane, prep planes and max |u|^2 partials the previous call's last step left
-    const bool carry = S->carry_on && S->carry_valid && S->carry_gen == ctx->bytes_gen;
+    const bool carry = S->carry_on && S->carry_valid && S->carry_gen == ctx->bytes_gen &&
+                       S->carry_cfg == extrap_config_gen();
     const bool m2_ok = carry && S->m2_valid;
     S->carry_valid = false;
     if (!carry) {
@@ -1149,6 +1150,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     S->carry_valid = S->carry_on && geo_ready;
     S->m2_valid = m2_last;
     S->carry_gen = ctx->bytes_gen;
+    S->carry_cfg = extrap_config_gen();
     return RMT_OK;
 }
 

@@ -409,6 +409,11 @@ class DistributedSim:
         if (math.isinf(t_end) and t_end > 0 and not getattr(self, "_prof", False)
                 and not int(os.environ.get("RMT_SLAB_SYNC", "0"))):
             return self._step_async(nsteps)
+        self._step_sync(nsteps, t_end)
+
+    def _step_sync(self, nsteps, t_end):
+        """The synchronous path: dt on the host, the rim allgathered at its exact counts."""
+        comm, S = self.comm, self.slabs
         self._set_dev_dt(False)
         geo = False
         for k in range(nsteps):
@@ -507,24 +512,65 @@ class DistributedSim:
         ring = torch.empty((self.sync_every, width), dtype=torch.float64,
                            device=S[0].view("scal").device)
         keep, slot = [], 0
+        # each window of sync_every steps starts from a snapshot of the slabs' owned rows: a
+        # rim that outgrows the fixed capacity (seen only at the window's read-back) sends the
+        # window back to it and through the synchronous path, which moves the exact counts --
+        # the same results the asynchronous path gives when the capacity holds
+        snap, done = None, 0
+
+        def snapshot():
+            own = [{f: s.view(f)[s.r0 - s.lo:s.r1 - s.lo].clone() for f in _STATE}
+                   for s in S]
+            return own, self.t, len(self.records), done
+
+        def restore(sn):
+            own, t, nrec, d = sn
+            for s, o in zip(S, own):
+                for f in _STATE:
+                    s.view(f)[s.r0 - s.lo:s.r1 - s.lo].copy_(o[f])
+            self.t = t
+            del self.records[nrec:]
+            return d
 
         def flush():
             nonlocal slot, keep
             if not slot:
-                return
+                return True
             rows = ring[:slot].cpu().numpy()
             slot, keep = 0, []
+            over = [int(np.bitwise_or.reduce(r[2:].reshape(G, SC_N)[:, SC_FLAGS].astype(np.int64))) & 8
+                    for r in rows]
+            if any(over):
+                need = max(float(r[2:].reshape(G, SC_N)[:, SC_COUNT].max()) for r in rows)
+                self._rim_cap = max(self._rim_cap, _rim_capacity(need))
+                return False
             for r in rows:
                 sc = r[2:].reshape(G, SC_N)
-                if int(np.bitwise_or.reduce(sc[:, SC_FLAGS].astype(np.int64))) & 8:
-                    raise L.RMTError(f"slab step: the rim exceeded its allgather capacity "
-                                     f"({self._rim_cap} entries per slab)")
                 self.t += float(r[0])
                 self._record(sc, float(r[0]), float(r[1]))
                 self._rim_cap = max(self._rim_cap, _rim_capacity(sc[:, SC_COUNT].max()))
+            return True
+
+        def rerun():
+            """back to the window's snapshot, the window's steps synchronously"""
+            nonlocal snap, geo
+            self._call("rmt_slab_drop_geometry")
+            d0 = restore(snap)
+            self.m2 = None
+            self._call("rmt_slab_begin")
+            self.m2 = float(self._scalars()[:, SC_M2].max())
+            self._step_sync(done - d0, math.inf)
+            self.reruns = getattr(self, "reruns", 0) + 1
+            self._set_dev_dt(True)
+            gs = comm.allgather([s.view("scal") for s in S])[0]
+            for s in S:
+                L.check(s.lib.rmt_slab_next_dt(s.h, gs.data_ptr(), G, None), "rmt_slab_next_dt")
+            geo = False
 
         geo = False
         for k in range(nsteps):
+            if slot == 0:
+                snap = snapshot()
             h = comm.halo_start(S, ("u", "v", "p", "X1", "X2"), HALO)
             self._call("rmt_slab_advect_interior", 0.0)
             comm.halo_finish(h)
@@ -567,10 +613,13 @@ class DistributedSim:
                         "rmt_slab_next_dt")
             keep += [gs, gs2]   # (librmt runs on torch's current stream: stream-ordered reuse)
             slot += 1
-            if slot == self.sync_every:
-                flush()
+            done += 1
+            if slot == self.sync_every and not flush():
+                rerun()
         self._call("rmt_slab_drop_geometry")
-        flush()
+        if not flush():
+            rerun()
+            self._call("rmt_slab_drop_geometry")
 
     def _sub_mean(self, which):
         roots = self.comm.allgather([s.view("scal")[SC_ROOT:SC_ROOT + 1] for s in self.slabs])
@@ -598,6 +647,9 @@ class DistributedSim:
     def diagnostics(self):
         keys = self.records[0].keys() if self.records else ()
         return {k: np.array([r[k] for r in self.records]) for k in keys}
+
+
+_STATE = ("u", "v", "p", "X1", "X2")   # a step's inputs (owned rows; the halo is exchanged)
 
 
 def _rim_capacity(count):

@@ -10,6 +10,7 @@ below set up the three configurations exactly as the reference scripts do:
 """
 import ctypes
 import math
+import weakref
 
 import numpy as np
 
@@ -55,8 +56,10 @@ class Simulation:
                 "rmt_sim_create")
         self.h = h
         self._views = {}
+        self._lent = []   # weak references to the views field() handed out
         # carry the last step's prepared state into the next step() call (rmt_sim_set_carry);
-        # every write path below (field views, set_field) invalidates it
+        # every write path below (field views, set_field) invalidates it, and so does step()
+        # while a view handed out by field() is alive (it may have been written through)
         L.check(L.lib().rmt_sim_set_carry(self.h, 1), "rmt_sim_set_carry")
 
     def __del__(self):
@@ -75,10 +78,15 @@ class Simulation:
 
     def field(self, name):
         """A torch CUDA view (no copy) of a state field: u/a, v/b, p, X1, X2, phi, J.  The
-        caller may write through it before the next step(); a view kept across step() calls
-        and written later needs invalidate() first."""
+        caller may write through it at any time: while the view is alive, every step() starts
+        from the fields as they are (the carried state of the previous call is dropped)."""
         self.invalidate()
-        return self._view(name)
+        fid = FIELDS[name]
+        ptr = ctypes.c_void_p()
+        L.check(L.lib().rmt_sim_field(self.h, fid, ctypes.byref(ptr)))
+        t = _wrap_device(self.torch, ptr.value, (self.N, self.N))
+        self._lent.append(weakref.ref(t))
+        return t
 
     def invalidate(self):
         """The state was changed from outside: the next step() recomputes everything it
@@ -95,6 +103,10 @@ class Simulation:
 
     def step(self, nsteps=1, t_end=math.inf):
         self.ctx.bind()
+        if self._lent:
+            self._lent = [r for r in self._lent if r() is not None]
+            if self._lent:
+                self.invalidate()
         L.check(L.lib().rmt_sim_step(self.h, int(nsteps), float(t_end)), "rmt_sim_step")
 
     PHASES = ("dt", "advect", "extrapolate", "momentum", "projection", "diagnostics",
@@ -212,7 +224,7 @@ def run_lid_driven_cavity(Re=100.0, N=129, max_steps=60000, steady_tol=2e-5, chu
     bulk between checks and snapshots u only before a checked step."""
     sim = lid_driven_cavity(Re, N)
     torch = sim.torch
-    u = sim.field("u")
+    u = sim._view("u")   # read only
     step = 0
     while step < max_steps:
         nxt = step + 1

@@ -65,7 +65,8 @@ def hard_operands(d, count=4000, seed=1):
 
 
 DIVISORS = [2.0 / 4095, 6.0 / 4095, 1.0 / 4095, 2.0 / 255, 6.0 / 255, 2.0 / 1023,
-            6.0 / 1023, 1.0 + 1e-12, 2.0 / 64, 1.0 / 8191, 0.7, 1.9999999999999]
+            6.0 / 1023, 1.0 + 1e-12, 2.0 / 64, 1.0 / 8191, 0.7, 1.9999999999999,
+            3.0e-9, 7.0e30]   # outside the certified exponents (IEEE division)
 
 
 def test_hard_operands_generator():

@@ -203,3 +203,67 @@ def test_config5_mac_N8192_vs_oracle_fixture(gpu):
           f"{np.max(np.abs(got - gd) / np.abs(gd)):.3g}")
     np.testing.assert_allclose(got, gd, rtol=1e-6)      # north star
     np.testing.assert_allclose(got, gd, rtol=1e-12)     # achieved
+
+
+def _diag100(sim):
+    d = sim.diagnostics()
+    return np.stack([d[k] for k in ("t", "dt", "cx", "cy", "minJ", "maxJ")], axis=1)
+
+
+def test_config4_N4096_100_steps_vs_fixture(gpu):
+    """The bench workload at the bench's length: 100 fused steps at N=4096 against the oracle's
+    100-step fixture (tests/golden/gen_config4_100.py; soft_disc_in_lid_driven.py:206-235):
+    the per-step t, dt, centroid and J range, and the final fields."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    g = golden("lid4096_100_oracle")
+    N, S, st = int(g["N"]), int(g["steps"]), int(g["stride"])
+    sim = soft_disc_in_lid_driven(N)
+    sim.step(S)
+    got, want = _diag100(sim), g["diag"]
+    rel = np.abs(got - want) / np.abs(want)
+    jc, ic = g["rowcol"]
+    fd = {}
+    for name in ("X1", "X2", "u", "v", "p", "phi"):
+        f = sim.get(name)
+        fd[name] = max(_maxdiff(f[::st, ::st], g[name + "_sub"]), _maxdiff(f[jc], g[name + "_row"]),
+                       _maxdiff(f[:, ic], g[name + "_col"]))
+        fd[name + "_sha"] = _sha(f) == str(g[name + "_sha"])
+    print(f"\n[config4 N=4096 x{S}] max rel: t {rel[:, 0].max():.3g} dt {rel[:, 1].max():.3g} "
+          f"cx {rel[:, 2].max():.3g} cy {rel[:, 3].max():.3g} minJ {rel[:, 4].max():.3g} "
+          f"maxJ {rel[:, 5].max():.3g}; final fields {fd}")
+    np.testing.assert_allclose(got[:, 2:4], want[:, 2:4], rtol=1e-6)     # north star
+    np.testing.assert_allclose(got[:, 0:2], want[:, 0:2], rtol=1e-12)
+    np.testing.assert_allclose(got[:, 4], want[:, 4], rtol=7e-4)         # noise floor x 2
+    np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=1.3e-3)
+    # achieved (MI355X, round 4): see DESIGN.md section 2
+    np.testing.assert_allclose(got[:, 2:4], want[:, 2:4], rtol=1e-12)
+    assert max(fd["u"], fd["v"]) <= 1e-12 and fd["p"] <= 1e-10
+
+
+def test_config4_N4096_100_steps_parallel_mode(gpu):
+    """The opt-in parallel extrapolation (extrap_par.hip: the reference's fits evaluated in
+    centred coordinates) over the bench's 100 steps against the same oracle fixture.  It is
+    not bit-exact: the reference's own 1-ulp noise moves the centroid by 4.8e-7 in 30 steps
+    (profiles/r03/noise/).  Reported: the worst centroid error and the first step past the
+    north-star bar 1e-6."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    g = golden("lid4096_100_oracle")
+    N, S = int(g["N"]), int(g["steps"])
+    gpu.extrapolation_parallel(True)
+    try:
+        sim = soft_disc_in_lid_driven(N)
+        sim.step(S)
+        got = _diag100(sim)
+    finally:
+        gpu.extrapolation_parallel(False)
+    want = g["diag"]
+    rel = np.abs(got - want) / np.abs(want)
+    cen = rel[:, 2:4].max(axis=1)
+    past = np.nonzero(cen > 1e-6)[0]
+    first = int(past[0]) + 1 if len(past) else None
+    print(f"\n[config4 N=4096 x{S}, parallel extrapolation] worst centroid rel {cen.max():.3g} "
+          f"(step {int(cen.argmax()) + 1}); first step past 1e-6: {first}; t {rel[:, 0].max():.3g} "
+          f"minJ {rel[:, 4].max():.3g} maxJ {rel[:, 5].max():.3g}")
+    # the documented envelope (DESIGN.md section 5): within the bar for the first 10 steps
+    assert np.all(cen[:10] <= 1e-6)
+    assert cen.max() <= 1e-4

@@ -19,6 +19,11 @@ projection (LDS DCT plan: 255 = 3 5 17) and with it the early transpose are on.
                           completing with them (hipExtLaunchKernel)
   RMT_MERGED_JOIN=0       the second stream joined twice (after its momentum, before the
                           projection) instead of once after its row passes
+  RMT_FIX_ALL=1           the fix-up re-runs phi, the prep and the four stages on EVERY tile
+                          (interior, edge and domain-boundary tiles through the list kernels;
+                          the default's fix-up list holds interior tiles only for this disc) --
+                          the regression test for the round-3 divergent list-kernel variant
+                          
 """
 import os
 import subprocess
@@ -69,7 +74,7 @@ def default_run(tmp_path_factory, gpu):
     {"RMT_CH_PARTS": "1"}, {"RMT_CH_VARIANT": "35"}, {"RMT_FUSED_FLUID": "0"},
     {"TEST_EX_MODE": "2"}, {"TEST_EX_MODE": "2", "RMT_FUSED_FIXPREP": "0"},
     {"RMT_FUSED_FIXPREP": "0"}, {"RMT_EXT_EVENTS": "0"},
-    {"RMT_MERGED_JOIN": "0"},
+    {"RMT_MERGED_JOIN": "0"}, {"RMT_FIX_ALL": "1"}, {"RMT_FIX_ALL": "1", "RMT_SIM_HIPRIO": "0"},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(tmp_path, default_run, env):
     got = _run(tmp_path, "variant", env)

@@ -79,3 +79,54 @@ def test_carry_invalidated_by_writes_and_workspace_reuse(gpu):
         F.extrapolate_reference_map(X1, X2, phi, 1.0 / 255, 1.0 / 255, 3)
         s.step(4)
     _same(a, b)
+
+
+def test_carry_with_a_kept_view_written_later(gpu):
+    """A field() view kept across step() calls and written through later, with no
+    invalidate(): while such a view is alive every step() starts from the fields as they are
+    (simulation.py), so the results equal the no-carry run's."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    a, b = soft_disc_in_lid_driven(256), soft_disc_in_lid_driven(256)
+    _carry_off(b)
+    for s in (a, b):
+        u = s.field("u")          # kept
+        s.step(3)
+        s.step(2)
+        u.mul_(0.5)               # written through the old view, no invalidate()
+        s.step(3)
+        del u
+        s.step(2)
+    _same(a, b)
+
+
+@pytest.mark.parametrize("toggle", ["parallel", "mode"])
+def test_carry_dropped_on_extrapolation_mode_change(gpu, toggle):
+    """Switching the extrapolation's configuration between step() calls (the parallel mode,
+    rmt_extrap_set_parallel; the path mode, rmt_extrap_set_mode) ends the carried geometry:
+    the next step runs the new configuration from scratch, bit-identical to a run with the
+    carry off (the carried geometry was the old mode's)."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    from pyrmt_amd import functions as F
+    def on():
+        if toggle == "parallel":
+            F.extrapolation_parallel(True)
+        else:
+            F.extrapolation_mode(1)
+    def off():
+        if toggle == "parallel":
+            F.extrapolation_parallel(False)
+        else:
+            F.extrapolation_mode(0)
+    a, b = soft_disc_in_lid_driven(256), soft_disc_in_lid_driven(256)
+    _carry_off(b)
+    try:
+        for s in (a, b):
+            off()
+            s.step(3)
+            on()
+            s.step(3)
+            off()
+            s.step(3)
+    finally:
+        off()
+    _same(a, b)

@@ -51,6 +51,8 @@ int main(int argc, char **argv) {
         }
         ds.push_back(1.0 + 1e-12);                           // rho + 1e-12 at rho = 1
         ds.push_back(0.3); ds.push_back(0.7); ds.push_back(1.9999999999999); ds.push_back(3.0);
+        // outside the certified divisor exponents (IEEE division): a tiny and a huge divisor
+        ds.push_back(3.0e-9); ds.push_back(7.0e30); ds.push_back(0x1p-20); ds.push_back(0x1.8p60);
     }
     std::mt19937_64 rng(12345);
     long total_bad = 0;
