@@ -4,7 +4,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librmt.so")
+# RMT_LIB: an alternative build of the same sources (A/B measurements of compile-time
+# variants, e.g. `make -C pyrmt_amd/csrc VARIANT=w16 DEFS=-DRMT_CH_W=16`)
+LIB_PATH = os.environ.get("RMT_LIB") or os.path.join(_HERE, "librmt.so")
 
 RMT_OK, RMT_EINVAL, RMT_ENONFINITE, RMT_EDEVICE, RMT_ENOTSUP, RMT_ENOMEM = range(6)
 

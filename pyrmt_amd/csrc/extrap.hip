@@ -663,12 +663,8 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bo
     w.loc = (int *)take(maxt * 4);
     w.inv = (int *)take(maxt * 4);
     w.gtag = (int *)take(maxt * 4);
-    w.rkey = (int *)take(maxt * 4);
     w.wnext = (int *)take(maxt * 4);
     w.gval = (double *)take(maxt * 16);
-    w.crit = (int2 *)take(maxt * 8);
-    w.pred = (double2 *)take(maxt * 16);
-    if (!(ch_variant() & 32)) { w.crit = nullptr; w.pred = nullptr; }   // fast fold only
     w.rej = (int *)take((size_t)ML * EX_MAXREJ * 4);
     w.ctl = (int *)take(EXC_WORDS * 4);
     // one fixed slot per fit id (no allocation cursor shared by every wave of k_ex_geom) when

@@ -10,7 +10,10 @@ typedef unsigned long long u64;
 
 constexpr int EX_MAXL = 8;          // layers the chain path handles (more -> fallback sweep)
 constexpr int CH_R = 2048;          // chain value ring (slots, chain order); deps < CH_R/2 back
-constexpr int CH_W = 12;            // chain workgroup waves (3 per SIMD)
+#ifndef RMT_CH_W
+#define RMT_CH_W 16
+#endif
+constexpr int CH_W = RMT_CH_W;      // chain workgroup waves (4 per SIMD)
 constexpr int CH_HDR = 24;          // record header, doubles
 constexpr int CH_TVS = 88;          // padded fold terms per sum (81 rounded up to 8)
 constexpr int CH_MAXREC = 8 * (CH_HDR + 6 * CH_TVS + 4 * 64);   // 6464 B (<= 64 sources)
@@ -48,15 +51,10 @@ struct ExWs {
     // meta bit 63 marks a fit read by another part)
     unsigned char *part;                      // MAXT
     int *loc, *inv, *gtag;                    // MAXT each
-    // wave assignment: rkey[x] = L * ny + j of chain index x; wnext[base_p + l] = the next
-    // ordinal of part p that ordinal l's wave runs (row runs: k_ex_runs)
-    int *rkey, *wnext;                        // MAXT each
+    // wave assignment: wnext[base_p + l] = the next ordinal of part p that ordinal l's wave
+    // runs (round robin, k_ex_runs)
+    int *wnext;                               // MAXT
     double *gval;                             // 2 * MAXT
-    int2 *crit;                               // MAXT by global slot: the fit's latest source
-                                              // in chain order {ring tag, or -1 when it
-                                              // lies in another part or none; its cell}
-    double2 *pred;                            // MAXT by global slot: that source's predicted
-                                              // (X1, X2) (k_ex_vals)
     int *rej;                                 // ML * EX_MAXREJ
     int *ctl;                                 // EXC_WORDS
     // parallel mode (extrap_par.hip; laid out after everything else, only when requested):
@@ -89,7 +87,6 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
                       double dx, double dy, int ML);
 int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
                         double dx, double dy, int ML);
-int ch_variant();   // RMT_CH_VARIANT (extrap_chain.hip)
 int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o, int ML);
 bool extrap_chain_supported(int ny, int nx, int ML);
 // chain prep without the chain-order passes and with no records (the parallel mode only

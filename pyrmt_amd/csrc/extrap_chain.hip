@@ -332,11 +332,6 @@ __global__ void __launch_bounds__(256) k_ex_geom(ExGeoArgs A) {
 
 __device__ __forceinline__ int ch_base(const int *ctl, int p);
 
-// RMT_CH_VARIANT (default 3; see ch_fit): read once per process
-int ch_variant() {
-    static const int var = getenv("RMT_CH_VARIANT") ? atoi(getenv("RMT_CH_VARIANT")) : 3;
-    return var;
-}
 
 // ------------------------------------------------------------------ 1. values ------
 // The value half of a record (k_ex_geom wrote the geometry): P[0..5] = the ordered sums of
@@ -344,8 +339,7 @@ int ch_variant() {
 // the 6 products w*a*X of every static term from there on, at the record's term slots.  The
 // same window analysis as ex_geom (final same-layer acceptance from ACC), the same operands.
 // One wave per accepted fit, every layer in one launch.
-__global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML, const double *P1,
-                                                 const double *P2) {
+__global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML) {
     __shared__ u64 tab[256];
     __shared__ __attribute__((aligned(16))) double tb[4][6 * EXS];
     for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
@@ -446,11 +440,6 @@ __global__ void __launch_bounds__(256) k_ex_vals(ExGeoArgs A, int ML, const doub
             tv[4 * npad + k] = wa1 * b2[h]; tv[5 * npad + k] = wa2 * b2[h];
         }
         if (lane < 6) rec[17 + lane] = acc;   // P[0..5]
-        if (lane == 0 && ws.pred) {   // the prediction of the fit's latest source (variant 35)
-            const int x = ws.chain_of[id], g = ch_base(ws.ctl, ws.part[x]) + ws.loc[x];
-            const int cc = ws.crit[g].y;
-            ws.pred[g] = cc >= 0 ? make_double2(P1[cc], P2[cc]) : make_double2(0.0, 0.0);
-        }
     }
 }
 
@@ -599,7 +588,6 @@ __global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, in
         const int x = ws.cbase[(long)L * ny + j] +
                       (id - ws.ctl[EXC_BASE + L] - ws.rowoff[(long)L * (ny + 1) + j]);
         ws.chain_of[id] = x;
-        ws.rkey[x] = L * ny + j;
         ws.part[x] = (unsigned char)ch_part_of(ws.ctl, (int)(ws.tcell[id] % nx));
         const long long r = ws.recoff[id];
         ws.rec_by_chain[x] = r;
@@ -664,55 +652,17 @@ __device__ __forceinline__ int ch_base(const int *ctl, int p) {
     return b;
 }
 
-// Wave assignment of part blockIdx.x.  Round robin (runs = 0): ordinal l on wave l % CH_W.
-// Row runs (runs = 1, RMT_CH_RUNS): the maximal runs of consecutive ordinals of one row and
-// layer go to one wave each, runs dealt round robin -- a fit's left neighbour (the critical
-// source of about half the chain's links) is then its own wave's previous fit, with no
-// hand-off to notice.  Measured slower (4.32 vs 3.0 ms at N=4096): the fit's record staging,
-// products and prefix fold, which overlap the predecessor's wait under round robin, become
-// serial.  Every wave's sequence increases either way (deadlock-free).  One block per part.
-__global__ void __launch_bounds__(1024) k_ex_runs(ExWs ws, int runs) {
-    __shared__ int sc[1024];
+// Wave assignment of part blockIdx.x: ordinal l on wave l % CH_W (round robin: a fit's record
+// staging and prefix fold overlap its predecessors' waits; giving each row run of fits to one
+// wave measured slower in round 3, 4.32 vs 3.0 ms at N=4096).  One block per part.
+__global__ void __launch_bounds__(1024) k_ex_runs(ExWs ws) {
     if (ws.ctl[EXC_FALLBACK]) return;
     const int p = blockIdx.x, t = threadIdx.x;
     if (p >= ws.ctl[EXC_NPART + CH_MAXP]) return;
     const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
     int *wst = ws.ctl + EXC_WSTART + p * CH_W;
-    if (!runs) {
-        for (int l = t; l < np; l += 1024) ws.wnext[base + l] = l + CH_W;
-        if (t < CH_W) wst[t] = min(t, np);
-        return;
-    }
-    const int per = (np + 1023) / 1024, a = min(np, t * per), b = min(np, a + per);
-    auto start = [&](int l) {
-        return l == 0 || ws.rkey[ws.inv[base + l]] != ws.rkey[ws.inv[base + l - 1]];
-    };
-    int cnt = 0;
-    for (int l = a; l < b; ++l) cnt += start(l);
-    sc[t] = cnt;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int v = t >= d ? sc[t - d] : 0;
-        __syncthreads();
-        sc[t] += v;
-        __syncthreads();
-    }
-    const int nruns = sc[1023];
-    // run r starts at ordinal rs(r): dmark (free after the fix-up passes) holds the starts
-    int *rs = ws.dmark + base;
-    int r = sc[t] - cnt;
-    for (int l = a; l < b; ++l)
-        if (start(l)) rs[r++] = l;
-    __threadfence_block();
-    __syncthreads();
-    r = sc[t] - cnt;   // runs started before a
-    for (int l = a; l < b; ++l) {
-        if (start(l)) ++r;          // l's run is r - 1
-        const int rr = r - 1;
-        const bool last = l + 1 >= np || start(l + 1);
-        ws.wnext[base + l] = !last ? l + 1 : rr + CH_W < nruns ? rs[rr + CH_W] : np;
-    }
-    if (t < CH_W) wst[t] = t < nruns ? rs[t] : np;
+    for (int l = t; l < np; l += 1024) ws.wnext[base + l] = l + CH_W;
+    if (t < CH_W) wst[t] = min(t, np);
 }
 
 // record sources: fit ids -> ring tags within the fit's part (the ring needs every source
@@ -734,16 +684,11 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
         int2 *dyn = (int2 *)(rec + CH_HDR);   // entry d at int2 index 2d: (k, src)
         const int x = ws.chain_of[id], p = ws.part[x], l = ws.loc[x];
         const int np = ws.ctl[EXC_NPART + p], base = ch_base(ws.ctl, p);
-        int2 crit = make_int2(-1, -1);   // the latest source in chain order (fast fold)
-        int xmax = -1, lmax = -1, dmax = -1;   // the latest local source: its ordinal, entry
+        int lmax = -1, dmax = -1;   // the latest local source: its ordinal, entry
         for (int d = lane; d < nd; d += 64) {
             const int src = dyn[4 * d].y;
             const int xs = ws.chain_of[src];
             dyn[4 * d].x &= 0xffff;
-            if (ws.crit && xs > xmax) {   // (variant 35 only: ws.crit is null otherwise)
-                xmax = xs;
-                crit = make_int2(ws.part[xs] == p ? ws.loc[xs] : -1, (int)ws.tcell[src]);
-            }
             if (xs >= x) { ws.ctl[EXC_ABORT] = 1; atomicExch(ws.status + 1, 1); }   // a bug
             if (ws.part[xs] == p) {
                 const int ls = ws.loc[xs];
@@ -764,19 +709,6 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
             if (m >= 0 && lmax == m) dyn[4 * dmax].x |= (int)CH_CRIT;
-        }
-        if (ws.crit) {
-            // the source with the largest chain index (sources are distinct fits)
-            int m = xmax;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
-            const unsigned long long who = __ballot(m >= 0 && xmax == m);
-            int2 c = make_int2(-1, -1);
-            if (who) {
-                const int src_l = __ffsll((long long)who) - 1;
-                c = make_int2(__shfl(crit.x, src_l), __shfl(crit.y, src_l));
-            }
-            if (lane == 0) ws.crit[base + l] = c;
         }
         if (lane == 0) {
             int ln = ws.wnext[base + l];
@@ -892,134 +824,6 @@ __device__ __forceinline__ double ch_fold(double acc, const double *row, int c0,
 }
 
 
-// Fast fold (VAR bit 5): the sums after a fit's latest source c, F(a) = fl(..fl(a + t1) ..
-// + tn), folded BEFORE c arrives.  a = fl(S_pre + cf X_c) is predicted as a^ from X^_c (the
-// previous step's map at c, k_ex_vals); lane 8k + r (sum k < 6, r < 8) folds the trailing
-// terms from a^ with its 3 low mantissa bits replaced by r.  If a and a^ share the binade and
-// every partial sum of lane (k, r = a mod 8 ulp) stays >= 2^-14 of its binade from the
-// binade's edges, at most 2 binades above a's, then rounding commutes with the shift
-// d = a - a_r (a multiple of 8 ulp(a), >= 2 ulp of every binade passed):
-// F(a) = F(a_r) + d exactly.  Otherwise the terms are folded after the arrival as before.
-// Returns 0: not taken (nothing changed), 1: the sums are in acc (lanes 0-5), -1: timeout.
-__device__ __forceinline__ double d_hl(unsigned h, unsigned l) {
-    return __hiloint2double((int)h, (int)l);
-}
-__device__ __forceinline__ int ch_fast(int lane, double *B, const double2 *val, const int *tag,
-                                       double *tv, int npad, int2 e, const double *cf,
-                                       bool &done, double &acc, int2 cr, double2 pr) {
-    if (cr.x < 0) return 0;
-    const u64 cl = __ballot(!done && e.y == cr.x);
-    if (!cl) return 0;
-    const int clane = __builtin_ctzll(cl);
-    const int slot = e.y & (CH_R - 1);
-    // every other missing source first (their products into tv, as pass 2 writes them)
-    long sp = 0;
-    while (__ballot(!done && lane != clane)) {
-        if (!done && lane != clane &&
-            __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
-            asm volatile("" ::: "memory");
-            const double2 v = val[slot];
-#pragma unroll
-            for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
-            done = true;
-        }
-        if (++sp > CH_SPIN_LIMIT) return -1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int kc = __builtin_amdgcn_readlane(e.x, clane);
-    const double c0 = rlf(cf[0], clane), c1 = rlf(cf[1], clane), c2 = rlf(cf[2], clane);
-    const int m3 = lane % 3;
-    const double cfl = m3 == 0 ? c0 : (m3 == 1 ? c1 : c2);
-    // the sums up to the latest source's term, in the reference's order
-    if (lane < 6) {
-        const double *row = tv + lane * npad;
-        acc = ch_fold(acc, row, 0, kc >> 3);
-        for (int j = kc & ~7; j < kc; ++j) acc += row[j];
-    }
-    double *sc = B + CH_BUFD - 8;
-    if (lane < 6) sc[lane] = acc + cfl * (lane < 3 ? pr.x : pr.y);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int kk = (lane >> 3) < 6 ? (lane >> 3) : 5, rr = lane & 7;
-    const double ah = sc[kk];
-    const unsigned hA = (unsigned)__double2hiint(ah), lA = (unsigned)__double2loint(ah);
-    double f = d_hl(hA, (lA & ~7u) | (unsigned)rr);
-    unsigned mx = hA, mn = hA;
-    bool nr = false;
-    const double *trow = tv + kk * npad;
-    auto trk = [&](double t) {
-        f += t;
-        const unsigned h = (unsigned)__double2hiint(f);
-        mx = max(mx, h); mn = min(mn, h);
-        nr = nr || ((h + 0x40u) & 0xFFF80u) == 0u;
-    };
-    const int t1 = (kc >> 3) + 1, nch = npad >> 3;
-    for (int j = kc + 1; j < 8 * t1; ++j) trk(trow[j]);
-    if (t1 < nch) {   // whole chunks, the next chunk's reads in flight (as ch_fold)
-        const double2 *r2 = (const double2 *)trow;
-        double2 a0 = r2[4 * t1], a1 = r2[4 * t1 + 1], a2 = r2[4 * t1 + 2], a3 = r2[4 * t1 + 3];
-        for (int c = t1; c < nch; ++c) {
-            double2 b0, b1, b2, b3;
-            const bool more = c + 1 < nch;
-            if (more) {
-                b0 = r2[4 * c + 4]; b1 = r2[4 * c + 5]; b2 = r2[4 * c + 6]; b3 = r2[4 * c + 7];
-            }
-            trk(a0.x); trk(a0.y); trk(a1.x); trk(a1.y);
-            trk(a2.x); trk(a2.y); trk(a3.x); trk(a3.y);
-            if (more) { a0 = b0; a1 = b1; a2 = b2; a3 = b3; }
-        }
-    }
-    // the latest source (low priority while polling, as pass 2)
-    double2 vc = make_double2(0.0, 0.0);
-    sp = 0;
-    __builtin_amdgcn_s_setprio(0);
-    for (;;) {
-        if (lane == clane && !done &&
-            __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
-            asm volatile("" ::: "memory");
-            vc = val[slot];
-            done = true;
-        }
-        if (__ballot(!done) == 0) break;
-        if (++sp > CH_SPIN_LIMIT) return -1;
-    }
-    __builtin_amdgcn_s_setprio(3);
-    const double v1 = rlf(vc.x, clane), v2 = rlf(vc.y, clane);
-    double a = 0.0;
-    if (lane < 6) a = acc + cfl * (lane < 3 ? v1 : v2);   // the reference's next operation
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (lane < 6) sc[lane] = a;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const double ak = sc[kk];
-    const unsigned hB = (unsigned)__double2hiint(ak), lB = (unsigned)__double2loint(ak);
-    const bool match = lane < 48 && (lB & 7u) == (unsigned)rr;
-    const unsigned e0 = hA & 0x7FF00000u, emn = (mn >> 20) & 0x7FFu;
-    const bool same = (hB & 0xFFF00000u) == (hA & 0xFFF00000u) && (hA >> 31) == 0u &&
-                      e0 >= (0x100u << 20) && e0 <= (0x700u << 20);
-    const bool okb = !nr && (mx >> 31) == 0u && (mx & 0x7FF00000u) <= e0 + (2u << 20) && emn > 64u;
-    const double del = d_hl(hB, lB & ~7u) - d_hl(hA, lA & ~7u);
-    const double lim = d_hl((emn - 15u) << 20, 0u);
-    const bool good = same && okb && fabs(del) <= lim;
-    const u64 mm = __ballot(match), mg = __ballot(match && good);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (mm == mg && __popcll(mm) == 6) {
-        if (match) sc[kk] = f + del;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (lane < 6) acc = sc[lane];
-    } else if (lane < 6) {
-        acc = a;
-        const double *row = tv + lane * npad;
-        for (int j = kc + 1; j < 8 * t1; ++j) acc += row[j];
-        acc = ch_fold(acc, row, t1, nch);
-    }
-    return 1;
-}
-
 __device__ __forceinline__ double dpp_shl(double v, int ctrl) {
     // row_shl:1 = 0x101, row_shl:2 = 0x102 (lanes read lane + k within their 16-lane row)
     const int lo = __double2loint(v), hi = __double2hiint(v);
@@ -1030,223 +834,31 @@ __device__ __forceinline__ double dpp_shl(double v, int ctrl) {
     return __hiloint2double(h2, l2);
 }
 
-// One fit of the chain: chain index x whose record is staged in this wave's buffer B.
-// Everything that does not need the last-arriving source runs before waiting for it: the
-// products of sources already published, the fold of the terms before the first missing
-// one, and the solve constants.  LDS hand-offs: a fit writes its value pair, then its tag; a
-// reader that sees the tag reads the values afterwards (one wave's LDS operations are
-// performed in issue order), so no fence is needed -- and none is wanted: a workgroup fence
-// would also drain the record prefetch in flight.  Returns false on a timeout (bug guard).
-// VAR (RMT_CH_VARIANT, default 3): bit 0 = wave priorities (low while polling, high from the
-// last source's arrival through the publish); bit 1 = poll without s_sleep.  Measured on the
-// 4096^2 disc: 0 -> 4.66 ms, 1 -> 4.50, 2 -> 4.74, 3 -> 4.45 (profiles/r01s3/chain_variants.log)
-template <bool PROF, int VAR>
-__device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
-                                       int *cur, int &wm, double &o_out, long &c_out,
-                                       long long *pr, long long &tl, int *gtag, double *gval,
-                                       int gslot, long long *trace = nullptr, int base = 0,
-                                       const int2 *crit = nullptr, const double2 *pred = nullptr) {
-    long long tr_start = 0, tr_ready = 0;
-    int tr_crit = -1;
-    // ring reuse: every fit < x - CH_R/2 is done (all their readers are < x)
-    long spins = 0;
-    while (x - CH_R / 2 >= wm) {
-        int m = 0x7fffffff;
-        for (int k = 0; k < CH_W; ++k)
-            m = min(m, __hip_atomic_load(&cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        wm = m;
-        if (x - CH_R / 2 >= wm) {
-            if (++spins > CH_SPIN_LIMIT) return false;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    CH_STAMP(1);
-    if constexpr (PROF) tr_start = __builtin_amdgcn_s_memrealtime();
-    const long long meta = __double_as_longlong(B[1]);
-    const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
-    const int nd = __builtin_amdgcn_readfirstlane((int)((meta >> 32) & 0x7fffffff));
-    const bool pub = !(VAR & 16) &&
-                     __builtin_amdgcn_readfirstlane((int)((unsigned long long)meta >> 63)) != 0;
-    if (npad > CH_TVS || nd > 64 || npad < 0 || nd < 0) return false;   // bug guard
-    const double *dyn = B + CH_HDR;
-    double *tv = B + CH_HDR + 4 * nd;
-    // solve constants (lanes 0, 3) and this lane's dynamic source with its coefficients
-    // wave-uniform solve constants, kept in SGPRs
-    auto U = [&](int k) {
-        const double v = B[k];
-        return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
-                                __builtin_amdgcn_readfirstlane(__double2loint(v)));
-    };
-    const double x0 = U(2), y0 = U(3), M0 = U(4), M1 = U(5), M2 = U(6), M3 = U(7), M4 = U(8);
-    const double M5 = U(9), M6 = U(10), M7 = U(11), M8 = U(12), C0 = U(13), C1 = U(14);
-    const double C2 = U(15), inv_det = U(16);
-    double acc = 0.0;
-    if (lane < 6) acc = B[17 + lane];
-    const bool has = lane < nd;
-    int2 e = make_int2(0, -1);
-    double cf[3] = {0.0, 0.0, 0.0};   // w*1, w*x, w*y (the same for the X1 and X2 sums)
-    if (has) {
-        const double2 q0 = ((const double2 *)dyn)[2 * lane], q1 = ((const double2 *)dyn)[2 * lane + 1];
-        const long long kk = __double_as_longlong(q0.x);
-        e = make_int2((int)(kk & 0xffff), (int)(kk >> 32));
-        cf[0] = q0.y; cf[1] = q1.x; cf[2] = q1.y;
-    }
-    bool done = !has;   // product written
-    // VAR bit 4: one part only (no far sources, nothing to publish).  Sources in another
-    // part (e.y < 0; rare: near the part boundaries, and usually published long before) are
-    // awaited first through HBM, so the LDS passes below stay the one-part code.
-    const int slot = e.y & (CH_R - 1);
-    const bool far = !(VAR & 16) && has && e.y < 0;
-    if (!(VAR & 16) && __ballot(far)) {
-        long sp = 0;
-        for (;;) {
-            double2 v;
-            if (far && !done && ch_probe(e.y, tag, val, gtag, gval, v)) {
+// terms [lo, hi) of the 8-term chunk c of row (lo, hi within the chunk), in order: the chunk's
+// four 16-byte reads issued together
+__device__ __forceinline__ double ch_part(double acc, const double *row, int c, int lo, int hi) {
+    const double2 *r2 = (const double2 *)(row + 8 * c);
+    const double2 a = r2[0], b = r2[1], d = r2[2], e = r2[3];
+    const double t[8] = {a.x, a.y, b.x, b.y, d.x, d.y, e.x, e.y};
+    lo -= 8 * c; hi -= 8 * c;
 #pragma unroll
-                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
-                done = true;
-            }
-            if (__ballot(far && !done) == 0) break;
-            if (++sp > CH_SPIN_LIMIT) return false;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    // pass 1: products of the sources already published; fold up to the first missing one
-    {
-        const bool ready = has && !done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP) == e.y;
-        asm volatile("" ::: "memory");
-        if (ready) {
-            const double2 v = val[slot];
-#pragma unroll
-            for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
-            done = true;
-        }
-    }
-    // first window term whose source is still missing: sources are listed in window order
-    int fastr = 0;
-    if constexpr ((VAR & 32) != 0 && !PROF) {
-        if (__ballot(!done))
-            fastr = ch_fast(lane, B, val, tag, tv, npad, e, cf, done, acc, crit[gslot], pred[gslot]);
-        if (fastr < 0) return false;
-    }
-    if (!fastr) {
-    const u64 pend = __ballot(!done);
-    const int kmiss = pend ? __builtin_amdgcn_readlane(e.x, __builtin_ctzll(pend)) : npad;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int c1 = kmiss >> 3, nch = npad >> 3;
-    if (lane < 6) acc = ch_fold(acc, tv + lane * npad, 0, c1);
-    CH_STAMP(3);
-    // pass 2: wait for the missing sources, then the rest of the fold
-    if (pend) {
-        long sp = 0;
-        if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-        for (;;) {
-            bool now = false;
-            if (!done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP) == e.y) {
-                asm volatile("" ::: "memory");
-                const double2 v = val[slot];
-#pragma unroll
-                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
-                done = true;
-                now = true;
-            }
-            if constexpr (PROF) {
-                const u64 fl = __ballot(now);
-                if (fl) tr_crit = __builtin_amdgcn_readlane(e.y, __builtin_ctzll(fl));
-            }
-            const u64 left = __ballot(!done);
-            if (left == 0) break;
-            if (++sp > CH_SPIN_LIMIT) return false;
-            if constexpr (PROF) pr[7] += 1;
-            if constexpr (!(VAR & 2)) __builtin_amdgcn_s_sleep(0);
-        }
-        if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(3);
-        CH_STAMP(2);
-        if constexpr (PROF) tr_ready = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
-    if (lane < 6) acc = ch_fold(acc, tv + lane * npad, c1, nch);
-    }
-    if constexpr (PROF) asm volatile("" : "+v"(acc));
-    CH_STAMP(4);
-    // utils.py:134-166 on lanes 0 (X1) and 3 (X2) with the precomputed cofactors
-    double bb1 = dpp_shl(acc, 1), bb2 = dpp_shl(acc, 2);
-    if constexpr (PROF) asm volatile("" : "+v"(bb1), "+v"(bb2));
-    CH_STAMP(8);
-    if (lane == 0 || lane == 3) {
-        const double b0 = acc, b1 = bb1, b2 = bb2;
-        const double xs = (b0 * C0 - M1 * (b1 * M8 - M5 * b2) + M2 * (b1 * M7 - M4 * b2)) * inv_det;
-        const double ys = (M0 * (b1 * M8 - M5 * b2) - b0 * C1 + M2 * (M3 * b2 - b1 * M6)) * inv_det;
-        const double zs = (M0 * (M4 * b2 - b1 * M7) - M1 * (M3 * b2 - b1 * M6) + b0 * C2) * inv_det;
-        double o = xs + ys * x0 + zs * y0;
-        if constexpr (PROF) asm volatile("" : "+v"(o));
-        CH_STAMP(9);
-        ((double *)&val[x & (CH_R - 1)])[lane == 0 ? 0 : 1] = o;
-        if (pub) gval[2 * gslot + (lane == 0 ? 0 : 1)] = o;
-        o_out = o;
-    }
-    asm volatile("" ::: "memory");
-    if (lane == 0)
-        __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (pub) {   // a fit of the other part reads this one: value, then tag (agent release)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0)
-            __hip_atomic_store(&gtag[gslot], gslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    CH_STAMP(10);
-    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
-    c_out = __double_as_longlong(B[0]);
-    if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    CH_STAMP(5);
-    if constexpr (PROF) {
-        if (trace && lane == 0) {
-            const long long tp = __builtin_amdgcn_s_memrealtime();
-            long long *t = trace + 6L * gslot;
-            t[0] = tr_start; t[1] = tr_ready ? tr_ready : tr_start; t[2] = tp;
-            t[3] = tr_crit >= 0 ? base + tr_crit : (tr_crit < -1 ? -tr_crit - 1 : -1);
-            t[4] = threadIdx.x >> 6; t[5] = c_out;
-        }
-    }
-    return true;
+    for (int k = 0; k < 8; ++k)
+        if (k >= lo && k < hi) acc += t[k];
+    return acc;
 }
-
-// fold row[a .. b) into acc in order; reads run 8 terms ahead of the adds (LDS reads past b
-// read unused words of the wave's buffer and are never added).  Fully unrolled over the
-// longest row: straight-line code keeps the compiler's LDS wait counts exact (a loop's back
-// edge makes it wait for every read in flight once per trip)
-#define CH_S(acc, row, n, r, k)                                                \
-    if ((k) >= (n)) break;                                                     \
-    acc += r[(k) & 7];                                                         \
-    r[(k) & 7] = (row)[(k) + 8];                                               \
-    __builtin_amdgcn_sched_barrier(0);
-#define CH_S8(acc, row, n, r, b)                                                       \
-    CH_S(acc, row, n, r, b) CH_S(acc, row, n, r, b + 1) CH_S(acc, row, n, r, b + 2)    \
-    CH_S(acc, row, n, r, b + 3) CH_S(acc, row, n, r, b + 4) CH_S(acc, row, n, r, b + 5) \
-    CH_S(acc, row, n, r, b + 6) CH_S(acc, row, n, r, b + 7)
-#define CH_TAIL(acc, row, n, r)                                                        \
-    do {                                                                               \
-        CH_S8(acc, row, n, r, 0) CH_S8(acc, row, n, r, 8) CH_S8(acc, row, n, r, 16)    \
-        CH_S8(acc, row, n, r, 24) CH_S8(acc, row, n, r, 32) CH_S8(acc, row, n, r, 40)  \
-        CH_S8(acc, row, n, r, 48) CH_S8(acc, row, n, r, 56) CH_S8(acc, row, n, r, 64)  \
-        CH_S8(acc, row, n, r, 72) CH_S8(acc, row, n, r, 80)                            \
-    } while (0)
-static_assert(CH_TVS <= 88, "CH_TAIL unrolls 88 terms");
-__device__ __forceinline__ double ch_fold_rng(double acc, const double *row, int a, int b) {
+// row[a .. b) in order: partial head chunk, whole chunks (ch_fold: 4-term groups, three
+// groups of reads ahead), partial last chunk
+__device__ __forceinline__ double ch_fold_span(double acc, const double *row, int a, int b) {
     if (a >= b) return acc;
-    row += a;
-    double r[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = row[k];
-    CH_TAIL(acc, row, b - a, r);
+    const int ca = a >> 3, cb = b >> 3;
+    if (ca == cb) return ch_part(acc, row, ca, a, b);
+    if (a & 7) acc = ch_part(acc, row, ca, a, 8 * ca + 8);
+    acc = ch_fold(acc, row, (a + 7) >> 3, cb);
+    if (b & 7) acc = ch_part(acc, row, cb, 8 * cb, b);
     return acc;
 }
 
-// The lean fit (VAR bit 6).  The fit's latest local source in chain order (marked CH_CRIT by
+// One fit of the chain, chain index x, its record staged in this wave's buffer B.  The fit's latest local source in chain order (marked CH_CRIT by
 // k_ex_relink) is the one its predecessor link hands over; everything else is done before it
 // arrives: the other sources' products (written to the staged record's term rows as they
 // arrive), the fold of the terms before the critical one's window position kc, and the
@@ -1255,8 +867,8 @@ __device__ __forceinline__ double ch_fold_rng(double acc, const double *row, int
 // order, and the producer writes the value before the tag), its product is added in
 // registers -- never written to LDS -- and the terms after kc follow: the reference's order,
 // the same operations.
-template <bool PROF, int VAR>
-__device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val, int *tag,
+template <bool PROF>
+__device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                         int *cur, int &wm, double &o_out, long &c_out,
                                         long long *pr, long long &tl, int *gtag, double *gval,
                                         int gslot, long long *trace = nullptr, int base = 0) {
@@ -1282,6 +894,8 @@ __device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val
     if (npad > CH_TVS || nd > 64 || npad < 0 || nd < 0) return false;   // bug guard
     const double *dyn = B + CH_HDR;
     double *tv = B + CH_HDR + 4 * nd;
+    // wave-uniform solve constants, kept in SGPRs (scalar loads of the global record measured
+    // no faster: their lgkm waits merge with the LDS ones)
     auto U = [&](int k) {
         const double v = B[k];
         return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
@@ -1309,20 +923,29 @@ __device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val
     bool done = !has || crit;
     if (__ballot(far)) {
         long sp = 0;
-        double2 v = make_double2(0.0, 0.0);
+        const unsigned long long *gv = (const unsigned long long *)gval;
+        const int g = -e.y - 1;
         for (;;) {
-            if (far && !done && ch_probe(e.y, tag, val, gtag, gval, v)) {
+            if (far && !done) {
+                const int t = __hip_atomic_load(&gtag[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                const double vx = __longlong_as_double((long long)__hip_atomic_load(
+                    &gv[2 * g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                const double vy = __longlong_as_double((long long)__hip_atomic_load(
+                    &gv[2 * g + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (t == g) {   // the value was read after the tag (acquire): it is final
 #pragma unroll
-                for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
-                done = true;
+                    for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? vx : vy);
+                    done = true;
+                }
+                // consumed on every path that loaded them: no load of this block stays pending
+                // (else later register reuse waits on vmcnt -- the record prefetch included)
+                asm volatile("" ::"v"(vx), "v"(vy));
             }
             if (__ballot(far && !done) == 0) break;
             if (++sp > CH_SPIN_LIMIT) return false;
             __builtin_amdgcn_s_sleep(1);
         }
-        // a use of the probe's registers on this path only: no probe load is left pending past
-        // here (else the critical poll below would wait on vmcnt -- the record prefetch too)
-        asm volatile("" ::"v"(v.x), "v"(v.y));
     }
     // the critical source: its term position, slot, tag and coefficients (uniform)
     const u64 cm = __ballot(crit);
@@ -1331,7 +954,8 @@ __device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val
     const int eyc = __builtin_amdgcn_readlane(e.y, cl);
     const int slc = eyc & (CH_R - 1);
     const int m3 = lane % 3;
-    const double cfc = rlf(m3 == 0 ? cf[0] : (m3 == 1 ? cf[1] : cf[2]), cl);
+    const double cc0 = rlf(cf[0], cl), cc1 = rlf(cf[1], cl), cc2 = rlf(cf[2], cl);
+    const double cfc = m3 == 0 ? cc0 : (m3 == 1 ? cc1 : cc2);   // lane k: w * a_(k % 3)
     // pass 1: products of the other sources already published
     {
         const bool ready = !done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
@@ -1350,7 +974,7 @@ __device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val
     if (kmiss > kc) kmiss = kc;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (lane < 6) acc = ch_fold_rng(acc, tv + lane * npad, 0, kmiss);
+    if (lane < 6) acc = ch_fold_span(acc, tv + lane * npad, 0, kmiss);
     CH_STAMP(3);
     if (pend) {
         long sp = 0;
@@ -1372,19 +996,34 @@ __device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    if (lane < 6) acc = ch_fold_rng(acc, tv + lane * npad, kmiss, kc);
+    if (lane < 6) acc = ch_fold_span(acc, tv + lane * npad, kmiss, kc);
     if (cm) {
-        // first reads of the terms after kc, then the critical value
-        const double *row = tv + lane * npad + kc + 1;
-        const int nt = npad - kc - 1;
-        double r[8];
+        // the terms after kc: their head chunk and the next two in registers before the
+        // critical value arrives (pure VALU adds after it), the rest from LDS.  Rows are padded
+        // with +0.0 to whole chunks (exact: a sum that starts at +0.0 is never -0.0).
+        // (lanes 0-5 only: 64 lanes at a row stride would conflict on every LDS bank)
+        const double *row = tv + lane * npad;
+        const int h0 = (kc + 1) >> 3, hs = kc + 1 - 8 * h0, nch = npad >> 3;
+        // (the profiled build keeps one chunk: its counters need the registers)
+        constexpr int NRT = PROF ? 8 : 24;
+        double rt[NRT];
+        if (lane < 6) {
+            const double2 *r2 = (const double2 *)(row + 8 * h0);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = row[k];
+            for (int k = 0; k < NRT / 2; ++k) {
+                const double2 q = r2[k];
+                rt[2 * k] = q.x; rt[2 * k + 1] = q.y;
+            }
+            // pinned here: the compiler would otherwise sink these reads past the poll loop
+#pragma unroll
+            for (int k = 0; k < NRT; ++k) asm volatile("" : "+v"(rt[k]));
+        }
         double2 vc;
         long sp = 0;
         // the tag and the value read back to back in one LDS round trip (relaxed atomic
         // loads: a plain value load would be sunk out of the loop)
         const unsigned long long *vq = (const unsigned long long *)&val[slc];
+        __builtin_amdgcn_s_setprio(0);   // polling: leave the SIMD to the producers
         for (;;) {
             const int tg = __hip_atomic_load(&tag[slc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             asm volatile("" ::: "memory");             // the tag read is issued first
@@ -1402,9 +1041,26 @@ __device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val
             CH_STAMP(2);
             tr_ready = __builtin_amdgcn_s_memrealtime();
         }
+        __builtin_amdgcn_s_setprio(3);   // from the arrival through the publish
         if (lane < 6) {
             acc += cfc * (lane < 3 ? vc.x : vc.y);
-            CH_TAIL(acc, row, nt, r);
+            do {   // (straight-line: rt indexed statically)
+                if (h0 >= nch) break;   // kc was the last term
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k >= hs) acc += rt[k];
+                if constexpr (NRT > 8) {
+                    if (h0 + 1 >= nch) break;
+                    acc += rt[8]; acc += rt[9]; acc += rt[10]; acc += rt[11];
+                    acc += rt[12]; acc += rt[13]; acc += rt[14]; acc += rt[15];
+                }
+                if constexpr (NRT > 16) {
+                    if (h0 + 2 >= nch) break;
+                    acc += rt[16]; acc += rt[17]; acc += rt[18]; acc += rt[19];
+                    acc += rt[20]; acc += rt[21]; acc += rt[22]; acc += rt[23];
+                }
+                acc = ch_fold(acc, row, h0 + NRT / 8, nch);
+            } while (0);
         }
     }
     if constexpr (PROF) asm volatile("" : "+v"(acc));
@@ -1450,7 +1106,7 @@ __device__ __forceinline__ bool ch_fit4(int x, int lane, double *B, double2 *val
     return true;
 }
 
-template <bool PROF, int VAR>
+template <bool PROF>
 __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *gprof) {
     __shared__ double2 val[CH_R];
     __shared__ int tag[CH_R];
@@ -1498,13 +1154,8 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         if (x2 <= x) { ok = false; break; }   // bug guard: the wave's sequence must advance
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
-        bool fit_ok;
-        if constexpr ((VAR & 64) != 0)
-            fit_ok = ch_fit4<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag,
-                                        C.ws.gval, base + x, C.trace, base);
-        else
-            fit_ok = ch_fit<PROF, VAR>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag,
-                                       C.ws.gval, base + x, C.trace, base, C.ws.crit, C.ws.pred);
+        const bool fit_ok = ch_fit<PROF>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag,
+                                         C.ws.gval, base + x, C.trace, base);
         if (!fit_ok) { ok = false; break; }
         x = x2; r = r2;
     }
@@ -1551,10 +1202,7 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
     const unsigned idb = grid1d(ws.maxt, 256);
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
     k_ex_local<<<1, 1024, 0, st>>>(ws, ML);
-    // RMT_CH_RUNS=1: row-run wave assignment (measured slower: chain 4.32 vs 3.0 ms at
-    // N=4096 -- a fit's own set-up and prefix fold no longer overlap its predecessor's wait)
-    static const int runs = getenv("RMT_CH_RUNS") ? atoi(getenv("RMT_CH_RUNS")) != 0 : 0;
-    k_ex_runs<<<nparts, 1024, 0, st>>>(ws, runs);
+    k_ex_runs<<<nparts, 1024, 0, st>>>(ws);
     k_ex_relink<<<std::min<unsigned>(grid1d(ws.maxt, 4), 2048), 256, 0, st>>>(ws, ML);
     RMT_LAUNCHED();
     return RMT_OK;
@@ -1588,8 +1236,7 @@ int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r, 0};
     const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
     RMT_HIP(launch_done(k_ex_vals, dim3(gblocks), dim3(256), 0, ctx->stream,
-                        ctx->ev_chain_vals ? ctx->ev_chain : nullptr, A, ML,
-                        ctx->ex_pred1 ? ctx->ex_pred1 : X1o, ctx->ex_pred2 ? ctx->ex_pred2 : X2o));
+                        ctx->ev_chain_vals ? ctx->ev_chain : nullptr, A, ML));
     return RMT_OK;
 }
 
@@ -1602,21 +1249,8 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
     if (ctx->ev_chain && !ctx->ev_chain_vals) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status, nullptr};
     static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
-    const int var = ch_variant();
     if (!prof) {
-        switch (var) {
-            case 0: k_ex_chain<false, 0><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 1: k_ex_chain<false, 1><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 2: k_ex_chain<false, 2><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 35: k_ex_chain<false, 35><<<nparts, CH_W * 64, 0, st>>>(C, nullptr); break;
-            case 67:
-                if (nparts == 1) k_ex_chain<false, 83><<<1, CH_W * 64, 0, st>>>(C, nullptr);
-                else k_ex_chain<false, 67><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
-                break;
-            default:
-                if (nparts == 1) k_ex_chain<false, 19><<<1, CH_W * 64, 0, st>>>(C, nullptr);
-                else k_ex_chain<false, 3><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
-        }
+        k_ex_chain<false><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
         RMT_LAUNCHED();
     } else {
         // diagnostic: per-phase shader clocks summed over the chain waves
@@ -1636,8 +1270,7 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
             C.trace = dtr;
         }
         RMT_HIP(hipEventRecord(e0, st));
-        if (var == 67) k_ex_chain<true, 67><<<nparts, CH_W * 64, 0, st>>>(C, gp);
-        else k_ex_chain<true, 3><<<nparts, CH_W * 64, 0, st>>>(C, gp);
+        k_ex_chain<true><<<nparts, CH_W * 64, 0, st>>>(C, gp);
         RMT_LAUNCHED();
         RMT_HIP(hipEventRecord(e1, st));
         RMT_HIP(hipMemcpyAsync(hp, gp, sizeof(hp), hipMemcpyDeviceToHost, st));

@@ -89,10 +89,6 @@ struct rmt_ctx {
     // optional (sim.hip overlap): recorded on the stream right before the extrapolation's
     // serial chain kernel starts (or after the call when no chain kernel runs)
     hipEvent_t ev_chain = nullptr;
-    // optional (sim.hip): the previous step's extrapolated map, read by k_ex_vals as the
-    // chain's prediction of each fit's latest source (extrap_chain.hip, fast fold); null:
-    // the input map
-    const double *ex_pred1 = nullptr, *ex_pred2 = nullptr;
     // optional (sim.hip overlap): extrap_finish leaves the fallback sweep (an early exit unless
     // a chain capacity limit tripped) to the caller, who runs extrap_sweep on another stream
     // after ev_chain, beside the chain instead of ahead of it

@@ -15,6 +15,20 @@
 
 namespace rmt {
 
+// Test switches RMT_TEST_DELAY_SIDE / RMT_TEST_DELAY_MAIN = <n>: a one-thread kernel that
+// sleeps ~3.4 us x n on the second stream as it starts this step's work beside the chain, or
+// on the critical stream right after the chain.  Every cross-stream dependency is an event,
+// so shifting either stream's timing must leave the results bit-identical
+// (tests/test_gpu_env_variants.py: the regression test for stream hazards).
+__global__ void k_delay(int n) {
+    for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(127);
+}
+static int test_delay(const char *var) {
+    const char *e = getenv(var);
+    return e ? std::max(0, atoi(e)) : 0;
+}
+
+
 
 constexpr int DIAG_VALS = 10, DIAG_BLOCKS = 512, DIAG_T = 256;
 // ring record: [0, DIAG_VALS) the diagnostics, then max |u|^2, dt, the 4 step flags
@@ -900,9 +914,6 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             // chip-wide passes are done and the one-workgroup chain kernel is launched
             if (overlap) ctx->ev_chain = S->e_sl;
             const bool kb = P.scheme == RMT_SCHEME_SEMILAGRANGIAN;   // k_sim_sl wrote kbits
-            // the previous step's map (intact until the second stream's phi rebuild, which
-            // starts at the chain's launch) predicts the chain's latest sources
-            ctx->ex_pred1 = S->X1; ctx->ex_pred2 = S->X2;
             if (geo_ready && !overlap) RMT_HIP(hipStreamWaitEvent(st, S->e_geo, 0));
             // with the fused fix-up prep (below) the status words are copied by its kernel
             static const bool fp_env = !(getenv("RMT_FUSED_FIXPREP") && !atoi(getenv("RMT_FUSED_FIXPREP")));
@@ -918,13 +929,14 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                : extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, P.dx, P.dy, P.layers,
                                              S->X1n, S->X2n, dstat, kb ? S->kbits : nullptr);
             geo_ready = false;
-            ctx->ex_pred1 = ctx->ex_pred2 = nullptr;
             ctx->ev_chain = nullptr;
             ctx->ex_sweep_defer = false;
             ctx->ev_chain_vals = false;
             RMT_TRY(es);
             if (overlap) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
+                static const int dly_side = test_delay("RMT_TEST_DELAY_SIDE");
+                if (dly_side) { k_delay<<<1, 1, 0, S->st2>>>(dly_side); RMT_LAUNCHED(); }
                 if (fixprep && ctx->ex_chain && !ctx->ex_par)
                     RMT_TRY(extrap_sweep(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->st2));
                 // the previous step's tail, beside the chain (e_sl, recorded by this step's
@@ -995,6 +1007,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         static const bool mj_env = !(getenv("RMT_MERGED_JOIN") && !atoi(getenv("RMT_MERGED_JOIN")));
         const bool mjoin = overlap && mj_env && !par;
         if (overlap) {
+            static const int dly_main = test_delay("RMT_TEST_DELAY_MAIN");
+            if (dly_main) { k_delay<<<1, 1, 0, st>>>(dly_main); RMT_LAUNCHED(); }
             // 4 + 5 on the tiles the extrapolation can reach
             RMT_HIP(hipStreamWaitEvent(st, mjoin ? S->e_rows : S->e_mom, 0));
             const int tiles_x = (nx + MOM_TX - 1) / MOM_TX;

@@ -66,6 +66,20 @@ for s in "$@"; do
                 > "$O/${s}_write.log" 2>&1 || exit 1
             unset RMT_EXTRAP_PARALLEL
             echo "pmc passes done" ;;
+        trace)   # per-fit chain trace (the profiled build at 12 waves: at 16 its counters spill)
+            RMT_LIB=pyrmt_amd/librmt_w12.so RMT_EX_PROFILE=1 RMT_EX_TRACE=$O/trace.bin timeout -k 10 200 \
+                python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/trace.log" 2>&1 || { tail -5 "$O/trace.log"; exit 1; }
+            grep chain-prof "$O/trace.log" | tail -1
+            python3 tools/chain_trace.py "$O/trace.bin" > "$O/trace.txt" && head -5 "$O/trace.txt" ;;
+        cfg:*)   # one BASELINE config's bench line (CPU baseline included) and its kernel stats
+            c=${s#cfg:}
+            timeout -k 10 600 python -u bench.py --config $c --steps 10 --warmup 2 > "$O/cfg$c.log" 2>&1 \
+                || { tail -20 "$O/cfg$c.log"; exit 1; }
+            tail -1 "$O/cfg$c.log" | cut -c1-500
+            timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/kt_cfg$c" -o bench -- \
+                python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline > "$O/kt_cfg$c.log" 2>&1 || exit 1
+            f=$(find "$O/kt_cfg$c" -name "*kernel_stats.csv" | head -1); cp "$f" "$O/kt_cfg${c}_stats.csv"
+            cut -d, -f1-4 "$f" | head -12 ;;
         out:*) O=$BASE/${s#out:}; mkdir -p "$O" ;;
         env:*) export "${s#env:}"; echo "exported ${s#env:}" ;;
         *) echo "unknown step $s"; exit 2 ;;

@@ -10,7 +10,7 @@ projection (LDS DCT plan: 255 = 3 5 17) and with it the early transpose are on.
   RMT_NO_OVERLAP=1        no second stream at all
   RMT_SIM_SYNC=1          dt read back on the host every step
   RMT_CH_PARTS=1          the chain in one workgroup
-  RMT_CH_VARIANT=35       the chain's residue fast fold (sim.hip / extrap_chain.hip ch_fast)
+  RMT_CH_PARTS=4          the chain in four column parts (more cross-part hand-offs)
   RMT_FUSED_FLUID=0       the momentum's pure-fluid flags from their own pass over phi
   TEST_EX_MODE=2          (this file's child) the extrapolation's forced fallback sweep, which
                           the fused step runs on its second stream beside the chain
@@ -19,6 +19,9 @@ projection (LDS DCT plan: 255 = 3 5 17) and with it the early transpose are on.
                           completing with them (hipExtLaunchKernel)
   RMT_MERGED_JOIN=0       the second stream joined twice (after its momentum, before the
                           projection) instead of once after its row passes
+  RMT_TEST_DELAY_SIDE=300 the second stream sleeps ~1 ms as its work beside the chain starts
+  RMT_TEST_DELAY_MAIN=300 the critical stream sleeps ~1 ms right after the chain (both: every
+                          cross-stream read is ordered by an event, whatever the timing)
   RMT_FIX_ALL=1           the fix-up re-runs phi, the prep and the four stages on EVERY tile
                           (interior, edge and domain-boundary tiles through the list kernels;
                           the default's fix-up list holds interior tiles only for this disc) --
@@ -71,10 +74,11 @@ def default_run(tmp_path_factory, gpu):
 @pytest.mark.parametrize("env", [
     {"RMT_SIM_HIPRIO": "0"}, {"RMT_EARLY_TRANSPOSE": "0"}, {"RMT_EARLY_GEOMETRY": "0"},
     {"RMT_SIDE_TAIL": "0"}, {"RMT_NO_OVERLAP": "1"}, {"RMT_SIM_SYNC": "1"},
-    {"RMT_CH_PARTS": "1"}, {"RMT_CH_VARIANT": "35"}, {"RMT_FUSED_FLUID": "0"},
+    {"RMT_CH_PARTS": "1"}, {"RMT_CH_PARTS": "4"}, {"RMT_FUSED_FLUID": "0"},
     {"TEST_EX_MODE": "2"}, {"TEST_EX_MODE": "2", "RMT_FUSED_FIXPREP": "0"},
     {"RMT_FUSED_FIXPREP": "0"}, {"RMT_EXT_EVENTS": "0"},
-    {"RMT_MERGED_JOIN": "0"}, {"RMT_FIX_ALL": "1"}, {"RMT_FIX_ALL": "1", "RMT_SIM_HIPRIO": "0"},
+    {"RMT_MERGED_JOIN": "0"}, {"RMT_TEST_DELAY_SIDE": "300"}, {"RMT_TEST_DELAY_MAIN": "300"},
+    {"RMT_TEST_DELAY_SIDE": "300", "RMT_FIX_ALL": "1"}, {"RMT_FIX_ALL": "1"}, {"RMT_FIX_ALL": "1", "RMT_SIM_HIPRIO": "0"},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(tmp_path, default_run, env):
     got = _run(tmp_path, "variant", env)
