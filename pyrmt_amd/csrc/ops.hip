@@ -417,6 +417,103 @@ __global__ void k_divergence_rc(const double *__restrict__ a, const double *__re
     if (i >= nx || j >= je) return;
     div_rc_cell(a, b, p, ny, nx, d_f, K, divU, rho, dt, j, i);
 }
+// k_divergence_rc over the whole grid in 64 x 16 tiles staged through LDS: p on the tile + 2
+// (rows and columns), a* on the tile + 1 column, b* on the tile + 1 row.  Each stencil value
+// is loaded from global memory once per tile (the row kernel's five p rows per output row
+// were five L2 round trips per cell, ~70 % of its wave time waiting); the arithmetic is
+// div_rc_cell's on the staged copies, operand for operand.  One-dimensional grid, tiles
+// grouped per XCD (each XCD's L2 sees a contiguous band of tile rows and their halos).
+constexpr int DVT_X = 64, DVT_Y = 16, DVT_PX = DVT_X + 4, DVT_PY = DVT_Y + 4;
+constexpr int DVT_AX = DVT_X + 2, DVT_BY = DVT_Y + 2;
+__global__ void __launch_bounds__(256) k_divergence_t(const double *__restrict__ a,
+                                                      const double *__restrict__ b,
+                                                      const double *__restrict__ p, int ny, int nx,
+                                                      double d_f, RcDiv K,
+                                                      double *__restrict__ divU, double rho,
+                                                      double dt, const double *__restrict__ dtp,
+                                                      int tiles_x, int ntiles) {
+    __shared__ double sp[DVT_PY * DVT_PX], sa[DVT_Y * DVT_AX], sb[DVT_BY * DVT_X];
+    if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
+    const int per = ntiles / 8, bk = blockIdx.x;
+    const int tile = bk < 8 * per ? (bk % 8) * per + bk / 8 : bk;
+    const int i0 = (tile % tiles_x) * DVT_X, j0 = (tile / tiles_x) * DVT_Y;
+    constexpr int NP = (DVT_PY * DVT_PX + 255) / 256, NA = (DVT_Y * DVT_AX + 255) / 256,
+                  NB = (DVT_BY * DVT_X + 255) / 256;
+    double vp[NP], va[NA], vb[NB];
+    // every load issued before the first LDS write (cells outside the grid: never read by an
+    // interior cell's stencil, which turns one-sided at the edges)
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const int q = threadIdx.x + 256 * k, r = q / DVT_PX, s = q % DVT_PX;
+        const int j = j0 - 2 + r, i = i0 - 2 + s;
+        const bool ok = q < DVT_PY * DVT_PX && j >= 0 && j < ny && i >= 0 && i < nx;
+        vp[k] = ok ? p[(long)j * nx + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        const int q = threadIdx.x + 256 * k, r = q / DVT_AX, s = q % DVT_AX;
+        const int j = j0 + r, i = i0 - 1 + s;
+        const bool ok = q < DVT_Y * DVT_AX && j < ny && i >= 0 && i < nx;
+        va[k] = ok ? a[(long)j * nx + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const int q = threadIdx.x + 256 * k, r = q / DVT_X, s = q % DVT_X;
+        const int j = j0 - 1 + r, i = i0 + s;
+        const bool ok = q < DVT_BY * DVT_X && j >= 0 && j < ny && i < nx;
+        vb[k] = ok ? b[(long)j * nx + i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const int q = threadIdx.x + 256 * k;
+        if (q < DVT_PY * DVT_PX) sp[q] = vp[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+        const int q = threadIdx.x + 256 * k;
+        if (q < DVT_Y * DVT_AX) sa[q] = va[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        const int q = threadIdx.x + 256 * k;
+        if (q < DVT_BY * DVT_X) sb[q] = vb[k];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 63, ty0 = threadIdx.x >> 6;
+#pragma unroll
+    for (int ty = ty0; ty < DVT_Y; ty += 4) {
+        const int j = j0 + ty, i = i0 + tx;
+        if (j >= ny || i >= nx) continue;
+        const long c = (long)j * nx + i;
+        if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) {
+            divU[c] = rho > 0 ? (rho * 0.0) / dt : 0.0;
+            continue;
+        }
+        // div_rc_cell, with p, a, b at the staged copies (strides DVT_PX, 1, DVT_X)
+        const double *pc = sp + (ty + 2) * DVT_PX + tx + 2;
+        const double *ac = sa + ty * DVT_AX + tx + 1;
+        const double *bc = sb + (ty + 1) * DVT_X + tx;
+        const long PS = DVT_PX, BS = DVT_X;
+        double gxl = grad2k(pc - 1, 1, i - 1, nx, K.x2), gxc = grad2k(pc, 1, i, nx, K.x2),
+               gxr = grad2k(pc + 1, 1, i + 1, nx, K.x2);
+        double gyd = grad2k(pc - PS, PS, j - 1, ny, K.y2), gyc = grad2k(pc, PS, j, ny, K.y2),
+               gyu = grad2k(pc + PS, PS, j + 1, ny, K.y2);
+        double ue = 0.5 * (ac[0] + ac[1]) - d_f * (divk(pc[1] - pc[0], K.x1) - 0.5 * (gxc + gxr));
+        double uw = 0.5 * (ac[-1] + ac[0]) - d_f * (divk(pc[0] - pc[-1], K.x1) - 0.5 * (gxl + gxc));
+        double vn = 0.5 * (bc[0] + bc[BS]) - d_f * (divk(pc[PS] - pc[0], K.y1) - 0.5 * (gyc + gyu));
+        double vs = 0.5 * (bc[-BS] + bc[0]) - d_f * (divk(pc[0] - pc[-PS], K.y1) - 0.5 * (gyd + gyc));
+        const double d = divk(ue - uw, K.x1) + divk(vn - vs, K.y1);
+        divU[c] = rho > 0 ? (rho * d) / dt : d;
+    }
+}
+static int divergence_full(hipStream_t st, const double *a, const double *b, const double *p,
+                           int ny, int nx, double d_f, const RcDiv &K, double *divU, double rho,
+                           double dt, const double *dtp) {
+    const int tx = (nx + DVT_X - 1) / DVT_X, nt = tx * ((ny + DVT_Y - 1) / DVT_Y);
+    k_divergence_t<<<nt, 256, 0, st>>>(a, b, p, ny, nx, d_f, K, divU, rho, dt, dtp, tx, nt);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
 // The rhs on the listed MOM_TX x MOM_TY tiles grown by one cell (the cells whose stencil
 // reads a u*, v* the momentum fix-up rewrote); one block per tile.  Overlapping grown tiles
 // write the same value twice.
@@ -771,7 +868,8 @@ int rmt_apply_velocity_bc(rmt_ctx *ctx, int bc_kind, double lid, double *u, doub
 }
 int rmt_divergence_rc(rmt_ctx *ctx, const double *a, const double *b, const double *p,
                       double d_f, double dx, double dy, double *divU) {
-    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a, b, p, ctx->ny, ctx->nx, d_f, rc_div(dx, dy), divU, 0, ctx->ny);
+    RMT_TRY(divergence_full(ctx->stream, a, b, p, ctx->ny, ctx->nx, d_f, rc_div(dx, dy), divU, 0.0,
+                            1.0, nullptr));
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -799,8 +897,8 @@ int rmt_pressure_projection(rmt_ctx *ctx, const double *a_star, const double *b_
     double *rhs = ctx->scratch, *pc = rhs + n;
     // functions.py:1292-1295 + :1331: rhs = rho * divU / dt, d_f = dt / mean(rho)
     if (p_prev && rho > 0) {
-        k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho,
-                                         rc_div(dx, dy), rhs, 0, ctx->ny, rho, dt);
+        RMT_TRY(divergence_full(ctx->stream, a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho,
+                                rc_div(dx, dy), rhs, rho, dt, nullptr));
         RMT_LAUNCHED();
     } else {
         if (p_prev) RMT_TRY(rmt_divergence_rc(ctx, a_star, b_star, p_prev, dt / rho, dx, dy, rhs));
@@ -858,6 +956,9 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
         k_divergence_tiles<<<list_grid(max_tiles), 256, 0, ctx->stream>>>(
             a_star, b_star, p_prev, ctx->ny, ctx->nx, rc_div(dx, dy), rhs, rho, dt, dtp, tiles, tcount,
             (ctx->nx + MOM_TX - 1) / MOM_TX);
+    else if (!rowmark)
+        RMT_TRY(divergence_full(ctx->stream, a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho,
+                                rc_div(dx, dy), rhs, rho, dt, dtp));
     else
         k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
             a_star, b_star, p_prev, ctx->ny, ctx->nx, dt / rho, rc_div(dx, dy), rhs, 0, ctx->ny, rho, dt,
@@ -889,9 +990,8 @@ int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, dou
     const long n = (long)ctx->ny * ctx->nx;
     RMT_TRY(ensure_scratch(ctx, 2 * n * sizeof(double)));
     double *rhs = ctx->scratch, *pc = rhs + n;
-    k_divergence_rc<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(
-        a_star, b_star, p_prev, ctx->ny, ctx->nx, 0.0, rc_div(dx, dy), rhs, 0, ctx->ny, rho, 1.0, dtp);
-    RMT_LAUNCHED();
+    RMT_TRY(divergence_full(ctx->stream, a_star, b_star, p_prev, ctx->ny, ctx->nx, 0.0,
+                            rc_div(dx, dy), rhs, rho, 1.0, dtp));
     double *root = ctx->red + RED_BLOCKS + 17;
     RMT_TRY(dct_solve(ctx, rhs, dx, dy, pc, root));
     k_project_correct<<<rows_grid(ctx->nx, 0, ctx->ny), 256, 0, ctx->stream>>>(

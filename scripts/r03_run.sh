@@ -66,6 +66,17 @@ for s in "$@"; do
                 > "$O/${s}_write.log" 2>&1 || exit 1
             unset RMT_EXTRAP_PARALLEL
             echo "pmc passes done" ;;
+        pmcchain)   # issue counters of the chain kernel (two passes)
+            timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS \
+                SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS \
+                --kernel-include-regex "k_ex_chain" --kernel-trace -T -f csv -d "$O/pmcchain1" -o c1 -- \
+                python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmcchain1.log" 2>&1 || exit 1
+            timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY \
+                SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_LDS_BANK_CONFLICT \
+                --kernel-include-regex "k_ex_chain" --kernel-trace -T -f csv -d "$O/pmcchain2" -o c2 -- \
+                python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmcchain2.log" 2>&1 || exit 1
+            for f in $(find "$O/pmcchain1" "$O/pmcchain2" -name "*counter_collection.csv"); do cp "$f" "$O/$(basename $(dirname $f))_$(basename $f)"; done
+            echo "pmcchain done" ;;
         trace)   # per-fit chain trace (the profiled build at 12 waves: at 16 its counters spill)
             RMT_LIB=pyrmt_amd/librmt_w12.so RMT_EX_PROFILE=1 RMT_EX_TRACE=$O/trace.bin timeout -k 10 200 \
                 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/trace.log" 2>&1 || { tail -5 "$O/trace.log"; exit 1; }
