@@ -172,8 +172,7 @@ int rmt_momentum_step_rk4(rmt_ctx *ctx, const rmt_momentum_params *prm, const do
                           double *sxy, double *syy, double *J);
 
 /* librmt diagnostic (no reference counterpart): 0 (default) one LDS-tiled kernel per RK4
- * stage, 1 the four stages of a tile in one temporally blocked kernel (per-stage kernels for
- * periodic BCs), 2 unfused per-cell passes.  Bit-identical results in every mode. */
+ * stage, 2 unfused per-cell passes.  Bit-identical results in both; other modes: RMT_EINVAL. */
 int rmt_momentum_set_mode(int mode);
 
 /* ---- projection (functions.py:1005-1364) ------------------------------------------- */

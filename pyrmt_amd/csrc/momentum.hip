@@ -867,515 +867,12 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
     return RMT_OK;
 }
 
-// ------------------------------------------------------------ row-streaming stage ----
-// mode 3: one RK4 stage with the same per-cell arithmetic, in the same order, as k_mom_stage
-// (bit-identical), organised for CDNA: one wave owns a strip of MR_OUT output columns and
-// walks MR_H rows down it.  Lane L holds column x0 - 2 + L (outputs on lanes 2..61); the
-// horizontal neighbours come from wave-wide DPP shifts, the vertical ones from rolling
-// register windows of rows (stage velocity: 7 rows, blended stress: 5, H: 3), so there is no
-// LDS, no barrier and no 2-D halo recompute (1.07x in x, (MR_H + 7) / MR_H in y).  Every
-// global load is issued one row ahead of its use.  Row r of the stage velocity arrives in
-// iteration r; the stress of row r - 2 and the RHS of row r - 4 follow in the same iteration.
-constexpr int MR_OUT = 60, MR_H = 64;
-
-struct MrArgs {
-    const double *u, *v, *kpu, *kpv, *p, *sxx, *sxy, *syy, *H;
-    const unsigned char *solid, *fluid;   // fluid: k_fluid_rows' flags, row lo first (or null)
-    const double *k1u, *k1v, *k2u, *k2v;  // stage 3: k1, k2 (k3 = kpu / kpv)
-    double *ku, *kv, *outu, *outv;
-    const double *dtp;
-    double coef, dt6, lid, mu_f, eta_s, rho_s, rho_f;
-    int stage, bc, visc, ny, nx, tiles_x, nstrips, nchunks;
-    RowWin rw;                            // outputs on rows [rw.jb, rw.je); resident [lo, hi)
-    MomDiv K;
-};
-
-// lane + 1 / lane - 1 of a double across the wave (DPP wave shifts; the edge lane gets 0)
-__device__ __forceinline__ double mr_next(double x) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x130, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x130, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double mr_prev(double x) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xf, 0xf, false);
-    return __hiloint2double(hi, lo);
-}
-// grad2 / upwind3 (rmt_internal.hpp) on the five values f[k-2 .. k+2] of a line, index k of n
-template <bool IN>
-__device__ __forceinline__ double mr_g2(double m2, double m1, double f0, double p1, double p2,
-                                        int k, int n, const DivK &K2) {
-    if (!IN) {
-        if (k == 0) return divk(-3 * f0 + 4 * p1 - p2, K2);
-        if (k == n - 1) return divk(3 * f0 - 4 * m1 + m2, K2);
-    }
-    return divk(p1 - m1, K2);
-}
-template <bool IN>
-__device__ __forceinline__ double mr_u3(double m2, double m1, double f0, double p1, double p2,
-                                        int k, int n, double vel, const DivK &K6,
-                                        const DivK &K1) {
-    if (IN || (k >= 2 && k < n - 2)) {
-        const double a = 2 * p1 + 3 * f0 - 6 * m1 + m2;
-        const double b = -p2 + 6 * p1 - 3 * f0 - 2 * m1;
-        return divk(vel > 0 ? a : b, K6);
-    }
-    if (vel > 0 && k > 0) return divk(f0 - m1, K1);
-    if (vel <= 0 && k < n - 1) return divk(p1 - f0, K1);
-    if (k > 0) return divk(f0 - m1, K1);
-    if (k < n - 1) return divk(p1 - f0, K1);
-    return 0.0;
-}
-
-template <bool IN, bool SQ, bool S3>
-__global__ void __launch_bounds__(256) k_mom_rows(MrArgs A) {
-    const int lane = threadIdx.x & 63;
-    const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (wid >= A.nstrips * A.nchunks) return;
-    const int strip = wid % A.nstrips, chunk = wid / A.nstrips;
-    const int nx = A.nx, ny = A.ny, lo = A.rw.lo, hi = A.rw.hi;
-    const int x0 = strip * MR_OUT, i = x0 - 2 + lane;
-    const int y0 = A.rw.jb + chunk * MR_H, y1 = min(A.rw.je, y0 + MR_H);
-    // interior wave: every column / row it touches is >= 2 from the domain edges and inside
-    // the resident rows (no BC source, no one-sided stencil, no zero fill)
-    const bool interior = x0 - 2 >= 2 && x0 + 61 <= nx - 3 && y0 - 4 >= max(lo, 2) &&
-                          y1 + 3 <= min(hi, ny - 2) - 1;
-    if (interior != IN) return;
-    const MomDiv &K = A.K;
-    const DivK &Ky2 = SQ ? K.x2 : K.y2, &Ky6 = SQ ? K.x6 : K.y6, &Ky1 = SQ ? K.x1 : K.y1;
-    double coef = A.coef, dt6 = A.dt6;
-    if (A.dtp) {   // the same roundings as mom_stage's host constants
-        const double dt = *A.dtp;
-        coef = A.stage == 0 ? 0.0 : A.stage == 3 ? dt : 0.5 * dt;
-        dt6 = dt / 6.0;
-    }
-    const int stage = S3 ? 3 : A.stage;   // S3: the last stage (u* = u + dt/6 (acc + k4))
-    const bool col_ok = i >= 0 && i < nx;
-    // windows: Wu/Wv rows r-6 .. r (index 6 = newest), S* stress rows r-6 .. r-2, Hw rows
-    // r-6 .. r-2 of H at the stress cells (RHS row r-4 reads index 2)
-    double Wu[7], Wv[7], Sx[5], Sm[5], Sy[5], Hw[5];
-#pragma unroll
-    for (int q = 0; q < 7; ++q) { Wu[q] = 0.0; Wv[q] = 0.0; }
-#pragma unroll
-    for (int q = 0; q < 5; ++q) { Sx[q] = 0.0; Sm[q] = 0.0; Sy[q] = 0.0; Hw[q] = 1.0; }
-    // prefetched operands of the next iteration
-    double na = 0.0, nb = 0.0, nka = 0.0, nkb = 0.0;   // W row r + 1 (at its BC sources)
-    bool nuc = false, nvc = false, nok = false;
-    double nuval = 0.0;
-    double ne1 = 0.0, ne2 = 0.0, ne3 = 0.0, nh = 1.0;  // stress row r - 1 inputs
-    bool nsol = false, nsok = false;
-    auto load_w = [&](int r) {
-        nok = col_ok && r >= lo && r < hi;
-        long cu, cv;
-        if (IN) {
-            nuc = false; nvc = false; nuval = 0.0;
-            cu = cv = (long)r * nx + i;
-        } else {
-            const BCSrc b = bc_source(A.bc, A.lid, nok ? r : 1, nok ? i : 1, ny, nx);
-            nuc = b.u_const; nvc = b.v_const; nuval = b.u_val;
-            cu = nok ? b.u_src : (long)lo * nx; cv = nok ? b.v_src : (long)lo * nx;
-        }
-        na = A.u[cu]; nb = A.v[cv];
-        nka = stage ? A.kpu[cu] : 0.0; nkb = stage ? A.kpv[cv] : 0.0;
-    };
-    auto load_s = [&](int j) {   // stress-row inputs (pure-fluid rows: the constants)
-        nsok = col_ok && j >= lo && j < hi;
-        bool fluid = false;
-        if (A.fluid && j >= lo && j < hi) {
-            const int ta = max(x0 - 1, 0) / 64, tb = min(x0 + 60, nx - 1) / 64;
-            const unsigned char *fr = A.fluid + (long)(j - lo) * A.tiles_x;
-            fluid = fr[ta] && fr[tb];
-        }
-        if (fluid) {
-            ne1 = 0.0; ne2 = 0.0; ne3 = 0.0; nh = 1.0; nsol = false;
-        } else {
-            const long c = nsok ? (long)j * nx + i : (long)lo * nx;
-            ne1 = A.sxx[c]; ne2 = A.syy[c]; ne3 = A.sxy[c]; nh = A.H[c];
-            nsol = A.solid[c] != 0;
-        }
-    };
-    const int r0 = y0 - 4, r1 = y1 + 3;   // W rows [r0, r1], stress rows [y0 - 2, y1 + 1]
-    load_w(r0);
-    load_s(r0 - 2);
-    for (int r = r0; r <= r1; ++r) {
-        // 1. the stage velocity of row r (BC applied), into the window
-        {
-            const double a = na, b = nb, ka = nka, kb = nkb, uval = nuval;
-            const bool ok = nok, uc = nuc, vc = nvc;
-            if (r + 1 <= r1) load_w(r + 1);
-            const double ru = stage == 0 ? a : a + coef * ka;
-            const double rv = stage == 0 ? b : b + coef * kb;
-#pragma unroll
-            for (int q = 0; q < 6; ++q) { Wu[q] = Wu[q + 1]; Wv[q] = Wv[q + 1]; }
-            Wu[6] = !ok ? 0.0 : uc ? uval : ru;
-            Wv[6] = !ok ? 0.0 : vc ? 0.0 : rv;
-        }
-        // 2. the blended stress of row j = r - 2 (rows j-2 .. j+2 of W at indices 2 .. 6)
-        {
-            const int j = r - 2;
-            const double e1i = ne1, e2i = ne2, e3i = ne3, hs = nh;
-            const bool sol = nsol, sok = nsok;
-            load_s(j + 1);
-            double oxx = 0.0, oxy = 0.0, oyy = 0.0;
-            const double u0 = Wu[4], v0 = Wv[4];
-            const double up1 = mr_next(u0), um1 = mr_prev(u0), vp1 = mr_next(v0), vm1 = mr_prev(v0);
-            // (every cross-lane read outside divergent code: all lanes active)
-            double up2 = 0.0, um2 = 0.0, vp2 = 0.0, vm2 = 0.0;
-            if (!IN) { up2 = mr_next(up1); um2 = mr_prev(um1); vp2 = mr_next(vp1); vm2 = mr_prev(vm1); }
-            if (sok && j >= y0 - 2) {
-                const double dudx = mr_g2<IN>(um2, um1, u0, up1, up2, i, nx, K.x2);
-                const double dvdy = mr_g2<IN>(Wv[2], Wv[3], v0, Wv[5], Wv[6], j, ny, Ky2);
-                const double dudy = mr_g2<IN>(Wu[2], Wu[3], u0, Wu[5], Wu[6], j, ny, Ky2);
-                const double dvdx = mr_g2<IN>(vm2, vm1, v0, vp1, vp2, i, nx, K.x2);
-                double e1 = e1i, e2 = e2i, e3 = e3i;
-                if (A.visc && sol) {
-                    e1 = e1 + A.eta_s * dudx;
-                    e2 = e2 + A.eta_s * dvdy;
-                    e3 = e3 + A.eta_s * 0.5 * (dudy + dvdx);
-                }
-                const double h = hs, omh = 1 - h;
-                oxx = h * (2 * A.mu_f * dudx) + omh * e1;
-                oyy = h * (2 * A.mu_f * dvdy) + omh * e2;
-                oxy = h * (A.mu_f * (dudy + dvdx)) + omh * e3;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { Sx[q] = Sx[q + 1]; Sm[q] = Sm[q + 1]; Sy[q] = Sy[q + 1]; Hw[q] = Hw[q + 1]; }
-            Sx[4] = oxx; Sm[4] = oxy; Sy[4] = oyy; Hw[4] = hs;
-        }
-        // 3. the RHS of row j = r - 4: stress rows j-2 .. j+2 at S[0..4], W rows j-2 .. j+2
-        //    at indices 0 .. 4
-        const int j = r - 4;
-        if (j < y0 || j >= y1) continue;
-        const bool out = col_ok && lane >= 2 && lane < 2 + MR_OUT && i < nx;
-        const long c = (long)j * nx + i;
-        // grad p operands (the same expressions as k_mom_stage)
-        double pc = 0.0, pxp = 0.0, pxm = 0.0, pyp = 0.0, pym = 0.0, px2 = 0.0, py2 = 0.0;
-        double x0v = 0.0, y0v = 0.0, x1v = 0.0, y1v = 0.0;
-        if (out) {
-            const bool exd = i == 0 || i == nx - 1, eyd = j == 0 || j == ny - 1;
-            const long sx = i == nx - 1 ? -1 : 1, sy = j == ny - 1 ? -(long)nx : (long)nx;
-            pc = A.p[c];
-            pxp = A.p[c + sx]; pxm = !exd ? A.p[c - 1] : 0.0;
-            pyp = A.p[c + sy]; pym = !eyd ? A.p[c - nx] : 0.0;
-            if (!IN) {
-                if (i == 0) px2 = A.p[c + 2]; else if (i == nx - 1) px2 = A.p[c - 2];
-                if (j == 0) py2 = A.p[c + 2L * nx]; else if (j == ny - 1) py2 = A.p[c - 2L * nx];
-            }
-            if (S3) {
-                x0v = (A.k1u[c] + 2 * A.k2u[c]) + 2 * A.kpu[c];
-                y0v = (A.k1v[c] + 2 * A.k2v[c]) + 2 * A.kpv[c];
-                x1v = A.u[c]; y1v = A.v[c];
-            }
-        }
-        const double gx0 = Sx[2], gm0 = Sm[2], gy0 = Sy[2];
-        const double gxp = mr_next(gx0), gxm = mr_prev(gx0), gmp = mr_next(gm0), gmm = mr_prev(gm0);
-        double gxp2 = 0.0, gxm2 = 0.0, gmp2 = 0.0, gmm2 = 0.0;
-        if (!IN) { gxp2 = mr_next(gxp); gxm2 = mr_prev(gxm); gmp2 = mr_next(gmp); gmm2 = mr_prev(gmm); }
-        const double u0 = Wu[2], v0 = Wv[2];
-        const double up1 = mr_next(u0), um1 = mr_prev(u0), vp1 = mr_next(v0), vm1 = mr_prev(v0);
-        const double up2 = mr_next(up1), um2 = mr_prev(um1), vp2 = mr_next(vp1), vm2 = mr_prev(vm1);
-        if (!out) continue;
-        const double divx = mr_g2<IN>(gxm2, gxm, gx0, gxp, gxp2, i, nx, K.x2) +
-                            mr_g2<IN>(Sm[0], Sm[1], gm0, Sm[3], Sm[4], j, ny, Ky2);
-        const double divy = mr_g2<IN>(gmm2, gmm, gm0, gmp, gmp2, i, nx, K.x2) +
-                            mr_g2<IN>(Sy[0], Sy[1], gy0, Sy[3], Sy[4], j, ny, Ky2);
-        const double uc = u0, vc = v0;
-        const double uadv = -uc * mr_u3<IN>(um2, um1, u0, up1, up2, i, nx, uc, K.x6, K.x1) -
-                            vc * mr_u3<IN>(Wu[0], Wu[1], u0, Wu[3], Wu[4], j, ny, vc, Ky6, Ky1);
-        const double vadv = -uc * mr_u3<IN>(vm2, vm1, v0, vp1, vp2, i, nx, uc, K.x6, K.x1) -
-                            vc * mr_u3<IN>(Wv[0], Wv[1], v0, Wv[3], Wv[4], j, ny, vc, Ky6, Ky1);
-        double dpx, dpy;
-        if (IN) {
-            dpx = divk(pxp - pxm, K.x2);
-            dpy = divk(pyp - pym, Ky2);
-        } else {
-            if (i == 0) dpx = divk(-3 * pc + 4 * pxp - px2, K.x2);
-            else if (i == nx - 1) dpx = divk(3 * pc - 4 * pxp + px2, K.x2);
-            else dpx = divk(pxp - pxm, K.x2);
-            if (j == 0) dpy = divk(-3 * pc + 4 * pyp - py2, Ky2);
-            else if (j == ny - 1) dpy = divk(3 * pc - 4 * pyp + py2, Ky2);
-            else dpy = divk(pyp - pym, Ky2);
-        }
-        const double h = Hw[2];
-        double k1, k2;
-        if (K.den_const) {
-            const double nu = divx + 0.0 - dpx, nv = divy + 0.0 - dpy;
-            k1 = uadv + divk(h == h ? nu : h, K.den);
-            k2 = vadv + divk(h == h ? nv : h, K.den);
-        } else {
-            const double den = ((1 - h) * A.rho_s + h * A.rho_f) + 1e-12;
-            k1 = uadv + (divx + 0.0 - dpx) / den;
-            k2 = vadv + (divy + 0.0 - dpy) / den;
-        }
-        if (!S3) {
-            A.ku[c] = k1; A.kv[c] = k2;
-        } else {
-            A.outu[c] = x1v + dt6 * (x0v + k1);
-            A.outv[c] = y1v + dt6 * (y0v + k2);
-        }
-    }
-}
-
-// one row-streaming stage launch (mode 3) over rows [ws.jb, ws.je); fluid: row flags
-static int mom_rows(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const double *u,
-                    const double *v, const double *p, const double *sxx, const double *sxy,
-                    const double *syy, const MomWork &W, double *u_new, double *v_new,
-                    RowWin ws, const unsigned char *fluid) {
-    const int nx = ctx->nx, ny = ctx->ny;
-    double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
-    MrArgs A{};
-    A.u = u; A.v = v; A.kpu = s ? ku[s - 1] : u; A.kpv = s ? kv[s - 1] : v; A.p = p;
-    A.sxx = sxx; A.sxy = sxy; A.syy = syy; A.H = W.H; A.solid = W.solid; A.fluid = fluid;
-    A.k1u = W.k1u; A.k1v = W.k1v; A.k2u = W.k2u; A.k2v = W.k2v;
-    A.ku = s < 3 ? ku[s] : nullptr; A.kv = s < 3 ? kv[s] : nullptr; A.outu = u_new; A.outv = v_new;
-    A.dtp = W.dtp;
-    A.coef = s == 0 ? 0.0 : s == 3 ? P->dt : 0.5 * P->dt; A.dt6 = P->dt / 6.0;
-    A.lid = P->lid; A.mu_f = P->mu_f; A.eta_s = P->eta_s; A.rho_s = P->rho_s; A.rho_f = P->rho_f;
-    A.stage = s; A.bc = P->bc_kind; A.visc = P->eta_s > 0.0; A.ny = ny; A.nx = nx;
-    A.tiles_x = (nx + MS_TX - 1) / MS_TX;
-    A.nstrips = (nx + MR_OUT - 1) / MR_OUT;
-    A.nchunks = (ws.je - ws.jb + MR_H - 1) / MR_H;
-    A.rw = ws;
-    A.K = mom_div(P->dx, P->dy, P->rho_s, P->rho_f);
-    const long waves = (long)A.nstrips * A.nchunks;
-    if (waves <= 0) return RMT_OK;
-    const unsigned blocks = grid1d(waves, 4);
-    auto launch = [&](auto kin, auto kedge) {
-        kin<<<blocks, 256, 0, ctx->stream>>>(A);
-        kedge<<<blocks, 256, 0, ctx->stream>>>(A);
-    };
-    const bool sq = P->dx == P->dy, s3 = s == 3;
-    if (sq && s3) launch(k_mom_rows<true, true, true>, k_mom_rows<false, true, true>);
-    else if (sq) launch(k_mom_rows<true, true, false>, k_mom_rows<false, true, false>);
-    else if (s3) launch(k_mom_rows<true, false, true>, k_mom_rows<false, false, true>);
-    else launch(k_mom_rows<true, false, false>, k_mom_rows<false, false, false>);
-    RMT_LAUNCHED();
-    return RMT_OK;
-}
-
-// ------------------------------------------------------------ temporally blocked RK4 --
-// The four stages of one MS_TX x MS_TY output tile in one workgroup.  Stage s needs stage s-1 two
-// cells out (upwind3 / grad2 of the blended stress), so on the tile plus an 8-cell halo the
-// stage velocity lives in LDS on halo 2(3-s)+2, the blended stress on 2(3-s)+1 and k is formed
-// on 2(3-s); the per-cell inputs (u, v, elastic stress, H, grad p) and the RK4 accumulators
-// stay in registers.  HBM sees u, v, p, sxx, sxy, syy, H, solid once and u*, v* once (the
-// per-stage kernel moves ~16 planes per stage).  The per-cell arithmetic and its order are
-// k_mom_stage's (bit-identical).  Not for periodic BCs, whose sources lie across the domain.
-struct Rk4Args {
-    const double *u, *v, *p, *sxx, *sxy, *syy, *H;
-    const unsigned char *solid;
-    double *outu, *outv;
-    const int *tlist, *tcount;   // listed tiles (fix-up), else every tile of rows [rw.jb, rw.je)
-    const double *dtp;           // device dt, or null: dt
-    double dt, lid, mu_f, eta_s, rho_s, rho_f, dx, dy;
-    int bc, visc, ny, nx, tiles_x, ntiles, olo, ohi;   // outputs on rows [olo, ohi)
-    RowWin rw;
-    MomDiv K;
-};
-constexpr int RK_HL = 8;
-template <int MS_TX, int MS_TY>
-constexpr int rk4_lds() { return 5 * (MS_TX + 2 * RK_HL) * (MS_TY + 2 * RK_HL) * (int)sizeof(double); }
-
-template <int MS_TX, int MS_TY, int NT>
-__global__ void __launch_bounds__(NT) k_mom_rk4(Rk4Args A) {
-    constexpr int HL = RK_HL, RX = MS_TX + 2 * HL, RY = MS_TY + 2 * HL, NR = RX * RY;
-    constexpr int NQ = (NR + NT - 1) / NT;
-    extern __shared__ double rk_lds[];
-    double *U = rk_lds, *V = U + NR, *GX = V + NR, *GM = GX + NR, *GY = GM + NR;
-    if (A.tlist && (int)blockIdx.x >= *A.tcount) return;
-    const int tile = A.tlist ? A.tlist[blockIdx.x] : xcd_tile(blockIdx.x, A.ntiles);
-    const int ri = (tile % A.tiles_x) * MS_TX - HL, rj = A.rw.jb + (tile / A.tiles_x) * MS_TY - HL;
-    const int nx = A.nx, ny = A.ny;
-    const MomDiv &K = A.K;
-    const double dt = A.dtp ? *A.dtp : A.dt;
-    // mom_stage's constants: coef {0, dt/2, dt/2, dt}, dt / 6
-    const double chalf = 0.5 * dt, dt6 = dt / 6.0;
-    const bool edge_fix = A.bc == RMT_BC_FREESLIP_BOX &&
-                          (ri <= 0 || rj <= 0 || ri + RX >= nx || rj + RY >= ny);
-    double u0[NQ], v0[NQ], ex[NQ], ey[NQ], exy[NQ], hh[NQ], dpx[NQ], dpy[NQ], au[NQ], av[NQ];
-    unsigned okm = 0, solm = 0, ucm = 0, vcm = 0;
-    // inputs: the region's u, v (BC'd into LDS), elastic stress, H, solid; grad p on the
-    // stage-0 k region (all loads before the LDS stores)
-    {
-        double su[NQ], sv[NQ];
-#pragma unroll
-        for (int m = 0; m < NQ; ++m) {
-            const int q = threadIdx.x + m * NT, ly = q / RX, lx = q % RX;
-            const int j = rj + ly, i = ri + lx;
-            const bool ok = q < NR && j >= A.rw.lo && j < A.rw.hi && i >= 0 && i < nx;
-            const long c = ok ? (long)j * nx + i : (long)A.rw.lo * nx;
-            const BCSrc s = bc_source(A.bc, A.lid, ok ? j : 1, ok ? i : 1, ny, nx);
-            okm |= (unsigned)ok << m;
-            ucm |= (unsigned)s.u_const << m;
-            vcm |= (unsigned)s.v_const << m;
-            const double a = A.u[ok ? s.u_src : c], b = A.v[ok ? s.v_src : c];
-            su[m] = !ok ? 0.0 : s.u_const ? s.u_val : a;
-            sv[m] = !ok ? 0.0 : s.v_const ? 0.0 : b;
-            u0[m] = A.u[c]; v0[m] = A.v[c];
-            ex[m] = A.sxx[c]; ey[m] = A.syy[c]; exy[m] = A.sxy[c]; hh[m] = A.H[c];
-            solm |= (unsigned)(A.solid[c] != 0) << m;
-            const bool k0 = ok && ly >= HL - 6 && ly < HL + MS_TY + 6 && lx >= HL - 6 && lx < HL + MS_TX + 6;
-            dpx[m] = k0 ? grad2k(A.p + c, 1, i, nx, K.x2) : 0.0;
-            dpy[m] = k0 ? grad2k(A.p + c, nx, j, ny, K.y2) : 0.0;
-            au[m] = 0.0; av[m] = 0.0;
-        }
-#pragma unroll
-        for (int m = 0; m < NQ; ++m) {
-            const int q = threadIdx.x + m * NT;
-            if (q < NR) { U[q] = su[m]; V[q] = sv[m]; }
-        }
-    }
-    __syncthreads();
-    for (int st = 0; st < 4; ++st) {
-        const int hk = 2 * (3 - st), hg = hk + 1;
-        // per-slot indices recomputed every stage (kept from being hoisted: registers)
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        // blended stress on halo hg (functions.py:717-735, 906-921)
-#pragma unroll
-        for (int m = 0; m < NQ; ++m) {
-            const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-            if (q >= NR || ly < HL - hg || ly >= HL + MS_TY + hg || lx < HL - hg || lx >= HL + MS_TX + hg)
-                continue;
-            const int j = rj + ly, i = ri + lx;
-            double oxx = 0.0, oxy = 0.0, oyy = 0.0;
-            if ((okm >> m) & 1) {
-                const double *pu = U + q, *pv = V + q;
-                const double dudx = grad2k(pu, 1, i, nx, K.x2), dvdy = grad2k(pv, RX, j, ny, K.y2);
-                const double dudy = grad2k(pu, RX, j, ny, K.y2), dvdx = grad2k(pv, 1, i, nx, K.x2);
-                double e1 = ex[m], e2 = ey[m], e3 = exy[m];
-                if (A.visc && ((solm >> m) & 1)) {
-                    e1 = e1 + A.eta_s * dudx;
-                    e2 = e2 + A.eta_s * dvdy;
-                    e3 = e3 + A.eta_s * 0.5 * (dudy + dvdx);
-                }
-                const double h = hh[m], omh = 1 - h;
-                oxx = h * (2 * A.mu_f * dudx) + omh * e1;
-                oyy = h * (2 * A.mu_f * dvdy) + omh * e2;
-                oxy = h * (A.mu_f * (dudy + dvdx)) + omh * e3;
-            }
-            GX[q] = oxx; GM[q] = oxy; GY[q] = oyy;
-        }
-        __syncthreads();
-        // RHS on halo hk, RK4 accumulation (functions.py:923-944, 743-758)
-        double ru[NQ], rv[NQ];
-#pragma unroll
-        for (int m = 0; m < NQ; ++m) {
-            ru[m] = 0.0; rv[m] = 0.0;
-            const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + MS_TY + hk ||
-                lx < HL - hk || lx >= HL + MS_TX + hk)
-                continue;
-            const int j = rj + ly, i = ri + lx;
-            if (st == 3 && (j < A.olo || j >= A.ohi)) continue;
-            const double divx = grad2k(GX + q, 1, i, nx, K.x2) + grad2k(GM + q, RX, j, ny, K.y2);
-            const double divy = grad2k(GM + q, 1, i, nx, K.x2) + grad2k(GY + q, RX, j, ny, K.y2);
-            const double *pu = U + q, *pv = V + q;
-            const double uc = *pu, vc = *pv;
-            const double uadv = -uc * upwind3k(pu, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * upwind3k(pu, RX, j, ny, vc, K.y6, K.y1);
-            const double vadv = -uc * upwind3k(pv, 1, i, nx, uc, K.x6, K.x1) -
-                                vc * upwind3k(pv, RX, j, ny, vc, K.y6, K.y1);
-            const double h = hh[m];
-            double k1, k2;
-            if (K.den_const) {   // (1 - h) rho + h rho == rho (MomDiv)
-                const double nu = divx + 0.0 - dpx[m], nv = divy + 0.0 - dpy[m];
-                k1 = uadv + divk(h == h ? nu : h, K.den);
-                k2 = vadv + divk(h == h ? nv : h, K.den);
-            } else {
-                const double den = ((1 - h) * A.rho_s + h * A.rho_f) + 1e-12;
-                k1 = uadv + (divx + 0.0 - dpx[m]) / den;
-                k2 = vadv + (divy + 0.0 - dpy[m]) / den;
-            }
-            if (st == 0) {
-                au[m] = k1; av[m] = k2;
-            } else if (st < 3) {
-                au[m] = au[m] + 2 * k1; av[m] = av[m] + 2 * k2;
-            }
-            if (st < 3) {   // the next stage's raw velocity u + coef k
-                const double cf = st == 2 ? dt : chalf;
-                ru[m] = u0[m] + cf * k1; rv[m] = v0[m] + cf * k2;
-            } else {
-                const long c = (long)j * nx + i;
-                if (ly >= HL && ly < HL + MS_TY && lx >= HL && lx < HL + MS_TX) {
-                    A.outu[c] = u0[m] + dt6 * (au[m] + k1);
-                    A.outv[c] = v0[m] + dt6 * (av[m] + k2);
-                }
-            }
-        }
-        if (st == 3) break;
-        __syncthreads();
-        // the next stage's velocity on halo hk: raw values, BC constants kept, BC copies after
-#pragma unroll
-        for (int m = 0; m < NQ; ++m) {
-            const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-            if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + MS_TY + hk ||
-                lx < HL - hk || lx >= HL + MS_TX + hk)
-                continue;
-            const int j = rj + ly, i = ri + lx;
-            const bool edge = i == 0 || i == nx - 1 || j == 0 || j == ny - 1;
-            if (!((ucm >> m) & 1) && !(edge_fix && edge)) U[q] = ru[m];
-            if (!((vcm >> m) & 1) && !(edge_fix && edge)) V[q] = rv[m];
-        }
-        if (edge_fix) {
-            __syncthreads();
-#pragma unroll
-            for (int m = 0; m < NQ; ++m) {
-                const int q = tid + m * NT, ly = q / RX, lx = q % RX;
-                if (q >= NR || !((okm >> m) & 1) || ly < HL - hk || ly >= HL + MS_TY + hk ||
-                    lx < HL - hk || lx >= HL + MS_TX + hk)
-                    continue;
-                const int j = rj + ly, i = ri + lx;
-                if (!(i == 0 || i == nx - 1 || j == 0 || j == ny - 1)) continue;
-                const BCSrc s = bc_source(A.bc, A.lid, j, i, ny, nx);
-                const long c = (long)j * nx + i;
-                auto loc = [&](long src) {
-                    const long d = src - c;
-                    return q + (d == nx ? RX : d == -(long)nx ? -RX : (int)d);
-                };
-                if (!s.u_const) U[q] = U[loc(s.u_src)];
-                if (!s.v_const) V[q] = V[loc(s.v_src)];
-            }
-        }
-        __syncthreads();
-    }
-}
-
-template <int MS_TX, int MS_TY, int NT>
-static int launch_rk4(rmt_ctx *ctx, const Rk4Args &A, int nblocks) {
-    static bool attr = false;
-    if (!attr) {
-        RMT_HIP(hipFuncSetAttribute((const void *)k_mom_rk4<MS_TX, MS_TY, NT>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, rk4_lds<MS_TX, MS_TY>()));
-        attr = true;
-    }
-    if (nblocks <= 0) return RMT_OK;
-    k_mom_rk4<MS_TX, MS_TY, NT><<<nblocks, NT, rk4_lds<MS_TX, MS_TY>(), ctx->stream>>>(A);
-    RMT_LAUNCHED();
-    return RMT_OK;
-}
-static Rk4Args rk4_args(const rmt_momentum_params *P, const double *u, const double *v,
-                        const double *p, const double *sxx, const double *sxy,
-                        const double *syy, const MomWork &W, double *u_new, double *v_new,
-                        int ny, int nx) {
-    Rk4Args A{};
-    A.u = u; A.v = v; A.p = p; A.sxx = sxx; A.sxy = sxy; A.syy = syy; A.H = W.H;
-    A.solid = W.solid; A.outu = u_new; A.outv = v_new; A.dtp = W.dtp;
-    A.dt = P->dt; A.lid = P->lid; A.mu_f = P->mu_f; A.eta_s = P->eta_s; A.rho_s = P->rho_s;
-    A.rho_f = P->rho_f; A.dx = P->dx; A.dy = P->dy; A.bc = P->bc_kind;
-    A.visc = P->eta_s > 0.0; A.ny = ny; A.nx = nx;
-    A.K = mom_div(P->dx, P->dy, P->rho_s, P->rho_f);
-    return A;
-}
-// 0: per-stage kernels (k_mom_stage), 1: temporally blocked RK4 (k_mom_rk4) where the BC
-// allows, 2: unfused per-cell passes (single domain).  Mode 1 moves ~9 planes per RK4 pass
-// instead of ~64 but measured slower at N = 4096 (2.50 vs 2.12 ms full pass, 0.36 vs 0.13 ms
-// fix-up): the fp64 divisions of ~1.7x halo recompute at 3 waves per SIMD are latency-bound.
-// RMT_MOM_MODE=<mode> (benchmarking) or RMT_MOM_UNFUSED=1 (mode 2)
-static int g_mom_mode = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED")) ? 2 :
-                        getenv("RMT_MOM_MODE") ? atoi(getenv("RMT_MOM_MODE")) : 0;
+// 0: per-stage kernels (k_mom_stage), 2: unfused per-cell passes (single domain, the
+// reference's pass structure; the schedule-independence tests' second opinion).  (A
+// temporally blocked RK4 kernel and a row-streaming stage kernel were measured slower in
+// rounds 2-3 and removed.)  RMT_MOM_UNFUSED=1 selects mode 2.
+static int g_mom_mode = getenv("RMT_MOM_UNFUSED") && atoi(getenv("RMT_MOM_UNFUSED")) ? 2 : 0;
 int momentum_mode() { return g_mom_mode; }
-constexpr int RK_TX = 48, RK_TY = 32, RK_T = 768;   // full pass: region 64 x 48 (one row a wave)
 
 // Final BC (functions.py:760) on the boundary cells of rows [jb, je) only: the bottom / top
 // rows when the window holds them, then the side columns.
@@ -1435,36 +932,23 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     double *kbu[2] = {W.k1u, W.k2u}, *kbv[2] = {W.k1v, W.k2v};
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
     const bool unfused = g_mom_mode == 2;
-    const bool blocked = g_mom_mode == 1 && P->bc_kind != RMT_BC_PERIODIC;
-    const bool rowstream = g_mom_mode == 3;
     const int tiles_x = (nx + MS_TX - 1) / MS_TX;
-    if (blocked) {
-        Rk4Args A = rk4_args(P, u, v, p, sxx, sxy, syy, W, u_new, v_new, ny, nx);
-        A.tiles_x = (nx + RK_TX - 1) / RK_TX;
-        A.ntiles = A.tiles_x * ((w0.je - w0.jb + RK_TY - 1) / RK_TY);
-        A.olo = w0.jb; A.ohi = w0.je; A.rw = w0;
-        RMT_TRY((launch_rk4<RK_TX, RK_TY, RK_T>(ctx, A, A.ntiles)));
-    }
     // pure-fluid tile rows for the stage kernels, on every resident row (a stage tile's
     // stress region may reach past its window; rows prep did not write only feed halo cells
     // that never reach the window's outputs)
     unsigned char *fluid_rows = fluid_rows_buf(W, w0.lo, nx);   // row w0.lo first
-    if (!unfused && !blocked) {
+    if (!unfused) {
         (void)w_cut;
         const double thr = fluid_threshold(P);
         const long nw = (long)(w0.hi - w0.lo) * tiles_x;
         if (!W.fluid_rows_ready)
             k_fluid_rows<<<grid1d(nw, 4), 256, 0, ctx->stream>>>(phi, thr, nx, tiles_x, w0.lo,
                                                                   w0.hi, fluid_rows);
-        if (!rowstream)
-            k_fluid_win<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(fluid_rows, tiles_x, w0.lo,
-                                                                   w0.hi, fluid_rows + nw);
+        k_fluid_win<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(fluid_rows, tiles_x, w0.lo, w0.hi,
+                                                               fluid_rows + nw);
         RMT_LAUNCHED();
     }
-    for (int s = 0; s < 4 && rowstream; ++s)
-        RMT_TRY(mom_rows(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, grow(2 * (3 - s)),
-                         fluid_rows));
-    for (int s = 0; s < 4 && !unfused && !blocked && !rowstream; ++s) {
+    for (int s = 0; s < 4 && !unfused; ++s) {
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
@@ -1533,12 +1017,6 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
         RMT_LAUNCHED();
     }
     const RowWin all{0, ny, w0.lo, w0.hi};
-    if (g_mom_mode == 1 && P->bc_kind != RMT_BC_PERIODIC) {
-        Rk4Args A = rk4_args(P, u, v, p, sxx, sxy, syy, W, u_new, v_new, ny, nx);
-        A.tlist = tiles; A.tcount = count; A.tiles_x = tiles_x;
-        A.olo = w0.jb; A.ohi = w0.je; A.rw = all;
-        RMT_TRY((launch_rk4<MOM_TX, MOM_TY, 640>(ctx, A, max_tiles)));
-    } else
     for (int s = 0; s < 4; ++s)
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, all, max_tiles,
                           tiles, count, grow(2 * (3 - s)).first, grow(2 * (3 - s)).second,
@@ -1554,7 +1032,7 @@ int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, 
 using namespace rmt;
 
 extern "C" int rmt_momentum_set_mode(int mode) {
-    RMT_CHECK(mode >= 0 && mode <= 3, RMT_EINVAL, "momentum mode must be 0 .. 3");
+    RMT_CHECK(mode == 0 || mode == 2, RMT_EINVAL, "momentum mode must be 0 or 2");
     rmt::g_mom_mode = mode;
     return RMT_OK;
 }

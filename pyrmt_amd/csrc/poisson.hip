@@ -681,9 +681,7 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     const size_t lds = (size_t)(n - 1) * sizeof(double2);
     const unsigned g = (unsigned)nrows;   // one row per workgroup
     hipStream_t st = ctx->stream;
-    // RMT_DCT_GENERIC=1: the runtime-plan kernel for n = 4096 too
-    static const bool generic = getenv("RMT_DCT_GENERIC") && atoi(getenv("RMT_DCT_GENERIC"));
-    const bool k4095 = n == 4096 && !P->big && !generic && np == 4 && rad[0] == 5 &&
+    const bool k4095 = n == 4096 && !P->big && np == 4 && rad[0] == 5 &&
                        rad[1] == 7 && rad[2] == 9 && rad[3] == 13;   // fft_4095's plan
     if (k4095 && solve)
         k_dct1<true, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);

@@ -120,7 +120,9 @@ __device__ __forceinline__ void sl_segment(
         const bool rim = in && ((rimw[(long)j * ((nx + 63) / 64) + (i >> 6)] >> (i & 63)) & 1);
         mine = (mode == 1) == rim;
     }
-    const bool zero = sl_skip_ok(m2, dt, fmin(Kx.d, Ky.d)) &&
+    // (a rim segment -- mode 1 -- borders the solid: its map is never +0.0 throughout, so
+    // the zero test's extra global round trip is skipped there)
+    const bool zero = mode != 1 && sl_skip_ok(m2, dt, fmin(Kx.d, Ky.d)) &&
                       sl_zero_block(X1, X2, ny, nx, j, i0, 256, 0, ny);
     bool known = false;
     if (in && zero) {

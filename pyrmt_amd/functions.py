@@ -364,8 +364,8 @@ def momentum_step_rk4(u, v, p, X1, X2, velocity_bc, mu_s, kappa, eta_s, dx, dy, 
 
 
 def momentum_mode(mode):
-    """librmt diagnostic: 0 one kernel per RK4 stage (default), 1 temporally blocked RK4,
-    2 unfused per-cell passes, 3 row-streaming stage kernels (all bit-identical)."""
+    """librmt diagnostic: 0 one kernel per RK4 stage (default), 2 unfused per-cell passes
+    (bit-identical); any other mode raises."""
     L.check(L.lib().rmt_momentum_set_mode(int(mode)), "rmt_momentum_set_mode")
 
 
