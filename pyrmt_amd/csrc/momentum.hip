@@ -808,7 +808,15 @@ static int stage_edge_tiles(rmt_ctx *ctx, RowWin ws, int ntiles, int tiles_x, co
         }
         slot = ctx->edge_next;
         ctx->edge_next = (ctx->edge_next + 1) % RMT_EDGE_SLOTS;
-        if (ctx->edge[slot].list) RMT_HIP(hipFree(ctx->edge[slot].list));
+        if (ctx->edge[slot].list) {
+            // an evicted list may still be read by a stage kernel queued on any of the
+            // context's streams (the slab step queues its speculative stages on a second,
+            // non-blocking stream): drain the device before the memory is freed and handed
+            // out again.  (Round 4: with 8 slots, G = 4 slabs cycled 16 keys per step and a
+            // slower stage kernel let a queued launch read a reallocated list.)
+            RMT_HIP(hipDeviceSynchronize());
+            RMT_HIP(hipFree(ctx->edge[slot].list));
+        }
         ctx->edge[slot].list = nullptr;
         RMT_HIP(hipMalloc(&ctx->edge[slot].list, std::max<size_t>(1, v.size()) * sizeof(int)));
         if (!v.empty())

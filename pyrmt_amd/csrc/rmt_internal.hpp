@@ -98,11 +98,12 @@ struct rmt_ctx {
     bool ev_chain_vals = false;
     // momentum.hip: the stage tiles a full launch's interior kernel skips, per row window
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
-    EdgeTiles edge[8];
+    EdgeTiles edge[64];   // RMT_EDGE_SLOTS
     int edge_next = 0;
     void *imex[2] = {nullptr, nullptr};   // imex.hip: the DST preconditioner plans (u, v)
 };
-#define RMT_EDGE_SLOTS 8
+#define RMT_EDGE_SLOTS 64   // >= every (window, grid) key of a step: 8 slabs x 4 stages + the fused 4
+static_assert(sizeof(((rmt_ctx *)nullptr)->edge) / sizeof(rmt_ctx::EdgeTiles) == RMT_EDGE_SLOTS, "edge slots");
 
 namespace rmt {
 

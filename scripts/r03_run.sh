@@ -91,6 +91,12 @@ for s in "$@"; do
                 python3 bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline > "$O/kt_cfg$c.log" 2>&1 || exit 1
             f=$(find "$O/kt_cfg$c" -name "*kernel_stats.csv" | head -1); cp "$f" "$O/kt_cfg${c}_stats.csv"
             cut -d, -f1-4 "$f" | head -12 ;;
+        local)   # LocalComm phase times of the slab step, G = 1, 2, 4, 8, exact and parallel mode
+            for m in 0 1; do for g in 1 2 4 8; do
+                RMT_EXTRAP_PARALLEL=$m timeout -k 10 300 python -u tools/dist_local_bench.py 4096 $g 5 \
+                    > "$O/local_m${m}_G$g.json" 2> "$O/local_m${m}_G$g.err" || { tail -5 "$O/local_m${m}_G$g.err"; exit 1; }
+                cut -c1-160 "$O/local_m${m}_G$g.json"
+            done; done ;;
         out:*) O=$BASE/${s#out:}; mkdir -p "$O" ;;
         env:*) export "${s#env:}"; echo "exported ${s#env:}" ;;
         *) echo "unknown step $s"; exit 2 ;;
