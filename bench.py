@@ -44,10 +44,10 @@ CONFIGS = {
 }
 # HBM bytes per launch and per step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
 # bench (scripts/gpu.sh pmc -> tools/pmc_traffic.py; FETCH x2 per the gfx950 calibration)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc_traffic_n4096.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04", "pmc_traffic_n4096.json")
 # fp64 VALU counts of the same kernel and the measured FMA peak (scripts/pmc_f64.sh ->
 # tools/f64_roof.py): k_mom_stage is VALU-issue-bound, not HBM-bound
-F64_ROOF = os.path.join(ROOT, "profiles", "r03", "f64_roof_n4096.json")
+F64_ROOF = os.path.join(ROOT, "profiles", "r04", "f64_roof_n4096.json")
 # dependent fits on the critical path of the bench-state extrapolation at N=4096 (per-fit
 # trace of the chain kernel, tools/chain_trace.py; profiles/r02/chain_trace/)
 CHAIN_DEPTH_4096 = 3257
@@ -183,7 +183,7 @@ def main_config(args, cfg):
     assert np.all(np.isfinite(np.asarray(d["cx"]))), "non-finite state"
     value = N * N * args.steps / el
     gbs = value * alg / 1e9
-    out = {"metric": "cell-updates/s (full RMT step) at N=4096; achieved HBM GB/s vs peak",
+    out = {"metric": f"cell-updates/s (full RMT step) at N={N}; achieved HBM GB/s vs peak",
            "value": value, "unit": "cell-updates/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
