@@ -235,9 +235,13 @@ def test_config4_N4096_100_steps_vs_fixture(gpu):
     np.testing.assert_allclose(got[:, 0:2], want[:, 0:2], rtol=1e-12)
     np.testing.assert_allclose(got[:, 4], want[:, 4], rtol=7e-4)         # noise floor x 2
     np.testing.assert_allclose(got[:, 5], want[:, 5], rtol=1.3e-3)
-    # achieved (MI355X, round 4): see DESIGN.md section 2
-    np.testing.assert_allclose(got[:, 2:4], want[:, 2:4], rtol=1e-12)
-    assert max(fd["u"], fd["v"]) <= 1e-12 and fd["p"] <= 1e-10
+    # achieved (MI355X, round 4): t, dt and the J range equal, centroid
+    # 1.7e-15, the map and phi equal on the sampled rows / columns / subgrid, u and v to
+    # 2.2e-16, p to 1.1e-12 (the DCT's rounding against pocketfft's)
+    np.testing.assert_allclose(got[:, 2:4], want[:, 2:4], rtol=1e-14)
+    np.testing.assert_allclose(got[:, 4:6], want[:, 4:6], rtol=1e-14)
+    assert max(fd["X1"], fd["X2"], fd["phi"]) <= 1e-14
+    assert max(fd["u"], fd["v"]) <= 1e-14 and fd["p"] <= 1e-11
 
 
 def test_config4_N4096_100_steps_parallel_mode(gpu):
@@ -264,6 +268,7 @@ def test_config4_N4096_100_steps_parallel_mode(gpu):
     print(f"\n[config4 N=4096 x{S}, parallel extrapolation] worst centroid rel {cen.max():.3g} "
           f"(step {int(cen.argmax()) + 1}); first step past 1e-6: {first}; t {rel[:, 0].max():.3g} "
           f"minJ {rel[:, 4].max():.3g} maxJ {rel[:, 5].max():.3g}")
-    # the documented envelope: within the bar for the first 10 steps
-    assert np.all(cen[:10] <= 1e-6)
-    assert cen.max() <= 1e-4
+    # the documented envelope (measured round 4: first past 1e-6 at
+    # step 23, worst 1.15e-6): within the bar for the first 20 steps, within 1e-5 over 100
+    assert np.all(cen[:20] <= 1e-6)
+    assert cen.max() <= 1e-5
