@@ -135,6 +135,31 @@ __global__ void __launch_bounds__(256) k_rowsum(const double *__restrict__ x, in
     }
     if (threadIdx.x == 0) rs[blockIdx.x] = s[0];
 }
+// k_rowsum of x = p + (pc - m) (m = *root / count, k_project_correct's mean of the raw solve),
+// x written back to p: the deferred half of the projection's pressure update, fused into the
+// mean removal's row pass (same expression and the same per-row summation order)
+__global__ void __launch_bounds__(256) k_rowsum_upd(double *__restrict__ p,
+                                                    const double *__restrict__ pc,
+                                                    const double *__restrict__ root, double count,
+                                                    int nx, double *__restrict__ rs) {
+    __shared__ double s[256];
+    const double m = *root / count;
+    double *r = p + (long)blockIdx.x * nx;
+    const double *q = pc + (long)blockIdx.x * nx;
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < nx; i += 256) {
+        const double v = r[i] + (q[i] - m);
+        r[i] = v;
+        acc += v;
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) s[threadIdx.x] = s[threadIdx.x] + s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rs[blockIdx.x] = s[0];
+}
 constexpr int TREE_MAX = 8192, TREE_T = 1024;
 __global__ void __launch_bounds__(TREE_T) k_rowtree(const double *__restrict__ rs, int m,
                                                     double *__restrict__ out) {
@@ -206,6 +231,17 @@ int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int 
             x, n, dev_roots, G, count);
     RMT_LAUNCHED();
     return RMT_OK;
+}
+// p = p + (pc - pc_root / (ny nx)), then p -= mean(p) (projection_finish's deferred update)
+int sub_mean_rows_upd(rmt_ctx *ctx, double *p, const double *pc, const double *pc_root, int ny,
+                      int nx) {
+    RMT_CHECK(ny >= 1 && ny <= TREE_MAX && ny <= ctx->rsum_len, RMT_EINVAL,
+              "sub_mean_rows_upd: rows out of range");
+    double *root = ctx->red + RED_BLOCKS + 16;
+    k_rowsum_upd<<<ny, 256, 0, ctx->stream>>>(p, pc, pc_root, (double)ny * nx, nx, ctx->rsum);
+    k_rowtree<<<1, TREE_T, 0, ctx->stream>>>(ctx->rsum, ny, root);
+    RMT_LAUNCHED();
+    return sub_tree_mean(ctx, p, (long)ny * nx, root, 1, (double)ny * nx);
 }
 int sub_mean_rows(rmt_ctx *ctx, double *x, int ny, int nx) {
     double *root = ctx->red + RED_BLOCKS + 16;
@@ -576,7 +612,7 @@ __global__ void k_project_correct(const double *__restrict__ a_s, const double *
                                   double *__restrict__ p, int jb, int je,
                                   const double *__restrict__ root, double count,
                                   const double *__restrict__ dtp = nullptr, double rho = 1.0,
-                                  double *__restrict__ m2part = nullptr) {
+                                  double *__restrict__ m2part = nullptr, int defer_p = 0) {
     const int j = jb + (int)blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
     double q = -INFINITY;
     if (i < nx && j < je) {
@@ -606,7 +642,9 @@ __global__ void k_project_correct(const double *__restrict__ a_s, const double *
             vb = s.v_const ? s.v_val : corrected(b_s, pc, s.v_src, ny, nx, Kx2, Ky2, dt_rho, 1, m);
         }
         a[c] = ua; b[c] = vb;
-        p[c] = p_prev ? p_prev[c] + (pc[c] - m) : (pc[c] - m);
+        // defer_p: p = p_prev + (pc - m) is formed by the step's deferred mean-removal pass
+        // instead (k_rowsum_upd, the same expression), off the critical path
+        if (!defer_p) p[c] = p_prev ? p_prev[c] + (pc[c] - m) : (pc[c] - m);
         q = ua * ua + vb * vb;
     }
     if (m2part) {
@@ -979,7 +1017,10 @@ int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, 
     RMT_HIP(launch_done(k_project_correct, rows_grid(ctx->nx, 0, ctx->ny), dim3(256), 0,
                         ctx->stream, done, a_star, b_star, (const double *)pc, p_prev, ctx->ny,
                         ctx->nx, divk_make(2 * dx), divk_make(2 * dy), dt / rho, bc_kind, lid, a,
-                        b, p, 0, ctx->ny, (const double *)root, (double)n, dtp, rho, m2part));
+                        b, p, 0, ctx->ny, (const double *)root, (double)n, dtp, rho, m2part,
+                        sub_mean ? 0 : 1));
+    // !sub_mean: the caller runs sub_mean_rows_upd(p, pc, root) later (the pressure update
+    // and the mean removal in one deferred pass; pc and root stay untouched until then)
     return sub_mean ? sub_mean_rows(ctx, p, ctx->ny, ctx->nx) : RMT_OK;
 }
 int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,

@@ -552,6 +552,10 @@ int projection_dev(rmt_ctx *ctx, const double *a_star, const double *b_star, dou
                    double dy, const double *dtp, double rho, int bc_kind, double lid,
                    const double *p_prev, double *a, double *b, double *p, double *m2part);
 int sub_mean_rows(rmt_ctx *ctx, double *x, int ny, int nx);
+// p = p + (pc - *pc_root / (ny nx)) then p -= mean(p): projection_finish(sub_mean = false)'s
+// deferred pressure update and mean removal in one pass
+int sub_mean_rows_upd(rmt_ctx *ctx, double *p, const double *pc, const double *pc_root, int ny,
+                      int nx);
 
 // Row window of a slab-decomposed call (slab.hip): planes are addressed with GLOBAL cell
 // indices j*nx + i (the caller offsets its pointers by -lo*nx), rows [lo, hi) are resident,

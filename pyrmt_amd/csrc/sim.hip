@@ -745,7 +745,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_HIP(hipStreamWaitEvent(S->st2, S->e_proj, 0));
         }
         ctx->stream = S->st2;
-        const int ts = sub_mean_rows(ctx, S->p, ny, nx);
+        // (the pending tail always follows a projection_finish that deferred the pressure
+        // update: pc and its mean's root are still where that projection left them)
+        const int ts = sub_mean_rows_upd(ctx, S->p, ctx->scratch + (long)ny * nx,
+                                         ctx->red + RED_BLOCKS + 17, ny, nx);
         ctx->stream = st;
         RMT_TRY(ts);
         k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
