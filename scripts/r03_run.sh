@@ -82,6 +82,12 @@ for s in "$@"; do
                 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/trace.log" 2>&1 || { tail -5 "$O/trace.log"; exit 1; }
             grep chain-prof "$O/trace.log" | tail -1
             python3 tools/chain_trace.py "$O/trace.bin" > "$O/trace.txt" && head -5 "$O/trace.txt" ;;
+        trace16)   # the same trace with the default 16-wave build (its profiled kernel fits
+                   # 128 VGPRs since round 4)
+            RMT_EX_PROFILE=1 RMT_EX_TRACE=$O/trace16.bin timeout -k 10 200 \
+                python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$O/trace16.log" 2>&1 || { tail -5 "$O/trace16.log"; exit 1; }
+            grep chain-prof "$O/trace16.log" | tail -1
+            python3 tools/chain_trace.py "$O/trace16.bin" > "$O/trace16.txt" && head -5 "$O/trace16.txt" ;;
         cfg:*)   # one BASELINE config's bench line (CPU baseline included) and its kernel stats
             c=${s#cfg:}
             timeout -k 10 600 python -u bench.py --config $c --steps 10 --warmup 2 > "$O/cfg$c.log" 2>&1 \
