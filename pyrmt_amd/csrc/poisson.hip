@@ -700,9 +700,47 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
 
 bool dct_lds_ready(rmt_ctx *ctx) { return ctx->dct && ctx->dct->lds; }
 
+// k_transpose with 16-B accesses (R, C even, 16-B aligned planes): a lane moves a pair of
+// adjacent doubles on both sides, through the same padded 64 x 64 LDS tile
+__global__ void __launch_bounds__(256) k_transpose2(const double *__restrict__ in, int R, int C,
+                                                    double *__restrict__ out,
+                                                    const unsigned char *__restrict__ rowmark,
+                                                    int mode) {
+    __shared__ double t[64][65];
+    const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    if (rowmark) {
+        const int l = threadIdx.x & 63;
+        const bool any = __syncthreads_or(threadIdx.x < 64 && r0 + l < R && rowmark[r0 + l] != 0);
+        if (any != (mode == 2)) return;
+    }
+    double2 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {   // rows ty + 8k, columns 2tx, 2tx + 1
+        const int r = r0 + ty + 8 * k, c = c0 + 2 * tx;
+        v[k] = (r < R && c < C) ? *(const double2 *)(in + (long)r * C + c) : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        t[ty + 8 * k][2 * tx] = v[k].x;
+        t[ty + 8 * k][2 * tx + 1] = v[k].y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {   // output row c0 + ty + 8k, columns r0 + 2tx, + 1
+        const int c = c0 + ty + 8 * k, r = r0 + 2 * tx;
+        if (c < C && r < R)
+            *(double2 *)(out + (long)c * R + r) = make_double2(t[2 * tx][ty + 8 * k], t[2 * tx + 1][ty + 8 * k]);
+    }
+}
+
 void transpose(hipStream_t st, const double *in, int R, int C, double *out,
                const unsigned char *rowmark, int mode) {
-    k_transpose<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out, rowmark, mode);
+    // RMT_TRANSPOSE2=0: the 8-B kernel
+    static const bool t2 = !(getenv("RMT_TRANSPOSE2") && !atoi(getenv("RMT_TRANSPOSE2")));
+    if (t2 && R % 2 == 0 && C % 2 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0)
+        k_transpose2<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out, rowmark, mode);
+    else
+        k_transpose<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out, rowmark, mode);
 }
 
 static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p, double *rs) {
