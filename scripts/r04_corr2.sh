@@ -1,3 +1,5 @@
+# Round-4 A/B of the two-cell correction kernel (RMT_CORRECT2; measured no faster and
+# reverted -- kept as the record of profiles/r04/correct2/, not runnable at HEAD)
 set -o pipefail
 O=gpurun_out/r04/corr2; mkdir -p $O; export TMPDIR=/tmp
 RMT_CORRECT2=0 timeout -k 10 300 python -u tools/fused_sha.py 4096 3 > $O/sha_one.txt 2>&1 || { tail -5 $O/sha_one.txt; exit 1; }
