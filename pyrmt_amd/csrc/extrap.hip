@@ -662,7 +662,6 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bo
     w.part = (unsigned char *)take(maxt);
     w.loc = (int *)take(maxt * 4);
     w.inv = (int *)take(maxt * 4);
-    w.gtag = (int *)take(maxt * 4);
     w.wnext = (int *)take(maxt * 4);
     w.gval = (double *)take(maxt * 16);
     w.rej = (int *)take((size_t)ML * EX_MAXREJ * 4);

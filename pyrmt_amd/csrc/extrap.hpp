@@ -22,13 +22,19 @@ constexpr int EX_DCAP = 8192;       // fix-up dirty-list capacity
 
 // ctl words (int): fallback flag, abort flag, accepted count, and 64-bit arena cursor
 // EXC_ANY / EXC_NOOP: k_ex_none's proof that no target can be accepted (both paths skip)
-// EXC_CMIN / EXC_CMAX: column range of the targets; EXC_NPART + p: fits in chain part p
-constexpr int CH_MAXP = 4;          // chain parts (workgroups), split by target column
+// EXC_CMIN / EXC_CMAX: column range of the targets; EXC_NPART + p: fits in chain part p,
+// EXC_NPART + CH_MAXP: the number of parts = EXC_NCOL column ranges x EXC_NLG layer groups
+constexpr int CH_MAXP = 8;          // chain parts (workgroups): target column range x layer group
 enum { EXC_FALLBACK = 0, EXC_ABORT = 1, EXC_FILLED = 2, EXC_ARENA = 4, EXC_REJ = 8,
        EXC_BASE = 8 + EX_MAXL, EXC_ANY = 8 + 2 * EX_MAXL, EXC_NOOP = EXC_ANY + 1,
        EXC_CMIN = EXC_ANY + 2, EXC_CMAX = EXC_ANY + 3, EXC_NPART = EXC_ANY + 4,
        EXC_WSTART = EXC_NPART + CH_MAXP + 1,                // + p * CH_W + w: wave w's first
-       EXC_WORDS = EXC_WSTART + CH_MAXP * CH_W + 8 };       // ordinal in part p
+       EXC_NCOL = EXC_WSTART + CH_MAXP * CH_W,              // ordinal in part p
+       EXC_NLG = EXC_NCOL + 1,
+       EXC_WORDS = EXC_NLG + 8 };
+// cross-part hand-off granules (gval) hold this signalling NaN until the fit is published: an
+// arithmetic result is never a signalling NaN (IEEE mode), so the value is its own flag
+constexpr unsigned long long CH_GSENT = 0x7ff00000000bad01ull;
 constexpr int PX_K = 64;            // parallel mode: fits per segment
 constexpr int PX_F = 64;            // frontier capacity (more: the segment is solved serially)
 constexpr int PX_S = 81;            // window sources per fit
@@ -47,10 +53,11 @@ struct ExWs {
     int *chain_of, *dmark;                    // MAXT each
     // parts: part[x] of chain index x, loc[x] its ordinal within the part, inv[base_p + l]
     // the chain index of ordinal l of part p (base_p = fits of the parts before p);
-    // cross-part hand-offs go through HBM: gval / gtag by global slot base_p + l (a record's
+    // cross-part hand-offs go through L2 / the fabric: gval by global slot base_p + l, two
+    // 8-byte granules (X1, X2) stored write-through, CH_GSENT until published (a record's
     // meta bit 63 marks a fit read by another part)
     unsigned char *part;                      // MAXT
-    int *loc, *inv, *gtag;                    // MAXT each
+    int *loc, *inv;                           // MAXT each
     // wave assignment: wnext[base_p + l] = the next ordinal of part p that ordinal l's wave
     // runs (round robin, k_ex_runs)
     int *wnext;                               // MAXT

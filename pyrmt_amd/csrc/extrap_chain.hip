@@ -545,10 +545,10 @@ __global__ void __launch_bounds__(1024) k_ex_order(ExWs ws, int ny, int ML) {
     }
 }
 
-// chain parts: split column = middle of the targets' column range (nparts == 2), so the two
-// workgroups take the two sides of the band; the few fits near the split column hand their
-// values across through HBM
-__global__ void __launch_bounds__(1024) k_ex_split(ExWs ws, int nx, int ML, int nparts) {
+// chain parts: split column = middle of the targets' column range (ncol == 2), so the two
+// sides of the band run apart; the few fits near the split column hand their values across
+// through L2 / the fabric, as every fit read by a later layer group does
+__global__ void __launch_bounds__(1024) k_ex_split(ExWs ws, int nx, int ML, int ncol, int nlg) {
     __shared__ int smin[1024], smax[1024];
     const int t = threadIdx.x, total = ws.ctl[EXC_BASE + ML];
     int mn = 0x7fffffff, mx = -1;
@@ -565,12 +565,14 @@ __global__ void __launch_bounds__(1024) k_ex_split(ExWs ws, int nx, int ML, int 
     if (t == 0) {
         ws.ctl[EXC_CMIN] = smin[0];
         ws.ctl[EXC_CMAX] = smax[0] >= smin[0] ? smax[0] - smin[0] + 1 : 1;   // span
-        ws.ctl[EXC_NPART + CH_MAXP] = nparts;
+        ws.ctl[EXC_NCOL] = ncol;
+        ws.ctl[EXC_NLG] = nlg;
+        ws.ctl[EXC_NPART + CH_MAXP] = ncol * nlg;
     }
 }
-// part of a target column: nparts equal column ranges over the targets' span
-__device__ __forceinline__ int ch_part_of(const int *ctl, int i) {
-    const int np = ctl[EXC_NPART + CH_MAXP];
+// column range of a target column: EXC_NCOL equal ranges over the targets' span
+__device__ __forceinline__ int ch_col_of(const int *ctl, int i) {
+    const int np = ctl[EXC_NCOL];
     if (np <= 1) return 0;
     const long q = (long)(i - ctl[EXC_CMIN]) * np / ctl[EXC_CMAX];
     return (int)min((long)np - 1, max(0L, q));
@@ -588,7 +590,12 @@ __global__ void __launch_bounds__(256) k_ex_chainidx(ExWs ws, int ny, int nx, in
         const int x = ws.cbase[(long)L * ny + j] +
                       (id - ws.ctl[EXC_BASE + L] - ws.rowoff[(long)L * (ny + 1) + j]);
         ws.chain_of[id] = x;
-        ws.part[x] = (unsigned char)ch_part_of(ws.ctl, (int)(ws.tcell[id] % nx));
+        // part = (column range, layer group): a layer's fits read the previous layers' only
+        // ~5 rows ahead of their own chain position (k_ex_order), so a layer group on a
+        // workgroup of its own hands values over off the critical path
+        const int nlg = ws.ctl[EXC_NLG];
+        ws.part[x] = (unsigned char)(ch_col_of(ws.ctl, (int)(ws.tcell[id] % nx)) * nlg +
+                                     L * nlg / ML);
         const long long r = ws.recoff[id];
         ws.rec_by_chain[x] = r;
         acc = r >= 0;
@@ -639,7 +646,8 @@ __global__ void __launch_bounds__(1024) k_ex_local(ExWs ws, int ML) {
             if (px == p) { l = run[p]++; bs = base[p]; }
         ws.loc[x] = l;
         ws.inv[bs + l] = x;
-        ws.gtag[x] = -1;
+        ((u64 *)ws.gval)[2 * x] = CH_GSENT;      // (slots 0 .. total - 1 in any order)
+        ((u64 *)ws.gval)[2 * x + 1] = CH_GSENT;
     }
     if (t == 1023) {
 #pragma unroll
@@ -721,7 +729,8 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
 }
 
 // ------------------------------------------------------------------ 3. the chain ---
-constexpr int CH_BUFD = CH_MAXREC / 8 + 8;          // doubles per wave record buffer
+constexpr int CH_BUFD = CH_MAXREC / 8 + 32;   // doubles per wave record buffer (+ the tail
+                                              // prefetch's NRT = 24 reads past a short record)
 constexpr long CH_SPIN_LIMIT = 1L << 25;
 
 struct ChainArgs {
@@ -732,29 +741,6 @@ struct ChainArgs {
     long long *trace;   // PROF diagnostic: per fit {start, ready, published, critical source,
                         // wave, cell} (s_memrealtime), indexed by global chain slot
 };
-
-// source of a record term: e.y >= 0 -> this part's LDS ring (tag e.y); e.y < 0 -> the other
-// part's HBM hand-off slot -e.y - 1 (tag written after the value, agent-scope release)
-__device__ __forceinline__ bool ch_probe(int ey, const int *tag, const double2 *val,
-                                         const int *gtag, const double *gval, double2 &v) {
-    if (ey >= 0) {
-        const int slot = ey & (CH_R - 1);
-        if (__hip_atomic_load(&tag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ey)
-            return false;
-        asm volatile("" ::: "memory");
-        v = val[slot];
-        return true;
-    }
-    const int g = -ey - 1;
-    if (__hip_atomic_load(&gtag[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != g) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const unsigned long long *gv = (const unsigned long long *)gval;
-    v.x = __longlong_as_double((long long)__hip_atomic_load(&gv[2 * g], __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT));
-    v.y = __longlong_as_double((long long)__hip_atomic_load(&gv[2 * g + 1], __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT));
-    return true;
-}
 
 // record r (packed: 64-B units of offset | size << 25) -> five 16-B pieces per lane; every
 // lane issues the same 5 loads (lanes past the record re-read its last piece, same line).
@@ -870,7 +856,7 @@ __device__ __forceinline__ double ch_fold_span(double acc, const double *row, in
 template <bool PROF>
 __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                         int *cur, int &wm, double &o_out, long &c_out,
-                                        long long *pr, long long &tl, int *gtag, double *gval,
+                                        long long *pr, long long &tl, double *gval,
                                         int gslot, long long *trace = nullptr, int base = 0) {
     long long tr_start = 0, tr_ready = 0;
     int tr_crit = -1;
@@ -918,29 +904,24 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         cf[0] = q0.y; cf[1] = q1.x; cf[2] = q1.y;
     }
     const int slot = e.y & (CH_R - 1);
-    // the other part's sources (rare) first, through HBM
+    // the other parts' sources first: 8-byte granules (X1, X2) stored write-through by their
+    // producers, read with agent-scope loads (no L1, no fence: the value is its own flag)
     const bool far = has && e.y < 0;
     bool done = !has || crit;
     if (__ballot(far)) {
         long sp = 0;
-        const unsigned long long *gv = (const unsigned long long *)gval;
-        const int g = -e.y - 1;
+        const u64 *gv = (const u64 *)gval + 2 * (long)(-e.y - 1);
         for (;;) {
             if (far && !done) {
-                const int t = __hip_atomic_load(&gtag[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                const double vx = __longlong_as_double((long long)__hip_atomic_load(
-                    &gv[2 * g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                const double vy = __longlong_as_double((long long)__hip_atomic_load(
-                    &gv[2 * g + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                if (t == g) {   // the value was read after the tag (acquire): it is final
+                const u64 bx = __hip_atomic_load(gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const u64 by = __hip_atomic_load(gv + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (bx != CH_GSENT && by != CH_GSENT) {
+                    const double vx = __longlong_as_double((long long)bx);
+                    const double vy = __longlong_as_double((long long)by);
 #pragma unroll
                     for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? vx : vy);
                     done = true;
                 }
-                // consumed on every path that loaded them: no load of this block stays pending
-                // (else later register reuse waits on vmcnt -- the record prefetch included)
-                asm volatile("" ::"v"(vx), "v"(vy));
             }
             if (__ballot(far && !done) == 0) break;
             if (++sp > CH_SPIN_LIMIT) return false;
@@ -1077,17 +1058,15 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         if constexpr (PROF) asm volatile("" : "+v"(o));
         CH_STAMP(9);
         ((double *)&val[x & (CH_R - 1)])[lane == 0 ? 0 : 1] = o;
-        if (pub) gval[2 * gslot + (lane == 0 ? 0 : 1)] = o;
         o_out = o;
     }
     asm volatile("" ::: "memory");
     if (lane == 0)
         __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (pub) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0)
-            __hip_atomic_store(&gtag[gslot], gslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (pub && (lane == 0 || lane == 3))   // after the LDS hand-off: the local reader first
+        __hip_atomic_store((u64 *)gval + 2L * gslot + (lane == 0 ? 0 : 1),
+                           (u64)__double_as_longlong(o_out), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     CH_STAMP(10);
     __builtin_amdgcn_s_setprio(1);
@@ -1154,7 +1133,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         if (x2 <= x) { ok = false; break; }   // bug guard: the wave's sequence must advance
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
-        const bool fit_ok = ch_fit<PROF>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gtag,
+        const bool fit_ok = ch_fit<PROF>(x, lane, B, val, tag, cur, wm, o, c, pr, tl,
                                          C.ws.gval, base + x, C.trace, base);
         if (!fit_ok) { ok = false; break; }
         x = x2; r = r2;
@@ -1170,6 +1149,14 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
     }
 }
 // ------------------------------------------------------------------ host side ------
+// the chain's workgroups: column ranges x layer groups (rmt_ctx::ch_cols, ch_lgroups)
+static int chain_parts(const rmt_ctx *ctx, int ML, int *ncol, int *nlg) {
+    *ncol = std::min(CH_MAXP, std::max(1, ctx->ch_cols));
+    int g = ctx->ch_lgroups > 0 ? ctx->ch_lgroups : ML;
+    *nlg = std::max(1, std::min({g, ML, CH_MAXP / *ncol}));
+    return *ncol * *nlg;
+}
+
 bool extrap_chain_supported(int ny, int nx, int ML) {
     return ML >= 1 && ML <= EX_MAXL && ny >= 3 && nx >= 3;
 }
@@ -1194,11 +1181,10 @@ int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const dou
         k_ex_fix<<<1, FIXW * 64, 0, st>>>(A);
         RMT_LAUNCHED();
     }
-    // RMT_CH_PARTS: workgroups running the chain, one per column range of the band
-    static const int nparts = getenv("RMT_CH_PARTS") ? std::min(CH_MAXP, std::max(1,
-                                  atoi(getenv("RMT_CH_PARTS")))) : 2;
+    int ncol, nlg;
+    const int nparts = chain_parts(ctx, ML, &ncol, &nlg);
     k_ex_order<<<1, 1024, 0, st>>>(ws, ny, ML);
-    k_ex_split<<<1, 1024, 0, st>>>(ws, nx, ML, nparts);
+    k_ex_split<<<1, 1024, 0, st>>>(ws, nx, ML, ncol, nlg);
     const unsigned idb = grid1d(ws.maxt, 256);
     k_ex_chainidx<<<idb, 256, 0, st>>>(ws, ny, nx, ML, ws.status);
     k_ex_local<<<1, 1024, 0, st>>>(ws, ML);
@@ -1243,8 +1229,8 @@ int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
 int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
                      int ML) {
     hipStream_t st = ctx->stream;
-    static const int nparts = getenv("RMT_CH_PARTS") ? std::min(CH_MAXP, std::max(1,
-                                  atoi(getenv("RMT_CH_PARTS")))) : 2;
+    int ncol, nlg;
+    const int nparts = chain_parts(ctx, ML, &ncol, &nlg);
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
     if (ctx->ev_chain && !ctx->ev_chain_vals) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status, nullptr};

@@ -712,6 +712,8 @@ int rmt_ctx_create(int ny, int nx, int device, void *stream, rmt_ctx **out) {
     RMT_HIP(hipSetDevice(device));
     rmt_ctx *c = new rmt_ctx;
     c->ny = ny; c->nx = nx; c->device = device; c->stream = (hipStream_t)stream;
+    if (const char *e = getenv("RMT_CH_PARTS")) c->ch_cols = atoi(e);     // column ranges
+    if (const char *e = getenv("RMT_CH_LAYERS")) c->ch_lgroups = atoi(e); // layer groups
     RMT_HIP(hipMalloc(&c->red, (RED_BLOCKS + 64) * sizeof(double)));
     c->rsum_len = ny > 8192 ? ny : 8192;
     RMT_HIP(hipMalloc(&c->rsum, c->rsum_len * sizeof(double)));

@@ -101,6 +101,9 @@ struct rmt_ctx {
     EdgeTiles edge[64];   // RMT_EDGE_SLOTS
     int edge_next = 0;
     void *imex[2] = {nullptr, nullptr};   // imex.hip: the DST preconditioner plans (u, v)
+    // extrap_chain.hip: the chain's workgroups = ch_cols column ranges of the band x
+    // ch_lgroups layer groups (0: one group per layer, as many as CH_MAXP allows)
+    int ch_cols = 2, ch_lgroups = 0;
 };
 #define RMT_EDGE_SLOTS 64   // >= every (window, grid) key of a step: 8 slabs x 4 stages + the fused 4
 static_assert(sizeof(((rmt_ctx *)nullptr)->edge) / sizeof(rmt_ctx::EdgeTiles) == RMT_EDGE_SLOTS, "edge slots");

@@ -78,15 +78,14 @@ class Simulation:
 
     def field(self, name):
         """A torch CUDA view (no copy) of a state field: u/a, v/b, p, X1, X2, phi, J.  The
-        caller may write through it at any time: while the view is alive, every step() starts
+        caller may write through it -- or through any view derived from it (a slice, .T,
+        .view) -- at any time: while any tensor on its storage is alive, every step() starts
         from the fields as they are (the carried state of the previous call is dropped)."""
         self.invalidate()
         fid = FIELDS[name]
         ptr = ctypes.c_void_p()
         L.check(L.lib().rmt_sim_field(self.h, fid, ctypes.byref(ptr)))
-        t = _wrap_device(self.torch, ptr.value, (self.N, self.N))
-        self._lent.append(weakref.ref(t))
-        return t
+        return _wrap_device(self.torch, ptr.value, (self.N, self.N), lent=self._lent)
 
     def invalidate(self):
         """The state was changed from outside: the next step() recomputes everything it
@@ -136,12 +135,25 @@ class Simulation:
         return {k: np.array([getattr(buf[i], k) for i in range(n.value)]) for k in keys}
 
 
-def _wrap_device(torch, ptr, shape):
-    """Zero-copy torch view of librmt-owned device memory (valid while the sim lives)."""
-    class _CAI:
-        __cuda_array_interface__ = {"shape": shape, "typestr": "<f8", "data": (ptr, False),
-                                    "version": 3, "strides": None}
-    return torch.as_tensor(_CAI(), device="cuda")
+class _CAI:
+    """__cuda_array_interface__ exporter of a librmt buffer.  torch.as_tensor keeps a strong
+    reference to it in the tensor's storage (released when the storage is freed), so a weak
+    reference to it is alive exactly while any tensor on that storage is: the returned view
+    and every view derived from it (slices, .T, .view, ...)."""
+
+    def __init__(self, ptr, shape):
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": "<f8", "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+
+def _wrap_device(torch, ptr, shape, lent=None):
+    """Zero-copy torch view of librmt-owned device memory (valid while the sim lives).
+    lent: a list that receives a weak reference that lives as long as the view's storage."""
+    cai = _CAI(ptr, shape)
+    t = torch.as_tensor(cai, device="cuda")
+    if lent is not None:
+        lent.append(weakref.ref(cai))
+    return t
 
 
 def _init_disc_map(sim, x0, y0, R, layers):
