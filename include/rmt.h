@@ -72,6 +72,16 @@ int rmt_ctx_sync(rmt_ctx *ctx);
  * extrapolation chain (0 if none was recorded).  Blocks until the events complete. */
 int rmt_ctx_set_profiling(rmt_ctx *ctx, int on);
 int rmt_ctx_kernel_ms(rmt_ctx *ctx, double *ms2);
+/* Per-context implementation switches (bit-identical alternatives of the schedule and the
+ * kernels, for A/B measurements and the regression tests): each starts from its environment
+ * variable at rmt_ctx_create.  Names: ext_events, ex_arena_bump, ex_profile, fix_all,
+ * dct_rocfft, transpose2, sim_hiprio, sim_sync, early_geometry, early_transpose, fused_fluid,
+ * no_overlap, side_tail, par_overlap, fused_fixprep, merged_join, test_delay_side,
+ * test_delay_main, chain_cols, chain_layer_groups.  Set them before creating a sim or slab on
+ * the context (sim_hiprio is read at rmt_sim_create); a change ends a carried step state.
+ * Unknown name: RMT_EINVAL. */
+int rmt_ctx_set_option(rmt_ctx *ctx, const char *name, int value);
+int rmt_ctx_get_option(rmt_ctx *ctx, const char *name, int *value);
 
 /* ---- finite-difference helpers (pyRMT/utils.py) ----------------------------------- */
 /* utils.py:4-14 grad_central_x_2nd / utils.py:16-25 grad_central_y_2nd */

@@ -69,6 +69,8 @@ SIGNATURES = {
     "rmt_ctx_sync": (_I, [_P]),
     "rmt_ctx_set_profiling": (_I, [_P, _I]),
     "rmt_ctx_kernel_ms": (_I, [_P, ctypes.POINTER(_D)]),
+    "rmt_ctx_set_option": (_I, [_P, ctypes.c_char_p, _I]),
+    "rmt_ctx_get_option": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_I)]),
     "rmt_grad_x_2nd": (_I, [_P, _P, _D, _P]),
     "rmt_grad_y_2nd": (_I, [_P, _P, _D, _P]),
     "rmt_diff_upwind_3rd": (_I, [_P, _P, _P, _D, _I, _P]),

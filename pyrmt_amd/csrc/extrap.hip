@@ -632,7 +632,8 @@ unsigned long extrap_config_gen() { return g_ex_cfg_gen; }
 void extrap_config_changed() { ++g_ex_cfg_gen; }
 
 // byte workspace: both paths' bit planes, the chain path's tables and its record arena
-ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bool px) {
+ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bool px,
+                   bool bump) {
     const int ML = std::max(max_layers, 1), W = (nx + 63) / 64;
     const long plane = (long)ny * W;
     const long interior = (long)std::max(ny - 2, 0) * std::max(nx - 2, 0);
@@ -667,9 +668,8 @@ ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bo
     w.rej = (int *)take((size_t)ML * EX_MAXREJ * 4);
     w.ctl = (int *)take(EXC_WORDS * 4);
     // one fixed slot per fit id (no allocation cursor shared by every wave of k_ex_geom) when
-    // it fits; else a bump allocator (~2 KB per record on average at the bench sizes).
+    // it fits and bump (rmt_opts::ex_arena_bump) is off; else a bump allocator (~2 KB per record on average at the bench sizes).
     // Offsets are stored in 64-B units.
-    static const bool bump = getenv("RMT_EX_ARENA") && !strcmp(getenv("RMT_EX_ARENA"), "bump");
     const long long cap = (1LL << 31) - 65536;
     w.slots = !bump && maxt * (long long)CH_MAXREC <= cap;
     w.arena_bytes = w.slots ? maxt * (long long)CH_MAXREC : std::min(maxt * 2560LL, cap);
@@ -731,7 +731,8 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
     // the parallel mode replaces the chain (never the diagnostic sweep modes)
     const bool par = chain && force == 0 && extrap_par_enabled();
     RMT_TRY(ensure_bytes(ctx, extrap_workspace(ny, nx, max_layers, par)));
-    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, par);
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, par,
+                                  ctx->opt.ex_arena_bump);
     ctx->ex_layers = max_layers;
     ctx->ex_chain = chain;
     ctx->ex_par = par;
@@ -780,7 +781,8 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
     const int ny = ctx->ny, nx = ctx->nx;
     const int W = (nx + 63) / 64;
     const bool par = ctx->ex_par;
-    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, par);
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, par,
+                                  ctx->opt.ex_arena_bump);
     const int force = g_ex_mode;
     const bool chain = ctx->ex_chain && !par;
     const int *ctl = ctx->ex_chain ? ws.ctl : nullptr;
@@ -788,7 +790,7 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
     if (ctx->prof && !chain && !par) RMT_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
     ExSweep A{X1o, X2o, ws.kbits, ws.cbits, ws.Kold, ws.rowcand, ws.jrange, ny, nx, W,
               max_layers, dx, dy, ws.status, ctl};
-    static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
+    const bool prof = ctx->opt.ex_profile != 0;
     const bool defer = chain && ctx->ex_sweep_defer && ctx->ev_chain;
     RMT_CHECK(!defer || !dev_status, RMT_EINVAL,
               "extrap_finish: a deferred sweep leaves the status to the caller");
@@ -850,7 +852,8 @@ int extrap_sweep(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o
     const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
     RMT_CHECK(ctx->ex_chain && !ctx->ex_par && ctx->ex_layers == max_layers, RMT_EINVAL,
               "extrap_sweep: follows an exact-chain extrap_finish of the same layers");
-    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, false,
+                                  ctx->opt.ex_arena_bump);
     ExSweep A{X1o, X2o, ws.kbits, ws.cbits, ws.Kold, ws.rowcand, ws.jrange, ny, nx, W,
               max_layers, dx, dy, ws.status, ws.ctl};
     k_ex_sweep<false><<<1, EXW * 64, 0, s>>>(A, nullptr);
@@ -859,7 +862,8 @@ int extrap_sweep(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o
 }
 
 const int *extrap_status(rmt_ctx *ctx, int max_layers) {
-    return extrap_layout(ctx->bytes, ctx->ny, ctx->nx, max_layers, nullptr, ctx->ex_par).status;
+    return extrap_layout(ctx->bytes, ctx->ny, ctx->nx, max_layers, nullptr, ctx->ex_par,
+                         ctx->opt.ex_arena_bump).status;
 }
 
 int extrapolate(rmt_ctx *ctx, const double *X1, const double *X2, const double *phi, double dx,
@@ -906,11 +910,12 @@ int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *c
     const int ny = ctx->ny, nx = ctx->nx, W = (nx + 63) / 64;
     const int tiles_x = (nx + MOM_TX - 1) / MOM_TX, ntiles = tiles_x * ((ny + MOM_TY - 1) / MOM_TY);
     RMT_CHECK(margin + max_layers <= 24 && margin >= 0, RMT_EINVAL, "fix-tile reach");
-    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr);
-    // RMT_FIX_ALL=1 (tests only): list every tile.  The fix-up then re-runs phi, the prep and
+    const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, false,
+                                  ctx->opt.ex_arena_bump);
+    // fix_all (RMT_FIX_ALL=1, tests only): list every tile.  The fix-up then re-runs phi, the prep and
     // the four stages on the whole grid from the same inputs: bit-identical to the default if
     // the tile-list kernels are right on interior, edge and domain-boundary tiles alike
-    static const int all = getenv("RMT_FIX_ALL") ? atoi(getenv("RMT_FIX_ALL")) != 0 : 0;
+    const int all = ctx->opt.fix_all != 0;
     RMT_HIP(hipMemsetAsync(count, 0, sizeof(int), ctx->stream));
     k_fix_tiles<<<grid1d(ntiles, 4), 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, margin + max_layers,
                                                              margin, tiles_x, ntiles, list, count,
@@ -923,7 +928,8 @@ int extrap_fix_tiles(rmt_ctx *ctx, int max_layers, int margin, int *list, int *c
 extern "C" int rmt_extrap_last_path(rmt_ctx *ctx, int *path) {
     RMT_CHECK(ctx && path, RMT_EINVAL, "null argument");
     RMT_CHECK(ctx->bytes, RMT_EINVAL, "no extrapolation has run on this context");
-    const rmt::ExWs ws = rmt::extrap_layout(ctx->bytes, ctx->ny, ctx->nx, ctx->ex_layers, nullptr);
+    const rmt::ExWs ws = rmt::extrap_layout(ctx->bytes, ctx->ny, ctx->nx, ctx->ex_layers, nullptr,
+                                            false, ctx->opt.ex_arena_bump);
     int fb[2] = {1, 0};   // EXC_FALLBACK, EXC_NOOP
     if (ctx->ex_chain) {
         RMT_HIP(hipMemcpyAsync(&fb[0], ws.ctl + rmt::EXC_FALLBACK, sizeof(int),

@@ -88,7 +88,8 @@ struct ExWs {
 
 // px: also lay out the parallel mode's arrays (after everything else: the other offsets do
 // not depend on it)
-ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bool px = false);
+ExWs extrap_layout(void *base, int ny, int nx, int max_layers, size_t *bytes, bool px = false,
+                   bool bump = false);
 // chain path: queue the kernels; they check ctl[EXC_FALLBACK] themselves
 int extrap_chain_prep(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const double *X2o,
                       double dx, double dy, int ML);

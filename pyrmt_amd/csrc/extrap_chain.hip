@@ -859,7 +859,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
                                         long long *pr, long long &tl, double *gval,
                                         int gslot, long long *trace = nullptr, int base = 0) {
     long long tr_start = 0, tr_ready = 0;
-    int tr_crit = -1;
+    int tr_crit = -1, tr_far = -1;   // the critical local ordinal / far global slot (PROF)
     long spins = 0;
     while (x - CH_R / 2 >= wm) {
         int m = 0x7fffffff;
@@ -924,9 +924,17 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
                 }
             }
             if (__ballot(far && !done) == 0) break;
+            if constexpr (PROF) {   // the far source still missing with the latest slot
+                int g = far && !done ? -e.y - 1 : -1;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) g = max(g, __shfl_xor(g, off));
+                tr_far = g;
+            }
             if (++sp > CH_SPIN_LIMIT) return false;
             __builtin_amdgcn_s_sleep(1);
         }
+        if constexpr (PROF)
+            if (sp) tr_ready = __builtin_amdgcn_s_memrealtime();
     }
     // the critical source: its term position, slot, tag and coefficients (uniform)
     const u64 cm = __ballot(crit);
@@ -1078,8 +1086,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             const long long tp = __builtin_amdgcn_s_memrealtime();
             long long *t = trace + 6L * gslot;
             t[0] = tr_start; t[1] = tr_ready ? tr_ready : tr_start; t[2] = tp;
-            t[3] = tr_crit >= 0 ? base + tr_crit : -1;
-            t[4] = threadIdx.x >> 6; t[5] = c_out;
+            t[3] = tr_crit >= 0 ? base + tr_crit : tr_far;
+            t[4] = (threadIdx.x >> 6) | (blockIdx.x << 8); t[5] = c_out;
         }
     }
     return true;
@@ -1151,8 +1159,8 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
 // ------------------------------------------------------------------ host side ------
 // the chain's workgroups: column ranges x layer groups (rmt_ctx::ch_cols, ch_lgroups)
 static int chain_parts(const rmt_ctx *ctx, int ML, int *ncol, int *nlg) {
-    *ncol = std::min(CH_MAXP, std::max(1, ctx->ch_cols));
-    int g = ctx->ch_lgroups > 0 ? ctx->ch_lgroups : ML;
+    *ncol = std::min(CH_MAXP, std::max(1, ctx->opt.ch_cols));
+    int g = ctx->opt.ch_lgroups > 0 ? ctx->opt.ch_lgroups : ML;
     *nlg = std::max(1, std::min({g, ML, CH_MAXP / *ncol}));
     return *ncol * *nlg;
 }
@@ -1221,7 +1229,7 @@ int extrap_chain_values(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const d
     const double r = 4 * std::sqrt(dx * dx + dy * dy);
     ExGeoArgs A{ws, X1o, X2o, ny, nx, W, 0, dx, dy, r * r, 0};
     const unsigned gblocks = (unsigned)std::min<long>(4096, std::max<long>(1, ws.maxt / 4));
-    RMT_HIP(launch_done(k_ex_vals, dim3(gblocks), dim3(256), 0, ctx->stream,
+    RMT_HIP(launch_done(ctx, k_ex_vals, dim3(gblocks), dim3(256), 0, ctx->stream,
                         ctx->ev_chain_vals ? ctx->ev_chain : nullptr, A, ML));
     return RMT_OK;
 }
@@ -1234,8 +1242,7 @@ int extrap_chain_run(rmt_ctx *ctx, const ExWs &ws, const double *X1o, const doub
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[2], st));
     if (ctx->ev_chain && !ctx->ev_chain_vals) RMT_HIP(hipEventRecord(ctx->ev_chain, st));
     ChainArgs C{ws, (double *)X1o, (double *)X2o, ML, ws.status, nullptr};
-    static const bool prof = getenv("RMT_EX_PROFILE") && atoi(getenv("RMT_EX_PROFILE"));
-    if (!prof) {
+    if (!ctx->opt.ex_profile) {
         k_ex_chain<false><<<nparts, CH_W * 64, 0, st>>>(C, nullptr);
         RMT_LAUNCHED();
     } else {

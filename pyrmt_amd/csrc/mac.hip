@@ -846,9 +846,9 @@ int rmt_mac_slab_project_cols(rmt_mac_slab *S) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
     rmt_ctx *ctx = S->ctx;
     const int nc = S->c1 - S->c0;
-    transpose(ctx->stream, S->B, S->N, nc, S->T);
+    transpose(ctx, ctx->stream, S->B, S->N, nc, S->T);
     RMT_TRY(dct2_pass(ctx, 1, 1, S->T, S->T, nc, S->c0));
-    transpose(ctx->stream, S->T, nc, S->N, S->B);
+    transpose(ctx, ctx->stream, S->T, nc, S->N, S->B);
     RMT_LAUNCHED();
     return RMT_OK;
 }

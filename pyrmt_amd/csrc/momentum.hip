@@ -997,7 +997,7 @@ int fixup_phi_prep(rmt_ctx *ctx, const rmt_momentum_params *P, const MomWork &W,
     RMT_CHECK(nx % 64 == 0 && g_mom_mode != 2, RMT_EINVAL,
               "fixup_phi_prep: nx % 64 == 0 and the fused momentum modes only");
     const double w_cut = P->stress_band ? P->w_t : 0.0, clamp = P->stress_band ? P->detg_clamp : 0.0;
-    RMT_HIP(launch_done(k_phi_prep_tiles, dim3(list_grid(max_tiles)), dim3(MOM_TX * MOM_TY), 0,
+    RMT_HIP(launch_done(ctx, k_phi_prep_tiles, dim3(list_grid(max_tiles)), dim3(MOM_TX * MOM_TY), 0,
                         ctx->stream, done, X1n, X2n, x0, y0, R, nbits, ny, nx, P->dx, P->dy,
                         P->mu_s, P->kappa, w_cut, clamp, P->w_t, X1, X2, phi, sxx, sxy, syy, J,
                         W.H, W.solid, tiles, count, nx / MOM_TX, 0, ny, W.prep_const, st_src,

@@ -12,9 +12,38 @@
 namespace rmt {
 static thread_local std::string g_err;
 void set_error(const std::string &m) { g_err = m; }
-bool ext_events() {
-    static const bool on = !(getenv("RMT_EXT_EVENTS") && !atoi(getenv("RMT_EXT_EVENTS")));
-    return on;
+// rmt_opts by name: (option name, environment variable, field)
+static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
+    {"ext_events", "RMT_EXT_EVENTS", &rmt_opts::ext_events},
+    {"ex_arena_bump", nullptr, &rmt_opts::ex_arena_bump},   // RMT_EX_ARENA=bump (below)
+    {"ex_profile", "RMT_EX_PROFILE", &rmt_opts::ex_profile},
+    {"fix_all", "RMT_FIX_ALL", &rmt_opts::fix_all},
+    {"dct_rocfft", "RMT_DCT_ROCFFT", &rmt_opts::dct_rocfft},
+    {"transpose2", "RMT_TRANSPOSE2", &rmt_opts::transpose2},
+    {"sim_hiprio", "RMT_SIM_HIPRIO", &rmt_opts::sim_hiprio},
+    {"sim_sync", "RMT_SIM_SYNC", &rmt_opts::sim_sync},
+    {"early_geometry", "RMT_EARLY_GEOMETRY", &rmt_opts::early_geometry},
+    {"early_transpose", "RMT_EARLY_TRANSPOSE", &rmt_opts::early_transpose},
+    {"fused_fluid", "RMT_FUSED_FLUID", &rmt_opts::fused_fluid},
+    {"no_overlap", "RMT_NO_OVERLAP", &rmt_opts::no_overlap},
+    {"side_tail", "RMT_SIDE_TAIL", &rmt_opts::side_tail},
+    {"par_overlap", "RMT_PAR_OVERLAP", &rmt_opts::par_overlap},
+    {"fused_fixprep", "RMT_FUSED_FIXPREP", &rmt_opts::fused_fixprep},
+    {"merged_join", "RMT_MERGED_JOIN", &rmt_opts::merged_join},
+    {"test_delay_side", "RMT_TEST_DELAY_SIDE", &rmt_opts::test_delay_side},
+    {"test_delay_main", "RMT_TEST_DELAY_MAIN", &rmt_opts::test_delay_main},
+    {"chain_cols", "RMT_CH_PARTS", &rmt_opts::ch_cols},
+    {"chain_layer_groups", "RMT_CH_LAYERS", &rmt_opts::ch_lgroups},
+};
+static rmt_opts opts_from_env() {
+    rmt_opts o;
+    for (const auto &k : kOpts)
+        if (k.env)
+            if (const char *e = getenv(k.env)) o.*(k.f) = atoi(e);
+    if (const char *e = getenv("RMT_EX_ARENA")) o.ex_arena_bump = !strcmp(e, "bump");
+    o.test_delay_side = std::max(0, o.test_delay_side);
+    o.test_delay_main = std::max(0, o.test_delay_main);
+    return o;
 }
 
 int ensure_scratch(rmt_ctx *ctx, size_t bytes) {
@@ -712,13 +741,30 @@ int rmt_ctx_create(int ny, int nx, int device, void *stream, rmt_ctx **out) {
     RMT_HIP(hipSetDevice(device));
     rmt_ctx *c = new rmt_ctx;
     c->ny = ny; c->nx = nx; c->device = device; c->stream = (hipStream_t)stream;
-    if (const char *e = getenv("RMT_CH_PARTS")) c->ch_cols = atoi(e);     // column ranges
-    if (const char *e = getenv("RMT_CH_LAYERS")) c->ch_lgroups = atoi(e); // layer groups
+    c->opt = opts_from_env();
     RMT_HIP(hipMalloc(&c->red, (RED_BLOCKS + 64) * sizeof(double)));
     c->rsum_len = ny > 8192 ? ny : 8192;
     RMT_HIP(hipMalloc(&c->rsum, c->rsum_len * sizeof(double)));
     *out = c;
     return RMT_OK;
+}
+int rmt_ctx_set_option(rmt_ctx *ctx, const char *name, int value) {
+    RMT_CHECK(ctx && name, RMT_EINVAL, "null argument");
+    for (const auto &k : kOpts)
+        if (!strcmp(k.name, name)) {
+            ctx->opt.*(k.f) = value;
+            ctx->bytes_gen++;   // a carried step state was prepared under the old options
+            return RMT_OK;
+        }
+    set_error(std::string("rmt_ctx_set_option: unknown option ") + name);
+    return RMT_EINVAL;
+}
+int rmt_ctx_get_option(rmt_ctx *ctx, const char *name, int *value) {
+    RMT_CHECK(ctx && name && value, RMT_EINVAL, "null argument");
+    for (const auto &k : kOpts)
+        if (!strcmp(k.name, name)) { *value = ctx->opt.*(k.f); return RMT_OK; }
+    set_error(std::string("rmt_ctx_get_option: unknown option ") + name);
+    return RMT_EINVAL;
 }
 int rmt_ctx_set_stream(rmt_ctx *ctx, void *stream) {
     RMT_CHECK(ctx, RMT_EINVAL, "null ctx");
@@ -1016,7 +1062,7 @@ int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, 
     double *pc = ctx->scratch + n, *root = ctx->red + RED_BLOCKS + 17;
     RMT_TRY(dct_solve_after_rows(ctx, pc, root, early_marks));
     RMT_CHECK(!done || !sub_mean, RMT_EINVAL, "projection_finish: done tracks the last kernel");
-    RMT_HIP(launch_done(k_project_correct, rows_grid(ctx->nx, 0, ctx->ny), dim3(256), 0,
+    RMT_HIP(launch_done(ctx, k_project_correct, rows_grid(ctx->nx, 0, ctx->ny), dim3(256), 0,
                         ctx->stream, done, a_star, b_star, (const double *)pc, p_prev, ctx->ny,
                         ctx->nx, divk_make(2 * dx), divk_make(2 * dy), dt / rho, bc_kind, lid, a,
                         b, p, 0, ctx->ny, (const double *)root, (double)n, dtp, rho, m2part,

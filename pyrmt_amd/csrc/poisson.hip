@@ -162,8 +162,7 @@ int dct_plan(rmt_ctx *ctx, double dx, double dy) {
         P->ny = ctx->ny; P->nx = ctx->nx;
         // k_dct1's complex FFT length: N = n - 1 (half the even extension)
         const int Nx = P->nx - 1, Ny = P->ny - 1;
-        static const bool force_rocfft = getenv("RMT_DCT_ROCFFT") && atoi(getenv("RMT_DCT_ROCFFT"));
-        P->lds = !force_rocfft && Nx >= 2 && Ny >= 2 && Nx < K1_MAXN && Ny < K1_MAXN &&
+        P->lds = !ctx->opt.dct_rocfft && Nx >= 2 && Ny >= 2 && Nx < K1_MAXN && Ny < K1_MAXN &&
                  factor(Nx, P->radx, &P->npx) && factor(Ny, P->rady, &P->npy) &&
                  lds_fits(Nx) && lds_fits(Ny);
         P->big = big_radix(P->radx, P->npx) || big_radix(P->rady, P->npy);
@@ -733,11 +732,10 @@ __global__ void __launch_bounds__(256) k_transpose2(const double *__restrict__ i
     }
 }
 
-void transpose(hipStream_t st, const double *in, int R, int C, double *out,
+void transpose(const rmt_ctx *ctx, hipStream_t st, const double *in, int R, int C, double *out,
                const unsigned char *rowmark, int mode) {
-    // RMT_TRANSPOSE2=0: the 8-B kernel
-    static const bool t2 = !(getenv("RMT_TRANSPOSE2") && !atoi(getenv("RMT_TRANSPOSE2")));
-    if (t2 && R % 2 == 0 && C % 2 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0)
+    // transpose2 = 0 (RMT_TRANSPOSE2=0): the 8-B kernel
+    if (ctx->opt.transpose2 && R % 2 == 0 && C % 2 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0)
         k_transpose2<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out, rowmark, mode);
     else
         k_transpose<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, out, rowmark, mode);
@@ -748,10 +746,10 @@ static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p,
     hipStream_t st = ctx->stream;
     // forward along x: p <- DCT_x(rhs) (p doubles as scratch), then T <- p^T (nx x ny)
     RMT_TRY(dct_pass(ctx, false, 0, rhs, p, ny, 0, 1.0));
-    transpose(st, p, ny, nx, P->T);
+    transpose(ctx, st, p, ny, nx, P->T);
     // columns: DCT_y, / eig, inverse DCT_y (scaled), in place on T
     RMT_TRY(dct_pass(ctx, true, 1, P->T, P->T, nx, 0, 1.0 / (2.0 * (ny - 1))));
-    transpose(st, P->T, nx, ny, p);
+    transpose(ctx, st, P->T, nx, ny, p);
     // inverse along x, in place (+ the row sums of the result)
     RMT_TRY(dct_pass(ctx, false, 0, p, p, ny, 0, 1.0 / (2.0 * (nx - 1)), rs));
     RMT_LAUNCHED();
@@ -764,7 +762,7 @@ static int dct_lds_solve(rmt_ctx *ctx, DctPlan *P, const double *rhs, double *p,
 int dct_transpose_unmarked(rmt_ctx *ctx, const double *pc, const unsigned char *rowmark) {
     DctPlan *P = ctx->dct;
     RMT_CHECK(P && P->lds && rowmark, RMT_ENOTSUP, "dct_transpose_unmarked: LDS DCT plan needed");
-    transpose(ctx->stream, pc, P->ny, P->nx, P->T, rowmark, 1);
+    transpose(ctx, ctx->stream, pc, P->ny, P->nx, P->T, rowmark, 1);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -775,9 +773,9 @@ int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root,
     RMT_CHECK(P && P->lds && P->ny <= ctx->rsum_len, RMT_ENOTSUP,
               "dct_solve_after_rows: LDS DCT plan needed");
     const int ny = P->ny, nx = P->nx;
-    transpose(ctx->stream, pc, ny, nx, P->T, early_marks, early_marks ? 2 : 0);
+    transpose(ctx, ctx->stream, pc, ny, nx, P->T, early_marks, early_marks ? 2 : 0);
     RMT_TRY(dct_pass(ctx, true, 1, P->T, P->T, nx, 0, 1.0 / (2.0 * (ny - 1))));
-    transpose(ctx->stream, P->T, nx, ny, pc);
+    transpose(ctx, ctx->stream, P->T, nx, ny, pc);
     RMT_TRY(dct_pass(ctx, false, 0, pc, pc, ny, 0, 1.0 / (2.0 * (nx - 1)), ctx->rsum));
     return rowtree_sums(ctx, ny, dev_root);
 }
@@ -1018,9 +1016,9 @@ int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p) {
     RMT_CHECK(P, RMT_EINVAL, "dct2_solve: no plan");
     const int ny = P->ny, nx = P->nx;
     RMT_TRY(dct2_pass(ctx, 0, 0, rhs, p, ny, 0));
-    transpose(ctx->stream, p, ny, nx, P->T);
+    transpose(ctx, ctx->stream, p, ny, nx, P->T);
     RMT_TRY(dct2_pass(ctx, 1, 1, P->T, P->T, nx, 0));
-    transpose(ctx->stream, P->T, nx, ny, p);
+    transpose(ctx, ctx->stream, P->T, nx, ny, p);
     return dct2_pass(ctx, 2, 0, p, p, ny, 0);
 }
 }  // namespace rmt

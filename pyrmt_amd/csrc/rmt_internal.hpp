@@ -64,6 +64,33 @@ struct PerPlan;   // periodic.hip (reduced-grid 2D FFT)
 
 }  // namespace rmt
 
+// Per-context implementation switches: bit-identical alternatives of the schedule and the
+// kernels (A/B measurements, regression tests).  Every field starts from its environment
+// variable at rmt_ctx_create (defaults below when unset) and can be changed per context with
+// rmt_ctx_set_option(ctx, name, value) (ops.hip: the name table).
+struct rmt_opts {
+    int ext_events = 1;       // RMT_EXT_EVENTS: cross-stream events complete with their kernel
+    int ex_arena_bump = 0;    // RMT_EX_ARENA=bump: record arena by bump allocation
+    int ex_profile = 0;       // RMT_EX_PROFILE: the chain's per-phase clocks (diagnostic)
+    int fix_all = 0;          // RMT_FIX_ALL: the fix-up lists every tile (regression switch)
+    int dct_rocfft = 0;       // RMT_DCT_ROCFFT: rocFFT for every DCT length
+    int transpose2 = 1;       // RMT_TRANSPOSE2: 16-byte transposes
+    int sim_hiprio = 1;       // RMT_SIM_HIPRIO: the step's internal stream at the highest priority
+    int sim_sync = 0;         // RMT_SIM_SYNC: the synchronous step path
+    int early_geometry = 1;   // RMT_EARLY_GEOMETRY
+    int early_transpose = 1;  // RMT_EARLY_TRANSPOSE
+    int fused_fluid = 1;      // RMT_FUSED_FLUID
+    int no_overlap = 0;       // RMT_NO_OVERLAP: no second stream
+    int side_tail = 1;        // RMT_SIDE_TAIL
+    int par_overlap = 1;      // RMT_PAR_OVERLAP
+    int fused_fixprep = 1;    // RMT_FUSED_FIXPREP
+    int merged_join = 1;      // RMT_MERGED_JOIN
+    int test_delay_side = 0;  // RMT_TEST_DELAY_SIDE: sleep units on the second stream (tests)
+    int test_delay_main = 0;  // RMT_TEST_DELAY_MAIN: ... on the main stream (tests)
+    int ch_cols = 2;          // RMT_CH_PARTS: chain workgroups per layer group (column ranges)
+    int ch_lgroups = 0;       // RMT_CH_LAYERS: chain layer groups (0: one per layer)
+};
+
 struct rmt_ctx {
     int ny = 0, nx = 0, device = 0;
     hipStream_t stream = nullptr;
@@ -101,9 +128,7 @@ struct rmt_ctx {
     EdgeTiles edge[64];   // RMT_EDGE_SLOTS
     int edge_next = 0;
     void *imex[2] = {nullptr, nullptr};   // imex.hip: the DST preconditioner plans (u, v)
-    // extrap_chain.hip: the chain's workgroups = ch_cols column ranges of the band x
-    // ch_lgroups layer groups (0: one group per layer, as many as CH_MAXP allows)
-    int ch_cols = 2, ch_lgroups = 0;
+    rmt_opts opt;   // implementation switches (above)
 };
 #define RMT_EDGE_SLOTS 64   // >= every (window, grid) key of a step: 8 slabs x 4 stages + the fused 4
 static_assert(sizeof(((rmt_ctx *)nullptr)->edge) / sizeof(rmt_ctx::EdgeTiles) == RMT_EDGE_SLOTS, "edge slots");
@@ -118,11 +143,10 @@ inline unsigned grid1d(long n, int block) { return (unsigned)((n + block - 1) / 
 // kernel itself: no marker packet between it and the stream's next launch -- an event record
 // there costs the in-order stream ~6-8 us of command-processor time).  RMT_EXT_EVENTS=0: the
 // launch, then a plain record.  done null: a plain launch.
-bool ext_events();
 template <typename... Formals, typename... Actuals>
-inline hipError_t launch_done(void (*k)(Formals...), dim3 g, dim3 b, uint32_t lds,
-                              hipStream_t s, hipEvent_t done, Actuals... a) {
-    if (done && ext_events()) {
+inline hipError_t launch_done(const rmt_ctx *ctx, void (*k)(Formals...), dim3 g, dim3 b,
+                              uint32_t lds, hipStream_t s, hipEvent_t done, Actuals... a) {
+    if (done && ctx->opt.ext_events) {
         hipExtLaunchKernelGGL(k, g, b, lds, s, nullptr, done, 0, a...);
         return hipGetLastError();
     }
@@ -668,7 +692,7 @@ int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root,
 // the row blocks of pc without a marked row, transposed into the plan's column buffer ahead
 // of dct_solve_after_rows(..., rowmark) (which then transposes only the others)
 int dct_transpose_unmarked(rmt_ctx *ctx, const double *pc, const unsigned char *rowmark);
-void transpose(hipStream_t st, const double *in, int R, int C, double *out,
+void transpose(const rmt_ctx *ctx, hipStream_t st, const double *in, int R, int C, double *out,
                const unsigned char *rowmark = nullptr, int mode = 0);
 // MAC grid (mac.py:104-123): DCT-II Neumann solve on a (ny, nx) cell grid, (0,0) -> 0
 int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);

@@ -23,10 +23,6 @@ namespace rmt {
 __global__ void k_delay(int n) {
     for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(127);
 }
-static int test_delay(const char *var) {
-    const char *e = getenv(var);
-    return e ? std::max(0, atoi(e)) : 0;
-}
 
 
 
@@ -167,6 +163,129 @@ __global__ void k_sim_sl(const double *__restrict__ X1, const double *__restrict
     const double dt = dtp ? *dtp : dt_arg;
     sl_segment(X1, X2, a, b, xs, ys, ny, nx, dt, Kx, Ky, x0, y0, R, X1n, X2n, phi_pre, bad, kbits,
                m2, mode, rimw, blockIdx.y, blockIdx.x * 256);
+}
+
+// Tiled SL advection (modes 0 and 2 of sl_segment, same per-cell arithmetic): a 64 x 4 tile
+// stages X1, X2 and -- unless the tile is certified +0.0 -- the velocity on the tile + (1, 2)
+// in LDS, so the RK4 backtrace's four dependent velocity gathers and the foot's map samples
+// are LDS reads instead of four-plus-one dependent global round trips.  The staged region is
+// exactly the union of the tile cells' zero-test neighbourhoods (rows j-1 .. j+2, columns
+// i-1 .. i+2 of sl_zero_block), which holds every bilinear stencil when dt sqrt(m2) <= 0.9 h;
+// a stencil outside it (a larger velocity) reads global memory: the same values either way.
+constexpr int SLT_X = 64, SLT_Y = 4, SLT_SX = SLT_X + 3, SLT_SY = SLT_Y + 3;
+
+// interpolators.py:4-61 at one query point (bilinear_t<false>), corners from the staged
+// tile s (origin row sj0, column si0) when they lie in it, else from g
+__device__ __forceinline__ double bl_tile(const double *__restrict__ s,
+                                          const double *__restrict__ g, double xq, double yq,
+                                          const DivK &Kx, const DivK &Ky, int nx, int ny,
+                                          int sj0, int si0) {
+    double x = divk(xq, Kx), y = divk(yq, Ky);
+    if (!(isfinite(x) && isfinite(y))) return __builtin_nan("");
+    if (x < 0.0) x = 0.0; else if (x > nx - 1.0) x = nx - 1.0;
+    if (y < 0.0) y = 0.0; else if (y > ny - 1.0) y = ny - 1.0;
+    int ix = (int)floor(x), iy = (int)floor(y);
+    if (ix >= nx - 1) ix = nx - 2;
+    if (iy >= ny - 1) iy = ny - 2;
+    const double fx = x - ix, fy = y - iy;
+    const int lx = ix - si0, ly = iy - sj0;
+    double v00, v10, v01, v11;
+    if ((unsigned)lx < (unsigned)(SLT_SX - 1) && (unsigned)ly < (unsigned)(SLT_SY - 1)) {
+        const double *r0 = s + ly * SLT_SX + lx, *r1 = r0 + SLT_SX;
+        v00 = r0[0]; v10 = r0[1]; v01 = r1[0]; v11 = r1[1];
+    } else {
+        const double *r0 = g + (long)iy * nx + ix, *r1 = r0 + nx;
+        v00 = r0[0]; v10 = r0[1]; v01 = r1[0]; v11 = r1[1];
+    }
+    return (1 - fx) * (1 - fy) * v00 + fx * (1 - fy) * v10 + (1 - fx) * fy * v01 + fx * fy * v11;
+}
+
+// grid ((nx + 63) / 64, (ny + 3) / 4); mode 0 (kbits optional) or 2 (the non-rim cells)
+__global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
+    const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ a,
+    const double *__restrict__ b, const double *__restrict__ xs, const double *__restrict__ ys,
+    int ny, int nx, double dt_arg, DivK Kx, DivK Ky, double x0, double y0, double R,
+    double *__restrict__ X1n, double *__restrict__ X2n, double *__restrict__ phi_pre, int *bad,
+    unsigned long long *__restrict__ kbits, const double *m2, const double *__restrict__ dtp,
+    int mode, const unsigned long long *__restrict__ rimw) {
+    __shared__ double s1[SLT_SY * SLT_SX], s2[SLT_SY * SLT_SX];
+    __shared__ double sa[SLT_SY * SLT_SX], sb[SLT_SY * SLT_SX];
+    const double dt = dtp ? *dtp : dt_arg;
+    const int i0 = blockIdx.x * SLT_X, j0 = blockIdx.y * SLT_Y;
+    const int tx = threadIdx.x & (SLT_X - 1), ty = threadIdx.x / SLT_X;
+    const int i = i0 + tx, j = j0 + ty, sj0 = j0 - 1, si0 = i0 - 1;
+    const bool in = i < nx && j < ny;
+    const long c = (long)j * nx + i;
+    unsigned long long bits = 0;
+    for (int q = threadIdx.x; q < SLT_SY * SLT_SX; q += SLT_X * SLT_Y) {
+        const int jj = sj0 + q / SLT_SX, ii = si0 + q % SLT_SX;
+        double v1 = 0.0, v2 = 0.0;
+        if (jj >= 0 && jj < ny && ii >= 0 && ii < nx) {
+            const long g = (long)jj * nx + ii;
+            v1 = X1[g]; v2 = X2[g];
+        }
+        s1[q] = v1; s2[q] = v2;
+        bits |= (unsigned long long)__double_as_longlong(v1) |
+                (unsigned long long)__double_as_longlong(v2);
+    }
+    // the staged region is the zero test's (clipped to the grid): rows j0-1 .. j0+5, columns
+    // i0-1 .. i0+65 (sl_zero_block over the tile's cells)
+    const bool nonzero = __syncthreads_or(bits != 0);
+    const bool zero = sl_skip_ok(m2, dt, fmin(Kx.d, Ky.d)) && !nonzero;
+    bool mine = true;
+    if (mode) {
+        const bool rim = in && ((rimw[(long)j * ((nx + 63) / 64) + (i >> 6)] >> (i & 63)) & 1);
+        mine = !rim;
+    }
+    bool known = false;
+    if (zero) {
+        if (in) {
+            const double ph = disc_phi(0.0, 0.0, x0, y0, R);
+            if (!kbits && !mode) phi_pre[c] = ph;
+            known = ph < 0;
+            if (mine) { X1n[c] = 0.0; X2n[c] = 0.0; }
+        }
+    } else {
+        for (int q = threadIdx.x; q < SLT_SY * SLT_SX; q += SLT_X * SLT_Y) {
+            const int jj = sj0 + q / SLT_SX, ii = si0 + q % SLT_SX;
+            double va = 0.0, vb = 0.0;
+            if (jj >= 0 && jj < ny && ii >= 0 && ii < nx) {
+                const long g = (long)jj * nx + ii;
+                va = a[g]; vb = b[g];
+            }
+            sa[q] = va; sb[q] = vb;
+        }
+        __syncthreads();
+        if (in) {
+            const int o = (ty + 1) * SLT_SX + tx + 1;
+            const double ph = disc_phi(s1[o], s2[o], x0, y0, R);
+            if (!kbits && !mode) phi_pre[c] = ph;
+            known = ph < 0;
+            if (mine) {
+                if (!(isfinite(sa[o]) && isfinite(sb[o]))) atomicOr(bad, 1);
+                const double m = ph <= 0 ? 1.0 : 0.0;
+#define BT_(S, G, X, Y) bl_tile(S, G, X, Y, Kx, Ky, nx, ny, sj0, si0)
+                // functions.py:194-227 (sl_backtrace_t's operations, in order)
+                const double x = xs[i], y = ys[j], hdt = 0.5 * dt, dt6 = dt / 6.0;
+                const double k1x = BT_(sa, a, x, y), k1y = BT_(sb, b, x, y);
+                const double x2 = x - hdt * k1x, y2 = y - hdt * k1y;
+                const double k2x = BT_(sa, a, x2, y2), k2y = BT_(sb, b, x2, y2);
+                const double x3 = x - hdt * k2x, y3 = y - hdt * k2y;
+                const double k3x = BT_(sa, a, x3, y3), k3y = BT_(sb, b, x3, y3);
+                const double x4 = x - dt * k3x, y4 = y - dt * k3y;
+                const double k4x = BT_(sa, a, x4, y4), k4y = BT_(sb, b, x4, y4);
+                const double xb = x - dt6 * (k1x + 2 * k2x + 2 * k3x + k4x);
+                const double yb = y - dt6 * (k1y + 2 * k2y + 2 * k3y + k4y);
+                X1n[c] = BT_(s1, X1, xb, yb) * m;
+                X2n[c] = BT_(s2, X2, xb, yb) * m;
+#undef BT_
+            }
+        }
+    }
+    if (kbits) {
+        const unsigned long long w = __ballot(known);
+        if (tx == 0 && j < ny) kbits[(long)j * ((nx + 63) / 64) + (i0 >> 6)] = w;
+    }
 }
 
 // the row segments holding a rim cell, listed (any order)
@@ -514,9 +633,10 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
                 double *phi_pre, int *bad, const double *dev_m2) {
-    k_sim_sl<<<dim3((ctx->nx + 255) / 256, ctx->ny), 256, 0, ctx->stream>>>(
-        X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx), divk_make(dy), RMT_SHAPE_DISC, x0, y0, R, X1n, X2n,
-        phi_pre, bad, nullptr, dev_m2);
+    k_sim_sl_t<<<dim3((ctx->nx + SLT_X - 1) / SLT_X, (ctx->ny + SLT_Y - 1) / SLT_Y), SLT_X * SLT_Y,
+                 0, ctx->stream>>>(X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx),
+                                   divk_make(dy), x0, y0, R, X1n, X2n, phi_pre, bad, nullptr,
+                                   dev_m2, nullptr, 0, nullptr);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -594,8 +714,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
         int least = 0, greatest = 0;
         RMT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         RMT_HIP(hipStreamCreateWithPriority(&S->st2, hipStreamNonBlocking, least));
-        static const bool hiprio = !getenv("RMT_SIM_HIPRIO") || atoi(getenv("RMT_SIM_HIPRIO"));
-        if (hiprio && greatest != least) {
+        if (ctx->opt.sim_hiprio && greatest != least) {
             RMT_HIP(hipStreamCreateWithPriority(&S->st1, hipStreamNonBlocking, greatest));
             RMT_HIP(hipEventCreateWithFlags(&S->e_in, hipEventDisableTiming));
             RMT_HIP(hipEventCreateWithFlags(&S->e_out, hipEventDisableTiming));
@@ -722,7 +841,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     // device, max |u|^2 comes out of the projection, and the per-step diagnostics go to a
     // device ring read back every RING_N steps -- no host round trip inside the loop.  The
     // synchronous path (t_end clip, profiling, the Eulerian schemes) reads dt back each step.
-    static const bool force_sync = getenv("RMT_SIM_SYNC") && atoi(getenv("RMT_SIM_SYNC"));
+    const bool force_sync = ctx->opt.sim_sync != 0;
     const bool async = !force_sync && !S->prof && std::isinf(t_end) && t_end > 0 &&
                        P.scheme == RMT_SCHEME_SEMILAGRANGIAN;
     int slot = 0;
@@ -802,13 +921,13 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     }
     // the next step's rim words and extrapolation geometry, prepared on the second stream
     // beside this step's projection (they depend on the known plane alone)
-    static const bool geo_env = !(getenv("RMT_EARLY_GEOMETRY") && !atoi(getenv("RMT_EARLY_GEOMETRY")));
+    const bool geo_env = ctx->opt.early_geometry != 0;
     // the column pass's transpose of the row blocks without fix-up rows beside the chain
     // (RMT_EARLY_TRANSPOSE, default on)
-    static const bool early_t_env = !(getenv("RMT_EARLY_TRANSPOSE") && !atoi(getenv("RMT_EARLY_TRANSPOSE")));
+    const bool early_t_env = ctx->opt.early_transpose != 0;
     bool early_t = false;
     // k_phi_rebuild writes the momentum's pure-fluid flags (RMT_FUSED_FLUID, default on)
-    static const bool fluid_env = !(getenv("RMT_FUSED_FLUID") && !atoi(getenv("RMT_FUSED_FLUID")));
+    const bool fluid_env = ctx->opt.fused_fluid != 0;
     bool geo_ready = carry;
     bool m2_last = false;   // the last step's projection wrote the max |u|^2 partials
     for (int it = 0; it < nsteps; ++it) {
@@ -851,13 +970,13 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // the extrapolation chain occupies one CU for milliseconds; everything it does not
         // feed runs beside it: the momentum of every cell, from the pre-extrapolation map, on
         // a second stream, re-run afterwards on the tiles within reach of a target
-        static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
-        static const bool side_tail = !(getenv("RMT_SIDE_TAIL") && !atoi(getenv("RMT_SIDE_TAIL")));
+        const bool no_overlap = ctx->opt.no_overlap != 0;
+        const bool side_tail = ctx->opt.side_tail != 0;
         // the parallel extrapolation: its values pass (~0.5 ms at N=4096, mostly the
         // one-workgroup combine) runs beside the speculative momentum too (RMT_PAR_OVERLAP=0:
         // in order, the momentum after it)
         const bool par = extrap_par_enabled();
-        static const bool par_ov = !(getenv("RMT_PAR_OVERLAP") && !atoi(getenv("RMT_PAR_OVERLAP")));
+        const bool par_ov = ctx->opt.par_overlap != 0;
         const bool overlap = solid && S->st2 && !no_overlap && (!par || par_ov);
         bool fixprep = false;   // the fused fix-up prep (set where the extrapolation runs)
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
@@ -888,9 +1007,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.x0, P.y0,
                     P.R, S->X1n, S->X2n, S->flag, sc, dtp, S->rimw, S->segs, scount);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
-                k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, st>>>(
-                    S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.shape,
-                    P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, S->kbits, sc, dtp);
+                k_sim_sl_t<<<dim3((nx + SLT_X - 1) / SLT_X, (ny + SLT_Y - 1) / SLT_Y), SLT_X * SLT_Y,
+                             0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt,
+                                      divk_make(P.dx), divk_make(P.dy), P.x0, P.y0, P.R, S->X1n,
+                                      S->X2n, S->phi_pre, S->flag, S->kbits, sc, dtp, 0, nullptr);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN_CUBIC) {
                 k_sim_sl_cubic<<<g, 256, 0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx,
                                                   dt, P.dx, P.dy, P.x0, P.y0, P.R, S->X1n,
@@ -921,7 +1041,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             const bool kb = P.scheme == RMT_SCHEME_SEMILAGRANGIAN;   // k_sim_sl wrote kbits
             if (geo_ready && !overlap) RMT_HIP(hipStreamWaitEvent(st, S->e_geo, 0));
             // with the fused fix-up prep (below) the status words are copied by its kernel
-            static const bool fp_env = !(getenv("RMT_FUSED_FIXPREP") && !atoi(getenv("RMT_FUSED_FIXPREP")));
+            const bool fp_env = ctx->opt.fused_fixprep != 0;
             fixprep = overlap && fp_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 &&
                       momentum_mode() != 2 && P.layers > 0;
             int *dstat = fixprep ? nullptr : S->flag + 2;
@@ -940,7 +1060,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_TRY(es);
             if (overlap) {
                 RMT_HIP(hipStreamWaitEvent(S->st2, S->e_sl, 0));
-                static const int dly_side = test_delay("RMT_TEST_DELAY_SIDE");
+                const int dly_side = ctx->opt.test_delay_side;
                 if (dly_side) { k_delay<<<1, 1, 0, S->st2>>>(dly_side); RMT_LAUNCHED(); }
                 if (fixprep && ctx->ex_chain && !ctx->ex_par)
                     RMT_TRY(extrap_sweep(ctx, P.dx, P.dy, P.layers, S->X1n, S->X2n, S->st2));
@@ -961,10 +1081,11 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits) {
                     // the advection of every non-rim cell, once the chain has started (earlier
                     // its blocks would crowd out the one-workgroup band passes)
-                    k_sim_sl<<<dim3((nx + 255) / 256, ny), 256, 0, S->st2>>>(
-                        S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.shape,
-                        P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag, nullptr, sc, dtp, 2,
-                        S->rimw);
+                    k_sim_sl_t<<<dim3((nx + SLT_X - 1) / SLT_X, (ny + SLT_Y - 1) / SLT_Y),
+                                 SLT_X * SLT_Y, 0, S->st2>>>(
+                        S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx),
+                        divk_make(P.dy), P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag,
+                        nullptr, sc, dtp, 2, S->rimw);
                     RMT_LAUNCHED();
                 }
                 MomWork Wf = W;
@@ -1009,10 +1130,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // the parallel mode, whose values pass ends long before that stream's row passes):
         // e_rows, after the speculative momentum AND the projection's rows, here -- beside the
         // ~3 ms chain both are done -- and no second wait before the projection
-        static const bool mj_env = !(getenv("RMT_MERGED_JOIN") && !atoi(getenv("RMT_MERGED_JOIN")));
+        const bool mj_env = ctx->opt.merged_join != 0;
         const bool mjoin = overlap && mj_env && !par;
         if (overlap) {
-            static const int dly_main = test_delay("RMT_TEST_DELAY_MAIN");
+            const int dly_main = ctx->opt.test_delay_main;
             if (dly_main) { k_delay<<<1, 1, 0, st>>>(dly_main); RMT_LAUNCHED(); }
             // 4 + 5 on the tiles the extrapolation can reach
             RMT_HIP(hipStreamWaitEvent(st, mjoin ? S->e_rows : S->e_mom, 0));

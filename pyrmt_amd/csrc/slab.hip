@@ -734,8 +734,7 @@ static int slab_extrapolate(rmt_slab *S, const double *gathered, const long long
                             long long cap, const double *gs) {
     rmt_ctx *ctx = S->ctx;
     const rmt_sim_params &P = S->P;
-    static const bool no_overlap = getenv("RMT_NO_OVERLAP") && atoi(getenv("RMT_NO_OVERLAP"));
-    S->spec = S->st2 && !no_overlap;
+    S->spec = S->st2 && !ctx->opt.no_overlap;
     const int jb = std::max(0, S->r0 - 10), je = std::min(S->NY, S->r1 + 10);
     if (S->spec) ctx->ev_chain = S->e_chain;
     const bool geo = S->geo_ready;
@@ -841,9 +840,9 @@ int rmt_slab_project_cols(rmt_slab *S) {
     RMT_CHECK(S, RMT_EINVAL, "null slab");
     rmt_ctx *ctx = S->ctx;
     const int nc = S->c1 - S->c0;
-    transpose(ctx->stream, S->B, S->NY, nc, S->T);
+    transpose(ctx, ctx->stream, S->B, S->NY, nc, S->T);
     RMT_TRY(dct_pass(ctx, true, 1, S->T, S->T, nc, S->c0, 1.0 / (2.0 * (S->NY - 1))));
-    transpose(ctx->stream, S->T, nc, S->NY, S->B);
+    transpose(ctx, ctx->stream, S->T, nc, S->NY, S->B);
     RMT_LAUNCHED();
     return RMT_OK;
 }

@@ -36,6 +36,23 @@ class _Ctx:
         L.check(L.lib().rmt_ctx_set_stream(self.h, torch.cuda.current_stream().cuda_stream))
         return self.h
 
+    def __del__(self):
+        try:
+            L.lib().rmt_ctx_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_option(self, name, value):
+        """A per-context implementation switch (include/rmt.h rmt_ctx_set_option)."""
+        L.check(L.lib().rmt_ctx_set_option(self.h, name.encode(), int(value)),
+                "rmt_ctx_set_option")
+
+    def get_option(self, name):
+        v = ctypes.c_int()
+        L.check(L.lib().rmt_ctx_get_option(self.h, name.encode(), ctypes.byref(v)),
+                "rmt_ctx_get_option")
+        return v.value
+
 
 def ctx_for(ny, nx):
     torch = _torch()

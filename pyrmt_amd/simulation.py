@@ -28,7 +28,7 @@ class Simulation:
     def __init__(self, N, *, scheme="semilagrangian", bc_kind=NOSLIP_LID, lid=1.0, disc=None,
                  mu_s=0.0, kappa=0.0, rho_s=1.0, eta_s=0.0, mu_f=0.01, rho_f=1.0, w_t=None,
                  layers=3, cfl=0.2, dt_cap=1e-3, stress_band=False, detg_clamp=3.0,
-                 energies=False):
+                 energies=False, options=None):
         if scheme not in SCHEMES:
             raise ValueError(f"Unknown advection scheme {scheme!r}")
         torch = F._torch()
@@ -38,7 +38,13 @@ class Simulation:
         self.xs = np.ascontiguousarray(self.X[0, :]); self.ys = np.ascontiguousarray(self.Y[:, 0])
         self.disc = disc
         w_t = 2.0 * self.dx if w_t is None else w_t
-        self.ctx = F.ctx_for(N, N)
+        if options:
+            # a context of its own with these implementation switches (rmt_ctx_set_option)
+            self.ctx = F._Ctx(N, N, torch.cuda.current_device())
+            for k, v in options.items():
+                self.ctx.set_option(k, v)
+        else:
+            self.ctx = F.ctx_for(N, N)
         P = L.rmt_sim_params()
         P.ny = P.nx = N; P.dx = self.dx; P.dy = self.dy
         P.xs = self.xs.ctypes.data; P.ys = self.ys.ctypes.data
@@ -186,11 +192,13 @@ def initial_disc_map(N, x0, y0, R, layers):
     return F.extrapolate_reference_map(X * m, Y * m, phi, dx, dy, layers)
 
 
-def soft_disc_in_lid_driven(N=128, scheme="semilagrangian", stress_band=False, detg_clamp=3.0):
+def soft_disc_in_lid_driven(N=128, scheme="semilagrangian", stress_band=False, detg_clamp=3.0,
+                            options=None):
     """Configs 2 and 4: neo-Hookean disc (0.6, 0.5, R=0.2) in the lid cavity
-    (soft_disc_in_lid_driven.py:165-199 parameters)."""
+    (soft_disc_in_lid_driven.py:165-199 parameters).  options: implementation switches of a
+    context of the sim's own (Simulation)."""
     kw = soft_disc_params(N, stress_band, detg_clamp)
-    sim = Simulation(N, scheme=scheme, **kw)
+    sim = Simulation(N, scheme=scheme, options=options, **kw)
     _init_disc_map(sim, 0.6, 0.5, 0.2, kw["layers"])
     return sim
 

@@ -16,7 +16,11 @@ ok = st > 0
 t0 = st[ok].min()
 col = cell % nx
 cmin, span = col[ok].min(), col[ok].max() - col[ok].min() + 1
-part = np.minimum(NP - 1, np.maximum(0, (col - cmin) * NP // span))
+if (wave >> 8).max() > 0:   # round 5: wave | part << 8 (parts: column range x layer group)
+    part = wave >> 8
+    wave = wave & 255
+else:
+    part = np.minimum(NP - 1, np.maximum(0, (col - cmin) * NP // span))
 print(f"{n} fits ({ok.sum()} traced); span {(pb.max() - t0) / 100:.1f} us; parts {np.bincount(part)}")
 det = np.where((crit >= 0) & ok, rd - pb[np.maximum(crit, 0)], -1)
 post = (pb - rd)
