@@ -136,7 +136,8 @@ __global__ void __launch_bounds__(MOM_TX * MOM_TY) k_phi_prep_tiles(
                 const double a = X1n[c], bb = X2n[c];
                 v = disc_phi(a, bb, x0, y0, R);
                 if (hy >= 1 && hy <= MOM_TY && hx >= 1 && hx <= MOM_TX) {
-                    X1[c] = a; X2[c] = bb; phi[c] = v;
+                    if (X1) { X1[c] = a; X2[c] = bb; }   // (null: the map stays in X1n)
+                    phi[c] = v;
                 }
             }
             ph[h] = v;

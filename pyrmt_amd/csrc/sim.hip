@@ -40,6 +40,7 @@ struct rmt_sim {
     double *u = nullptr, *v = nullptr, *p = nullptr, *X1 = nullptr, *X2 = nullptr;
     double *phi = nullptr, *phi_pre = nullptr, *J = nullptr;
     double *X1n = nullptr, *X2n = nullptr, *us = nullptr, *vs = nullptr;
+    double *X1h = nullptr, *X2h = nullptr;   // the map buffers rmt_sim_field hands out
     double *sxx = nullptr, *sxy = nullptr, *syy = nullptr;
     double *mw = nullptr;            // momentum workspace (8 planes)
     unsigned long long *kbits = nullptr;   // known plane (phi_pre < 0) from k_sim_sl
@@ -387,7 +388,7 @@ __global__ void k_phi_rebuild(const double *__restrict__ X1n, const double *__re
     if (c < n) {
         if (shape == RMT_SHAPE_DISC) {
             double a = X1n[c], b = X2n[c];
-            X1[c] = a; X2[c] = b;
+            if (X1) { X1[c] = a; X2[c] = b; }
             const double ph = disc_phi(a, b, x0, y0, R);
             phi[c] = ph;
             known = ph < 0;
@@ -414,7 +415,7 @@ __global__ void __launch_bounds__(256) k_phi_rebuild_fluid(
     const int lane = threadIdx.x & 63;
     if (c - lane >= n) return;   // wave-uniform (n is a multiple of 64)
     const double a = X1n[c], b = X2n[c];
-    X1[c] = a; X2[c] = b;
+    if (X1) { X1[c] = a; X2[c] = b; }
     const double ph = disc_phi(a, b, x0, y0, R);
     phi[c] = ph;
     if (nbits) {
@@ -455,7 +456,7 @@ __global__ void __launch_bounds__(256) k_phi_tiles(const double *__restrict__ X1
         if (j < ny && i < nx) {
             const long c = (long)j * nx + i;
             const double a = X1n[c], b = X2n[c];
-            X1[c] = a; X2[c] = b;
+            if (X1) { X1[c] = a; X2[c] = b; }
             const double ph = disc_phi(a, b, x0, y0, R);
             phi[c] = ph;
             known = ph < 0;
@@ -685,6 +686,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     double **planes[] = {&S->u, &S->v, &S->p, &S->X1, &S->X2, &S->phi, &S->phi_pre, &S->J,
                          &S->X1n, &S->X2n, &S->us, &S->vs, &S->sxx, &S->sxy, &S->syy};
     for (auto pp : planes) { *pp = q; q += n; }
+    S->X1h = S->X1; S->X2h = S->X2;
     S->kbits = (unsigned long long *)q; q += n;   // ny * ceil(nx / 64) words fit a plane
     S->mw = q; q += MOM_WORK_PLANES * n;
     S->xs = q; q += nx;
@@ -830,6 +832,20 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             c->stream = user;
         }
     } on_hi{ctx, ctx->stream, S};
+    // the map buffers swap roles every step; at the call's end the state is copied back into
+    // the buffers rmt_sim_field hands out (one copy per call instead of one per step).  Runs
+    // on the step's stream before on_hi hands the stream back (destroyed first).
+    struct MapHome {
+        rmt_sim *S;
+        ~MapHome() {
+            if (S->X1 == S->X1h) return;
+            const size_t b = (size_t)S->P.ny * S->P.nx * sizeof(double);
+            (void)hipMemcpyAsync(S->X1h, S->X1, b, hipMemcpyDeviceToDevice, S->ctx->stream);
+            (void)hipMemcpyAsync(S->X2h, S->X2, b, hipMemcpyDeviceToDevice, S->ctx->stream);
+            std::swap(S->X1, S->X1n);
+            std::swap(S->X2, S->X2n);
+        }
+    } map_home{S};
     if (S->st1) {
         RMT_HIP(hipEventRecord(S->e_in, ctx->stream));
         RMT_HIP(hipStreamWaitEvent(S->st1, S->e_in, 0));
@@ -1092,16 +1108,16 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 if (fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 && MOM_TX == 64) {
                     // phi and the stage kernels' pure-fluid flags in one pass
                     k_phi_rebuild_fluid<<<g, 256, 0, S->st2>>>(
-                        S->X1n, S->X2n, n, nx, (nx + 63) / 64, P.x0, P.y0, P.R, S->phi, S->X1,
-                        S->X2, nb, fluid_threshold(&M), fluid_rows_buf(W, 0, nx));
+                        S->X1n, S->X2n, n, nx, (nx + 63) / 64, P.x0, P.y0, P.R, S->phi, nullptr,
+                        nullptr, nb, fluid_threshold(&M), fluid_rows_buf(W, 0, nx));
                     Wf.fluid_rows_ready = true;
                 } else {
                     k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0,
-                                                          P.R, S->phi, S->X1, S->X2, nb);
+                                                          P.R, S->phi, nullptr, nullptr, nb);
                 }
                 RMT_LAUNCHED();
                 ctx->stream = S->st2;
-                int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi,
+                int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1n, S->X2n, S->phi,
                                       S->us, S->vs, S->sxx, S->sxy, S->syy, S->J, Wf);
                 if (ms == RMT_OK) ms = hipEventRecord(S->e_mom, S->st2) ? RMT_EDEVICE : RMT_OK;
                 // and the projection's rows from the speculative u*, v* (the fix-up tiles the
@@ -1144,13 +1160,13 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             const bool geo_next = async && geo_env && nb && P.layers > 0 &&
                                   (it + 1 < nsteps || S->carry_on);
             if (fixprep) {
-                RMT_TRY(fixup_phi_prep(ctx, &M, W, S->X1n, S->X2n, P.x0, P.y0, P.R, S->X1, S->X2,
+                RMT_TRY(fixup_phi_prep(ctx, &M, W, S->X1n, S->X2n, P.x0, P.y0, P.R, nullptr, nullptr,
                                        S->phi, nb, S->sxx, S->sxy, S->syy, S->J, S->tiles,
                                        S->tcount, S->max_tiles, extrap_status(ctx, P.layers),
                                        S->flag + 2, geo_next ? S->e_kb : nullptr));
             } else {
                 k_phi_tiles<<<list_grid(S->max_tiles), 256, 0, st>>>(S->X1n, S->X2n, ny, nx, P.x0, P.y0, P.R,
-                                                           S->phi, S->X1, S->X2, S->tiles, S->tcount,
+                                                           S->phi, nullptr, nullptr, S->tiles, S->tcount,
                                                            tiles_x, nb);
                 RMT_LAUNCHED();
             }
@@ -1180,19 +1196,19 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 RMT_HIP(hipEventRecord(S->e_geo, sg));
                 geo_ready = true;
             }
-            RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
+            RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1n, S->X2n, S->phi, S->us, S->vs,
                                    S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,
                                    S->max_tiles, nullptr, fixprep));
         } else {
             // 4. phi from the advected + extrapolated map (and the momentum's pure-fluid flags)
             if (fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 && MOM_TX == 64) {
                 k_phi_rebuild_fluid<<<g, 256, 0, st>>>(
-                    S->X1n, S->X2n, n, nx, (nx + 63) / 64, P.x0, P.y0, P.R, S->phi, S->X1,
-                    S->X2, nb, fluid_threshold(&M), fluid_rows_buf(W, 0, nx));
+                    S->X1n, S->X2n, n, nx, (nx + 63) / 64, P.x0, P.y0, P.R, S->phi, nullptr,
+                    nullptr, nb, fluid_threshold(&M), fluid_rows_buf(W, 0, nx));
                 W.fluid_rows_ready = true;
             } else {
                 k_phi_rebuild<<<g, 256, 0, st>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0, P.R,
-                                                  S->phi, S->X1, S->X2, nb);
+                                                  S->phi, nullptr, nullptr, nb);
             }
             RMT_LAUNCHED();
             if (par && async && geo_env && nb && P.layers > 0 && S->st2 && it + 1 < nsteps) {
@@ -1209,7 +1225,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 geo_ready = true;
             }
             // 5. momentum (RK4)
-            RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1, S->X2, S->phi, S->us, S->vs,
+            RMT_TRY(momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1n, S->X2n, S->phi, S->us, S->vs,
                                  S->sxx, S->sxy, S->syy, S->J, W));
         }
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[4], st));
@@ -1233,6 +1249,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                             P.bc_kind, P.lid, S->p, S->u, S->v, S->p));
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[5], st));
         m2_last = async;
+        // the advected + extrapolated map (X1n, X2n) is the state from here on: the two map
+        // buffers swap roles instead of copying the map back (restored at the call's end)
+        std::swap(S->X1, S->X1n);
+        std::swap(S->X2, S->X2n);
         // 7. diagnostics (running them beside the projection on the second stream measured
         // no gain: both are HBM-bound)
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,
