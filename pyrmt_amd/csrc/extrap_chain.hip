@@ -729,6 +729,7 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
 }
 
 // ------------------------------------------------------------------ 3. the chain ---
+constexpr int CH_XL2 = 3;   // the lane of a fit's X2 result (ch_fit)
 constexpr int CH_BUFD = CH_MAXREC / 8 + 32;   // doubles per wave record buffer (+ the tail
                                               // prefetch's NRT = 24 reads past a short record)
 constexpr long CH_SPIN_LIMIT = 1L << 25;
@@ -890,8 +891,12 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     const double x0 = U(2), y0 = U(3), M0 = U(4), M1 = U(5), M2 = U(6), M3 = U(7), M4 = U(8);
     const double M5 = U(9), M6 = U(10), M7 = U(11), M8 = U(12), C0 = U(13), C1 = U(14);
     const double C2 = U(15), inv_det = U(16);
+    // fold lanes: one per ordered sum (row of the term table: X1's three, then X2's three)
+    const int fs = lane % 3, fc = lane >= 3 ? 1 : 0, frow = lane;
+    const bool fl = lane < 6;
+    constexpr int XL2 = CH_XL2;   // the lane holding X2's result
     double acc = 0.0;
-    if (lane < 6) acc = B[17 + lane];
+    if (fl) acc = B[17 + frow];
     const bool has = lane < nd;
     int2 e = make_int2(0, -1);
     bool crit = false;
@@ -942,9 +947,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     const int kc = cm ? __builtin_amdgcn_readlane(e.x, cl) : npad;
     const int eyc = __builtin_amdgcn_readlane(e.y, cl);
     const int slc = eyc & (CH_R - 1);
-    const int m3 = lane % 3;
     const double cc0 = rlf(cf[0], cl), cc1 = rlf(cf[1], cl), cc2 = rlf(cf[2], cl);
-    const double cfc = m3 == 0 ? cc0 : (m3 == 1 ? cc1 : cc2);   // lane k: w * a_(k % 3)
+    const double cfc = fs == 0 ? cc0 : (fs == 1 ? cc1 : cc2);   // fold lane: w * a_s
     // pass 1: products of the other sources already published
     {
         const bool ready = !done && __hip_atomic_load(&tag[slot], __ATOMIC_RELAXED,
@@ -963,7 +967,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     if (kmiss > kc) kmiss = kc;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (lane < 6) acc = ch_fold_span(acc, tv + lane * npad, 0, kmiss);
+    if (fl) acc = ch_fold_span(acc, tv + frow * npad, 0, kmiss);
     CH_STAMP(3);
     if (pend) {
         long sp = 0;
@@ -985,18 +989,18 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
-    if (lane < 6) acc = ch_fold_span(acc, tv + lane * npad, kmiss, kc);
+    if (fl) acc = ch_fold_span(acc, tv + frow * npad, kmiss, kc);
     if (cm) {
         // the terms after kc: their head chunk and the next two in registers before the
         // critical value arrives (pure VALU adds after it), the rest from LDS.  Rows are padded
         // with +0.0 to whole chunks (exact: a sum that starts at +0.0 is never -0.0).
         // (lanes 0-5 only: 64 lanes at a row stride would conflict on every LDS bank)
-        const double *row = tv + lane * npad;
+        const double *row = tv + frow * npad;
         const int h0 = (kc + 1) >> 3, hs = kc + 1 - 8 * h0, nch = npad >> 3;
         // (the profiled build keeps one chunk: its counters need the registers)
         constexpr int NRT = PROF ? 8 : 24;
         double rt[NRT];
-        if (lane < 6) {
+        if (fl) {
             const double2 *r2 = (const double2 *)(row + 8 * h0);
 #pragma unroll
             for (int k = 0; k < NRT / 2; ++k) {
@@ -1021,6 +1025,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
                                                                      __HIP_MEMORY_SCOPE_WORKGROUP));
             vc.y = __longlong_as_double((long long)__hip_atomic_load(vq + 1, __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_WORKGROUP));
+            __builtin_amdgcn_sched_barrier(0);   // all three reads issued, then the tag test
             if (__builtin_amdgcn_readfirstlane(tg) == eyc) break;
             if (++sp > CH_SPIN_LIMIT) return false;
         }
@@ -1031,8 +1036,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             tr_ready = __builtin_amdgcn_s_memrealtime();
         }
         __builtin_amdgcn_s_setprio(3);   // from the arrival through the publish
-        if (lane < 6) {
-            acc += cfc * (lane < 3 ? vc.x : vc.y);
+        if (fl) {
+            acc += cfc * (fc == 0 ? vc.x : vc.y);
             do {   // (straight-line: rt indexed statically)
                 if (h0 >= nch) break;   // kc was the last term
 #pragma unroll
@@ -1071,7 +1076,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
     asm volatile("" ::: "memory");
     if (lane == 0)
         __hip_atomic_store(&tag[x & (CH_R - 1)], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (pub && (lane == 0 || lane == 3))   // after the LDS hand-off: the local reader first
+    if (pub && (lane == 0 || lane == XL2))   // after the LDS hand-off: the local reader first
         __hip_atomic_store((u64 *)gval + 2L * gslot + (lane == 0 ? 0 : 1),
                            (u64)__double_as_longlong(o_out), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -1133,7 +1138,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         CH_STAMP(0);
         // the previous fit's stores go out BEFORE the prefetch, so that waiting for the
         // prefetched record next trip never waits on a younger store
-        if (c >= 0 && (lane == 0 || lane == 3)) (lane == 0 ? X1e : X2e)[c] = o;
+        if (c >= 0 && (lane == 0 || lane == CH_XL2)) (lane == 0 ? X1e : X2e)[c] = o;
         // prefetch the next record of this wave into the registers just staged
         const long long nx = __double_as_longlong(B[23]);
         const int x2 = __builtin_amdgcn_readfirstlane((int)(nx >> 32));
@@ -1149,7 +1154,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
     if constexpr (PROF)
         if (lane == 0)
             for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long *)&gprof[k], pr[k]);
-    if (ok && c >= 0 && (lane == 0 || lane == 3)) (lane == 0 ? X1e : X2e)[c] = o;
+    if (ok && c >= 0 && (lane == 0 || lane == CH_XL2)) (lane == 0 ? X1e : X2e)[c] = o;
     __hip_atomic_store(&cur[wv], 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (!ok && lane == 0) {
         C.ws.ctl[EXC_ABORT] = 1;
