@@ -672,7 +672,10 @@ __device__ __forceinline__ void ms_tile(
 // DC: K.den_const known on the host (drops the IEEE density division's registers: the
 // interior stages 0-2 then run 6 waves per SIMD, LDS 50 KB per block)
 template <bool IN, bool SQ, bool S3, bool DC>
-__global__ void __launch_bounds__(IN ? MS_TI : MS_T, 4) k_mom_stage(
+#ifndef RMT_MS_WAVES
+#define RMT_MS_WAVES 4
+#endif
+__global__ void __launch_bounds__(IN ? MS_TI : MS_T, (IN && DC && !S3) ? RMT_MS_WAVES : 4) k_mom_stage(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
     const double *__restrict__ sxx, const double *__restrict__ sxy,

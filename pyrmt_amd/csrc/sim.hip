@@ -867,6 +867,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     // not crowd the next step's rim advection and record values either.
     bool tail = false, pending = false;
     double *pend_e = nullptr;
+    // the pending tail's diagnostics already ran (on the second stream after the next step's
+    // geometry, beside the projection: they read phi and J only, final after the fix-up)
+    bool pend_diag_done = false, diag_early = false;
     // after_sl: the second stream already waits for this step's e_sl, recorded on the main
     // stream after the tail's projection -- no event of its own (a record right after the
     // velocity correction cost the critical path ~5 us); else one recorded now
@@ -886,9 +889,11 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                          ctx->red + RED_BLOCKS + 17, ny, nx);
         ctx->stream = st;
         RMT_TRY(ts);
-        k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
-        k_diag_p2<<<1, DIAG_T, 0, S->st2>>>(S->dscr, pend_e);
-        RMT_LAUNCHED();
+        if (!pend_diag_done) {
+            k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
+            k_diag_p2<<<1, DIAG_T, 0, S->st2>>>(S->dscr, pend_e);
+            RMT_LAUNCHED();
+        }
         RMT_HIP(hipEventRecord(S->e_tail, S->st2));
         tail = true;
         return RMT_OK;
@@ -1195,6 +1200,18 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 RMT_TRY(gs);
                 RMT_HIP(hipEventRecord(S->e_geo, sg));
                 geo_ready = true;
+                if (side_tail && S->split_proj && !P.energies) {
+                    // this step's diagnostics (phi, J: final after the fix-up prep) behind the
+                    // geometry, beside the projection, instead of in the tail beside the next
+                    // chain; they land in the ring slot this step's record takes below
+                    DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1n, S->X2n, ny, nx,
+                               P.energies, P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s,
+                               P.mu_s, P.kappa, 0, ny};
+                    k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, sg>>>(D, S->dscr);
+                    k_diag_p2<<<1, DIAG_T, 0, sg>>>(S->dscr, S->ring + (size_t)slot * RING_VALS);
+                    RMT_LAUNCHED();
+                    diag_early = true;
+                }
             }
             RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1n, S->X2n, S->phi, S->us, S->vs,
                                    S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,
@@ -1264,6 +1281,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             double *e = S->ring + (size_t)slot * RING_VALS;
             pend_e = e;
             pending = true;
+            pend_diag_done = diag_early;
+            diag_early = false;
             ring_e = e;
             if (nb) { std::swap(S->kbits, S->kbits_next); S->bits_ready = true; }
             if (++slot == S->sync_every) RMT_TRY(flush());
