@@ -48,9 +48,15 @@ PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04", "pmc_traffic_n4096.json")
 # fp64 VALU counts of the same kernel and the measured FMA peak (scripts/pmc_f64.sh ->
 # tools/f64_roof.py): k_mom_stage is VALU-issue-bound, not HBM-bound
 F64_ROOF = os.path.join(ROOT, "profiles", "r04", "f64_roof_n4096.json")
-# dependent fits on the critical path of the bench-state extrapolation at N=4096 (per-fit
-# trace of the chain kernel, tools/chain_trace.py; profiles/r02/chain_trace/)
-CHAIN_DEPTH_4096 = 3257
+# dependency depth of the bench-state extrapolation chain at N=4096: the longest sequence of
+# fits each reading the previous one (tools/chain_dag_depth.py over the exact DAG)
+CHAIN_DAG = os.path.join(ROOT, "profiles", "r05", "chain_dag_n4096.json")
+
+
+def _chain_depth(n):
+    if n != 4096 or not os.path.exists(CHAIN_DAG):
+        return None
+    return json.load(open(CHAIN_DAG))["depth"]
 # the reference's only published timing: the collocated soft-disc step at N=128 on "CPU
 # (8 threads)", ~31 ms/step (docs/PERFORMANCE.md:3-5) = 0.53 M cell-updates/s
 REF_PUBLISHED = {"value": 128 * 128 / 0.031, "unit": "cell-updates/s", "grid": 128,
@@ -307,7 +313,10 @@ def main():
             # chain runs on one workgroup, bounded by its dependency depth
             "latency_bound": {"kernel": "k_ex_chain (exact serial-order extrapolation chain)",
                               "ms_per_step": ex_ms / max(1, ex_calls),
-                              "critical_path_fits": CHAIN_DEPTH_4096 if N == 4096 else None},
+                              "dag_depth_fits": _chain_depth(N),
+                              "us_per_link": (ex_ms / max(1, ex_calls) * 1e3 / _chain_depth(N)
+                                              if _chain_depth(N) else None),
+                              "dag_source": "profiles/r05/chain_dag_n4096.json"},
             "step_roofline": {"alg_bytes_per_cell": STEP_ALG_BYTES_PER_CELL,
                               "per_gpu": True,
                               "achieved_GBs": value / ws * STEP_ALG_BYTES_PER_CELL / 1e9,

@@ -730,6 +730,12 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
 
 // ------------------------------------------------------------------ 3. the chain ---
 constexpr int CH_XL2 = 3;   // the lane of a fit's X2 result (ch_fit)
+#ifndef RMT_CH_PEND_SLEEP
+#define RMT_CH_PEND_SLEEP 0     // s_sleep units between polls of a fit's non-critical sources
+#endif
+#ifndef RMT_CH_POLL_SLEEP
+#define RMT_CH_POLL_SLEEP 0     // ... of its critical source (0: none)
+#endif
 constexpr int CH_BUFD = CH_MAXREC / 8 + 32;   // doubles per wave record buffer (+ the tail
                                               // prefetch's NRT = 24 reads past a short record)
 constexpr long CH_SPIN_LIMIT = 1L << 25;
@@ -983,7 +989,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             }
             if (__ballot(!done) == 0) break;
             if (++sp > CH_SPIN_LIMIT) return false;
-            __builtin_amdgcn_s_sleep(0);
+            __builtin_amdgcn_s_sleep(RMT_CH_PEND_SLEEP);
         }
         __builtin_amdgcn_s_setprio(3);
         __builtin_amdgcn_wave_barrier();
@@ -1028,6 +1034,9 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             __builtin_amdgcn_sched_barrier(0);   // all three reads issued, then the tag test
             if (__builtin_amdgcn_readfirstlane(tg) == eyc) break;
             if (++sp > CH_SPIN_LIMIT) return false;
+#if RMT_CH_POLL_SLEEP > 0
+            __builtin_amdgcn_s_sleep(RMT_CH_POLL_SLEEP);   // A/B: fewer LDS polls per waiting wave
+#endif
         }
         if constexpr (PROF) {
             if (sp) tr_crit = eyc;

@@ -290,7 +290,7 @@ static int axis_make(DstAxis &a, int M, long rows) {
         h[m] = make_double2((double)cosl(t), (double)-sinl(t));
     }
     RMT_HIP(hipMalloc(&a.tw, (M + 1) * sizeof(double2)));
-    RMT_HIP(hipMemcpy(a.tw, h.data(), (M + 1) * sizeof(double2), hipMemcpyHostToDevice));
+    RMT_UPLOAD(a.tw, h.data(), (M + 1) * sizeof(double2));
     return RMT_OK;
 }
 

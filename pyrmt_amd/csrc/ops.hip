@@ -34,6 +34,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"test_delay_main", "RMT_TEST_DELAY_MAIN", &rmt_opts::test_delay_main},
     {"chain_cols", "RMT_CH_PARTS", &rmt_opts::ch_cols},
     {"chain_layer_groups", "RMT_CH_LAYERS", &rmt_opts::ch_lgroups},
+    {"edge_slots", "RMT_EDGE_SLOTS_USED", &rmt_opts::edge_slots},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;
@@ -46,8 +47,12 @@ static rmt_opts opts_from_env() {
     return o;
 }
 
+// Growing a context buffer frees the old one, which kernels queued on any of the context's
+// streams may still read: the device is drained first (hipFree's implicit synchronisation,
+// made explicit), and the new buffer's contents are written by stream-ordered kernels only.
 int ensure_scratch(rmt_ctx *ctx, size_t bytes) {
     if (ctx->scratch_bytes >= bytes) return RMT_OK;
+    RMT_HIP(hipDeviceSynchronize());
     if (ctx->scratch) RMT_HIP(hipFree(ctx->scratch));
     ctx->scratch = nullptr; ctx->scratch_bytes = 0;
     RMT_HIP(hipMalloc(&ctx->scratch, bytes));
@@ -57,6 +62,7 @@ int ensure_scratch(rmt_ctx *ctx, size_t bytes) {
 int ensure_bytes(rmt_ctx *ctx, size_t bytes) {
     ++ctx->bytes_gen;   // (rmt_sim's carried geometry lives there: any other user ends it)
     if (ctx->bytes_len >= bytes) return RMT_OK;
+    RMT_HIP(hipDeviceSynchronize());
     if (ctx->bytes) RMT_HIP(hipFree(ctx->bytes));
     ctx->bytes = nullptr; ctx->bytes_len = 0;
     RMT_HIP(hipMalloc(&ctx->bytes, bytes));

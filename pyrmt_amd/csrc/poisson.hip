@@ -146,7 +146,7 @@ static int twiddles(int M, const int *rad, int np, double2 **W, bool post = fals
         for (long k = 0; k <= M; ++k) h.push_back(unit_root(k, 2L * M));
     h.push_back(make_double2(1.0, 0.0));
     RMT_HIP(hipMalloc(W, h.size() * sizeof(double2)));
-    RMT_HIP(hipMemcpy(*W, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice));
+    RMT_UPLOAD(*W, h.data(), h.size() * sizeof(double2));
     return RMT_OK;
 }
 
@@ -201,8 +201,8 @@ int dct_plan(rmt_ctx *ctx, double dx, double dy) {
     std::vector<double> lx, ly;
     host_lambda(P->nx, dx, lx);
     host_lambda(P->ny, dy, ly);
-    RMT_HIP(hipMemcpy(P->lamx, lx.data(), lx.size() * 8, hipMemcpyHostToDevice));
-    RMT_HIP(hipMemcpy(P->lamy, ly.data(), ly.size() * 8, hipMemcpyHostToDevice));
+    RMT_UPLOAD(P->lamx, lx.data(), lx.size() * 8);
+    RMT_UPLOAD(P->lamy, ly.data(), ly.size() * 8);
     P->dx = dx; P->dy = dy;
     return RMT_OK;
 }
@@ -927,7 +927,7 @@ static int quarter_twiddles(int n, double2 **Q) {
         h[k] = make_double2((double)cosl(a), (double)-sinl(a));
     }
     RMT_HIP(hipMalloc(Q, n * sizeof(double2)));
-    RMT_HIP(hipMemcpy(*Q, h.data(), n * sizeof(double2), hipMemcpyHostToDevice));
+    RMT_UPLOAD(*Q, h.data(), n * sizeof(double2));
     return RMT_OK;
 }
 
@@ -962,8 +962,8 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
     mac_lambda(ny, dy, ly);
     RMT_HIP(hipMalloc(&P->lamx, nx * sizeof(double)));
     RMT_HIP(hipMalloc(&P->lamy, ny * sizeof(double)));
-    RMT_HIP(hipMemcpy(P->lamx, lx.data(), nx * 8, hipMemcpyHostToDevice));
-    RMT_HIP(hipMemcpy(P->lamy, ly.data(), ny * 8, hipMemcpyHostToDevice));
+    RMT_UPLOAD(P->lamx, lx.data(), nx * 8);
+    RMT_UPLOAD(P->lamy, ly.data(), ny * 8);
     RMT_HIP(hipMalloc(&P->T, (size_t)nx * ny * sizeof(double)));
     static bool attr = false;
     if (!attr) {

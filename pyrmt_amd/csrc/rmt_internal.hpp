@@ -55,6 +55,14 @@ void set_error(const std::string &msg);
     do {                                                                                \
         if (!(cond)) { ::rmt::set_error(msg); return (code); }                          \
     } while (0)
+// Host -> device upload of a table that kernels on any of the context's streams read: a
+// plain hipMemcpy from pageable memory may return once the data is staged, before its DMA
+// lands, and kernels on non-blocking streams are not ordered after it -- so drain the device.
+#define RMT_UPLOAD(dst, src, bytes)                                                     \
+    do {                                                                                \
+        RMT_HIP(hipMemcpy((dst), (src), (bytes), hipMemcpyHostToDevice));               \
+        RMT_HIP(hipDeviceSynchronize());                                                \
+    } while (0)
 #define RMT_TRY(expr)                                                                   \
     do { int s_ = (expr); if (s_ != RMT_OK) return s_; } while (0)
 
@@ -89,8 +97,12 @@ struct rmt_opts {
     int test_delay_main = 0;  // RMT_TEST_DELAY_MAIN: ... on the main stream (tests)
     int ch_cols = 2;          // RMT_CH_PARTS: chain workgroups per layer group (column ranges)
     int ch_lgroups = 0;       // RMT_CH_LAYERS: chain layer groups (0: one per layer)
+    int edge_slots = 64;      // RMT_EDGE_SLOTS_USED: edge-tile lists kept (1..64; fewer evict)
 };
 
+#ifndef RMT_EDGE_SLOTS
+#define RMT_EDGE_SLOTS 64   // >= every (window, grid) key of a step: 8 slabs x 4 stages + the fused 4
+#endif
 struct rmt_ctx {
     int ny = 0, nx = 0, device = 0;
     hipStream_t stream = nullptr;
@@ -125,12 +137,11 @@ struct rmt_ctx {
     bool ev_chain_vals = false;
     // momentum.hip: the stage tiles a full launch's interior kernel skips, per row window
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
-    EdgeTiles edge[64];   // RMT_EDGE_SLOTS
+    EdgeTiles edge[RMT_EDGE_SLOTS];
     int edge_next = 0;
     void *imex[2] = {nullptr, nullptr};   // imex.hip: the DST preconditioner plans (u, v)
     rmt_opts opt;   // implementation switches (above)
 };
-#define RMT_EDGE_SLOTS 64   // >= every (window, grid) key of a step: 8 slabs x 4 stages + the fused 4
 static_assert(sizeof(((rmt_ctx *)nullptr)->edge) / sizeof(rmt_ctx::EdgeTiles) == RMT_EDGE_SLOTS, "edge slots");
 
 namespace rmt {

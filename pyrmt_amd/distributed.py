@@ -519,9 +519,17 @@ class DistributedSim:
         snap, done = None, 0
 
         def snapshot():
-            own = [{f: s.view(f)[s.r0 - s.lo:s.r1 - s.lo].clone() for f in _STATE}
-                   for s in S]
-            return own, self.t, len(self.records), done
+            # one preallocated buffer per slab and field, reused by every window (copy_: no
+            # allocation, and no second copy of the state alive per window)
+            buf = getattr(self, "_snap_buf", None)
+            if buf is None:
+                buf = self._snap_buf = [{f: s.view(f)[s.r0 - s.lo:s.r1 - s.lo].clone()
+                                         for f in _STATE} for s in S]
+            else:
+                for s, b in zip(S, buf):
+                    for f in _STATE:
+                        b[f].copy_(s.view(f)[s.r0 - s.lo:s.r1 - s.lo])
+            return buf, self.t, len(self.records), done
 
         def restore(sn):
             own, t, nrec, d = sn
@@ -565,6 +573,7 @@ class DistributedSim:
             gs = comm.allgather([s.view("scal") for s in S])[0]
             for s in S:
                 L.check(s.lib.rmt_slab_next_dt(s.h, gs.data_ptr(), G, None), "rmt_slab_next_dt")
+            self._dev_dt = True   # the next step() need not repeat the dt allgather
             geo = False
 
         geo = False

@@ -153,6 +153,29 @@ def test_config4_slab_step_N4096(gpu, G):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("G", [4, 8])
+def test_config4_slab_step_N4096_evicting_edge_lists(gpu, G):
+    """As above with only 8 edge-tile lists kept on the context (edge_slots = 8): G slabs
+    cycle 4 G + 4 (window, grid) keys per step, so lists are evicted, freed and re-uploaded
+    every step while stage kernels of both streams are queued -- the configuration of the
+    round-4 failure.  3 steps, bit-identical to the fused step."""
+    from pyrmt_amd import distributed as D
+    from pyrmt_amd import functions as F
+    N, K = 4096, 3
+    c = F.ctx_for(N, N)
+    old = c.get_option("edge_slots")
+    c.set_option("edge_slots", 8)
+    try:
+        ref = _fused(gpu, N, K)
+        sim = D.soft_disc_in_lid_driven(N, D.LocalComm(G))
+        sim.step(K)
+        for f in ("u", "v", "p", "X1", "X2"):
+            np.testing.assert_array_equal(sim.gather(f), ref.get(f), err_msg=f)
+    finally:
+        c.set_option("edge_slots", old)
+
+
+@pytest.mark.gpu
 def test_slab_step_two_processes_gloo_N4096(gpu):
     """The TorchComm path at config 4's own size (two processes on cuda:0 over gloo, 2 steps).
     (The slab step's LDS DCT-I needs 2(N-1) to factor into radices <= 23: N = 4096 and 256
