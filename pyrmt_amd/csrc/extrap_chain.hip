@@ -730,12 +730,15 @@ __global__ void __launch_bounds__(256) k_ex_relink(ExWs ws, int ML) {
 
 // ------------------------------------------------------------------ 3. the chain ---
 constexpr int CH_XL2 = 3;   // the lane of a fit's X2 result (ch_fit)
-#ifndef RMT_CH_PEND_SLEEP
-#define RMT_CH_PEND_SLEEP 0     // s_sleep units between polls of a fit's non-critical sources
+#ifndef RMT_CH_POLL_PRIO
+#define RMT_CH_POLL_PRIO 3   // wave priority while polling a fit's critical source (the
+#endif                       // highest: 0 measured 2.19 ms per chain, 2 2.15, 3 2.15)
+#ifndef RMT_CH_WORK_PRIO
+#define RMT_CH_WORK_PRIO 1   // ... during a fit's pre-arrival work (0: 2.17 ms, no better)
 #endif
-#ifndef RMT_CH_POLL_SLEEP
-#define RMT_CH_POLL_SLEEP 0     // ... of its critical source (0: none)
-#endif
+#ifndef RMT_CH_ABL
+#define RMT_CH_ABL 0   // timing ablations (wrong results, A/B only): 1 no tail fold, 2 no
+#endif                 // solve, 4 no waits for sources
 constexpr int CH_BUFD = CH_MAXREC / 8 + 32;   // doubles per wave record buffer (+ the tail
                                               // prefetch's NRT = 24 reads past a short record)
 constexpr long CH_SPIN_LIMIT = 1L << 25;
@@ -934,7 +937,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
                     done = true;
                 }
             }
-            if (__ballot(far && !done) == 0) break;
+            if (__ballot(far && !done) == 0 || (RMT_CH_ABL & 4)) break;
             if constexpr (PROF) {   // the far source still missing with the latest slot
                 int g = far && !done ? -e.y - 1 : -1;
 #pragma unroll
@@ -987,9 +990,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
                 for (int s = 0; s < 6; ++s) tv[s * npad + e.x] = cf[s % 3] * (s < 3 ? v.x : v.y);
                 done = true;
             }
-            if (__ballot(!done) == 0) break;
+            if (__ballot(!done) == 0 || (RMT_CH_ABL & 4)) break;
             if (++sp > CH_SPIN_LIMIT) return false;
-            __builtin_amdgcn_s_sleep(RMT_CH_PEND_SLEEP);
         }
         __builtin_amdgcn_s_setprio(3);
         __builtin_amdgcn_wave_barrier();
@@ -1022,7 +1024,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         // the tag and the value read back to back in one LDS round trip (relaxed atomic
         // loads: a plain value load would be sunk out of the loop)
         const unsigned long long *vq = (const unsigned long long *)&val[slc];
-        __builtin_amdgcn_s_setprio(0);   // polling: leave the SIMD to the producers
+        __builtin_amdgcn_s_setprio(RMT_CH_POLL_PRIO);   // polling the critical source
         for (;;) {
             const int tg = __hip_atomic_load(&tag[slc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             asm volatile("" ::: "memory");             // the tag read is issued first
@@ -1032,11 +1034,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
             vc.y = __longlong_as_double((long long)__hip_atomic_load(vq + 1, __ATOMIC_RELAXED,
                                                                      __HIP_MEMORY_SCOPE_WORKGROUP));
             __builtin_amdgcn_sched_barrier(0);   // all three reads issued, then the tag test
-            if (__builtin_amdgcn_readfirstlane(tg) == eyc) break;
+            if (__builtin_amdgcn_readfirstlane(tg) == eyc || (RMT_CH_ABL & 4)) break;
             if (++sp > CH_SPIN_LIMIT) return false;
-#if RMT_CH_POLL_SLEEP > 0
-            __builtin_amdgcn_s_sleep(RMT_CH_POLL_SLEEP);   // A/B: fewer LDS polls per waiting wave
-#endif
         }
         if constexpr (PROF) {
             if (sp) tr_crit = eyc;
@@ -1048,6 +1047,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         if (fl) {
             acc += cfc * (fc == 0 ? vc.x : vc.y);
             do {   // (straight-line: rt indexed statically)
+                if (RMT_CH_ABL & 1) break;   // timing ablation (wrong results): no tail
                 if (h0 >= nch) break;   // kc was the last term
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
@@ -1076,7 +1076,8 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
         const double xs = (b0 * C0 - M1 * (b1 * M8 - M5 * b2) + M2 * (b1 * M7 - M4 * b2)) * inv_det;
         const double ys = (M0 * (b1 * M8 - M5 * b2) - b0 * C1 + M2 * (M3 * b2 - b1 * M6)) * inv_det;
         const double zs = (M0 * (M4 * b2 - b1 * M7) - M1 * (M3 * b2 - b1 * M6) + b0 * C2) * inv_det;
-        double o = xs + ys * x0 + zs * y0;
+        // (ablation 2: no solve -- the identity map's value, still after acc)
+        double o = (RMT_CH_ABL & 2) ? (lane == 0 ? x0 : y0) + 0.0 * acc : xs + ys * x0 + zs * y0;
         if constexpr (PROF) asm volatile("" : "+v"(o));
         CH_STAMP(9);
         ((double *)&val[x & (CH_R - 1)])[lane == 0 ? 0 : 1] = o;
@@ -1091,7 +1092,7 @@ __device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val,
                            __HIP_MEMORY_SCOPE_AGENT);
     if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     CH_STAMP(10);
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(RMT_CH_WORK_PRIO);   // the next fit's pre-arrival work
     c_out = __double_as_longlong(B[0]);
     if constexpr (PROF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     CH_STAMP(5);
