@@ -779,6 +779,18 @@ __global__ void __launch_bounds__(256) k_fluid_rows(const double *__restrict__ p
     if (lane == 0) out[(long)(j - jlo) * tiles_x + tx] = all == ~0ull;
 }
 
+// k_fluid_rows' flags from k_sim_sl_t's per-tile bits: row j, tile tx is pure fluid when its
+// own 64 cells and the two columns on each side (the neighbour tiles' edge bits) all are
+__global__ void __launch_bounds__(256) k_fluid_rows_bits(const unsigned char *__restrict__ fbits,
+                                                         int tiles_x, int jlo, int jhi,
+                                                         unsigned char *__restrict__ out) {
+    const long w = (long)blockIdx.x * 256 + threadIdx.x;
+    if (w >= (long)(jhi - jlo) * tiles_x) return;
+    const int tx = (int)(w % tiles_x);
+    const unsigned char *b = fbits + (long)jlo * tiles_x + w;
+    out[w] = (b[0] & 1) && (tx == 0 || (b[-1] & 4)) && (tx == tiles_x - 1 || (b[1] & 2));
+}
+
 // tile flag for a stage tile whose first output row is j: rows [j - 2, j + MS_TY + 2) of
 // [jlo, jhi) all fluid (k_fluid_rows); rows outside the window are never loaded
 __global__ void __launch_bounds__(256) k_fluid_win(const unsigned char *__restrict__ rows,
@@ -853,6 +865,28 @@ static int stage_edge_tiles(rmt_ctx *ctx, RowWin ws, int ntiles, int tiles_x, co
     return RMT_OK;
 }
 
+// The edge-tile stream of the full-grid stages (opt.edge_stream; nullptr: off, or no stream of
+// the context's own to pair with), created at the priority of the stream it serves.
+static int edge_stream(rmt_ctx *ctx, hipStream_t *out) {
+    *out = nullptr;
+    if (!ctx->opt.edge_stream || !ctx->stream) return RMT_OK;
+    int prio = 0;
+    RMT_HIP(hipStreamGetPriority(ctx->stream, &prio));
+    if (ctx->edge_st && ctx->edge_prio != prio) {
+        RMT_HIP(hipStreamSynchronize(ctx->edge_st));
+        RMT_HIP(hipStreamDestroy(ctx->edge_st));
+        ctx->edge_st = nullptr;
+    }
+    if (!ctx->edge_st) {
+        RMT_HIP(hipStreamCreateWithPriority(&ctx->edge_st, hipStreamNonBlocking, prio));
+        ctx->edge_prio = prio;
+    }
+    for (auto &e : ctx->edge_ev)
+        if (!e) RMT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *out = ctx->edge_st;
+    return RMT_OK;
+}
+
 // One fused stage launch: k_{s+1} -> (k1 | k2 | k3)[s], acc1 / acc2 / u* (see MomWork)
 // tlist: tiles of the whole grid (ws.jb = 0), outputs on rows [olo, ohi); else the tiles of
 // rows [ws.jb, ws.je)
@@ -860,7 +894,7 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
                      const double *v, const double *p, const double *sxx, const double *sxy,
                      const double *syy, const MomWork &W, double *u_new, double *v_new,
                      RowWin ws, int ntiles, const int *tlist, const int *tcount, int olo,
-                     int ohi, const unsigned char *fluid_rows) {
+                     int ohi, const unsigned char *fluid_rows, hipStream_t es = nullptr) {
     const int nx = ctx->nx, ny = ctx->ny, tiles_x = (nx + MS_TX - 1) / MS_TX;
     const double coef[4] = {0.0, 0.5 * P->dt, 0.5 * P->dt, P->dt}, dt6 = P->dt / 6.0;
     double *ku[3] = {W.k1u, W.k2u, W.k3u}, *kv[3] = {W.k1v, W.k2v, W.k3v};
@@ -889,6 +923,19 @@ static int mom_stage(rmt_ctx *ctx, const rmt_momentum_params *P, int s, const do
     if (tlist) {
         auto kl = sq ? k_mom_stage_list<true> : k_mom_stage_list<false>;
         kl<<<list_grid(ntiles), MS_T, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
+    } else if (es) {
+        // the edge tiles on their own stream, beside the interior launch: stage s's interior
+        // waits for stage s - 1's edge tiles, its edge tiles for stage s - 1's interior (and
+        // for the stage inputs at s = 0); the two write disjoint tiles of the same planes
+        hipEvent_t *ev = ctx->edge_ev;
+        if (s > 0) RMT_HIP(hipStreamWaitEvent(ctx->stream, ev[4 + s], 0));
+        RMT_HIP(launch_done(ctx, kin, dim3(ntiles), dim3(MS_TI), 0, ctx->stream, ev[1 + s],
+                            MS_ARGS(tlist, tcount, ntiles)));
+        if (enb > 0) {
+            RMT_HIP(hipStreamWaitEvent(es, ev[s], 0));
+            RMT_HIP(launch_done(ctx, kedge, dim3(enb), dim3(MS_T), 0, es, ev[5 + s],
+                                MS_ARGS(elist, ecount, enb)));
+        }
     } else {
         kin<<<ntiles, MS_TI, 0, ctx->stream>>>(MS_ARGS(tlist, tcount, ntiles));
         if (enb > 0) kedge<<<enb, MS_T, 0, ctx->stream>>>(MS_ARGS(elist, ecount, enb));
@@ -940,13 +987,27 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     const RowWin wp = grow(7);
     // skip the pure-fluid segments whose planes already hold the constants: needs the fluid
     // flags before the prep (written by the phi producer) and 64-column segments
-    const bool pskip = W.prep_const && W.fluid_rows_ready && nx % 64 == 0 && MS_TX == 64 &&
+    const int tiles_x = (nx + MS_TX - 1) / MS_TX;
+    // pure-fluid tile rows for the stage kernels, on every resident row (a stage tile's
+    // stress region may reach past its window; rows prep did not write only feed halo cells
+    // that never reach the window's outputs)
+    unsigned char *fluid_rows = fluid_rows_buf(W, w0.lo, nx);   // row w0.lo first
+    bool rows_ready = W.fluid_rows_ready;
+    if (W.fluid_bits && g_mom_mode != 2 && nx % 64 == 0 && MS_TX == 64) {
+        // the phi producer left per-tile bits (k_sim_sl_t): the row flags from them
+        const long nw = (long)(w0.hi - w0.lo) * tiles_x;
+        k_fluid_rows_bits<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(W.fluid_bits, tiles_x, w0.lo,
+                                                                     w0.hi, fluid_rows);
+        RMT_LAUNCHED();
+        rows_ready = true;
+    }
+    const bool pskip = W.prep_const && rows_ready && nx % 64 == 0 && MS_TX == 64 &&
                        g_mom_mode != 2;
     if (pskip) {
         const long nseg = (long)(wp.je - wp.jb) * (nx / 64);
         k_mom_prep_seg<<<(unsigned)((nseg + 4 * PS_SEGS - 1) / (4 * PS_SEGS)), 256, 0, ctx->stream>>>(
             X1, X2, phi, ny, nx, P->dx, P->dy, P->mu_s, P->kappa, w_cut, clamp, P->w_t,
-            sxx, sxy, syy, J, W.H, W.solid, wp.jb, wp.je, fluid_rows_buf(W, w0.lo, nx), w0.lo,
+            sxx, sxy, syy, J, W.H, W.solid, wp.jb, wp.je, fluid_rows, w0.lo,
             W.prep_const);
     } else {
         k_mom_prep<<<grid1d((long)(wp.je - wp.jb) * nx, 256), 256, 0, ctx->stream>>>(
@@ -963,29 +1024,30 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
     double *kbu[2] = {W.k1u, W.k2u}, *kbv[2] = {W.k1v, W.k2v};
     if (ctx->prof) RMT_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
     const bool unfused = g_mom_mode == 2;
-    const int tiles_x = (nx + MS_TX - 1) / MS_TX;
-    // pure-fluid tile rows for the stage kernels, on every resident row (a stage tile's
-    // stress region may reach past its window; rows prep did not write only feed halo cells
-    // that never reach the window's outputs)
-    unsigned char *fluid_rows = fluid_rows_buf(W, w0.lo, nx);   // row w0.lo first
+    hipStream_t es = nullptr;   // the edge-tile stream (edge_stream), when on
     if (!unfused) {
         (void)w_cut;
         const double thr = fluid_threshold(P);
         const long nw = (long)(w0.hi - w0.lo) * tiles_x;
-        if (!W.fluid_rows_ready)
+        if (!rows_ready)
             k_fluid_rows<<<grid1d(nw, 4), 256, 0, ctx->stream>>>(phi, thr, nx, tiles_x, w0.lo,
                                                                   w0.hi, fluid_rows);
-        k_fluid_win<<<grid1d(nw, 256), 256, 0, ctx->stream>>>(fluid_rows, tiles_x, w0.lo, w0.hi,
-                                                               fluid_rows + nw);
-        RMT_LAUNCHED();
+        // (its completion: the stage inputs are ready for the edge-tile stream)
+        RMT_TRY(edge_stream(ctx, &es));
+        RMT_HIP(launch_done(ctx, k_fluid_win, dim3(grid1d(nw, 256)), dim3(256), 0, ctx->stream,
+                            es ? ctx->edge_ev[0] : nullptr, (const unsigned char *)fluid_rows,
+                            tiles_x, w0.lo, w0.hi, fluid_rows + nw));
     }
     for (int s = 0; s < 4 && !unfused; ++s) {
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);
         RMT_TRY(mom_stage(ctx, P, s, u, v, p, sxx, sxy, syy, W, u_new, v_new, ws, ntiles,
                           nullptr, nullptr, ws.jb, ws.je,
-                          fluid_rows + (long)(w0.hi - w0.lo) * tiles_x));
+                          fluid_rows + (long)(w0.hi - w0.lo) * tiles_x, es));
     }
+    // the last stage's edge tiles joined (a record of an earlier call, when that stage had
+    // none, is long complete)
+    if (es) RMT_HIP(hipStreamWaitEvent(ctx->stream, ctx->edge_ev[8], 0));
     RMT_CHECK(!unfused || (!win && !W.dtp), RMT_ENOTSUP,
               "RMT_MOM_UNFUSED: single-domain, host-dt only");
     for (int s = 0; s < 4 && unfused; ++s) {

@@ -35,6 +35,8 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"chain_cols", "RMT_CH_PARTS", &rmt_opts::ch_cols},
     {"chain_layer_groups", "RMT_CH_LAYERS", &rmt_opts::ch_lgroups},
     {"edge_slots", "RMT_EDGE_SLOTS_USED", &rmt_opts::edge_slots},
+    {"edge_stream", "RMT_EDGE_STREAM", &rmt_opts::edge_stream},
+    {"sl_phi", "RMT_SL_PHI", &rmt_opts::sl_phi},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;
@@ -809,8 +811,14 @@ int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (ctx->dct) dct_destroy(ctx->dct);
     if (ctx->dct2) dct2_destroy(ctx->dct2);
     if (ctx->per) per_destroy(ctx->per);
+    if (ctx->edge_st) (void)hipStreamSynchronize(ctx->edge_st);
     for (auto &e : ctx->edge)
         if (e.list) (void)hipFree(e.list);
+    if (ctx->edge_st) (void)hipStreamDestroy(ctx->edge_st);
+    for (auto &e : ctx->edge_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
     imex_destroy(ctx);
     delete ctx;
     return RMT_OK;

@@ -98,6 +98,8 @@ struct rmt_opts {
     int ch_cols = 2;          // RMT_CH_PARTS: chain workgroups per layer group (column ranges)
     int ch_lgroups = 0;       // RMT_CH_LAYERS: chain layer groups (0: one per layer)
     int edge_slots = 64;      // RMT_EDGE_SLOTS_USED: edge-tile lists kept (1..64; fewer evict)
+    int edge_stream = 1;      // RMT_EDGE_STREAM: a full stage's edge tiles beside its interior
+    int sl_phi = 1;           // RMT_SL_PHI: the side stream's SL pass also writes phi + fluid bits
 };
 
 #ifndef RMT_EDGE_SLOTS
@@ -139,6 +141,12 @@ struct rmt_ctx {
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
     EdgeTiles edge[RMT_EDGE_SLOTS];
     int edge_next = 0;
+    // momentum.hip (opt.edge_stream): the stream the edge-tile launches of the full-grid stages
+    // run on, beside the interior launch, at the priority of the stream it serves; events:
+    // [0] the stage inputs ready, [1 + s] interior stage s done, [5 + s] edge stage s done
+    hipStream_t edge_st = nullptr;
+    int edge_prio = 0;
+    hipEvent_t edge_ev[9] = {};
     void *imex[2] = {nullptr, nullptr};   // imex.hip: the DST preconditioner plans (u, v)
     rmt_opts opt;   // implementation switches (above)
 };
@@ -639,6 +647,8 @@ struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + 
     // the pure-fluid row flags (k_fluid_rows' output, at fluid_rows_buf) were already written
     // by the producer of phi (the fused step's k_phi_rebuild): momentum_rk4 skips that pass
     bool fluid_rows_ready = false;
+    // or k_sim_sl_t left per-(row, tile) bits there (its phi output; k_fluid_rows_bits)
+    const unsigned char *fluid_bits = nullptr;
     // per 64-column row segment (nx % 64 == 0), persistent across steps: the last write of the
     // prep planes there was a pure-fluid segment's constants, so k_mom_prep may skip it while
     // it stays pure fluid (null: prep every cell)
@@ -648,12 +658,14 @@ inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
     return MomWork{w,          w + n,      w + 2 * n,  w + 3 * n,  w + 4 * n,  w + 5 * n,
                    w + 6 * n,  w + 7 * n,  w + 8 * n,  w + 9 * n,  w + 10 * n, w + 11 * n,
                    w + 12 * n, w + 13 * n, w + 14 * n, w + 15 * n, w + 16 * n, solid, flag,
-                   nullptr, false};
+                   nullptr, false, nullptr};
 }
 // where momentum_rk4 keeps the per-(row, 64-column tile) pure-fluid flags of rows [lo, ...)
 inline unsigned char *fluid_rows_buf(const MomWork &W, int lo, int nx) {
     return (unsigned char *)(W.acc2u + (long)lo * nx);
 }
+// where k_sim_sl_t leaves its per-(row, 64-column tile) fluid bits (the fused step: whole grid)
+inline unsigned char *fluid_bits_buf(const MomWork &W) { return (unsigned char *)W.acc2v; }
 // the flags' threshold: a stage tile is pure fluid where every phi > max(w_t, w_cut, 0)
 inline double fluid_threshold(const rmt_momentum_params *P) {
     const double w_cut = P->stress_band ? P->w_t : 0.0;

@@ -208,7 +208,9 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
     int ny, int nx, double dt_arg, DivK Kx, DivK Ky, double x0, double y0, double R,
     double *__restrict__ X1n, double *__restrict__ X2n, double *__restrict__ phi_pre, int *bad,
     unsigned long long *__restrict__ kbits, const double *m2, const double *__restrict__ dtp,
-    int mode, const unsigned long long *__restrict__ rimw) {
+    int mode, const unsigned long long *__restrict__ rimw, double *__restrict__ phi = nullptr,
+    double thr = 0.0, unsigned char *__restrict__ fbits = nullptr,
+    unsigned long long *__restrict__ nbits = nullptr) {
     __shared__ double s1[SLT_SY * SLT_SX], s2[SLT_SY * SLT_SX];
     __shared__ double sa[SLT_SY * SLT_SX], sb[SLT_SY * SLT_SX];
     const double dt = dtp ? *dtp : dt_arg;
@@ -239,6 +241,7 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
         mine = !rim;
     }
     bool known = false;
+    double o1 = 0.0, o2 = 0.0;   // this cell's advected map, when mine (phi below)
     if (zero) {
         if (in) {
             const double ph = disc_phi(0.0, 0.0, x0, y0, R);
@@ -277,8 +280,10 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
                 const double k4x = BT_(sa, a, x4, y4), k4y = BT_(sb, b, x4, y4);
                 const double xb = x - dt6 * (k1x + 2 * k2x + 2 * k3x + k4x);
                 const double yb = y - dt6 * (k1y + 2 * k2y + 2 * k3y + k4y);
-                X1n[c] = BT_(s1, X1, xb, yb) * m;
-                X2n[c] = BT_(s2, X2, xb, yb) * m;
+                o1 = BT_(s1, X1, xb, yb) * m;
+                o2 = BT_(s2, X2, xb, yb) * m;
+                X1n[c] = o1;
+                X2n[c] = o2;
 #undef BT_
             }
         }
@@ -286,6 +291,30 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
     if (kbits) {
         const unsigned long long w = __ballot(known);
         if (tx == 0 && j < ny) kbits[(long)j * ((nx + 63) / 64) + (i0 >> 6)] = w;
+    }
+    if (phi) {
+        // k_phi_rebuild_fluid's phi from the map this pass leaves (a rim cell's as the rim
+        // pass and the chain have it: read back, as that kernel reads it), and the pure-fluid
+        // test of each cell as bits per (row, 64-column tile): bit 0 every cell, bit 1 columns
+        // 0-1, bit 2 columns 62-63 (k_fluid_rows_bits adds the neighbours' halo columns).
+        // One wave is one row of the tile (nx % 64 == 0).
+        // nbits (nullable): k_phi_rebuild_fluid's known-plane words of this map
+        bool ok = true, neg = false;
+        if (in) {
+            const double a1 = mine ? o1 : X1n[c], a2 = mine ? o2 : X2n[c];
+            const double ph = disc_phi(a1, a2, x0, y0, R);
+            phi[c] = ph;
+            ok = ph > thr;   // (NaN phi is not fluid)
+            neg = ph < 0;
+        }
+        if (nbits) {
+            const unsigned long long wn = __ballot(neg);
+            if (tx == 0 && j < ny) nbits[(long)j * (nx >> 6) + (i0 >> 6)] = wn;
+        }
+        const unsigned long long w = __ballot(ok);
+        if (tx == 0 && j < ny)
+            fbits[(long)j * (nx >> 6) + (i0 >> 6)] =
+                (unsigned char)((w == ~0ull) | (((w & 3ull) == 3ull) << 1) | (((w >> 62) == 3ull) << 2));
     }
 }
 
@@ -1099,6 +1128,13 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                         S->tiles, S->tcount, (nx + MOM_TX - 1) / MOM_TX, ny, S->rowmark);
                     RMT_LAUNCHED();
                 }
+                MomWork Wf = W;
+                const bool fl_ok = fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 &&
+                                   MOM_TX == 64;
+                // the SL pass also leaves phi, the known-plane words and per-tile fluid bits
+                // (RMT_SL_PHI, default on): k_phi_rebuild_fluid's outputs without its pass
+                const bool sl_phi = P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits &&
+                                    fl_ok && ctx->opt.sl_phi;
                 if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits) {
                     // the advection of every non-rim cell, once the chain has started (earlier
                     // its blocks would crowd out the one-workgroup band passes)
@@ -1106,21 +1142,25 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                  SLT_X * SLT_Y, 0, S->st2>>>(
                         S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx),
                         divk_make(P.dy), P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag,
-                        nullptr, sc, dtp, 2, S->rimw);
+                        nullptr, sc, dtp, 2, S->rimw, sl_phi ? S->phi : nullptr,
+                        fluid_threshold(&M), sl_phi ? fluid_bits_buf(W) : nullptr,
+                        sl_phi ? nb : nullptr);
                     RMT_LAUNCHED();
                 }
-                MomWork Wf = W;
-                if (fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 && MOM_TX == 64) {
+                if (sl_phi) {
+                    Wf.fluid_bits = fluid_bits_buf(W);
+                } else if (fl_ok) {
                     // phi and the stage kernels' pure-fluid flags in one pass
                     k_phi_rebuild_fluid<<<g, 256, 0, S->st2>>>(
                         S->X1n, S->X2n, n, nx, (nx + 63) / 64, P.x0, P.y0, P.R, S->phi, nullptr,
                         nullptr, nb, fluid_threshold(&M), fluid_rows_buf(W, 0, nx));
                     Wf.fluid_rows_ready = true;
+                    RMT_LAUNCHED();
                 } else {
                     k_phi_rebuild<<<g, 256, 0, S->st2>>>(S->X1n, S->X2n, n, P.shape, P.x0, P.y0,
                                                           P.R, S->phi, nullptr, nullptr, nb);
+                    RMT_LAUNCHED();
                 }
-                RMT_LAUNCHED();
                 ctx->stream = S->st2;
                 int ms = momentum_rk4(ctx, &M, S->u, S->v, S->p, S->X1n, S->X2n, S->phi,
                                       S->us, S->vs, S->sxx, S->sxy, S->syy, S->J, Wf);
@@ -1357,7 +1397,8 @@ int rmt_sim_set_profiling(rmt_sim *S, int on) {
     RMT_CHECK(S, RMT_EINVAL, "null sim");
     if (on && !S->pev[0]) {
         for (auto &e : S->pev) RMT_HIP(hipEventCreate(&e));
-        for (auto &e : S->ctx->ev) RMT_HIP(hipEventCreate(&e));
+        if (!S->ctx->ev[0])
+            for (auto &e : S->ctx->ev) RMT_HIP(hipEventCreate(&e));
     }
     S->prof = on != 0;
     S->ctx->prof = on != 0;

@@ -31,6 +31,10 @@ environment variables still set a new context's defaults.
                         the regression test for the round-3 divergent list-kernel variant
                         
   transpose2=0          the 8-byte transposes
+  edge_stream=0         a full stage's edge tiles after its interior launch on the same stream
+                        instead of beside it on a stream of their own
+  sl_phi=0              phi, the known-plane words and the fluid flags from k_phi_rebuild_fluid
+                        after the side stream's SL pass instead of from that pass itself
 """
 import os
 import subprocess
@@ -80,6 +84,8 @@ def _same(got, ref):
     {"fused_fixprep": 0}, {"ext_events": 0}, {"transpose2": 0},
     {"merged_join": 0}, {"test_delay_side": 300}, {"test_delay_main": 300},
     {"test_delay_side": 300, "fix_all": 1}, {"fix_all": 1}, {"fix_all": 1, "sim_hiprio": 0},
+    {"edge_stream": 0}, {"sl_phi": 0}, {"sl_phi": 0, "fused_fluid": 0},
+    {"edge_stream": 0, "sl_phi": 0, "test_delay_side": 300},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(default_run, opts):
     _same(_run(opts), default_run)
