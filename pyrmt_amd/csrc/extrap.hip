@@ -756,7 +756,8 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
         const double r = 4 * std::sqrt(dx * dx + dy * dy);
         // 64 workgroups: the disc's first rim rows end the search (this runs beside the
         // critical path when sim.hip prepares the next step's geometry early)
-        k_ex_none<<<std::min<unsigned>(grid1d(ny, 4), 64), 256, 0, ctx->stream>>>(
+        k_ex_none<<<ctx->ex_none_wide ? grid1d(ny, 4) : std::min<unsigned>(grid1d(ny, 4), 64),
+                    256, 0, ctx->stream>>>(
             ws.kbits, ny, nx, W, dx, dy, r * r, ws.ctl, 0, ny);
         k_ex_none_fin<<<1, 1, 0, ctx->stream>>>(ws.ctl);
         RMT_LAUNCHED();

@@ -43,14 +43,17 @@ __global__ void k_mac_centres(const double *__restrict__ u, const double *__rest
     if (!(isfinite(a) && isfinite(b))) atomicOr(bad, 1);
 }
 
+// big (nullable): set when a phi is NaN, infinite or >= 2^928 in magnitude (k_mac_stress)
 __global__ void k_mac_phi(const double *__restrict__ X1n, const double *__restrict__ X2n, long n,
                           double x0, double y0, double R, double *__restrict__ X1,
-                          double *__restrict__ X2, double *__restrict__ phi) {
+                          double *__restrict__ X2, double *__restrict__ phi, int *big = nullptr) {
     const long c = blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (c >= n) return;
     const double a = X1n[c], b = X2n[c];
     X1[c] = a; X2[c] = b;
-    phi[c] = disc_phi(a, b, x0, y0, R);
+    const double ph = disc_phi(a, b, x0, y0, R);
+    phi[c] = ph;
+    if (big && !(fabs(ph) < 0x1p928)) atomicOr(big, 1);
 }
 
 // mac.py:729-749 at one cell: f(phi) = 1/2 (1 - phi/eps) below eps; d = phi_a - phi_b with
@@ -94,7 +97,9 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
                                                        double *__restrict__ Sxy,
                                                        double *__restrict__ Syy,
                                                        double *__restrict__ part, int jb, int je,
-                                                       int jr0, int jr1) {
+                                                       int jr0, int jr1, bool skip_ok,
+                                                       const int *__restrict__ phi_big = nullptr) {
+    const bool phi_ok = phi_big && *phi_big == 0;
     // S on rows [jb, je); the J range over rows [jr0, jr1)
     __shared__ double smin[MS_TPB], smax[MS_TPB];
     double jmin = 1.0, jmax = 1.0;
@@ -103,22 +108,44 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
          c += (long)MS_BLOCKS * MS_TPB) {
         const int j = (int)(c / N), i = (int)(c % N);
         const bool own = j >= jr0 && j < jr1;
+        // The sums start at +0.0 and only add, so they are never -0.0: adding a +-0.0 term
+        // leaves them bit for bit unchanged.  Two kinds of term are exactly +-0.0 and skipped:
+        //  * a disc's stress outside its solid (solid_stress_cell: sigma = 0) with a finite
+        //    phi there (omh finite: omh * 0 = +-0; a NaN phi takes the product, NaN);
+        //  * a contact pair where either phi >= eps or is NaN (fc = min(fa, fb) = +0.0, s =
+        //    -0.0) and both gradient numerators are finite and below 2^930: then |gx|, |gy| <
+        //    2^930 / (2 h) (host: 2 h >= 2^-30), nx, ny are finite (|n| <= 1 or mag = inf),
+        //    and txx, txy, tyy = -0.0 * finite = +-0.0.  With phi_big clear (k_mac_phi: every
+        //    phi finite and below 2^928) every numerator is, and the test is skipped.
         double axx = 0.0, axy = 0.0, ayy = 0.0;
+        const bool inner = j >= 1 && j < N - 1 && i >= 1 && i < N - 1;
         for (int k = 0; k < D.K; ++k) {
             Stress s{0.0, 0.0, 0.0, 1.0};
-            if (j >= 1 && j < N - 1 && i >= 1 && i < N - 1)
-                solid_stress_cell(D.X1[k], D.X2[k], D.phi[k], c, N, dx, dy, mu_s, 0.0, 0.0, 0.0,
-                                  false, s);
-            const double omh = 1 - heaviside(D.phi[k][c], w_t);
-            axx = axx + omh * s.sxx; axy = axy + omh * s.sxy; ayy = ayy + omh * s.syy;
+            const bool st = inner && solid_stress_cell(D.X1[k], D.X2[k], D.phi[k], c, N, dx, dy,
+                                                       mu_s, 0.0, 0.0, 0.0, false, s);
+            const double ph = D.phi[k][c];
+            if (st || ph != ph) {
+                const double omh = 1 - heaviside(ph, w_t);
+                axx = axx + omh * s.sxx; axy = axy + omh * s.sxy; ayy = ayy + omh * s.syy;
+            }
             if (own) { jmin = fmin(jmin, s.J); jmax = fmax(jmax, s.J); }
         }
         if (eta > 0)
             for (int a = 0; a < D.K; ++a)
                 for (int b = a + 1; b < D.K; ++b) {
+                    const double *pa = D.phi[a], *pb = D.phi[b];
+                    if (skip_ok && !(pa[c] < eps && pb[c] < eps)) {
+                        if (phi_ok) continue;
+                        const double gxn = i >= 1 && i < N - 1
+                                               ? (pa[c + 1] - pb[c + 1]) - (pa[c - 1] - pb[c - 1])
+                                               : 0.0;
+                        const double gyn = j >= 1 && j < N - 1
+                                               ? (pa[c + N] - pb[c + N]) - (pa[c - N] - pb[c - N])
+                                               : 0.0;
+                        if (fabs(gxn) < 0x1p930 && fabs(gyn) < 0x1p930) continue;
+                    }
                     double txx, txy, tyy;
-                    contact_cell(D.phi[a], D.phi[b], c, j, i, N, eta, 2 * mu_s, eps, dx, dy, txx,
-                                 txy, tyy);
+                    contact_cell(pa, pb, c, j, i, N, eta, 2 * mu_s, eps, dx, dy, txx, txy, tyy);
                     axx = axx + txx; axy = axy + txy; ayy = ayy + tyy;
                 }
         Sxx[c] = axx; Sxy[c] = axy; Syy[c] = ayy;
@@ -133,6 +160,11 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
         __syncthreads();
     }
     if (threadIdx.x == 0) { part[2 * blockIdx.x] = smin[0]; part[2 * blockIdx.x + 1] = smax[0]; }
+}
+
+// k_mac_stress's zero-term skip needs 2 h >= 2^-30 and finite contact constants (see there)
+static bool stress_skip_ok(const rmt_mac_params &P) {
+    return 2.0 * P.dx >= 0x1p-30 && std::isfinite(P.eta) && std::isfinite(2.0 * P.mu_s);
 }
 
 // utils.py grad_central at cell (j, i) of an N x N plane (one-sided at the edges)
@@ -241,14 +273,37 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
     double acc[MD_VALS];
     for (int k = 0; k < MD_VALS; ++k) acc[k] = 0.0;
     const long n = (long)(je - jb) * N, nf = (long)(je - jb) * (N + 1);
-    for (long t = blockIdx.x * (long)MS_TPB + threadIdx.x; t < nf; t += (long)MS_BLOCKS * MS_TPB) {
-        acc[3 * MAC_MAXD] = nanmax(acc[3 * MAC_MAXD], fabs(u[(long)jb * (N + 1) + t]));
-        if (t < n) {
-            const long c = (long)jb * N + t;
-            const int j = (int)(c / N), i = (int)(c % N);
-            const double xc = (i + 0.5) * dx, yc = (j + 0.5) * dx;
-            for (int k = 0; k < D.K; ++k)
-                if (D.phi[k][c] <= 0.0) { acc[3 * k] += xc; acc[3 * k + 1] += yc; acc[3 * k + 2] += 1.0; }
+    // MD_U grid-stride items per trip: their loads are issued together, then accumulated in
+    // item order (the same sums as one item per trip)
+    constexpr int MD_U = 4;
+    const long S = (long)MS_BLOCKS * MS_TPB;
+    for (long t0 = blockIdx.x * (long)MS_TPB + threadIdx.x; t0 < nf; t0 += MD_U * S) {
+        double ua[MD_U];
+        unsigned in[MD_U];   // bit k: phi_k <= 0 at the item's cell
+#pragma unroll
+        for (int m = 0; m < MD_U; ++m) {
+            const long t = t0 + m * S;
+            ua[m] = t < nf ? u[(long)jb * (N + 1) + t] : 0.0;
+            in[m] = 0;
+            if (t < n) {
+                const long c = (long)jb * N + t;
+#pragma unroll
+                for (int k = 0; k < MAC_MAXD; ++k)
+                    if (k < D.K && D.phi[k][c] <= 0.0) in[m] |= 1u << k;
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < MD_U; ++m) {
+            const long t = t0 + m * S;
+            if (t >= nf) break;
+            acc[3 * MAC_MAXD] = nanmax(acc[3 * MAC_MAXD], fabs(ua[m]));
+            if (t < n) {
+                const long c = (long)jb * N + t;
+                const int j = (int)(c / N), i = (int)(c % N);
+                const double xc = (i + 0.5) * dx, yc = (j + 0.5) * dx;
+                for (int k = 0; k < D.K; ++k)
+                    if ((in[m] >> k) & 1) { acc[3 * k] += xc; acc[3 * k + 1] += yc; acc[3 * k + 2] += 1.0; }
+            }
         }
     }
     for (int k = 0; k < MD_VALS; ++k) {
@@ -291,6 +346,7 @@ struct rmt_mac_sim {
     double *u, *v, *p, *us, *vs, *uc, *vc, *X1n, *X2n, *phi_pre, *Sxx, *Sxy, *Syy;
     double *X1[RMT_MAC_MAXD], *X2[RMT_MAC_MAXD], *phi[RMT_MAC_MAXD];
     double *xs, *ys, *part, *out;
+    unsigned long long *kbits;   // the advection's known plane (phi_pre < 0), 64-cell words
     int *flags;
     double t = 0;
     bool diverged = false;
@@ -380,7 +436,8 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     double *q = (double *)S->block;
     double **faces[] = {&S->u, &S->v, &S->us, &S->vs};
     for (auto pp : faces) { *pp = q; q += nf; }
-    q += nf;   // spare
+    S->kbits = (unsigned long long *)q;   // (ceil(N / 64) words per row: << nf doubles)
+    q += nf;
     double **cells[] = {&S->p, &S->uc, &S->vc, &S->X1n, &S->X2n, &S->phi_pre, &S->Sxx, &S->Sxy,
                         &S->Syy};
     for (auto pp : cells) { *pp = q; q += n; }
@@ -438,7 +495,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         if (!(S->t < t_end) || S->diverged) break;
         double dt = P.dt;
         if (S->t + dt > t_end) dt = t_end - S->t;
-        RMT_HIP(hipMemsetAsync(S->flags, 0, 4 * sizeof(int), st));
+        RMT_HIP(hipMemsetAsync(S->flags, 0, 5 * sizeof(int), st));   // [4]: k_mac_phi's big
         k_mac_centres<<<grid1d(n, 256), 256, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags, 0,
                                                       N);
         RMT_LAUNCHED();
@@ -448,15 +505,21 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
             // phi from the current map (already S->phi[k]), advect with the pre-advection mask
             RMT_TRY(sl_disc_map(ctx, S->X1[k], S->X2[k], S->uc, S->vc, S->xs, S->ys, dt, dx, dx,
                                 P.cx[k], P.cy[k], P.R[k], S->X1n, S->X2n, S->phi_pre,
-                                S->flags + 1, S->out + 8));
-            RMT_TRY(extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, dx, dx, P.layers, S->X1n, S->X2n,
-                                S->flags + 2));
+                                S->flags + 1, S->out + 8, S->kbits));
+            // the known plane from the advection pass (its k_ex_bits pass over phi_pre saved);
+            // the no-op test over every row at once (a disc with nothing to fit scans them all)
+            ctx->ex_none_wide = true;
+            const int es = extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, dx, dx, P.layers, S->X1n,
+                                       S->X2n, S->flags + 2, S->kbits);
+            ctx->ex_none_wide = false;
+            RMT_TRY(es);
             k_mac_phi<<<grid1d(n, 256), 256, 0, st>>>(S->X1n, S->X2n, n, P.cx[k], P.cy[k], P.R[k],
-                                                      S->X1[k], S->X2[k], S->phi[k]);
+                                                      S->X1[k], S->X2[k], S->phi[k], S->flags + 4);
             RMT_LAUNCHED();
         }
         k_mac_stress<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, N, dx, dx, P.mu_s, w_t, P.eta, eps, S->Sxx,
-                                                    S->Sxy, S->Syy, S->part, 0, N, 0, N);
+                                                    S->Sxy, S->Syy, S->part, 0, N, 0, N,
+                                                    stress_skip_ok(P), S->flags + 4);
         RMT_LAUNCHED();
         double jr[2 * MS_BLOCKS];
         RMT_HIP(hipMemcpyAsync(jr, S->part, sizeof(jr), hipMemcpyDeviceToHost, st));
@@ -818,7 +881,8 @@ int rmt_mac_slab_predict(rmt_mac_slab *S, double dt) {
     const DiscSet D = S->discs();
     k_mac_stress<<<MS_BLOCKS, MS_TPB, 0, ctx->stream>>>(
         D, N, dx, dx, P.mu_s, w_t, P.eta, eps, S->gc(S->Sxx), S->gc(S->Sxy), S->gc(S->Syy),
-        S->part, std::max(0, S->r0 - 2), std::min(N, S->r1 + 2), S->r0, S->r1);
+        S->part, std::max(0, S->r0 - 2), std::min(N, S->r1 + 2), S->r0, S->r1,
+        stress_skip_ok(P));
     RMT_LAUNCHED();
     const FaceRows F{S->r0, S->r1, S->r0, std::min(S->r1 + 1, N + 1)};
     k_mac_predict<<<grid1d(face_count(F, N), 256), 256, 0, ctx->stream>>>(

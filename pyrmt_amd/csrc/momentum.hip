@@ -41,7 +41,10 @@ __global__ void k_mom_prep(const double *__restrict__ X1, const double *__restri
 // two flags, the wave then runs the segments to be written one after the other (64 lanes =
 // 64 cells; few per wave, so that the serial chain of segment latencies stays short).  Same
 // per-cell arithmetic as k_mom_prep (no rho plane).
-constexpr int PS_SEGS = 8;
+#ifndef RMT_PS_SEGS
+#define RMT_PS_SEGS 8
+#endif
+constexpr int PS_SEGS = RMT_PS_SEGS;
 __global__ void __launch_bounds__(256) k_mom_prep_seg(
     const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ phi,
     int ny, int nx, double dx, double dy, double mu_s, double kappa, double w_cut, double clamp,

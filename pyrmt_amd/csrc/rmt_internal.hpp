@@ -137,6 +137,9 @@ struct rmt_ctx {
     // optional (sim.hip overlap, with ex_sweep_defer): ev_chain tracks the completion of the
     // values pass right before the chain (launch_done) instead of a record of its own
     bool ev_chain_vals = false;
+    // optional (mac.hip: the extrapolation on the critical stream, where the no-op test finds
+    // nothing to fit as often as not): k_ex_none on a wave per row instead of 64 workgroups
+    bool ex_none_wide = false;
     // momentum.hip: the stage tiles a full launch's interior kernel skips, per row window
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
     EdgeTiles edge[RMT_EDGE_SLOTS];
@@ -365,12 +368,14 @@ __device__ __forceinline__ double disc_phi(double X1, double X2, double x0, doub
 }
 
 // functions.py:660-671 smoothed_heaviside.
+// The two constant branches are taken before the sine (the values the reference's np.where
+// keeps; a NaN v fails both tests and takes the formula, as there): most cells of a grid lie
+// outside the band, and an f64 sine is ~100 instructions.
 __device__ __forceinline__ double heaviside(double v, double w_t) {
+    if (v > w_t) return 1.0;
+    if (v < -w_t) return 0.0;
     const double inv_wt = 1.0 / w_t, inv_pi = 1.0 / M_PI;
-    double h = 0.5 * (1.0 + v * inv_wt + inv_pi * sin(M_PI * v * inv_wt));
-    if (v > w_t) h = 1.0;
-    if (v < -w_t) h = 0.0;
-    return h;
+    return 0.5 * (1.0 + v * inv_wt + inv_pi * sin(M_PI * v * inv_wt));
 }
 
 // output.py:41-134 strain-energy density at one cell (4-cell edge-padded central grads).
@@ -627,11 +632,13 @@ int diag_rows(rmt_ctx *ctx, const double *phi, const double *J, const double *xs
               const double *X2, const rmt_sim_params &P, int jb, int je, double *part,
               double *out);
 
-// dev_m2 (optional, device): a bound on a^2 + b^2 over the grid (enables the block skip)
+// dev_m2 (optional, device): a bound on a^2 + b^2 over the grid (enables the block skip);
+// kbits (optional): the known plane (phi_pre < 0) as 64-cell words instead of phi_pre
 int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
-                double *phi_pre, int *bad, const double *dev_m2 = nullptr);
+                double *phi_pre, int *bad, const double *dev_m2 = nullptr,
+                unsigned long long *kbits = nullptr);
 
 // --------------------------------------------------------------------- momentum --
 // every stage keeps its own k plane (k1, k2, k3; the last stage forms (k1 + 2 k2) + 2 k3

@@ -662,10 +662,10 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p2(const double *__restrict__ p
 int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
-                double *phi_pre, int *bad, const double *dev_m2) {
+                double *phi_pre, int *bad, const double *dev_m2, unsigned long long *kbits) {
     k_sim_sl_t<<<dim3((ctx->nx + SLT_X - 1) / SLT_X, (ctx->ny + SLT_Y - 1) / SLT_Y), SLT_X * SLT_Y,
                  0, ctx->stream>>>(X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx),
-                                   divk_make(dy), x0, y0, R, X1n, X2n, phi_pre, bad, nullptr,
+                                   divk_make(dy), x0, y0, R, X1n, X2n, phi_pre, bad, kbits,
                                    dev_m2, nullptr, 0, nullptr);
     RMT_LAUNCHED();
     return RMT_OK;
