@@ -18,6 +18,7 @@
 #include "rmt_internal.hpp"
 #include "extrap.hpp"
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <vector>
 
@@ -54,6 +55,89 @@ __global__ void k_mac_phi(const double *__restrict__ X1n, const double *__restri
     const double ph = disc_phi(a, b, x0, y0, R);
     phi[c] = ph;
     if (big && !(fabs(ph) < 0x1p928)) atomicOr(big, 1);
+}
+
+// The support box of a disc's map: cells where X1 or X2 is not +-0 (NaN included), as
+// {min row, max row, min col, max col} (box[0..3]; empty: {INT_MAX, -1, INT_MAX, -1}).
+// Each block (256 cells of one row) leaves its column extent in bres[block] (x = INT_MAX:
+// none), from its waves' ballots; k_box_reduce folds them (no contended atomics).
+__device__ __forceinline__ void box_fold(bool nz, int i, int2 *bres) {
+    __shared__ int smin[4], smax[4];
+    const unsigned long long m = __ballot(nz);
+    const int w = threadIdx.x >> 6, l0 = i - (int)(threadIdx.x & 63);   // lane 0's column
+    if ((threadIdx.x & 63) == 0) {
+        smin[w] = m ? l0 + __builtin_ctzll(m) : INT_MAX;
+        smax[w] = m ? l0 + 63 - __builtin_clzll(m) : -1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int a = INT_MAX, b = -1;
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { a = min(a, smin[k]); b = max(b, smax[k]); }
+        bres[(long)blockIdx.y * gridDim.x + blockIdx.x] = make_int2(a, b);
+    }
+}
+// one workgroup: the box of nrows x nbx block extents (row r of them is grid row j0 + r)
+__global__ void __launch_bounds__(1024) k_box_reduce(const int2 *__restrict__ bres, int nbx,
+                                                     int nrows, int j0, int *box) {
+    __shared__ int s[4][1024];
+    int jmin = INT_MAX, jmax = -1, imin = INT_MAX, imax = -1;
+    for (long e = threadIdx.x; e < (long)nbx * nrows; e += 1024) {
+        const int2 v = bres[e];
+        if (v.y >= 0) {
+            const int j = j0 + (int)(e / nbx);
+            jmin = min(jmin, j); jmax = max(jmax, j);
+            imin = min(imin, v.x); imax = max(imax, v.y);
+        }
+    }
+    s[0][threadIdx.x] = jmin; s[1][threadIdx.x] = jmax; s[2][threadIdx.x] = imin; s[3][threadIdx.x] = imax;
+    __syncthreads();
+    for (int h = 512; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) {
+            s[0][threadIdx.x] = min(s[0][threadIdx.x], s[0][threadIdx.x + h]);
+            s[1][threadIdx.x] = max(s[1][threadIdx.x], s[1][threadIdx.x + h]);
+            s[2][threadIdx.x] = min(s[2][threadIdx.x], s[2][threadIdx.x + h]);
+            s[3][threadIdx.x] = max(s[3][threadIdx.x], s[3][threadIdx.x + h]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 4) box[threadIdx.x] = s[threadIdx.x][0];
+}
+// phi = disc_phi(X1, X2) over the grid and the support box (rmt_mac_sim_step's start in the
+// box mode: phi then holds disc_phi(0, 0) wherever the map is zero, as every later step keeps)
+__global__ void __launch_bounds__(256) k_mac_box_phi(const double *__restrict__ X1,
+                                                     const double *__restrict__ X2, int N,
+                                                     double x0, double y0, double R,
+                                                     double *__restrict__ phi, int2 *bres) {
+    const int j = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    bool nz = false;
+    if (i < N) {
+        const long c = (long)j * N + i;
+        const double a = X1[c], b = X2[c];
+        phi[c] = disc_phi(a, b, x0, y0, R);
+        nz = !(a == 0.0 && b == 0.0);
+    }
+    box_fold(nz, i, bres);
+}
+// k_mac_phi on the cells [j0, j1) x [i0, i1) only, and the new map's support box
+__global__ void __launch_bounds__(256) k_mac_phi_box(const double *__restrict__ X1n,
+                                                     const double *__restrict__ X2n, int N, int j0,
+                                                     int i0, int i1, double x0, double y0,
+                                                     double R, double *__restrict__ X1,
+                                                     double *__restrict__ X2,
+                                                     double *__restrict__ phi, int *big,
+                                                     int2 *bres) {
+    const int j = j0 + blockIdx.y, i = i0 + blockIdx.x * 256 + threadIdx.x;
+    bool nz = false;
+    if (i < i1) {
+        const long c = (long)j * N + i;
+        const double a = X1n[c], b = X2n[c];
+        X1[c] = a; X2[c] = b;
+        const double ph = disc_phi(a, b, x0, y0, R);
+        phi[c] = ph;
+        if (!(fabs(ph) < 0x1p928)) atomicOr(big, 1);
+        nz = !(a == 0.0 && b == 0.0);
+    }
+    box_fold(nz, i, bres);
 }
 
 // mac.py:729-749 at one cell: f(phi) = 1/2 (1 - phi/eps) below eps; d = phi_a - phi_b with
@@ -348,6 +432,9 @@ struct rmt_mac_sim {
     double *xs, *ys, *part, *out;
     unsigned long long *kbits;   // the advection's known plane (phi_pre < 0), 64-cell words
     int *flags;
+    int2 *bres;                  // per-block column extents of the box passes (box_fold)
+    int *dbox;                   // [K][4] device support boxes (k_box_reduce), host copy:
+    int hbox[RMT_MAC_MAXD][4];
     double t = 0;
     bool diverged = false;
     std::vector<rmt_mac_diag> diag;
@@ -430,13 +517,16 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     S->ctx = ctx; S->P = *prm;
     const long n = (long)N * N, nf = (long)N * (N + 1);
     const int K = prm->n_discs;
-    const size_t dbl = 5 * nf + (9 + 3 * K) * n + 2 * N + (2 + MD_VALS) * MS_BLOCKS + 64;
+    const size_t dbl = 5 * nf + (9 + 3 * K) * n + 2 * N + (2 + MD_VALS) * MS_BLOCKS + 64 + 32;
     RMT_HIP(hipMalloc(&S->block, dbl * 8 + 64));
     RMT_HIP(hipMemsetAsync(S->block, 0, dbl * 8 + 64, ctx->stream));
     double *q = (double *)S->block;
     double **faces[] = {&S->u, &S->v, &S->us, &S->vs};
     for (auto pp : faces) { *pp = q; q += nf; }
-    S->kbits = (unsigned long long *)q;   // (ceil(N / 64) words per row: << nf doubles)
+    // the spare face plane: the known-plane words (ceil(N / 64) per row), then the box
+    // pass's per-block extents ((N / 256 + 1) x N) -- together far below nf doubles
+    S->kbits = (unsigned long long *)q;
+    S->bres = (int2 *)(q + (long)N * ((N + 63) / 64));
     q += nf;
     double **cells[] = {&S->p, &S->uc, &S->vc, &S->X1n, &S->X2n, &S->phi_pre, &S->Sxx, &S->Sxy,
                         &S->Syy};
@@ -448,6 +538,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     S->ys = q; q += N;
     S->part = q; q += (2 + MD_VALS) * MS_BLOCKS;   // J range, then centroid partials
     S->out = q; q += 32;
+    S->dbox = (int *)q; q += 4 * RMT_MAC_MAXD / 2;
     S->flags = (int *)q;
     // index-grid coordinates (mac_multi_disc_lid.py:41): Xg = arange(N) * dx
     std::vector<double> g(N);
@@ -491,6 +582,28 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
     for (int k = 0; k < K; ++k) { D.X1[k] = S->X1[k]; D.X2[k] = S->X2[k]; D.phi[k] = S->phi[k]; }
     const double dx = P.dx, w_t = 2.0 * dx, eps = 3.0 * dx, nu = P.mu_f / P.rho;
     const double dx2 = std::pow(dx, 2.0);
+    // Box mode: a disc's advection, extrapolation and phi run only on its map's support box
+    // grown by G cells.  Exact when the origin lies outside every reference disc (disc_phi(0,
+    // 0) > 0): then a zero map cell is not known and its SL mask is 0, so the advected map is
+    // zero outside the old support, the extrapolation's targets lie within `layers` cells of
+    // known cells and it reads values within 4 more (9 x 9 windows), and phi = disc_phi(0, 0)
+    // wherever the map stays zero.  The box comes back with each step's diagnostics (no
+    // extra host round trip); a call starts with one full pass per disc (phi, box).
+    const int G = P.layers + 6;
+    bool box_mode = ctx->opt.mac_boxes != 0 && P.layers > 0;
+    for (int k = 0; k < K; ++k)
+        box_mode = box_mode && std::sqrt(P.cx[k] * P.cx[k] + P.cy[k] * P.cy[k]) - P.R[k] > 0.0;
+    const size_t kb_bytes = (size_t)N * ((N + 63) / 64) * sizeof(unsigned long long);
+    if (box_mode && nsteps > 0 && S->t < t_end && !S->diverged) {
+        for (int k = 0; k < K; ++k) {
+            k_mac_box_phi<<<dim3((N + 255) / 256, N), 256, 0, st>>>(
+                S->X1[k], S->X2[k], N, P.cx[k], P.cy[k], P.R[k], S->phi[k], S->bres);
+            k_box_reduce<<<1, 1024, 0, st>>>(S->bres, (N + 255) / 256, N, 0, S->dbox + 4 * k);
+            RMT_LAUNCHED();
+        }
+        RMT_HIP(hipMemcpyAsync(S->hbox, S->dbox, 4 * K * sizeof(int), hipMemcpyDeviceToHost, st));
+        RMT_HIP(hipStreamSynchronize(st));
+    }
     for (int it = 0; it < nsteps; ++it) {
         if (!(S->t < t_end) || S->diverged) break;
         double dt = P.dt;
@@ -502,10 +615,23 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         // max |u_c|^2 bounds every velocity sample of the backtraces (the SL block skip)
         RMT_TRY(reduce_maxsq2_nan(ctx, S->uc, S->vc, n, S->out + 8));
         for (int k = 0; k < K; ++k) {
+            int cb[4] = {0, N, 0, N};   // the cells this disc's passes cover
+            if (box_mode) {
+                const int *b = S->hbox[k];
+                if (b[1] < b[0]) { cb[1] = 0; cb[3] = 0; }   // empty map
+                else {
+                    cb[0] = std::max(0, b[0] - G); cb[1] = std::min(N, b[1] + 1 + G);
+                    cb[2] = std::max(0, b[2] - G); cb[3] = std::min(N, b[3] + 1 + G);
+                    // whole SL tiles: the phi pass covers exactly the cells they advected
+                    cb[0] -= cb[0] % 4; cb[1] = std::min(N, (cb[1] + 3) / 4 * 4);
+                    cb[2] -= cb[2] % 64; cb[3] = std::min(N, (cb[3] + 63) / 64 * 64);
+                }
+                RMT_HIP(hipMemsetAsync(S->kbits, 0, kb_bytes, st));
+            }
             // phi from the current map (already S->phi[k]), advect with the pre-advection mask
             RMT_TRY(sl_disc_map(ctx, S->X1[k], S->X2[k], S->uc, S->vc, S->xs, S->ys, dt, dx, dx,
                                 P.cx[k], P.cy[k], P.R[k], S->X1n, S->X2n, S->phi_pre,
-                                S->flags + 1, S->out + 8, S->kbits));
+                                S->flags + 1, S->out + 8, S->kbits, box_mode ? cb : nullptr));
             // the known plane from the advection pass (its k_ex_bits pass over phi_pre saved);
             // the no-op test over every row at once (a disc with nothing to fit scans them all)
             ctx->ex_none_wide = true;
@@ -513,8 +639,20 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
                                        S->X2n, S->flags + 2, S->kbits);
             ctx->ex_none_wide = false;
             RMT_TRY(es);
-            k_mac_phi<<<grid1d(n, 256), 256, 0, st>>>(S->X1n, S->X2n, n, P.cx[k], P.cy[k], P.R[k],
-                                                      S->X1[k], S->X2[k], S->phi[k], S->flags + 4);
+            if (!box_mode)
+                k_mac_phi<<<grid1d(n, 256), 256, 0, st>>>(S->X1n, S->X2n, n, P.cx[k], P.cy[k],
+                                                          P.R[k], S->X1[k], S->X2[k], S->phi[k],
+                                                          S->flags + 4);
+            else if (cb[1] > cb[0] && cb[3] > cb[2]) {
+                const int nbx = (cb[3] - cb[2] + 255) / 256;
+                k_mac_phi_box<<<dim3(nbx, cb[1] - cb[0]), 256, 0, st>>>(
+                    S->X1n, S->X2n, N, cb[0], cb[2], cb[3], P.cx[k], P.cy[k], P.R[k], S->X1[k],
+                    S->X2[k], S->phi[k], S->flags + 4, S->bres);
+                k_box_reduce<<<1, 1024, 0, st>>>(S->bres, nbx, cb[1] - cb[0], cb[0],
+                                                  S->dbox + 4 * k);
+            } else {
+                k_box_reduce<<<1, 1024, 0, st>>>(S->bres, 0, 0, 0, S->dbox + 4 * k);   // empty
+            }
             RMT_LAUNCHED();
         }
         k_mac_stress<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, N, dx, dx, P.mu_s, w_t, P.eta, eps, S->Sxx,
@@ -537,6 +675,8 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
                                hipMemcpyDeviceToHost, st));
         int fl[4];
         RMT_HIP(hipMemcpyAsync(fl, S->flags, sizeof(fl), hipMemcpyDeviceToHost, st));
+        if (box_mode)   // the next step's boxes, with the diagnostics
+            RMT_HIP(hipMemcpyAsync(S->hbox, S->dbox, 4 * K * sizeof(int), hipMemcpyDeviceToHost, st));
         RMT_HIP(hipStreamSynchronize(st));
         RMT_CHECK(!fl[0] && !fl[1], RMT_ENONFINITE,
                   "advect_reference_map: non-finite velocity (the simulation diverged)");

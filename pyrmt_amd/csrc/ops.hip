@@ -37,6 +37,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"edge_slots", "RMT_EDGE_SLOTS_USED", &rmt_opts::edge_slots},
     {"edge_stream", "RMT_EDGE_STREAM", &rmt_opts::edge_stream},
     {"sl_phi", "RMT_SL_PHI", &rmt_opts::sl_phi},
+    {"mac_boxes", "RMT_MAC_BOXES", &rmt_opts::mac_boxes},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;

@@ -100,6 +100,7 @@ struct rmt_opts {
     int edge_slots = 64;      // RMT_EDGE_SLOTS_USED: edge-tile lists kept (1..64; fewer evict)
     int edge_stream = 1;      // RMT_EDGE_STREAM: a full stage's edge tiles beside its interior
     int sl_phi = 1;           // RMT_SL_PHI: the side stream's SL pass also writes phi + fluid bits
+    int mac_boxes = 1;        // RMT_MAC_BOXES: config 5's per-disc passes on the map's support box
 };
 
 #ifndef RMT_EDGE_SLOTS
@@ -633,12 +634,13 @@ int diag_rows(rmt_ctx *ctx, const double *phi, const double *J, const double *xs
               double *out);
 
 // dev_m2 (optional, device): a bound on a^2 + b^2 over the grid (enables the block skip);
-// kbits (optional): the known plane (phi_pre < 0) as 64-cell words instead of phi_pre
+// kbits (optional): the known plane (phi_pre < 0) as 64-cell words instead of phi_pre;
+// cbox (optional, host {j0, j1, i0, i1}): only the 64 x 4 tiles meeting those cells
 int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
                 double *phi_pre, int *bad, const double *dev_m2 = nullptr,
-                unsigned long long *kbits = nullptr);
+                unsigned long long *kbits = nullptr, const int *cbox = nullptr);
 
 // --------------------------------------------------------------------- momentum --
 // every stage keeps its own k plane (k1, k2, k3; the last stage forms (k1 + 2 k2) + 2 k3

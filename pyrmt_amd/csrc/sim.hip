@@ -210,11 +210,12 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
     unsigned long long *__restrict__ kbits, const double *m2, const double *__restrict__ dtp,
     int mode, const unsigned long long *__restrict__ rimw, double *__restrict__ phi = nullptr,
     double thr = 0.0, unsigned char *__restrict__ fbits = nullptr,
-    unsigned long long *__restrict__ nbits = nullptr) {
+    unsigned long long *__restrict__ nbits = nullptr, int tbx0 = 0, int tby0 = 0) {
     __shared__ double s1[SLT_SY * SLT_SX], s2[SLT_SY * SLT_SX];
     __shared__ double sa[SLT_SY * SLT_SX], sb[SLT_SY * SLT_SX];
     const double dt = dtp ? *dtp : dt_arg;
-    const int i0 = blockIdx.x * SLT_X, j0 = blockIdx.y * SLT_Y;
+    // (tbx0, tby0: the tile of block (0, 0) -- a launch over a box of tiles)
+    const int i0 = (blockIdx.x + tbx0) * SLT_X, j0 = (blockIdx.y + tby0) * SLT_Y;
     const int tx = threadIdx.x & (SLT_X - 1), ty = threadIdx.x / SLT_X;
     const int i = i0 + tx, j = j0 + ty, sj0 = j0 - 1, si0 = i0 - 1;
     const bool in = i < nx && j < ny;
@@ -662,11 +663,20 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p2(const double *__restrict__ p
 int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *a,
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
-                double *phi_pre, int *bad, const double *dev_m2, unsigned long long *kbits) {
-    k_sim_sl_t<<<dim3((ctx->nx + SLT_X - 1) / SLT_X, (ctx->ny + SLT_Y - 1) / SLT_Y), SLT_X * SLT_Y,
-                 0, ctx->stream>>>(X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx),
-                                   divk_make(dy), x0, y0, R, X1n, X2n, phi_pre, bad, kbits,
-                                   dev_m2, nullptr, 0, nullptr);
+                double *phi_pre, int *bad, const double *dev_m2, unsigned long long *kbits,
+                const int *cbox) {
+    // cbox {j0, j1, i0, i1}: only the tiles meeting those cells (kbits words outside them
+    // are left alone: the caller clears them)
+    int ty0 = 0, ty1 = (ctx->ny + SLT_Y - 1) / SLT_Y, tx0 = 0, tx1 = (ctx->nx + SLT_X - 1) / SLT_X;
+    if (cbox) {
+        ty0 = cbox[0] / SLT_Y; ty1 = (cbox[1] + SLT_Y - 1) / SLT_Y;
+        tx0 = cbox[2] / SLT_X; tx1 = (cbox[3] + SLT_X - 1) / SLT_X;
+        if (ty1 <= ty0 || tx1 <= tx0) return RMT_OK;
+    }
+    k_sim_sl_t<<<dim3(tx1 - tx0, ty1 - ty0), SLT_X * SLT_Y, 0, ctx->stream>>>(
+        X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx), divk_make(dy), x0, y0, R, X1n,
+        X2n, phi_pre, bad, kbits, dev_m2, nullptr, 0, nullptr, nullptr, 0.0, nullptr, nullptr,
+        tx0, ty0);
     RMT_LAUNCHED();
     return RMT_OK;
 }

@@ -302,7 +302,7 @@ class MacMultiDisc:
     FIELDS = {"u": 0, "v": 1, "p": 2, "X1": 3, "X2": 4, "phi": 5}
 
     def __init__(self, N=128, n_discs=3, seed=3, U_lid=1.0, mu_s=0.3, mu_f=0.01, rho=1.0,
-                 eta=2.0, specs=None):
+                 eta=2.0, specs=None, options=None):
         import torch
         if not torch.cuda.is_available():
             raise RuntimeError("pyrmt_amd needs a visible MI355X")
@@ -313,7 +313,14 @@ class MacMultiDisc:
         if not 1 <= len(self.specs) <= 8:
             raise ValueError("1..8 discs")
         P, self.dt = mac_params(N, self.specs, U_lid, mu_s, mu_f, rho, eta)
-        self.ctx = ctx_for(N, N)
+        if options:
+            # a context of its own with these implementation switches (rmt_ctx_set_option)
+            from .functions import _Ctx
+            self.ctx = _Ctx(N, N, torch.cuda.current_device())
+            for k, v in options.items():
+                self.ctx.set_option(k, v)
+        else:
+            self.ctx = ctx_for(N, N)
         h = ctypes.c_void_p()
         L.check(L.lib().rmt_mac_sim_create(self.ctx.bind(), ctypes.byref(P), ctypes.byref(h)),
                 "rmt_mac_sim_create")

@@ -96,6 +96,27 @@ def test_mac_multi_disc_trace(M):
         np.testing.assert_allclose(sim.get("X2", k), g[f"X2_{k}_end"], rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("N,calls", [(64, (3, 1, 4)), (256, (5, 5))])
+def test_mac_box_mode_is_bit_identical(M, N, calls):
+    """The per-disc passes on each map's support box (mac_boxes, default on) against the
+    full-grid passes: every field and diagnostic bit for bit, over several calls (each call
+    starts from a full pass; the boxes then come back with the per-step diagnostics)."""
+    out = []
+    for boxes in (0, 1):
+        sim = M.MacMultiDisc(N, n_discs=3, seed=3, options={"mac_boxes": boxes})
+        for c in calls:
+            sim.step(c)
+        d = sim.diagnostics()
+        f = {f"{n}{k}": sim.get(n, k) for n in ("X1", "X2", "phi") for k in range(3)}
+        f.update({n: sim.get(n) for n in ("u", "v", "p")})
+        out.append((d, f))
+    (d0, f0), (d1, f1) = out
+    for k in d0:
+        np.testing.assert_array_equal(d1[k], d0[k], err_msg=k)
+    for k in f0:
+        np.testing.assert_array_equal(f1[k], f0[k], err_msg=k)
+
+
 def test_mac_sim_stops_on_divergence(M):
     """mac_multi_disc_lid.py:100-103: the loop stops after a step with J < 0 (a folded map);
     the record of that step is kept and flagged, later steps are not run."""
