@@ -25,9 +25,28 @@
 namespace rmt {
 
 constexpr int MAC_MAXD = 8;
+// Box mode (rmt_mac_sim_step): disc k's map is zero and its phi = disc_phi(0, 0) > 0 outside
+// the cells b[k] = {j0, j1, i0, i1} (half-open); n = 0: no boxes (every cell may hold
+// anything).  contact: every disc_phi(0, 0) >= eps too, so a contact pair is +0.0 outside
+// either disc's box and the stress S is +0.0 outside the union of the boxes.
+struct SBox {
+    int n, contact;
+    int b[MAC_MAXD][4];
+    __device__ __forceinline__ bool in(int k, int j, int i, int r = 0) const {
+        return j >= b[k][0] - r && j < b[k][1] + r && i >= b[k][2] - r && i < b[k][3] + r;
+    }
+    // S may be nonzero within r cells of (j, i)
+    __device__ __forceinline__ bool near(int j, int i, int r) const {
+        if (!n || !contact) return true;
+        for (int k = 0; k < n; ++k)
+            if (in(k, j, i, r)) return true;
+        return false;
+    }
+};
 struct DiscSet {
     const double *X1[MAC_MAXD], *X2[MAC_MAXD], *phi[MAC_MAXD];
     int K;
+    SBox bx;
 };
 
 // Every kernel takes global row ranges and global-index plane pointers (pointer - lo * row
@@ -204,6 +223,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
         double axx = 0.0, axy = 0.0, ayy = 0.0;
         const bool inner = j >= 1 && j < N - 1 && i >= 1 && i < N - 1;
         for (int k = 0; k < D.K; ++k) {
+            if (D.bx.n && !D.bx.in(k, j, i)) continue;   // phi_k = disc_phi(0, 0) > 0: no term
             Stress s{0.0, 0.0, 0.0, 1.0};
             const bool st = inner && solid_stress_cell(D.X1[k], D.X2[k], D.phi[k], c, N, dx, dy,
                                                        mu_s, 0.0, 0.0, 0.0, false, s);
@@ -218,6 +238,10 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
             for (int a = 0; a < D.K; ++a)
                 for (int b = a + 1; b < D.K; ++b) {
                     const double *pa = D.phi[a], *pb = D.phi[b];
+                    // outside a box with contact set, that disc's phi is >= eps (fc = +0.0)
+                    if (skip_ok && phi_ok && D.bx.n && D.bx.contact &&
+                        !(D.bx.in(a, j, i) && D.bx.in(b, j, i)))
+                        continue;
                     if (skip_ok && !(pa[c] < eps && pb[c] < eps)) {
                         if (phi_ok) continue;
                         const double gxn = i >= 1 && i < N - 1
@@ -277,7 +301,8 @@ __global__ void k_mac_predict(const double *__restrict__ u, const double *__rest
                               const double *__restrict__ Syy, const double *__restrict__ fu,
                               const double *__restrict__ fv, int N, double nu, double dx,
                               double dy, double dx2, double dy2, double dt, double U, double rho,
-                              double *__restrict__ us, double *__restrict__ vs, FaceRows F) {
+                              double *__restrict__ us, double *__restrict__ vs, FaceRows F,
+                              SBox bx = SBox{}) {
     // dx2, dy2: the reference's dx**2 on a Python float (libm pow), computed on the host
     const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
     const int W = N + 1;
@@ -294,7 +319,9 @@ __global__ void k_mac_predict(const double *__restrict__ u, const double *__rest
         const long cv = (long)j * N + i;   // v[j][i]
         const double vu = 0.25 * (((v[cv - 1] + v[cv]) + v[cv + N - 1]) + v[cv + N]);
         double r = -(uc * dudx + vu * dudy) + nu * lap;
-        if (Sxx) r = r + 0.5 * (divx_at(Sxx, Sxy, j, i, N, dx, dy) + divx_at(Sxx, Sxy, j, i - 1, N, dx, dy)) / rho;
+        // (where S is +0.0 on the whole stencil the divergences are +0.0: the same sum)
+        if (Sxx && !bx.near(j, i, 3)) r = r + 0.5 * (0.0 + 0.0) / rho;
+        else if (Sxx) r = r + 0.5 * (divx_at(Sxx, Sxy, j, i, N, dx, dy) + divx_at(Sxx, Sxy, j, i - 1, N, dx, dy)) / rho;
         else if (fu) r = r + fu[q] / rho;
         us[q] = uc + dt * r;
     } else if (t < nuf + (long)(F.v1 - F.v0) * N) {   // v face (j, i), row stride N
@@ -310,7 +337,8 @@ __global__ void k_mac_predict(const double *__restrict__ u, const double *__rest
         const long cu = (long)(j - 1) * W + i;   // u[j-1][i]
         const double uv = 0.25 * (((u[cu] + u[cu + 1]) + u[cu + W]) + u[cu + W + 1]);
         double r = -(uv * dvdx + vc * dvdy) + nu * lap;
-        if (Sxx) r = r + 0.5 * (divy_at(Sxy, Syy, j, i, N, dx, dy) + divy_at(Sxy, Syy, j - 1, i, N, dx, dy)) / rho;
+        if (Sxx && !bx.near(j, i, 3)) r = r + 0.5 * (0.0 + 0.0) / rho;
+        else if (Sxx) r = r + 0.5 * (divy_at(Sxy, Syy, j, i, N, dx, dy) + divy_at(Sxy, Syy, j - 1, i, N, dx, dy)) / rho;
         else if (fv) r = r + fv[p] / rho;
         vs[p] = vc + dt * r;
     }
@@ -371,9 +399,11 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
             in[m] = 0;
             if (t < n) {
                 const long c = (long)jb * N + t;
+                const int j = (int)(c / N), i = (int)(c % N);
 #pragma unroll
-                for (int k = 0; k < MAC_MAXD; ++k)
-                    if (k < D.K && D.phi[k][c] <= 0.0) in[m] |= 1u << k;
+                for (int k = 0; k < MAC_MAXD; ++k)   // (outside its box phi_k > 0)
+                    if (k < D.K && (!D.bx.n || D.bx.in(k, j, i)) && D.phi[k][c] <= 0.0)
+                        in[m] |= 1u << k;
             }
         }
 #pragma unroll
@@ -591,8 +621,13 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
     // extra host round trip); a call starts with one full pass per disc (phi, box).
     const int G = P.layers + 6;
     bool box_mode = ctx->opt.mac_boxes != 0 && P.layers > 0;
-    for (int k = 0; k < K; ++k)
-        box_mode = box_mode && std::sqrt(P.cx[k] * P.cx[k] + P.cy[k] * P.cy[k]) - P.R[k] > 0.0;
+    D.bx.contact = 1;
+    for (int k = 0; k < K; ++k) {
+        const double p0 = std::sqrt(P.cx[k] * P.cx[k] + P.cy[k] * P.cy[k]) - P.R[k];
+        box_mode = box_mode && p0 > 0.0;
+        D.bx.contact = D.bx.contact && p0 >= eps;   // (a contact term needs both phi < eps)
+    }
+    D.bx.n = 0;   // set per step once the boxes are known
     const size_t kb_bytes = (size_t)N * ((N + 63) / 64) * sizeof(unsigned long long);
     if (box_mode && nsteps > 0 && S->t < t_end && !S->diverged) {
         for (int k = 0; k < K; ++k) {
@@ -617,6 +652,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         for (int k = 0; k < K; ++k) {
             int cb[4] = {0, N, 0, N};   // the cells this disc's passes cover
             if (box_mode) {
+                D.bx.n = K;
                 const int *b = S->hbox[k];
                 if (b[1] < b[0]) { cb[1] = 0; cb[3] = 0; }   // empty map
                 else {
@@ -628,6 +664,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
                 }
                 RMT_HIP(hipMemsetAsync(S->kbits, 0, kb_bytes, st));
             }
+            for (int q = 0; q < 4; ++q) D.bx.b[k][q] = cb[q];   // (the stress / diag passes)
             // phi from the current map (already S->phi[k]), advect with the pre-advection mask
             RMT_TRY(sl_disc_map(ctx, S->X1[k], S->X2[k], S->uc, S->vc, S->xs, S->ys, dt, dx, dx,
                                 P.cx[k], P.cy[k], P.R[k], S->X1n, S->X2n, S->phi_pre,
@@ -664,7 +701,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         k_mac_predict<<<grid1d(2 * nf, 256), 256, 0, st>>>(S->u, S->v, S->Sxx, S->Sxy, S->Syy,
                                                             nullptr, nullptr, N, nu, dx, dx, dx2,
                                                             dx2, dt, P.U_lid, P.rho, S->us, S->vs,
-                                                            FaceRows{0, N, 0, N + 1});
+                                                            FaceRows{0, N, 0, N + 1}, D.bx);
         RMT_LAUNCHED();
         RMT_TRY(mac_project_impl(ctx, S->us, S->vs, dx, dx, dt, P.rho, S->u, S->v, S->p,
                                  S->X1n));
