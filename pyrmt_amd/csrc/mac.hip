@@ -64,6 +64,40 @@ __global__ void k_mac_centres(const double *__restrict__ u, const double *__rest
 }
 
 // big (nullable): set when a phi is NaN, infinite or >= 2^928 in magnitude (k_mac_stress)
+// k_mac_centres over the whole grid on RED_BLOCKS x RED_T threads, also folding max(u_c^2 +
+// v_c^2) (NaN-propagating, k_reduce_p1<3>'s rule: a max is exact in any order) into one
+// partial per block -- reduce_maxsq2_nan's pass over u_c, v_c saved
+__global__ void __launch_bounds__(RED_T) k_mac_centres_m2(const double *__restrict__ u,
+                                                          const double *__restrict__ v, int N,
+                                                          double *__restrict__ uc,
+                                                          double *__restrict__ vc, int *bad,
+                                                          double *__restrict__ part) {
+    __shared__ double s[RED_T];
+    double acc = -INFINITY;
+    bool fin = true;
+    const long n = (long)N * N;
+    for (long c = blockIdx.x * (long)RED_T + threadIdx.x; c < n; c += (long)RED_BLOCKS * RED_T) {
+        const int j = (int)(c / N), i = (int)(c % N);
+        const double a = 0.5 * (u[(long)j * (N + 1) + i] + u[(long)j * (N + 1) + i + 1]);
+        const double b = 0.5 * (v[c] + v[c + N]);
+        uc[c] = a; vc[c] = b;
+        fin = fin && isfinite(a) && isfinite(b);
+        const double x = a * a + b * b;
+        acc = (x > acc || x != x) ? x : acc;
+    }
+    if (!fin) atomicOr(bad, 1);
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = RED_T / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            const double y = s[threadIdx.x + w];
+            s[threadIdx.x] = (y > s[threadIdx.x] || y != y) ? y : s[threadIdx.x];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+
 __global__ void k_mac_phi(const double *__restrict__ X1n, const double *__restrict__ X2n, long n,
                           double x0, double y0, double R, double *__restrict__ X1,
                           double *__restrict__ X2, double *__restrict__ phi, int *big = nullptr) {
@@ -220,6 +254,9 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
         //    2^930 / (2 h) (host: 2 h >= 2^-30), nx, ny are finite (|n| <= 1 or mag = inf),
         //    and txx, txy, tyy = -0.0 * finite = +-0.0.  With phi_big clear (k_mac_phi: every
         //    phi finite and below 2^928) every numerator is, and the test is skipped.
+        // S is +0.0 away from every box and k_mac_predict reads it only within 3 cells of a
+        // face within 3 cells of a box: cells farther than 6 from every box are not written
+        if (D.bx.n && D.bx.contact && !D.bx.near(j, i, 6)) continue;
         double axx = 0.0, axy = 0.0, ayy = 0.0;
         const bool inner = j >= 1 && j < N - 1 && i >= 1 && i < N - 1;
         for (int k = 0; k < D.K; ++k) {
@@ -644,11 +681,12 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         double dt = P.dt;
         if (S->t + dt > t_end) dt = t_end - S->t;
         RMT_HIP(hipMemsetAsync(S->flags, 0, 5 * sizeof(int), st));   // [4]: k_mac_phi's big
-        k_mac_centres<<<grid1d(n, 256), 256, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags, 0,
-                                                      N);
+        // with max |u_c|^2, which bounds every velocity sample of the backtraces (the SL
+        // block skip)
+        k_mac_centres_m2<<<RED_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags,
+                                                         ctx->red);
         RMT_LAUNCHED();
-        // max |u_c|^2 bounds every velocity sample of the backtraces (the SL block skip)
-        RMT_TRY(reduce_maxsq2_nan(ctx, S->uc, S->vc, n, S->out + 8));
+        RMT_TRY(reduce_max_partials_nan(ctx, S->out + 8));
         for (int k = 0; k < K; ++k) {
             int cb[4] = {0, N, 0, N};   // the cells this disc's passes cover
             if (box_mode) {

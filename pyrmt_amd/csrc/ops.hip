@@ -152,6 +152,12 @@ int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double
 int reduce_maxsq2_nan(rmt_ctx *ctx, const double *a, const double *b, long n, double *o) {
     return reduce_impl(ctx, 3, a, b, n, o, 1.0);
 }
+// the second pass of reduce_maxsq2_nan over RED_BLOCKS partials a fused kernel left in ctx->red
+int reduce_max_partials_nan(rmt_ctx *ctx, double *o) {
+    k_reduce_p2<3><<<1, RED_T, 0, ctx->stream>>>(ctx->red, o, 1.0);
+    RMT_LAUNCHED();
+    return RMT_OK;
+}
 int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *o) {
     return reduce_impl(ctx, 0, x, x, n, o, 1.0 / (double)n);
 }

@@ -577,6 +577,7 @@ int reduce_max(rmt_ctx *ctx, const double *x, long n, double *dev_out);
 int reduce_maxsq2(rmt_ctx *ctx, const double *a, const double *b, long n, double *dev_out);
 // the same with NaN propagating (a non-finite velocity makes the bound NaN: no SL block skip)
 int reduce_maxsq2_nan(rmt_ctx *ctx, const double *a, const double *b, long n, double *dev_out);
+int reduce_max_partials_nan(rmt_ctx *ctx, double *o);   // (RED_BLOCKS partials in ctx->red)
 int reduce_mean(rmt_ctx *ctx, const double *x, long n, double *dev_out);
 int read_scalar(rmt_ctx *ctx, const double *dev, double *host);
 // row-tree sums (ops.hip): root of rows [0, nrows) of x (row length nx) into *dev_root;
