@@ -247,9 +247,12 @@ def test_config4_N4096_100_steps_vs_fixture(gpu):
 def test_config4_N4096_100_steps_parallel_mode(gpu):
     """The opt-in parallel extrapolation (extrap_par.hip: the reference's fits evaluated in
     centred coordinates) over the bench's 100 steps against the same oracle fixture.  It is
-    not bit-exact: the reference's own 1-ulp noise moves the centroid by 4.8e-7 in 30 steps
-    (profiles/r03/noise/).  Reported: the worst centroid error and the first step past the
-    north-star bar 1e-6."""
+    not bit-exact.  Its bar is the reference's own noise floor over the same 100 steps at
+    N=4096 (profiles/r05/noise/lid_n4096_100.json, tools/noise_floor.py): a 1-ulp nudge of
+    the fit weights moves the reference's centroid by up to 5.78e-7 (cy, step 5), and the
+    reference evaluated in centred coordinates on the CPU -- this mode's arithmetic -- lands
+    1.147e-6 away, the same as this GPU mode.  Asserted: within twice the 1-ulp floor on
+    every one of the 100 steps."""
     from pyrmt_amd.simulation import soft_disc_in_lid_driven
     g = golden("lid4096_100_oracle")
     N, S = int(g["N"]), int(g["steps"])
@@ -268,7 +271,5 @@ def test_config4_N4096_100_steps_parallel_mode(gpu):
     print(f"\n[config4 N=4096 x{S}, parallel extrapolation] worst centroid rel {cen.max():.3g} "
           f"(step {int(cen.argmax()) + 1}); first step past 1e-6: {first}; t {rel[:, 0].max():.3g} "
           f"minJ {rel[:, 4].max():.3g} maxJ {rel[:, 5].max():.3g}")
-    # the documented envelope (measured round 4: first past 1e-6 at
-    # step 23, worst 1.15e-6): within the bar for the first 20 steps, within 1e-5 over 100
-    assert np.all(cen[:20] <= 1e-6)
-    assert cen.max() <= 1e-5
+    floor = 5.781624386615219e-07   # lid_n4096_100.json: nudge_1ulp, max of cx / cy max_rel
+    assert np.all(cen <= 2 * floor), (cen.max(), int(cen.argmax()) + 1)
