@@ -6,7 +6,10 @@ calibrated on librmt's own 8-B/lane pattern in round 1, profiles/r01/hbm_traffic
 WRITE_SIZE is taken as is.  Per step: the dispatches from the second step boundary (a k_dt or
 k_dt_part launch: the first kernel of every step) to the end, divided by the steps they cover.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [git-rev]
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [git-rev] [step-start kernels]
+
+(step-start kernels: comma-separated names of the first kernel of a step; default
+k_dt,k_dt_part -- config 5's step starts with k_mac_centres_m2)
 """
 import csv
 import glob
@@ -60,7 +63,8 @@ def main():
         per_launch[n] = [a + b for a, b in zip(fseq[n], wseq.get(n, []))]
     # per step, from the fetch pass's dispatch order
     order = sorted(fe)
-    starts = [d for d in order if fe[d][0] in ("k_dt", "k_dt_part")]
+    marks = tuple(sys.argv[5].split(",")) if len(sys.argv) > 5 else ("k_dt", "k_dt_part")
+    starts = [d for d in order if fe[d][0] in marks]
     nsteps = len(starts) - 1
     step = {}
     for label, per, scale in (("fetch", fe, 2.0), ("write", wr, 1.0)):
