@@ -49,6 +49,10 @@ struct DiscSet {
     SBox bx;
 };
 
+// Index math of the per-cell / per-face kernels in 32 bits (a 64-bit division by a runtime
+// divisor is a long emulated sequence): every index fits, N <= 32768 (rmt_mac_sim_create).
+__device__ __forceinline__ int dv32(long x, int d) { return (int)((unsigned)x / (unsigned)d); }
+
 // Every kernel takes global row ranges and global-index plane pointers (pointer - lo * row
 // length), so the slab-decomposed step (rmt_mac_slab below) runs the same per-element code.
 __global__ void k_mac_centres(const double *__restrict__ u, const double *__restrict__ v, int N,
@@ -56,7 +60,7 @@ __global__ void k_mac_centres(const double *__restrict__ u, const double *__rest
                               int je) {
     const long c = (long)jb * N + blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (c >= (long)je * N) return;
-    const int j = (int)(c / N), i = (int)(c % N);
+    const int j = dv32(c, N), i = (int)(c - (long)j * N);
     const double a = 0.5 * (u[(long)j * (N + 1) + i] + u[(long)j * (N + 1) + i + 1]);
     const double b = 0.5 * (v[c] + v[c + N]);
     uc[c] = a; vc[c] = b;
@@ -64,7 +68,31 @@ __global__ void k_mac_centres(const double *__restrict__ u, const double *__rest
 }
 
 // big (nullable): set when a phi is NaN, infinite or >= 2^928 in magnitude (k_mac_stress)
-// k_mac_centres over the whole grid on RED_BLOCKS x RED_T threads, also folding max(u_c^2 +
+// one workgroup: the NaN-propagating max of G partials (NAN_MAX: nanmax, else k_reduce_p1<3>'s
+// rule -- either is exact in any order) into *out
+template <bool NAN_MAX>
+__global__ void __launch_bounds__(1024) k_max_partials(const double *__restrict__ part, int G,
+                                                      double init, double *__restrict__ out) {
+    __shared__ double s[1024];
+    double acc = init;
+    for (int k = threadIdx.x; k < G; k += 1024) {
+        const double y = part[k];
+        acc = NAN_MAX ? nanmax(acc, y) : ((y > acc || y != y) ? y : acc);
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            const double y = s[threadIdx.x + w], x = s[threadIdx.x];
+            s[threadIdx.x] = NAN_MAX ? nanmax(x, y) : ((y > x || y != y) ? y : x);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = s[0];
+}
+constexpr int MP_BLOCKS = 8192;   // the fused reduction passes' workgroups (one partial each)
+
+// k_mac_centres over the whole grid on MP_BLOCKS x RED_T threads, also folding max(u_c^2 +
 // v_c^2) (NaN-propagating, k_reduce_p1<3>'s rule: a max is exact in any order) into one
 // partial per block -- reduce_maxsq2_nan's pass over u_c, v_c saved
 __global__ void __launch_bounds__(RED_T) k_mac_centres_m2(const double *__restrict__ u,
@@ -76,14 +104,31 @@ __global__ void __launch_bounds__(RED_T) k_mac_centres_m2(const double *__restri
     double acc = -INFINITY;
     bool fin = true;
     const long n = (long)N * N;
-    for (long c = blockIdx.x * (long)RED_T + threadIdx.x; c < n; c += (long)RED_BLOCKS * RED_T) {
-        const int j = (int)(c / N), i = (int)(c % N);
-        const double a = 0.5 * (u[(long)j * (N + 1) + i] + u[(long)j * (N + 1) + i + 1]);
-        const double b = 0.5 * (v[c] + v[c + N]);
-        uc[c] = a; vc[c] = b;
-        fin = fin && isfinite(a) && isfinite(b);
-        const double x = a * a + b * b;
-        acc = (x > acc || x != x) ? x : acc;
+    constexpr int CM_U = 2;   // cells per trip, loads first (the max is exact in any order)
+    const long S = (long)gridDim.x * RED_T;
+    for (long c0 = blockIdx.x * (long)RED_T + threadIdx.x; c0 < n; c0 += CM_U * S) {
+        double ul[CM_U], ur[CM_U], vd[CM_U], vu[CM_U];
+#pragma unroll
+        for (int m = 0; m < CM_U; ++m) {
+            const long c = c0 + m * S;
+            ul[m] = ur[m] = vd[m] = vu[m] = 0.0;
+            if (c < n) {
+                const int j = dv32(c, N), i = (int)(c - (long)j * N);
+                ul[m] = u[(long)j * (N + 1) + i]; ur[m] = u[(long)j * (N + 1) + i + 1];
+                vd[m] = v[c]; vu[m] = v[c + N];
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < CM_U; ++m) {
+            const long c = c0 + m * S;
+            if (c >= n) break;
+            const double a = 0.5 * (ul[m] + ur[m]);
+            const double b = 0.5 * (vd[m] + vu[m]);
+            uc[c] = a; vc[c] = b;
+            fin = fin && isfinite(a) && isfinite(b);
+            const double x = a * a + b * b;
+            acc = (x > acc || x != x) ? x : acc;
+        }
     }
     if (!fin) atomicOr(bad, 1);
     s[threadIdx.x] = acc;
@@ -235,15 +280,28 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
                                                        double *__restrict__ Syy,
                                                        double *__restrict__ part, int jb, int je,
                                                        int jr0, int jr1, bool skip_ok,
-                                                       const int *__restrict__ phi_big = nullptr) {
+                                                       const int *__restrict__ phi_big = nullptr,
+                                                       bool box_launch = false) {
     const bool phi_ok = phi_big && *phi_big == 0;
-    // S on rows [jb, je); the J range over rows [jr0, jr1)
+    // S on rows [jb, je); the J range over rows [jr0, jr1).  box_launch (box mode with
+    // contact set): block row y covers disc y's box grown by 6 cells -- every cell the
+    // predictor reads S at (see below); overlapping boxes compute a cell twice, the same
+    // values.  Partials: one (min J, max J) pair per block.
     __shared__ double smin[MS_TPB], smax[MS_TPB];
     double jmin = 1.0, jmax = 1.0;
-    const long n = (long)je * N;
-    for (long c = (long)jb * N + blockIdx.x * (long)MS_TPB + threadIdx.x; c < n;
-         c += (long)MS_BLOCKS * MS_TPB) {
-        const int j = (int)(c / N), i = (int)(c % N);
+    int r0 = jb, c0 = 0, w = N;
+    long area = (long)(je - jb) * N;
+    if (box_launch) {
+        const int *b = D.bx.b[blockIdx.y];
+        r0 = max(jb, b[0] - 6); c0 = max(0, b[2] - 6);
+        w = max(0, min(N, b[3] + 6) - c0);
+        area = (long)max(0, min(je, b[1] + 6) - r0) * w;
+    }
+    for (long t = blockIdx.x * (long)MS_TPB + threadIdx.x; t < area;
+         t += (long)gridDim.x * MS_TPB) {
+        const int tj = dv32(t, w);
+        const int j = r0 + tj, i = c0 + (int)(t - (long)tj * w);
+        const long c = (long)j * N + i;
         const bool own = j >= jr0 && j < jr1;
         // The sums start at +0.0 and only add, so they are never -0.0: adding a +-0.0 term
         // leaves them bit for bit unchanged.  Two kinds of term are exactly +-0.0 and skipped:
@@ -304,7 +362,10 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_stress(DiscSet D, int N, double 
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { part[2 * blockIdx.x] = smin[0]; part[2 * blockIdx.x + 1] = smax[0]; }
+    if (threadIdx.x == 0) {
+        const long pb = (long)blockIdx.y * gridDim.x + blockIdx.x;
+        part[2 * pb] = smin[0]; part[2 * pb + 1] = smax[0];
+    }
 }
 
 // k_mac_stress's zero-term skip needs 2 h >= 2^-30 and finite contact constants (see there)
@@ -345,7 +406,7 @@ __global__ void k_mac_predict(const double *__restrict__ u, const double *__rest
     const int W = N + 1;
     const long nuf = (long)(F.u1 - F.u0) * W, q = (long)F.u0 * W + t;
     if (t < nuf) {   // u face (j, i), row stride N + 1
-        const int j = (int)(q / W), i = (int)(q % W);
+        const int j = dv32(q, W), i = (int)(q - (long)j * W);
         if (i == 0 || i == N) { us[q] = 0.0; return; }
         const double uc = u[q], ul = u[q - 1], ur = u[q + 1];
         const double dn = j > 0 ? u[q - W] : -u[q];                 // ghost: -u[0]
@@ -363,7 +424,7 @@ __global__ void k_mac_predict(const double *__restrict__ u, const double *__rest
         us[q] = uc + dt * r;
     } else if (t < nuf + (long)(F.v1 - F.v0) * N) {   // v face (j, i), row stride N
         const long p = (long)F.v0 * N + (t - nuf);
-        const int j = (int)(p / N), i = (int)(p % N);
+        const int j = dv32(p, N), i = (int)(p - (long)j * N);
         if (j == 0 || j == N) { vs[p] = 0.0; return; }
         const double vc = v[p], vd = v[p - N], vup = v[p + N];
         const double vl = i > 0 ? v[p - 1] : -v[p];
@@ -387,7 +448,7 @@ __global__ void k_mac_rhs(const double *__restrict__ u, const double *__restrict
                           int je) {
     const long c = (long)jb * N + blockIdx.x * (long)blockDim.x + threadIdx.x;
     if (c >= (long)je * N) return;
-    const int j = (int)(c / N), i = (int)(c % N);
+    const int j = dv32(c, N), i = (int)(c - (long)j * N);
     const long cu = (long)j * (N + 1) + i;
     const double d = (u[cu + 1] - u[cu]) / dx + (v[c + N] - v[c]) / dy;
     rhs[c] = coef * d;
@@ -401,18 +462,79 @@ __global__ void k_mac_correct(const double *__restrict__ us, const double *__res
     const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
     const long nuf = (long)(F.u1 - F.u0) * (N + 1), q = (long)F.u0 * (N + 1) + t;
     if (t < nuf) {
-        const int j = (int)(q / (N + 1)), i = (int)(q % (N + 1));
+        const int j = dv32(q, N + 1), i = (int)(q - (long)j * (N + 1));
         const double g = (i == 0 || i == N) ? 0.0 : (phi[(long)j * N + i] - phi[(long)j * N + i - 1]) / dx;
         u[q] = us[q] - c0 * g;
     } else if (t < nuf + (long)(F.v1 - F.v0) * N) {
         const long p = (long)F.v0 * N + (t - nuf);
-        const int j = (int)(p / N);
+        const int j = dv32(p, N);
         const double g = (j == 0 || j == N) ? 0.0 : (phi[p] - phi[p - N]) / dy;
         v[p] = vs[p] - c0 * g;
     }
 }
 
-// per-disc centroid sums over phi <= 0 (x, y, count) and max|u| partials
+// k_mac_correct over the whole grid on MP_BLOCKS x RED_T threads (u faces, then v faces),
+// also folding max |u| over the u faces (nanmax: exact in any order) into one partial per
+// block -- k_mac_diag's pass over u saved (it is then launched with u = nullptr)
+__global__ void __launch_bounds__(RED_T) k_mac_correct_um(const double *__restrict__ us,
+                                                          const double *__restrict__ vs,
+                                                          const double *__restrict__ phi, int N,
+                                                          double dx, double dy, double c0,
+                                                          double *__restrict__ u,
+                                                          double *__restrict__ v,
+                                                          double *__restrict__ part) {
+    __shared__ double s[RED_T];
+    double acc = 0.0;
+    const long nuf = (long)N * (N + 1), tot = 2 * nuf;
+    // CU_U faces per trip: their loads issued together, then written in face order (the max
+    // is exact in any order)
+    constexpr int CU_U = 2;
+    const long S = (long)gridDim.x * RED_T;
+    for (long t0 = blockIdx.x * (long)RED_T + threadIdx.x; t0 < tot; t0 += CU_U * S) {
+        double a[CU_U], p1[CU_U], p0[CU_U];
+#pragma unroll
+        for (int m = 0; m < CU_U; ++m) {
+            const long t = t0 + m * S;
+            a[m] = 0.0; p1[m] = 0.0; p0[m] = 0.0;
+            if (t < nuf) {
+                const int j = dv32(t, N + 1), i = (int)(t - (long)j * (N + 1));
+                a[m] = us[t];
+                if (!(i == 0 || i == N)) { p1[m] = phi[(long)j * N + i]; p0[m] = phi[(long)j * N + i - 1]; }
+            } else if (t < tot) {
+                const long q = t - nuf;
+                const int j = dv32(q, N);
+                a[m] = vs[q];
+                if (!(j == 0 || j == N)) { p1[m] = phi[q]; p0[m] = phi[q - N]; }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < CU_U; ++m) {
+            const long t = t0 + m * S;
+            if (t < nuf) {
+                const int j = dv32(t, N + 1), i = (int)(t - (long)j * (N + 1));
+                const double g = (i == 0 || i == N) ? 0.0 : (p1[m] - p0[m]) / dx;
+                const double x = a[m] - c0 * g;
+                u[t] = x;
+                acc = nanmax(acc, fabs(x));
+            } else if (t < tot) {
+                const long q = t - nuf;
+                const int j = dv32(q, N);
+                const double g = (j == 0 || j == N) ? 0.0 : (p1[m] - p0[m]) / dy;
+                v[q] = a[m] - c0 * g;
+            }
+        }
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = RED_T / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) s[threadIdx.x] = nanmax(s[threadIdx.x], s[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+}
+
+// per-disc centroid sums over phi <= 0 (x, y, count) and max|u| partials (u nullable: the
+// max comes from k_mac_correct_um)
 constexpr int MD_VALS = 3 * MAC_MAXD + 1;
 // (rows [jb, je): cells and u faces)
 __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__restrict__ u,
@@ -432,11 +554,11 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
 #pragma unroll
         for (int m = 0; m < MD_U; ++m) {
             const long t = t0 + m * S;
-            ua[m] = t < nf ? u[(long)jb * (N + 1) + t] : 0.0;
+            ua[m] = t < nf && u ? u[(long)jb * (N + 1) + t] : 0.0;
             in[m] = 0;
             if (t < n) {
                 const long c = (long)jb * N + t;
-                const int j = (int)(c / N), i = (int)(c % N);
+                const int j = dv32(c, N), i = (int)(c - (long)j * N);
 #pragma unroll
                 for (int k = 0; k < MAC_MAXD; ++k)   // (outside its box phi_k > 0)
                     if (k < D.K && (!D.bx.n || D.bx.in(k, j, i)) && D.phi[k][c] <= 0.0)
@@ -450,7 +572,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
             acc[3 * MAC_MAXD] = nanmax(acc[3 * MAC_MAXD], fabs(ua[m]));
             if (t < n) {
                 const long c = (long)jb * N + t;
-                const int j = (int)(c / N), i = (int)(c % N);
+                const int j = dv32(c, N), i = (int)(c - (long)j * N);
                 const double xc = (i + 0.5) * dx, yc = (j + 0.5) * dx;
                 for (int k = 0; k < D.K; ++k)
                     if ((in[m] >> k) & 1) { acc[3 * k] += xc; acc[3 * k + 1] += yc; acc[3 * k + 2] += 1.0; }
@@ -473,7 +595,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
 
 static int mac_project_impl(rmt_ctx *ctx, const double *us, const double *vs, double dx,
                             double dy, double dt, double rho, double *u, double *v, double *phi,
-                            double *rhs, bool plan = true) {
+                            double *rhs, bool plan = true, double *umax_part = nullptr) {
     const int N = ctx->nx;
     const long n = (long)N * N, nf = (long)N * (N + 1);
     if (plan) RMT_TRY(dct2_plan(ctx, N, N, dx, dy));
@@ -481,8 +603,13 @@ static int mac_project_impl(rmt_ctx *ctx, const double *us, const double *vs, do
     RMT_LAUNCHED();
     RMT_TRY(sub_mean_rows(ctx, rhs, N, N));     // rhs - rhs.mean() (mac.py:135)
     RMT_TRY(dct2_solve(ctx, rhs, phi));
-    k_mac_correct<<<grid1d(2 * nf, 256), 256, 0, ctx->stream>>>(us, vs, phi, N, dx, dy, dt / rho,
-                                                                u, v, FaceRows{0, N, 0, N + 1});
+    if (umax_part)
+        k_mac_correct_um<<<MP_BLOCKS, RED_T, 0, ctx->stream>>>(us, vs, phi, N, dx, dy, dt / rho,
+                                                                u, v, umax_part);
+    else
+        k_mac_correct<<<grid1d(2 * nf, 256), 256, 0, ctx->stream>>>(us, vs, phi, N, dx, dy,
+                                                                    dt / rho, u, v,
+                                                                    FaceRows{0, N, 0, N + 1});
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -500,6 +627,7 @@ struct rmt_mac_sim {
     unsigned long long *kbits;   // the advection's known plane (phi_pre < 0), 64-cell words
     int *flags;
     int2 *bres;                  // per-block column extents of the box passes (box_fold)
+    double *mpart;               // per-block maxima of the fused reduction passes
     int *dbox;                   // [K][4] device support boxes (k_box_reduce), host copy:
     int hbox[RMT_MAC_MAXD][4];
     double t = 0;
@@ -577,6 +705,7 @@ int rmt_mac_contact_stress(rmt_ctx *ctx, const double *phi_a, const double *phi_
 int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **out) {
     RMT_CHECK(ctx && prm && out, RMT_EINVAL, "null argument");
     RMT_CHECK(prm->n_discs >= 1 && prm->n_discs <= RMT_MAC_MAXD, RMT_EINVAL, "1..8 discs");
+    RMT_CHECK(prm->N >= 4 && prm->N <= 32768, RMT_EINVAL, "N in 4..32768 (32-bit face indices)");
     RMT_CHECK(ctx->nx == prm->N && ctx->ny == prm->N, RMT_EINVAL, "ctx grid != N x N");
     const int N = prm->N;
     RMT_TRY(dct2_plan(ctx, N, N, prm->dx, prm->dx));
@@ -584,7 +713,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     S->ctx = ctx; S->P = *prm;
     const long n = (long)N * N, nf = (long)N * (N + 1);
     const int K = prm->n_discs;
-    const size_t dbl = 5 * nf + (9 + 3 * K) * n + 2 * N + (2 + MD_VALS) * MS_BLOCKS + 64 + 32;
+    const size_t dbl = 5 * nf + (9 + 3 * K) * n + 2 * N + (2 + MD_VALS) * MS_BLOCKS + 64 + 32 + MP_BLOCKS;
     RMT_HIP(hipMalloc(&S->block, dbl * 8 + 64));
     RMT_HIP(hipMemsetAsync(S->block, 0, dbl * 8 + 64, ctx->stream));
     double *q = (double *)S->block;
@@ -594,6 +723,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     // pass's per-block extents ((N / 256 + 1) x N) -- together far below nf doubles
     S->kbits = (unsigned long long *)q;
     S->bres = (int2 *)(q + (long)N * ((N + 63) / 64));
+
     q += nf;
     double **cells[] = {&S->p, &S->uc, &S->vc, &S->X1n, &S->X2n, &S->phi_pre, &S->Sxx, &S->Sxy,
                         &S->Syy};
@@ -605,6 +735,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     S->ys = q; q += N;
     S->part = q; q += (2 + MD_VALS) * MS_BLOCKS;   // J range, then centroid partials
     S->out = q; q += 32;
+    S->mpart = q; q += MP_BLOCKS;
     S->dbox = (int *)q; q += 4 * RMT_MAC_MAXD / 2;
     S->flags = (int *)q;
     // index-grid coordinates (mac_multi_disc_lid.py:41): Xg = arange(N) * dx
@@ -683,10 +814,10 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         RMT_HIP(hipMemsetAsync(S->flags, 0, 5 * sizeof(int), st));   // [4]: k_mac_phi's big
         // with max |u_c|^2, which bounds every velocity sample of the backtraces (the SL
         // block skip)
-        k_mac_centres_m2<<<RED_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags,
-                                                         ctx->red);
+        k_mac_centres_m2<<<MP_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags,
+                                                        S->mpart);
+        k_max_partials<false><<<1, 1024, 0, st>>>(S->mpart, MP_BLOCKS, -INFINITY, S->out + 8);
         RMT_LAUNCHED();
-        RMT_TRY(reduce_max_partials_nan(ctx, S->out + 8));
         for (int k = 0; k < K; ++k) {
             int cb[4] = {0, N, 0, N};   // the cells this disc's passes cover
             if (box_mode) {
@@ -730,24 +861,33 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
             }
             RMT_LAUNCHED();
         }
-        k_mac_stress<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, N, dx, dx, P.mu_s, w_t, P.eta, eps, S->Sxx,
-                                                    S->Sxy, S->Syy, S->part, 0, N, 0, N,
-                                                    stress_skip_ok(P), S->flags + 4);
+        // box mode with contact: only the discs' boxes grown by 6 (MS_BLOCKS / K blocks each,
+        // one J partial per block); otherwise the whole grid
+        const bool sbox = D.bx.n > 0 && D.bx.contact;
+        const dim3 sg = sbox ? dim3(MS_BLOCKS / K, K) : dim3(MS_BLOCKS);
+        k_mac_stress<<<sg, MS_TPB, 0, st>>>(D, N, dx, dx, P.mu_s, w_t, P.eta, eps, S->Sxx,
+                                            S->Sxy, S->Syy, S->part, 0, N, 0, N,
+                                            stress_skip_ok(P), S->flags + 4, sbox);
         RMT_LAUNCHED();
+        const int npart = (int)(sg.x * sg.y);
         double jr[2 * MS_BLOCKS];
-        RMT_HIP(hipMemcpyAsync(jr, S->part, sizeof(jr), hipMemcpyDeviceToHost, st));
+        RMT_HIP(hipMemcpyAsync(jr, S->part, 2 * npart * sizeof(double), hipMemcpyDeviceToHost, st));
         k_mac_predict<<<grid1d(2 * nf, 256), 256, 0, st>>>(S->u, S->v, S->Sxx, S->Sxy, S->Syy,
                                                             nullptr, nullptr, N, nu, dx, dx, dx2,
                                                             dx2, dt, P.U_lid, P.rho, S->us, S->vs,
                                                             FaceRows{0, N, 0, N + 1}, D.bx);
         RMT_LAUNCHED();
+        // max |u| from the correction's pass, folded on the device into out[9]
         RMT_TRY(mac_project_impl(ctx, S->us, S->vs, dx, dx, dt, P.rho, S->u, S->v, S->p,
-                                 S->X1n));
-        k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, S->u, N, dx, S->part + 2 * MS_BLOCKS, 0, N);
+                                 S->X1n, true, S->mpart));
+        k_max_partials<true><<<1, 1024, 0, st>>>(S->mpart, MP_BLOCKS, 0.0, S->out + 9);
+        k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, nullptr, N, dx, S->part + 2 * MS_BLOCKS, 0, N);
         RMT_LAUNCHED();
         std::vector<double> dp((size_t)MS_BLOCKS * MD_VALS);
         RMT_HIP(hipMemcpyAsync(dp.data(), S->part + 2 * MS_BLOCKS, dp.size() * 8,
                                hipMemcpyDeviceToHost, st));
+        double um = 0.0;
+        RMT_HIP(hipMemcpyAsync(&um, S->out + 9, sizeof(double), hipMemcpyDeviceToHost, st));
         int fl[4];
         RMT_HIP(hipMemcpyAsync(fl, S->flags, sizeof(fl), hipMemcpyDeviceToHost, st));
         if (box_mode)   // the next step's boxes, with the diagnostics
@@ -760,7 +900,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         rmt_mac_diag r{};
         r.t = S->t; r.dt = dt; r.n_discs = K;
         r.minJ = 1.0; r.maxJ = 1.0;
-        for (int b = 0; b < MS_BLOCKS; ++b) {
+        for (int b = 0; b < npart; ++b) {
             r.minJ = std::fmin(r.minJ, jr[2 * b]); r.maxJ = std::fmax(r.maxJ, jr[2 * b + 1]);
         }
         double acc[MD_VALS] = {0};
@@ -773,6 +913,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
             r.cx[k] = acc[3 * k + 2] > 0 ? acc[3 * k] / acc[3 * k + 2] : NAN;
             r.cy[k] = acc[3 * k + 2] > 0 ? acc[3 * k + 1] / acc[3 * k + 2] : NAN;
         }
+        acc[3 * MAC_MAXD] = nanmax(acc[3 * MAC_MAXD], um);
         r.umax = acc[3 * MAC_MAXD];
         // mac_multi_disc_lid.py:100-103: the driver stops on a non-finite u, a folded (J < 0)
         // or over-stretched (J > 20) map, or a disc with no phi <= 0 cell left
@@ -922,6 +1063,7 @@ int rmt_mac_slab_create(rmt_ctx *ctx, const rmt_mac_params *prm, int G, int rank
     RMT_CHECK(ctx && prm && row_splits && col_splits && out, RMT_EINVAL, "null argument");
     RMT_CHECK(G >= 1 && G <= MSL_MAXG && rank >= 0 && rank < G, RMT_EINVAL, "slab: bad G/rank");
     RMT_CHECK(prm->n_discs >= 1 && prm->n_discs <= RMT_MAC_MAXD, RMT_EINVAL, "1..8 discs");
+    RMT_CHECK(prm->N >= 4 && prm->N <= 32768, RMT_EINVAL, "N in 4..32768 (32-bit face indices)");
     const int N = prm->N;
     RMT_CHECK(ctx->nx == N && ctx->ny == N, RMT_EINVAL, "slab: ctx must be the global N x N");
     RMT_CHECK(N <= 8192, RMT_ENOTSUP, "MAC slab step: N <= 8192");
