@@ -38,6 +38,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"edge_stream", "RMT_EDGE_STREAM", &rmt_opts::edge_stream},
     {"sl_phi", "RMT_SL_PHI", &rmt_opts::sl_phi},
     {"mac_boxes", "RMT_MAC_BOXES", &rmt_opts::mac_boxes},
+    {"skip_marked_rows", "RMT_SKIP_MARKED_ROWS", &rmt_opts::skip_marked_rows},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;
@@ -1053,7 +1054,7 @@ namespace rmt {
 int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                     double dy, const double *dtp, double dt, double rho, const double *p_prev,
                     const unsigned char *rowmark, const int *tiles, const int *tcount,
-                    int max_tiles) {
+                    int max_tiles, const unsigned char *dct_skip) {
     RMT_CHECK(p_prev && rho > 0 && (!tiles || rowmark), RMT_EINVAL,
               "projection_rows: bad arguments");
     const long n = (long)ctx->ny * ctx->nx;
@@ -1072,6 +1073,10 @@ int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, do
             dtp, rowmark);
     RMT_LAUNCHED();
     RMT_TRY(dct_plan(ctx, dx, dy));
+    // dct_skip (the speculative full-grid call, rowmark null): the rows marked there are
+    // transformed again after the fix-up -- this pass leaves them out
+    if (!rowmark && dct_skip)
+        return dct_pass(ctx, false, 0, rhs, pc, ctx->ny, 0, 1.0, nullptr, dct_skip, true);
     return dct_pass(ctx, false, 0, rhs, pc, ctx->ny, 0, 1.0, nullptr, rowmark);
 }
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,

@@ -525,8 +525,10 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
                                                       const double *__restrict__ lamr,
                                                       const double *__restrict__ lamk, int row0,
                                                       double *__restrict__ rs,
-                                                      const unsigned char *__restrict__ rowmark) {
-    if (rowmark && !rowmark[blockIdx.x]) return;   // only the listed rows
+                                                      const unsigned char *__restrict__ rowmark,
+                                                      int rm_inv = 0) {
+    // only the listed rows (rm_inv: only the others)
+    if (rowmark && (rowmark[blockIdx.x] != 0) == (rm_inv != 0)) return;
     constexpr int NT = K1T<BIG>::T;
     constexpr int PP = (K1_MAXN / 2 + NT - 1) / NT;   // (k, N - k) pairs per thread, N < K1_MAXN
     extern __shared__ double2 z[];
@@ -656,7 +658,7 @@ static Radices radices(const int *rad, int np) {
 // One LDS DCT-I pass over nrows rows of length n (axis 0: n = nx, axis 1: n = ny).  SOLVE
 // (axis 1 only): forward, / eig, inverse, with rows = x-frequencies row0 .. row0 + nrows.
 int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
-             int row0, double scale, double *rs, const unsigned char *rowmark) {
+             int row0, double scale, double *rs, const unsigned char *rowmark, bool unmarked) {
     DctPlan *P = ctx->dct;
     RMT_CHECK(P && P->lds, RMT_ENOTSUP, "dct_pass: no LDS DCT plan for this grid");
     RMT_CHECK(!solve || axis == 1, RMT_EINVAL, "dct_pass: the solve pass runs along y");
@@ -685,13 +687,13 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     if (k4095 && solve)
         k_dct1<true, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
     else if (k4095)
-        k_dct1<false, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark);
+        k_dct1<false, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark, unmarked);
     else if (solve) {
         if (P->big) k_dct1<true, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
         else k_dct1<true, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
     } else {
-        if (P->big) k_dct1<false, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark);
-        else k_dct1<false, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark);
+        if (P->big) k_dct1<false, 1><<<g, K1T<1>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark, unmarked);
+        else k_dct1<false, 0><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark, unmarked);
     }
     RMT_LAUNCHED();
     return RMT_OK;

@@ -101,6 +101,8 @@ struct rmt_opts {
     int edge_stream = 1;      // RMT_EDGE_STREAM: a full stage's edge tiles beside its interior
     int sl_phi = 1;           // RMT_SL_PHI: the side stream's SL pass also writes phi + fluid bits
     int mac_boxes = 1;        // RMT_MAC_BOXES: config 5's per-disc passes on the map's support box
+    int skip_marked_rows = 1; // RMT_SKIP_MARKED_ROWS: the speculative row DCT leaves out the rows
+                              // the fix-up transforms again
 };
 
 #ifndef RMT_EDGE_SLOTS
@@ -595,7 +597,8 @@ int sub_tree_mean(rmt_ctx *ctx, double *x, long n, const double *dev_roots, int 
 int projection_rows(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                     double dy, const double *dtp, double dt, double rho, const double *p_prev,
                     const unsigned char *rowmark, const int *tiles = nullptr,
-                    const int *tcount = nullptr, int max_tiles = 0);
+                    const int *tcount = nullptr, int max_tiles = 0,
+                    const unsigned char *dct_skip = nullptr);
 int projection_finish(rmt_ctx *ctx, const double *a_star, const double *b_star, double dx,
                       double dy, const double *dtp, double dt, double rho, int bc_kind,
                       double lid, const double *p_prev, double *a, double *b, double *p,
@@ -714,10 +717,11 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
 int dct_plan(rmt_ctx *ctx, double dx, double dy);
 bool dct_lds_ready(rmt_ctx *ctx);
 // rs (nullable): per-row sums of the output, in k_rowsum's order (rowtree_sums finishes them);
-// rowmark (nullable): transform only the rows r with rowmark[r] != 0
+// rowmark (nullable): transform only the rows r with rowmark[r] != 0 (unmarked: only the
+// others)
 int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst, int nrows,
              int row0, double scale, double *rs = nullptr,
-             const unsigned char *rowmark = nullptr);
+             const unsigned char *rowmark = nullptr, bool unmarked = false);
 // the LDS solve after its forward row pass (pc holds DCT_x of the rhs): columns, inverse rows,
 // the row-tree sum of the result into *dev_root (mean not subtracted)
 int dct_solve_after_rows(rmt_ctx *ctx, double *pc, double *dev_root,

@@ -1179,7 +1179,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 // main stream re-runs meanwhile only feed rows it redoes afterwards)
                 if (ms == RMT_OK && S->split_proj)
                     ms = projection_rows(ctx, S->us, S->vs, P.dx, P.dy, dtp, dt, P.rho_f, S->p,
-                                         nullptr);
+                                         nullptr, nullptr, nullptr, 0,
+                                         ctx->opt.skip_marked_rows ? S->rowmark : nullptr);
                 // and the row blocks no fix-up row falls in, transposed for the column pass
                 if (ms == RMT_OK && S->split_proj && early_t_env) {
                     ms = dct_transpose_unmarked(ctx, ctx->scratch + n, S->rowmark);

@@ -35,6 +35,8 @@ environment variables still set a new context's defaults.
                         instead of beside it on a stream of their own
   sl_phi=0              phi, the known-plane words and the fluid flags from k_phi_rebuild_fluid
                         after the side stream's SL pass instead of from that pass itself
+  skip_marked_rows=0    the speculative row DCT also transforms the rows the fix-up transforms
+                        again afterwards
 """
 import os
 import subprocess
@@ -85,7 +87,7 @@ def _same(got, ref):
     {"merged_join": 0}, {"test_delay_side": 300}, {"test_delay_main": 300},
     {"test_delay_side": 300, "fix_all": 1}, {"fix_all": 1}, {"fix_all": 1, "sim_hiprio": 0},
     {"edge_stream": 0}, {"sl_phi": 0}, {"sl_phi": 0, "fused_fluid": 0},
-    {"edge_stream": 0, "sl_phi": 0, "test_delay_side": 300},
+    {"edge_stream": 0, "sl_phi": 0, "test_delay_side": 300}, {"skip_marked_rows": 0},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(default_run, opts):
     _same(_run(opts), default_run)
