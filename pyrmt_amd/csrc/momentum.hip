@@ -870,7 +870,7 @@ static int stage_edge_tiles(rmt_ctx *ctx, RowWin ws, int ntiles, int tiles_x, co
 
 // The edge-tile stream of the full-grid stages (opt.edge_stream; nullptr: off, or no stream of
 // the context's own to pair with), created at the priority of the stream it serves.
-static int edge_stream(rmt_ctx *ctx, hipStream_t *out) {
+int edge_stream(rmt_ctx *ctx, hipStream_t *out) {
     *out = nullptr;
     if (!ctx->opt.edge_stream || !ctx->stream) return RMT_OK;
     int prio = 0;
@@ -1041,6 +1041,9 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
                             es ? ctx->edge_ev[0] : nullptr, (const unsigned char *)fluid_rows,
                             tiles_x, w0.lo, w0.hi, fluid_rows + nw));
     }
+    // the stages read p: a pressure update running on another stream (sim.hip's tail on the
+    // edge-tile stream) joins here, after the prep
+    if (W.wait_p) RMT_HIP(hipStreamWaitEvent(ctx->stream, W.wait_p, 0));
     for (int s = 0; s < 4 && !unfused; ++s) {
         const RowWin ws = grow(2 * (3 - s));
         const int ntiles = tiles_x * ((ws.je - ws.jb + MS_TY - 1) / MS_TY);

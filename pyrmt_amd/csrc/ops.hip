@@ -39,6 +39,8 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"sl_phi", "RMT_SL_PHI", &rmt_opts::sl_phi},
     {"mac_boxes", "RMT_MAC_BOXES", &rmt_opts::mac_boxes},
     {"skip_marked_rows", "RMT_SKIP_MARKED_ROWS", &rmt_opts::skip_marked_rows},
+    {"tail_stream", "RMT_TAIL_STREAM", &rmt_opts::tail_stream},
+    {"diag_first", "RMT_DIAG_FIRST", &rmt_opts::diag_first},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;

@@ -103,6 +103,8 @@ struct rmt_opts {
     int mac_boxes = 1;        // RMT_MAC_BOXES: config 5's per-disc passes on the map's support box
     int skip_marked_rows = 1; // RMT_SKIP_MARKED_ROWS: the speculative row DCT leaves out the rows
                               // the fix-up transforms again
+    int tail_stream = 1;      // RMT_TAIL_STREAM: the pressure update beside the SL and prep
+    int diag_first = 0;       // RMT_DIAG_FIRST: the step's diagnostics ahead of the next geometry
 };
 
 #ifndef RMT_EDGE_SLOTS
@@ -662,6 +664,8 @@ struct MomWork {                 // MOM_WORK_PLANES planes + solid byte plane + 
     bool fluid_rows_ready = false;
     // or k_sim_sl_t left per-(row, tile) bits there (its phi output; k_fluid_rows_bits)
     const unsigned char *fluid_bits = nullptr;
+    // (nullable) an event the stages wait for before they read p (sim.hip's tail_stream)
+    hipEvent_t wait_p = nullptr;
     // per 64-column row segment (nx % 64 == 0), persistent across steps: the last write of the
     // prep planes there was a pure-fluid segment's constants, so k_mom_prep may skip it while
     // it stays pure fluid (null: prep every cell)
@@ -671,7 +675,7 @@ inline MomWork mom_work(double *w, long n, unsigned char *solid, int *flag) {
     return MomWork{w,          w + n,      w + 2 * n,  w + 3 * n,  w + 4 * n,  w + 5 * n,
                    w + 6 * n,  w + 7 * n,  w + 8 * n,  w + 9 * n,  w + 10 * n, w + 11 * n,
                    w + 12 * n, w + 13 * n, w + 14 * n, w + 15 * n, w + 16 * n, solid, flag,
-                   nullptr, false, nullptr};
+                   nullptr, false, nullptr, nullptr};
 }
 // where momentum_rk4 keeps the per-(row, 64-column tile) pure-fluid flags of rows [lo, ...)
 inline unsigned char *fluid_rows_buf(const MomWork &W, int lo, int nx) {
@@ -692,6 +696,9 @@ int momentum_rk4(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, co
 // a speculative momentum_rk4 whose inputs changed only inside them (sim.hip overlap)
 constexpr int MOM_TX = 64, MOM_TY = 16;
 int momentum_mode();   // rmt_momentum_set_mode / RMT_MOM_MODE
+// the context's edge-tile stream at ctx->stream's priority (nullptr: opt.edge_stream off or no
+// stream of the context's own)
+int edge_stream(rmt_ctx *ctx, hipStream_t *out);
 // skip_prep: the caller ran fixup_phi_prep on the same tiles
 int momentum_fixup(rmt_ctx *ctx, const rmt_momentum_params *P, const double *u, const double *v,
                    const double *p, const double *X1, const double *X2, const double *phi,

@@ -73,6 +73,7 @@ struct rmt_sim {
     unsigned long long *rimw = nullptr;
     int *rimcnt = nullptr;
     hipEvent_t e_bits = nullptr, e_proj = nullptr, e_tail = nullptr, e_kb = nullptr, e_geo = nullptr;
+    hipEvent_t e_tailp = nullptr;   // the pressure update done (tail_stream)
     // the next step's known plane, written by the phi kernels of this step (nx % 64 == 0):
     // double-buffered with kbits, valid from the second step of a call on
     unsigned long long *kbits_next = nullptr;
@@ -785,6 +786,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
         RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_proj, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_tail, hipEventDisableTiming));
+        RMT_HIP(hipEventCreateWithFlags(&S->e_tailp, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_kb, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_geo, hipEventDisableTiming));
     }
@@ -809,6 +811,7 @@ int rmt_sim_destroy(rmt_sim *S) {
     if (S->e_bits) (void)hipEventDestroy(S->e_bits);
     if (S->e_proj) (void)hipEventDestroy(S->e_proj);
     if (S->e_tail) (void)hipEventDestroy(S->e_tail);
+    if (S->e_tailp) (void)hipEventDestroy(S->e_tailp);
     if (S->e_kb) (void)hipEventDestroy(S->e_kb);
     if (S->e_geo) (void)hipEventDestroy(S->e_geo);
     if (S->st2) (void)hipStreamDestroy(S->st2);
@@ -905,6 +908,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     // Deferred to the second stream's next start (the next chain's launch), so that it does
     // not crowd the next step's rim advection and record values either.
     bool tail = false, pending = false;
+    bool tail_p = false;   // the pending tail's pressure update ran on the edge-tile stream
     double *pend_e = nullptr;
     // the pending tail's diagnostics already ran (on the second stream after the next step's
     // geometry, beside the projection: they read phi and J only, final after the fix-up)
@@ -922,12 +926,29 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             RMT_HIP(hipStreamWaitEvent(S->st2, S->e_proj, 0));
         }
         ctx->stream = S->st2;
+        // beside the chain (after_sl), the pressure update runs on the edge-tile stream,
+        // beside the second stream's SL and prep; that stream's momentum stages wait for it
+        // (tail_p, MomWork::wait_p) before they read p, and nothing else of the step touches
+        // p, pc or the root before then (RMT_TAIL_STREAM)
+        hipStream_t ts_st = S->st2;
+        if (after_sl && ctx->opt.tail_stream) {
+            hipStream_t es = nullptr;
+            const int e = edge_stream(ctx, &es);
+            if (e != RMT_OK) { ctx->stream = st; return e; }
+            if (es) {
+                RMT_HIP(hipStreamWaitEvent(es, S->e_sl, 0));
+                ts_st = es;
+            }
+        }
+        ctx->stream = ts_st;
         // (the pending tail always follows a projection_finish that deferred the pressure
         // update: pc and its mean's root are still where that projection left them)
         const int ts = sub_mean_rows_upd(ctx, S->p, ctx->scratch + (long)ny * nx,
                                          ctx->red + RED_BLOCKS + 17, ny, nx);
         ctx->stream = st;
         RMT_TRY(ts);
+        tail_p = ts_st != S->st2;
+        if (tail_p) RMT_HIP(hipEventRecord(S->e_tailp, ts_st));
         if (!pend_diag_done) {
             k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
             k_diag_p2<<<1, DIAG_T, 0, S->st2>>>(S->dscr, pend_e);
@@ -940,7 +961,9 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     auto join = [&]() -> int {
         RMT_TRY(emit_tail(false));
         if (tail) RMT_HIP(hipStreamWaitEvent(st, S->e_tail, 0));
+        if (tail && tail_p) RMT_HIP(hipStreamWaitEvent(st, S->e_tailp, 0));
         tail = false;
+        tail_p = false;
         return RMT_OK;
     };
     // the last step's ring record, completed by the next step's k_dt_part (or here)
@@ -1139,6 +1162,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     RMT_LAUNCHED();
                 }
                 MomWork Wf = W;
+                if (tail_p) Wf.wait_p = S->e_tailp;   // (emit_tail above: p on another stream)
                 const bool fl_ok = fluid_env && P.shape == RMT_SHAPE_DISC && nx % 64 == 0 &&
                                    MOM_TX == 64;
                 // the SL pass also leaves phi, the known-plane words and per-tile fluid bits
@@ -1235,6 +1259,21 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 hipStream_t sg = S->st2;
                 if (!fixprep) RMT_HIP(hipEventRecord(S->e_kb, st));   // (else: with the prep)
                 RMT_HIP(hipStreamWaitEvent(sg, S->e_kb, 0));
+                // this step's diagnostics (phi, J: final after the fix-up prep) on the second
+                // stream, beside the projection, instead of in the tail beside the next chain;
+                // they land in the ring slot this step's record takes below.  diag_first: ahead
+                // of the geometry, beside the latency-bound fix-up stages (behind it they
+                // overlapped the projection's DCT passes)
+                const bool early_diag = side_tail && S->split_proj && !P.energies;
+                auto diag_now = [&]() {
+                    DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1n, S->X2n, ny, nx,
+                               P.energies, P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s,
+                               P.mu_s, P.kappa, 0, ny};
+                    k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, sg>>>(D, S->dscr);
+                    k_diag_p2<<<1, DIAG_T, 0, sg>>>(S->dscr, S->ring + (size_t)slot * RING_VALS);
+                    diag_early = true;
+                };
+                if (early_diag && ctx->opt.diag_first) { diag_now(); RMT_LAUNCHED(); }
                 const long nseg = (long)ny * ((nx + 255) / 256);
                 int *scount = S->segs + nseg;
                 ctx->stream = sg;
@@ -1251,18 +1290,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 RMT_TRY(gs);
                 RMT_HIP(hipEventRecord(S->e_geo, sg));
                 geo_ready = true;
-                if (side_tail && S->split_proj && !P.energies) {
-                    // this step's diagnostics (phi, J: final after the fix-up prep) behind the
-                    // geometry, beside the projection, instead of in the tail beside the next
-                    // chain; they land in the ring slot this step's record takes below
-                    DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1n, S->X2n, ny, nx,
-                               P.energies, P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s,
-                               P.mu_s, P.kappa, 0, ny};
-                    k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, sg>>>(D, S->dscr);
-                    k_diag_p2<<<1, DIAG_T, 0, sg>>>(S->dscr, S->ring + (size_t)slot * RING_VALS);
-                    RMT_LAUNCHED();
-                    diag_early = true;
-                }
+                if (early_diag && !ctx->opt.diag_first) { diag_now(); RMT_LAUNCHED(); }
             }
             RMT_TRY(momentum_fixup(ctx, &M, S->u, S->v, S->p, S->X1n, S->X2n, S->phi, S->us, S->vs,
                                    S->sxx, S->sxy, S->syy, S->J, W, S->tiles, S->tcount,

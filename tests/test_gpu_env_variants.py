@@ -37,6 +37,10 @@ environment variables still set a new context's defaults.
                         after the side stream's SL pass instead of from that pass itself
   skip_marked_rows=0    the speculative row DCT also transforms the rows the fix-up transforms
                         again afterwards
+  tail_stream=0         the pressure update (p + (pc - m), p -= mean p) on the second stream
+                        ahead of its SL pass instead of beside it on the edge-tile stream
+  diag_first=1          the step's diagnostics ahead of the next step's geometry instead of
+                        behind it
 """
 import os
 import subprocess
@@ -88,6 +92,7 @@ def _same(got, ref):
     {"test_delay_side": 300, "fix_all": 1}, {"fix_all": 1}, {"fix_all": 1, "sim_hiprio": 0},
     {"edge_stream": 0}, {"sl_phi": 0}, {"sl_phi": 0, "fused_fluid": 0},
     {"edge_stream": 0, "sl_phi": 0, "test_delay_side": 300}, {"skip_marked_rows": 0},
+    {"tail_stream": 0}, {"tail_stream": 1, "test_delay_side": 300}, {"diag_first": 1},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(default_run, opts):
     _same(_run(opts), default_run)
