@@ -135,6 +135,63 @@ __global__ void __launch_bounds__(256) k_ex_dilate(const u64 *__restrict__ kbits
 // the window sums keep the reference's order (raster within the clipped 9x9 window).
 // Rows [jb, je) only (the MAC slabs split the candidates by rows; the known plane is whole).
 // Each lane builds the candidate mask of one word, the wave then walks the candidate words.
+// the no-op test's fit of candidate (j, i) against the original known set: true if accepted
+// (the window sums in the reference's order; t: this wave's 6 x 96 LDS rows)
+__device__ __forceinline__ bool ex_none_fit(const u64 *__restrict__ kbits, int ny, int nx, int W,
+                                            double dx, double dy, double r2, const u64 *tab,
+                                            double (*t)[96], int lane, int j, int i) {
+    auto K = [&](int jj, int w) -> u64 {
+        return (jj < 0 || jj >= ny || w < 0 || w >= W) ? 0 : kbits[(long)jj * W + w];
+    };
+    const double x0 = dx * i, y0 = dy * j;
+    int inc_n = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
+        bool inc = false;
+        double xi = 0.0, yi = 0.0, w = 0.0;
+        if (q < EX_WIN && jj >= 0 && jj < ny && ii >= 0 && ii < nx &&
+            ((K(jj, ii >> 6) >> (ii & 63)) & 1)) {
+            xi = dx * ii; yi = dy * jj;
+            const double ax = xi - x0, ay = yi - y0, d2 = ax * ax + ay * ay;
+            if (d2 <= r2) { inc = true; w = exp_glibc_tab(-d2 / r2, tab); }
+        }
+        inc_n += __popcll(__ballot(inc));
+        if (q < 96) {
+            const double wa0 = w * 1.0, wa1 = w * xi, wa2 = w * yi;
+            t[0][q] = inc ? wa0 * 1.0 : 0.0;  t[1][q] = inc ? wa0 * xi : 0.0;
+            t[2][q] = inc ? wa0 * yi : 0.0;   t[3][q] = inc ? wa1 * xi : 0.0;
+            t[4][q] = inc ? wa1 * yi : 0.0;   t[5][q] = inc ? wa2 * yi : 0.0;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    double acc = 0.0;
+    if (lane < 6)
+        for (int q = 0; q < EX_WIN; ++q) acc += t[lane][q];
+    __builtin_amdgcn_wave_barrier();
+    const double A00 = __shfl(acc, 0), A01 = __shfl(acc, 1), A02 = __shfl(acc, 2);
+    const double A11 = __shfl(acc, 3), A12 = __shfl(acc, 4), A22 = __shfl(acc, 5);
+    const double M[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
+    const double det = (M[0] * (M[4] * M[8] - M[5] * M[7])
+                      - M[1] * (M[3] * M[8] - M[5] * M[6])
+                      + M[2] * (M[3] * M[7] - M[4] * M[6]));
+    return inc_n >= 3 && fabs(det) > 1e-10;
+}
+// candidate mask of word w0 of row j: unknown interior cells with a known 8-neighbour
+__device__ __forceinline__ u64 ex_none_cands(const u64 *__restrict__ kbits, int ny, int nx, int W,
+                                             int j, int w0) {
+    auto K = [&](int jj, int w) -> u64 {
+        return (jj < 0 || jj >= ny || w < 0 || w >= W) ? 0 : kbits[(long)jj * W + w];
+    };
+    u64 d = 0;
+    for (int jj = j - 1; jj <= j + 1; ++jj) {
+        const u64 a = K(jj, w0 - 1), b = K(jj, w0), e = K(jj, w0 + 1);
+        d |= b | (b << 1) | (a >> 63) | (b >> 1) | (e << 63);
+    }
+    const int i0 = 64 * w0, lo = max(1, i0) - i0, hi = min(nx - 2, i0 + 63) - i0;
+    return hi >= lo ? d & ~K(j, w0) & (~0ull >> (63 - hi)) & (~0ull << lo) : 0;
+}
 __global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, int ny, int nx,
                                                  int W, double dx, double dy, double r2,
                                                  int *__restrict__ ctl, int jb, int je) {
@@ -143,29 +200,14 @@ __global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, 
     for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    double (*t)[96] = tb[wv];
-    auto K = [&](int jj, int w) -> u64 {
-        return (jj < 0 || jj >= ny || w < 0 || w >= W) ? 0 : kbits[(long)jj * W + w];
-    };
     // a wave per row, rows strided over the grid (a grid smaller than the rows stops every
     // wave soon after the first fit is found)
     for (int j = jb + blockIdx.x * 4 + wv; j < je && j <= ny - 2; j += gridDim.x * 4) {
     if (j < 1) continue;
     for (int wb = 0; wb < W; wb += 64) {
         if (__hip_atomic_load(ctl + EXC_ANY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-        u64 mine = 0;
-        {
-            const int w0 = wb + lane;
-            if (w0 < W) {
-                u64 d = 0;
-                for (int jj = j - 1; jj <= j + 1; ++jj) {
-                    const u64 a = K(jj, w0 - 1), b = K(jj, w0), e = K(jj, w0 + 1);
-                    d |= b | (b << 1) | (a >> 63) | (b >> 1) | (e << 63);
-                }
-                const int i0 = 64 * w0, lo = max(1, i0) - i0, hi = min(nx - 2, i0 + 63) - i0;
-                if (hi >= lo) mine = d & ~K(j, w0) & (~0ull >> (63 - hi)) & (~0ull << lo);
-            }
-        }
+        const int w0 = wb + lane;
+        const u64 mine = w0 < W ? ex_none_cands(kbits, ny, nx, W, j, w0) : 0;
         u64 words = __ballot(mine != 0);
         while (words) {
             const int l = __builtin_ctzll(words);
@@ -175,46 +217,75 @@ __global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, 
             while (cand) {
                 const int i = i0 + __builtin_ctzll(cand);
                 cand &= cand - 1;
-                const double x0 = dx * i, y0 = dy * j;
-                int inc_n = 0;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int q = lane + 64 * h, jj = j - 4 + q / 9, ii = i - 4 + q % 9;
-                    bool inc = false;
-                    double xi = 0.0, yi = 0.0, w = 0.0;
-                    if (q < EX_WIN && jj >= 0 && jj < ny && ii >= 0 && ii < nx &&
-                        ((K(jj, ii >> 6) >> (ii & 63)) & 1)) {
-                        xi = dx * ii; yi = dy * jj;
-                        const double ax = xi - x0, ay = yi - y0, d2 = ax * ax + ay * ay;
-                        if (d2 <= r2) { inc = true; w = exp_glibc_tab(-d2 / r2, tab); }
-                    }
-                    inc_n += __popcll(__ballot(inc));
-                    if (q < 96) {
-                        const double wa0 = w * 1.0, wa1 = w * xi, wa2 = w * yi;
-                        t[0][q] = inc ? wa0 * 1.0 : 0.0;  t[1][q] = inc ? wa0 * xi : 0.0;
-                        t[2][q] = inc ? wa0 * yi : 0.0;   t[3][q] = inc ? wa1 * xi : 0.0;
-                        t[4][q] = inc ? wa1 * yi : 0.0;   t[5][q] = inc ? wa2 * yi : 0.0;
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                double acc = 0.0;
-                if (lane < 6)
-                    for (int q = 0; q < EX_WIN; ++q) acc += t[lane][q];
-                __builtin_amdgcn_wave_barrier();
-                const double A00 = __shfl(acc, 0), A01 = __shfl(acc, 1), A02 = __shfl(acc, 2);
-                const double A11 = __shfl(acc, 3), A12 = __shfl(acc, 4), A22 = __shfl(acc, 5);
-                const double M[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
-                const double det = (M[0] * (M[4] * M[8] - M[5] * M[7])
-                                  - M[1] * (M[3] * M[8] - M[5] * M[6])
-                                  + M[2] * (M[3] * M[7] - M[4] * M[6]));
-                if (inc_n >= 3 && fabs(det) > 1e-10) {
+                if (ex_none_fit(kbits, ny, nx, W, dx, dy, r2, tab, tb[wv], lane, j, i)) {
                     if (lane == 0) atomicOr(ctl + EXC_ANY, 1);
                     return;
                 }
             }
         }
     }
+    }
+}
+// The same test with a fit per wave instead of a row per wave (mac.hip, where no candidate is
+// accepted as often as not and the disc's top / bottom rows hold long candidate runs):
+// k_ex_cand lists the candidates of rows [jb, je) (a thread per word), k_ex_none_list fits
+// them.  Over capacity (cnt > cap), k_ex_none_list runs the row walk above instead.
+__global__ void __launch_bounds__(256) k_ex_cand(const u64 *__restrict__ kbits, int ny, int nx,
+                                                 int W, int jb, int je, int *__restrict__ list,
+                                                 int cap, int *__restrict__ cnt) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    const int j = jb + (int)(t / W), w0 = (int)(t % W);
+    if (j >= je || j < 1 || j > ny - 2) return;
+    u64 m = ex_none_cands(kbits, ny, nx, W, j, w0);
+    if (!m) return;
+    int p = atomicAdd(cnt, __popcll(m));
+    for (; m && p < cap; m &= m - 1, ++p) list[p] = j * nx + 64 * w0 + __builtin_ctzll(m);
+}
+__global__ void __launch_bounds__(256) k_ex_none_list(const u64 *__restrict__ kbits, int ny,
+                                                      int nx, int W, double dx, double dy,
+                                                      double r2, int *__restrict__ ctl, int jb,
+                                                      int je, const int *__restrict__ list,
+                                                      int cap, const int *__restrict__ cnt) {
+    __shared__ double tb[4][6][96];
+    __shared__ u64 tab[256];
+    for (int s = threadIdx.x; s < 256; s += blockDim.x) tab[s] = kExpTab[s];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int n = *cnt;
+    if (n > cap) {   // (the list overflowed: the row walk of k_ex_none)
+        for (int j = jb + blockIdx.x * 4 + wv; j < je && j <= ny - 2; j += gridDim.x * 4) {
+            if (j < 1) continue;
+            for (int wb = 0; wb < W; wb += 64) {
+                if (__hip_atomic_load(ctl + EXC_ANY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    return;
+                const int w0 = wb + lane;
+                const u64 mine = w0 < W ? ex_none_cands(kbits, ny, nx, W, j, w0) : 0;
+                u64 words = __ballot(mine != 0);
+                while (words) {
+                    const int l = __builtin_ctzll(words);
+                    words &= words - 1;
+                    u64 cand = __shfl(mine, l);
+                    const int i0 = 64 * (wb + l);
+                    while (cand) {
+                        const int i = i0 + __builtin_ctzll(cand);
+                        cand &= cand - 1;
+                        if (ex_none_fit(kbits, ny, nx, W, dx, dy, r2, tab, tb[wv], lane, j, i)) {
+                            if (lane == 0) atomicOr(ctl + EXC_ANY, 1);
+                            return;
+                        }
+                    }
+                }
+            }
+        }
+        return;
+    }
+    for (int q = blockIdx.x * 4 + wv; q < n; q += gridDim.x * 4) {
+        if (__hip_atomic_load(ctl + EXC_ANY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        const int c = list[q], j = c / nx, i = c - j * nx;
+        if (ex_none_fit(kbits, ny, nx, W, dx, dy, r2, tab, tb[wv], lane, j, i)) {
+            if (lane == 0) atomicOr(ctl + EXC_ANY, 1);
+            return;
+        }
     }
 }
 __global__ void k_ex_none_fin(int *ctl) {
@@ -756,11 +827,37 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
         const double r = 4 * std::sqrt(dx * dx + dy * dy);
         // 64 workgroups: the disc's first rim rows end the search (this runs beside the
         // critical path when sim.hip prepares the next step's geometry early)
-        k_ex_none<<<ctx->ex_none_wide ? grid1d(ny, 4) : std::min<unsigned>(grid1d(ny, 4), 64),
-                    256, 0, ctx->stream>>>(
-            ws.kbits, ny, nx, W, dx, dy, r * r, ws.ctl, 0, ny);
+        int jb = 0, je = ny;
+        if (ctx->ex_none_rows[1] > ctx->ex_none_rows[0]) {
+            jb = std::max(0, ctx->ex_none_rows[0]);
+            je = std::min(ny, ctx->ex_none_rows[1]);
+        }
+        if (ctx->ex_none_wide && ctx->ex_cand && je > jb) {
+            int *cnt = ctx->ex_cand + ctx->ex_cand_cap;
+            RMT_HIP(hipMemsetAsync(cnt, 0, sizeof(int), ctx->stream));
+            k_ex_cand<<<grid1d((long)(je - jb) * W, 256), 256, 0, ctx->stream>>>(
+                ws.kbits, ny, nx, W, jb, je, ctx->ex_cand, ctx->ex_cand_cap, cnt);
+            k_ex_none_list<<<1024, 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, dx, dy, r * r,
+                                                           ws.ctl, jb, je, ctx->ex_cand,
+                                                           ctx->ex_cand_cap, cnt);
+        } else {
+            k_ex_none<<<ctx->ex_none_wide ? grid1d(std::max(je - jb, 1), 4)
+                                          : std::min<unsigned>(grid1d(ny, 4), 64),
+                        256, 0, ctx->stream>>>(
+                ws.kbits, ny, nx, W, dx, dy, r * r, ws.ctl, jb, je);
+        }
         k_ex_none_fin<<<1, 1, 0, ctx->stream>>>(ws.ctl);
         RMT_LAUNCHED();
+        if (ctx->ex_none_host && force == 0) {
+            // the verdict on the host: with no acceptable target every later pass of the call
+            // exits at once on the device, so none is launched (extrap_finish: the status words
+            // the identity leaves, both zero)
+            int any = 1;
+            RMT_HIP(hipMemcpyAsync(&any, ws.ctl + EXC_ANY, sizeof(int), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+            RMT_HIP(hipStreamSynchronize(ctx->stream));
+            if (!any) { ctx->ex_noop_skip = true; return RMT_OK; }
+        }
         if (par) {
             RMT_TRY(extrap_chain_prep_px(ctx, ws, dx, dy, max_layers));
             RMT_TRY(extrap_par_geometry(ctx, ws, dx, dy, max_layers));
@@ -785,6 +882,12 @@ int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1
     const ExWs ws = extrap_layout(ctx->bytes, ny, nx, max_layers, nullptr, par,
                                   ctx->opt.ex_arena_bump);
     const int force = g_ex_mode;
+    if (ctx->ex_noop_skip) {   // (extrap_geometry: nothing to fit, the map is left as it is)
+        ctx->ex_noop_skip = false;
+        if (dev_status) RMT_HIP(hipMemsetAsync(dev_status, 0, 2 * sizeof(int), ctx->stream));
+        if (ctx->ev_chain) RMT_HIP(hipEventRecord(ctx->ev_chain, ctx->stream));
+        return RMT_OK;
+    }
     const bool chain = ctx->ex_chain && !par;
     const int *ctl = ctx->ex_chain ? ws.ctl : nullptr;
     if (chain) RMT_TRY(extrap_chain_values(ctx, ws, X1o, X2o, dx, dy, max_layers));

@@ -621,6 +621,7 @@ struct rmt_mac_sim {
     rmt_ctx *ctx = nullptr;
     rmt_mac_params P{};
     void *block = nullptr;
+    int *cand = nullptr;   // the no-op test's candidate list (CAND_CAP cells + counter)
     double *u, *v, *p, *us, *vs, *uc, *vc, *X1n, *X2n, *phi_pre, *Sxx, *Sxy, *Syy;
     double *X1[RMT_MAC_MAXD], *X2[RMT_MAC_MAXD], *phi[RMT_MAC_MAXD];
     double *xs, *ys, *part, *out;
@@ -702,6 +703,10 @@ int rmt_mac_contact_stress(rmt_ctx *ctx, const double *phi_a, const double *phi_
                            double Gsum, double eps, double dx, double dy, double *txx,
                            double *txy, double *tyy);
 
+// candidate capacity of the no-op test's list: 32 cells per grid row (a disc's rim holds
+// about 4 per row it spans; beyond the capacity k_ex_none_list walks the rows instead)
+static int mac_cand_cap(int N) { return 32 * N; }
+
 int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **out) {
     RMT_CHECK(ctx && prm && out, RMT_EINVAL, "null argument");
     RMT_CHECK(prm->n_discs >= 1 && prm->n_discs <= RMT_MAC_MAXD, RMT_EINVAL, "1..8 discs");
@@ -744,6 +749,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     RMT_HIP(hipMemcpyAsync(S->xs, g.data(), N * 8, hipMemcpyHostToDevice, ctx->stream));
     RMT_HIP(hipMemcpyAsync(S->ys, g.data(), N * 8, hipMemcpyHostToDevice, ctx->stream));
     RMT_TRY(ensure_bytes(ctx, extrap_workspace(N, N, prm->layers)));
+    RMT_HIP(hipMalloc(&S->cand, (mac_cand_cap(N) + 1) * sizeof(int)));
     RMT_HIP(hipStreamSynchronize(ctx->stream));
     *out = S;
     return RMT_OK;
@@ -752,6 +758,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
 int rmt_mac_sim_destroy(rmt_mac_sim *S) {
     if (!S) return RMT_OK;
     (void)hipFree(S->block);
+    (void)hipFree(S->cand);
     delete S;
     return RMT_OK;
 }
@@ -841,9 +848,21 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
             // the known plane from the advection pass (its k_ex_bits pass over phi_pre saved);
             // the no-op test over every row at once (a disc with nothing to fit scans them all)
             ctx->ex_none_wide = true;
+            // box mode: the known cells lie in rows [cb0, cb1) (kbits cleared elsewhere), so a
+            // candidate -- an unknown 8-neighbour of a known cell -- in [cb0 - 1, cb1 + 1)
+            if (box_mode) {
+                ctx->ex_none_rows[0] = std::max(0, cb[0] - 1);
+                ctx->ex_none_rows[1] = cb[1] > cb[0] ? std::min(N, cb[1] + 1) : 1;
+                if (cb[1] <= cb[0]) ctx->ex_none_rows[0] = 0;   // (empty map: one row, no candidate)
+            }
+            ctx->ex_cand = S->cand; ctx->ex_cand_cap = mac_cand_cap(N);
+            ctx->ex_none_host = ctx->opt.mac_noop_host != 0;
             const int es = extrapolate(ctx, S->X1n, S->X2n, S->phi_pre, dx, dx, P.layers, S->X1n,
                                        S->X2n, S->flags + 2, S->kbits);
             ctx->ex_none_wide = false;
+            ctx->ex_none_rows[0] = ctx->ex_none_rows[1] = 0;
+            ctx->ex_cand = nullptr; ctx->ex_cand_cap = 0;
+            ctx->ex_none_host = false;
             RMT_TRY(es);
             if (!box_mode)
                 k_mac_phi<<<grid1d(n, 256), 256, 0, st>>>(S->X1n, S->X2n, n, P.cx[k], P.cy[k],

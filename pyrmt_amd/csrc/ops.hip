@@ -41,6 +41,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"skip_marked_rows", "RMT_SKIP_MARKED_ROWS", &rmt_opts::skip_marked_rows},
     {"tail_stream", "RMT_TAIL_STREAM", &rmt_opts::tail_stream},
     {"diag_first", "RMT_DIAG_FIRST", &rmt_opts::diag_first},
+    {"mac_noop_host", "RMT_MAC_NOOP_HOST", &rmt_opts::mac_noop_host},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;

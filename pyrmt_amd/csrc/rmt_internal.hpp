@@ -105,6 +105,7 @@ struct rmt_opts {
                               // the fix-up transforms again
     int tail_stream = 1;      // RMT_TAIL_STREAM: the pressure update beside the SL and prep
     int diag_first = 0;       // RMT_DIAG_FIRST: the step's diagnostics ahead of the next geometry
+    int mac_noop_host = 1;    // RMT_MAC_NOOP_HOST: MAC extrapolation's no-op verdict read on the host
 };
 
 #ifndef RMT_EDGE_SLOTS
@@ -145,6 +146,16 @@ struct rmt_ctx {
     // optional (mac.hip: the extrapolation on the critical stream, where the no-op test finds
     // nothing to fit as often as not): k_ex_none on a wave per row instead of 64 workgroups
     bool ex_none_wide = false;
+    // optional (mac.hip box mode): the rows [ex_none_rows[0], ex_none_rows[1]) hold every
+    // candidate target (the known plane is zero outside them); je <= jb: every row
+    int ex_none_rows[2] = {0, 0};
+    // optional (mac.hip): a candidate list of ex_cand_cap cells + its counter, for the
+    // no-op test's fit-per-wave form (k_ex_cand / k_ex_none_list) under ex_none_wide
+    int *ex_cand = nullptr;
+    int ex_cand_cap = 0;
+    // optional (mac.hip): read the no-op test's verdict back on the host, and when no target
+    // can be accepted skip the rest of the call's launches (the identity: ex_noop_skip)
+    bool ex_none_host = false, ex_noop_skip = false;
     // momentum.hip: the stage tiles a full launch's interior kernel skips, per row window
     struct EdgeTiles { int *list = nullptr; int n = 0; long key[6] = {}; };
     EdgeTiles edge[RMT_EDGE_SLOTS];

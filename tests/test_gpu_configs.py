@@ -205,6 +205,28 @@ def test_config5_mac_N8192_vs_oracle_fixture(gpu):
     np.testing.assert_allclose(got, gd, rtol=1e-12)     # achieved
 
 
+def test_config5_noop_verdict_on_host_is_bit_identical(gpu):
+    """N=8192, 3 discs: no first-layer fit is acceptable (det ~ 1e-14), so every extrapolation
+    call is the identity.  The default reads k_ex_none's verdict back and launches nothing
+    more (mac_noop_host); with it off every pass is launched and exits on the device flag.
+    Both must give the same bits over 3 steps."""
+    import gc
+    from pyrmt_amd.mac import MacMultiDisc
+    out = []
+    for host in (1, 0):
+        sim = MacMultiDisc(8192, n_discs=3, seed=3, options={"mac_noop_host": host})
+        sim.step(3)
+        d = sim.diagnostics()
+        out.append((d, {f"{n}{k}": _sha(sim.get(n, k)) for n in ("X1", "X2", "phi")
+                        for k in range(3)} | {n: _sha(sim.get(n)) for n in ("u", "v", "p")}))
+        del sim
+        gc.collect()
+    (d0, f0), (d1, f1) = out
+    assert f0 == f1
+    for k in d0:
+        np.testing.assert_array_equal(d0[k], d1[k], err_msg=k)
+
+
 def _diag100(sim):
     d = sim.diagnostics()
     return np.stack([d[k] for k in ("t", "dt", "cx", "cy", "minJ", "maxJ")], axis=1)

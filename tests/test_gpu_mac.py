@@ -100,21 +100,24 @@ def test_mac_multi_disc_trace(M):
 def test_mac_box_mode_is_bit_identical(M, N, calls):
     """The per-disc passes on each map's support box (mac_boxes, default on) against the
     full-grid passes: every field and diagnostic bit for bit, over several calls (each call
-    starts from a full pass; the boxes then come back with the per-step diagnostics)."""
+    starts from a full pass; the boxes then come back with the per-step diagnostics).  Also
+    the no-op verdict kept on the device (mac_noop_host = 0: every extrapolation pass launched
+    and exiting on the device flag) against the default host read-back."""
     out = []
-    for boxes in (0, 1):
-        sim = M.MacMultiDisc(N, n_discs=3, seed=3, options={"mac_boxes": boxes})
+    for opts in ({"mac_boxes": 0}, {"mac_boxes": 1}, {"mac_boxes": 1, "mac_noop_host": 0}):
+        sim = M.MacMultiDisc(N, n_discs=3, seed=3, options=opts)
         for c in calls:
             sim.step(c)
         d = sim.diagnostics()
         f = {f"{n}{k}": sim.get(n, k) for n in ("X1", "X2", "phi") for k in range(3)}
         f.update({n: sim.get(n) for n in ("u", "v", "p")})
         out.append((d, f))
-    (d0, f0), (d1, f1) = out
-    for k in d0:
-        np.testing.assert_array_equal(d1[k], d0[k], err_msg=k)
-    for k in f0:
-        np.testing.assert_array_equal(f1[k], f0[k], err_msg=k)
+    d0, f0 = out[0]
+    for d1, f1 in out[1:]:
+        for k in d0:
+            np.testing.assert_array_equal(d1[k], d0[k], err_msg=k)
+        for k in f0:
+            np.testing.assert_array_equal(f1[k], f0[k], err_msg=k)
 
 
 def test_mac_sim_stops_on_divergence(M):
