@@ -234,11 +234,21 @@ __global__ void __launch_bounds__(256) k_ex_cand(const u64 *__restrict__ kbits, 
                                                  int W, int jb, int je, int *__restrict__ list,
                                                  int cap, int *__restrict__ cnt) {
     const long t = (long)blockIdx.x * 256 + threadIdx.x;
-    const int j = jb + (int)(t / W), w0 = (int)(t % W);
-    if (j >= je || j < 1 || j > ny - 2) return;
-    u64 m = ex_none_cands(kbits, ny, nx, W, j, w0);
-    if (!m) return;
-    int p = atomicAdd(cnt, __popcll(m));
+    const int j = jb + (int)(t / W), w0 = (int)(t % W), lane = threadIdx.x & 63;
+    u64 m = (j < je && j >= 1 && j <= ny - 2) ? ex_none_cands(kbits, ny, nx, W, j, w0) : 0;
+    // one counter update per wave (a single counter: per-word atomics serialise)
+    const int c = __popcll(m);
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const int tot = __shfl(incl, 63);
+    if (!tot) return;
+    int base = 0;
+    if (lane == 63) base = atomicAdd(cnt, tot);
+    int p = __shfl(base, 63) + incl - c;
     for (; m && p < cap; m &= m - 1, ++p) list[p] = j * nx + 64 * w0 + __builtin_ctzll(m);
 }
 __global__ void __launch_bounds__(256) k_ex_none_list(const u64 *__restrict__ kbits, int ny,

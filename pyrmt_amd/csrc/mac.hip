@@ -95,6 +95,8 @@ constexpr int MP_BLOCKS = 8192;   // the fused reduction passes' workgroups (one
 // k_mac_centres over the whole grid on MP_BLOCKS x RED_T threads, also folding max(u_c^2 +
 // v_c^2) (NaN-propagating, k_reduce_p1<3>'s rule: a max is exact in any order) into one
 // partial per block -- reduce_maxsq2_nan's pass over u_c, v_c saved
+// WRITE: also the centre planes (off: the advection samples the faces itself, k_sim_sl_t<1>)
+template <bool WRITE>
 __global__ void __launch_bounds__(RED_T) k_mac_centres_m2(const double *__restrict__ u,
                                                           const double *__restrict__ v, int N,
                                                           double *__restrict__ uc,
@@ -124,7 +126,7 @@ __global__ void __launch_bounds__(RED_T) k_mac_centres_m2(const double *__restri
             if (c >= n) break;
             const double a = 0.5 * (ul[m] + ur[m]);
             const double b = 0.5 * (vd[m] + vu[m]);
-            uc[c] = a; vc[c] = b;
+            if (WRITE) { uc[c] = a; vc[c] = b; }
             fin = fin && isfinite(a) && isfinite(b);
             const double x = a * a + b * b;
             acc = (x > acc || x != x) ? x : acc;
@@ -821,8 +823,13 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         RMT_HIP(hipMemsetAsync(S->flags, 0, 5 * sizeof(int), st));   // [4]: k_mac_phi's big
         // with max |u_c|^2, which bounds every velocity sample of the backtraces (the SL
         // block skip)
-        k_mac_centres_m2<<<MP_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc, S->flags,
-                                                        S->mpart);
+        const bool face_sl = ctx->opt.mac_face_sl != 0;
+        if (face_sl)
+            k_mac_centres_m2<false><<<MP_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc,
+                                                                 S->flags, S->mpart);
+        else
+            k_mac_centres_m2<true><<<MP_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc,
+                                                                S->flags, S->mpart);
         k_max_partials<false><<<1, 1024, 0, st>>>(S->mpart, MP_BLOCKS, -INFINITY, S->out + 8);
         RMT_LAUNCHED();
         for (int k = 0; k < K; ++k) {
@@ -842,9 +849,10 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
             }
             for (int q = 0; q < 4; ++q) D.bx.b[k][q] = cb[q];   // (the stress / diag passes)
             // phi from the current map (already S->phi[k]), advect with the pre-advection mask
-            RMT_TRY(sl_disc_map(ctx, S->X1[k], S->X2[k], S->uc, S->vc, S->xs, S->ys, dt, dx, dx,
-                                P.cx[k], P.cy[k], P.R[k], S->X1n, S->X2n, S->phi_pre,
-                                S->flags + 1, S->out + 8, S->kbits, box_mode ? cb : nullptr));
+            RMT_TRY(sl_disc_map(ctx, S->X1[k], S->X2[k], face_sl ? S->u : S->uc,
+                                face_sl ? S->v : S->vc, S->xs, S->ys, dt, dx, dx, P.cx[k],
+                                P.cy[k], P.R[k], S->X1n, S->X2n, S->phi_pre, S->flags + 1,
+                                S->out + 8, S->kbits, box_mode ? cb : nullptr, face_sl));
             // the known plane from the advection pass (its k_ex_bits pass over phi_pre saved);
             // the no-op test over every row at once (a disc with nothing to fit scans them all)
             ctx->ex_none_wide = true;

@@ -106,6 +106,7 @@ struct rmt_opts {
     int tail_stream = 1;      // RMT_TAIL_STREAM: the pressure update beside the SL and prep
     int diag_first = 0;       // RMT_DIAG_FIRST: the step's diagnostics ahead of the next geometry
     int mac_noop_host = 1;    // RMT_MAC_NOOP_HOST: MAC extrapolation's no-op verdict read on the host
+    int mac_face_sl = 1;      // RMT_MAC_FACE_SL: MAC advection samples the face planes (no centre planes)
 };
 
 #ifndef RMT_EDGE_SLOTS
@@ -657,7 +658,8 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
                 double *phi_pre, int *bad, const double *dev_m2 = nullptr,
-                unsigned long long *kbits = nullptr, const int *cbox = nullptr);
+                unsigned long long *kbits = nullptr, const int *cbox = nullptr,
+                bool faces = false);
 
 // --------------------------------------------------------------------- momentum --
 // every stage keeps its own k plane (k1, k2, k3; the last stage forms (k1 + 2 k2) + 2 k3

@@ -178,6 +178,21 @@ constexpr int SLT_X = 64, SLT_Y = 4, SLT_SX = SLT_X + 3, SLT_SY = SLT_Y + 3;
 
 // interpolators.py:4-61 at one query point (bilinear_t<false>), corners from the staged
 // tile s (origin row sj0, column si0) when they lie in it, else from g
+// FACE: g is a MAC face plane and a cell's value the mean of its two faces (mac.py's cell
+// centre velocity, k_mac_centres_m2's expression): V 0 = u (nx + 1 faces a row), 1 = v (a
+// row of nx faces, one row more)
+template <int FACE, int V>
+__device__ __forceinline__ double cell_vel(const double *__restrict__ g, int jj, int ii, int nx) {
+    if constexpr (!FACE) return g[(long)jj * nx + ii];
+    else if constexpr (V == 0) {
+        const long f = (long)jj * (nx + 1) + ii;
+        return 0.5 * (g[f] + g[f + 1]);
+    } else {
+        const long f = (long)jj * nx + ii;
+        return 0.5 * (g[f] + g[f + nx]);
+    }
+}
+template <int FACE = 0, int V = 0>
 __device__ __forceinline__ double bl_tile(const double *__restrict__ s,
                                           const double *__restrict__ g, double xq, double yq,
                                           const DivK &Kx, const DivK &Ky, int nx, int ny,
@@ -195,6 +210,9 @@ __device__ __forceinline__ double bl_tile(const double *__restrict__ s,
     if ((unsigned)lx < (unsigned)(SLT_SX - 1) && (unsigned)ly < (unsigned)(SLT_SY - 1)) {
         const double *r0 = s + ly * SLT_SX + lx, *r1 = r0 + SLT_SX;
         v00 = r0[0]; v10 = r0[1]; v01 = r1[0]; v11 = r1[1];
+    } else if constexpr (FACE) {
+        v00 = cell_vel<FACE, V>(g, iy, ix, nx); v10 = cell_vel<FACE, V>(g, iy, ix + 1, nx);
+        v01 = cell_vel<FACE, V>(g, iy + 1, ix, nx); v11 = cell_vel<FACE, V>(g, iy + 1, ix + 1, nx);
     } else {
         const double *r0 = g + (long)iy * nx + ix, *r1 = r0 + nx;
         v00 = r0[0]; v10 = r0[1]; v01 = r1[0]; v11 = r1[1];
@@ -202,7 +220,9 @@ __device__ __forceinline__ double bl_tile(const double *__restrict__ s,
     return (1 - fx) * (1 - fy) * v00 + fx * (1 - fy) * v10 + (1 - fx) * fy * v01 + fx * fy * v11;
 }
 
-// grid ((nx + 63) / 64, (ny + 3) / 4); mode 0 (kbits optional) or 2 (the non-rim cells)
+// grid ((nx + 63) / 64, (ny + 3) / 4); mode 0 (kbits optional) or 2 (the non-rim cells).
+// FACE: a, b are the MAC u / v face planes (cell_vel), nx == ny
+template <int FACE = 0>
 __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
     const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ a,
     const double *__restrict__ b, const double *__restrict__ xs, const double *__restrict__ ys,
@@ -256,8 +276,7 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
             const int jj = sj0 + q / SLT_SX, ii = si0 + q % SLT_SX;
             double va = 0.0, vb = 0.0;
             if (jj >= 0 && jj < ny && ii >= 0 && ii < nx) {
-                const long g = (long)jj * nx + ii;
-                va = a[g]; vb = b[g];
+                va = cell_vel<FACE, 0>(a, jj, ii, nx); vb = cell_vel<FACE, 1>(b, jj, ii, nx);
             }
             sa[q] = va; sb[q] = vb;
         }
@@ -271,15 +290,17 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
                 if (!(isfinite(sa[o]) && isfinite(sb[o]))) atomicOr(bad, 1);
                 const double m = ph <= 0 ? 1.0 : 0.0;
 #define BT_(S, G, X, Y) bl_tile(S, G, X, Y, Kx, Ky, nx, ny, sj0, si0)
+#define BTA_(X, Y) bl_tile<FACE, 0>(sa, a, X, Y, Kx, Ky, nx, ny, sj0, si0)
+#define BTB_(X, Y) bl_tile<FACE, 1>(sb, b, X, Y, Kx, Ky, nx, ny, sj0, si0)
                 // functions.py:194-227 (sl_backtrace_t's operations, in order)
                 const double x = xs[i], y = ys[j], hdt = 0.5 * dt, dt6 = dt / 6.0;
-                const double k1x = BT_(sa, a, x, y), k1y = BT_(sb, b, x, y);
+                const double k1x = BTA_(x, y), k1y = BTB_(x, y);
                 const double x2 = x - hdt * k1x, y2 = y - hdt * k1y;
-                const double k2x = BT_(sa, a, x2, y2), k2y = BT_(sb, b, x2, y2);
+                const double k2x = BTA_(x2, y2), k2y = BTB_(x2, y2);
                 const double x3 = x - hdt * k2x, y3 = y - hdt * k2y;
-                const double k3x = BT_(sa, a, x3, y3), k3y = BT_(sb, b, x3, y3);
+                const double k3x = BTA_(x3, y3), k3y = BTB_(x3, y3);
                 const double x4 = x - dt * k3x, y4 = y - dt * k3y;
-                const double k4x = BT_(sa, a, x4, y4), k4y = BT_(sb, b, x4, y4);
+                const double k4x = BTA_(x4, y4), k4y = BTB_(x4, y4);
                 const double xb = x - dt6 * (k1x + 2 * k2x + 2 * k3x + k4x);
                 const double yb = y - dt6 * (k1y + 2 * k2y + 2 * k3y + k4y);
                 o1 = BT_(s1, X1, xb, yb) * m;
@@ -287,6 +308,8 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
                 X1n[c] = o1;
                 X2n[c] = o2;
 #undef BT_
+#undef BTA_
+#undef BTB_
             }
         }
     }
@@ -665,7 +688,7 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
                 const double *b, const double *xs, const double *ys, double dt, double dx,
                 double dy, double x0, double y0, double R, double *X1n, double *X2n,
                 double *phi_pre, int *bad, const double *dev_m2, unsigned long long *kbits,
-                const int *cbox) {
+                const int *cbox, bool faces) {
     // cbox {j0, j1, i0, i1}: only the tiles meeting those cells (kbits words outside them
     // are left alone: the caller clears them)
     int ty0 = 0, ty1 = (ctx->ny + SLT_Y - 1) / SLT_Y, tx0 = 0, tx1 = (ctx->nx + SLT_X - 1) / SLT_X;
@@ -674,7 +697,10 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
         tx0 = cbox[2] / SLT_X; tx1 = (cbox[3] + SLT_X - 1) / SLT_X;
         if (ty1 <= ty0 || tx1 <= tx0) return RMT_OK;
     }
-    k_sim_sl_t<<<dim3(tx1 - tx0, ty1 - ty0), SLT_X * SLT_Y, 0, ctx->stream>>>(
+    // faces: a, b are MAC face planes (k_sim_sl_t<1>)
+    RMT_CHECK(!faces || ctx->nx == ctx->ny, RMT_EINVAL, "sl_disc_map: faces need a square grid");
+    auto *kern = faces ? k_sim_sl_t<1> : k_sim_sl_t<0>;
+    kern<<<dim3(tx1 - tx0, ty1 - ty0), SLT_X * SLT_Y, 0, ctx->stream>>>(
         X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx), divk_make(dy), x0, y0, R, X1n,
         X2n, phi_pre, bad, kbits, dev_m2, nullptr, 0, nullptr, nullptr, 0.0, nullptr, nullptr,
         tx0, ty0);
@@ -1090,7 +1116,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx), divk_make(P.dy), P.x0, P.y0,
                     P.R, S->X1n, S->X2n, S->flag, sc, dtp, S->rimw, S->segs, scount);
             } else if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN) {
-                k_sim_sl_t<<<dim3((nx + SLT_X - 1) / SLT_X, (ny + SLT_Y - 1) / SLT_Y), SLT_X * SLT_Y,
+                k_sim_sl_t<0><<<dim3((nx + SLT_X - 1) / SLT_X, (ny + SLT_Y - 1) / SLT_Y), SLT_X * SLT_Y,
                              0, st>>>(S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt,
                                       divk_make(P.dx), divk_make(P.dy), P.x0, P.y0, P.R, S->X1n,
                                       S->X2n, S->phi_pre, S->flag, S->kbits, sc, dtp, 0, nullptr);
@@ -1172,7 +1198,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits) {
                     // the advection of every non-rim cell, once the chain has started (earlier
                     // its blocks would crowd out the one-workgroup band passes)
-                    k_sim_sl_t<<<dim3((nx + SLT_X - 1) / SLT_X, (ny + SLT_Y - 1) / SLT_Y),
+                    k_sim_sl_t<0><<<dim3((nx + SLT_X - 1) / SLT_X, (ny + SLT_Y - 1) / SLT_Y),
                                  SLT_X * SLT_Y, 0, S->st2>>>(
                         S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx),
                         divk_make(P.dy), P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag,

@@ -205,16 +205,17 @@ def test_config5_mac_N8192_vs_oracle_fixture(gpu):
     np.testing.assert_allclose(got, gd, rtol=1e-12)     # achieved
 
 
-def test_config5_noop_verdict_on_host_is_bit_identical(gpu):
+def test_config5_schedule_switches_are_bit_identical(gpu):
     """N=8192, 3 discs: no first-layer fit is acceptable (det ~ 1e-14), so every extrapolation
     call is the identity.  The default reads k_ex_none's verdict back and launches nothing
     more (mac_noop_host); with it off every pass is launched and exits on the device flag.
-    Both must give the same bits over 3 steps."""
+    The advection samples the face planes (mac_face_sl) instead of centre planes a separate
+    pass writes.  Defaults and both switches off must give the same bits over 3 steps."""
     import gc
     from pyrmt_amd.mac import MacMultiDisc
     out = []
-    for host in (1, 0):
-        sim = MacMultiDisc(8192, n_discs=3, seed=3, options={"mac_noop_host": host})
+    for opts in ({}, {"mac_noop_host": 0, "mac_face_sl": 0}):
+        sim = MacMultiDisc(8192, n_discs=3, seed=3, options=opts or None)
         sim.step(3)
         d = sim.diagnostics()
         out.append((d, {f"{n}{k}": _sha(sim.get(n, k)) for n in ("X1", "X2", "phi")

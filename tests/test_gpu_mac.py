@@ -102,9 +102,11 @@ def test_mac_box_mode_is_bit_identical(M, N, calls):
     full-grid passes: every field and diagnostic bit for bit, over several calls (each call
     starts from a full pass; the boxes then come back with the per-step diagnostics).  Also
     the no-op verdict kept on the device (mac_noop_host = 0: every extrapolation pass launched
-    and exiting on the device flag) against the default host read-back."""
+    and exiting on the device flag) against the default host read-back, and the advection
+    through the cell-centre planes (mac_face_sl = 0) against its default face sampling."""
     out = []
-    for opts in ({"mac_boxes": 0}, {"mac_boxes": 1}, {"mac_boxes": 1, "mac_noop_host": 0}):
+    for opts in ({"mac_boxes": 0}, {"mac_boxes": 1}, {"mac_boxes": 1, "mac_noop_host": 0},
+                 {"mac_boxes": 1, "mac_face_sl": 0}, {"mac_boxes": 0, "mac_face_sl": 0}):
         sim = M.MacMultiDisc(N, n_discs=3, seed=3, options=opts)
         for c in calls:
             sim.step(c)
