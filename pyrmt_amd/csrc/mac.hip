@@ -538,10 +538,12 @@ __global__ void __launch_bounds__(RED_T) k_mac_correct_um(const double *__restri
 // per-disc centroid sums over phi <= 0 (x, y, count) and max|u| partials (u nullable: the
 // max comes from k_mac_correct_um)
 constexpr int MD_VALS = 3 * MAC_MAXD + 1;
-// (rows [jb, je): cells and u faces)
+// (rows [jb, je): cells and u faces).  Without u, only the items of rows [r0, r1) are
+// visited, the rows holding every box (outside its box phi_k > 0 adds nothing): each thread
+// still takes its items in increasing order, so the sums are those of the whole range.
 __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__restrict__ u,
                                                      int N, double dx, double *__restrict__ part,
-                                                     int jb, int je) {
+                                                     int jb, int je, int r0, int r1) {
     __shared__ double s[MS_TPB];
     double acc[MD_VALS];
     for (int k = 0; k < MD_VALS; ++k) acc[k] = 0.0;
@@ -550,7 +552,13 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
     // item order (the same sums as one item per trip)
     constexpr int MD_U = 4;
     const long S = (long)MS_BLOCKS * MS_TPB;
-    for (long t0 = blockIdx.x * (long)MS_TPB + threadIdx.x; t0 < nf; t0 += MD_U * S) {
+    long tfirst = blockIdx.x * (long)MS_TPB + threadIdx.x, tend = nf;
+    if (!u) {
+        const long tlo = (long)(max(r0, jb) - jb) * N;
+        tend = min(n, (long)(max(r1, jb) - jb) * N);
+        if (tlo > tfirst) tfirst += (tlo - tfirst) / S * S;   // (the last item of this thread below tlo)
+    }
+    for (long t0 = tfirst; t0 < tend; t0 += MD_U * S) {
         double ua[MD_U];
         unsigned in[MD_U];   // bit k: phi_k <= 0 at the item's cell
 #pragma unroll
@@ -558,7 +566,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
             const long t = t0 + m * S;
             ua[m] = t < nf && u ? u[(long)jb * (N + 1) + t] : 0.0;
             in[m] = 0;
-            if (t < n) {
+            if (t < n && t < tend) {
                 const long c = (long)jb * N + t;
                 const int j = dv32(c, N), i = (int)(c - (long)j * N);
 #pragma unroll
@@ -570,7 +578,7 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
 #pragma unroll
         for (int m = 0; m < MD_U; ++m) {
             const long t = t0 + m * S;
-            if (t >= nf) break;
+            if (t >= tend) break;
             acc[3 * MAC_MAXD] = nanmax(acc[3 * MAC_MAXD], fabs(ua[m]));
             if (t < n) {
                 const long c = (long)jb * N + t;
@@ -908,7 +916,16 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         RMT_TRY(mac_project_impl(ctx, S->us, S->vs, dx, dx, dt, P.rho, S->u, S->v, S->p,
                                  S->X1n, true, S->mpart));
         k_max_partials<true><<<1, 1024, 0, st>>>(S->mpart, MP_BLOCKS, 0.0, S->out + 9);
-        k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, nullptr, N, dx, S->part + 2 * MS_BLOCKS, 0, N);
+        int dr0 = 0, dr1 = N;   // the rows holding every box
+        if (D.bx.n) {
+            dr0 = N; dr1 = 0;
+            for (int k = 0; k < K; ++k)
+                if (D.bx.b[k][1] > D.bx.b[k][0]) {
+                    dr0 = std::min(dr0, D.bx.b[k][0]); dr1 = std::max(dr1, D.bx.b[k][1]);
+                }
+        }
+        k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, st>>>(D, nullptr, N, dx, S->part + 2 * MS_BLOCKS, 0, N,
+                                                 dr0, dr1);
         RMT_LAUNCHED();
         std::vector<double> dp((size_t)MS_BLOCKS * MD_VALS);
         RMT_HIP(hipMemcpyAsync(dp.data(), S->part + 2 * MS_BLOCKS, dp.size() * 8,
@@ -1320,7 +1337,7 @@ int rmt_mac_slab_correct(rmt_mac_slab *S, double dt) {
         S->gc(S->v), F);
     RMT_LAUNCHED();
     k_mac_diag<<<MS_BLOCKS, MS_TPB, 0, ctx->stream>>>(S->discs(), S->gu(S->u), N, P.dx,
-                                                     S->part + 2 * MS_BLOCKS, S->r0, S->r1);
+                                                     S->part + 2 * MS_BLOCKS, S->r0, S->r1, S->r0, S->r1);
     RMT_LAUNCHED();
     k_mac_slab_scal<<<1, 256, 0, ctx->stream>>>(S->part, S->flags, P.n_discs, S->scal);
     RMT_LAUNCHED();

@@ -819,7 +819,18 @@ int dct_solve(rmt_ctx *ctx, const double *rhs, double dx, double dy, double *p,
 //   solve); 2: inverse along rows.
 __device__ __forceinline__ int mk_src(int m, int n) { return m < n / 2 ? 2 * m : 2 * (n - 1 - m) + 1; }
 
-template <int MODE, int BIG>
+// factor(8192)'s plan: radices 2, 8, 8, 8, 8 (ascending), twiddle offsets 0, 1, 15, 127, 1023
+template <int NT>
+__device__ __forceinline__ void fft_8192(double2 *z, const double2 *__restrict__ W) {
+    fft_pass_k<2, 1, NT, 8192>(z, W);
+    fft_pass_k<8, 2, NT, 8192>(z, W + 1);
+    fft_pass_k<8, 16, NT, 8192>(z, W + 15);
+    fft_pass_k<8, 128, NT, 8192>(z, W + 127);
+    fft_pass_k<8, 1024, NT, 8192>(z, W + 1023);
+}
+
+// PLAN 2: n = 8192 (compile-time passes, fft_8192: the same arithmetic as fft_lds)
+template <int MODE, int BIG, int PLAN = 0>
 __global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict__ src,
                                                        double *__restrict__ dst, int rows, int n,
                                                        const double2 *__restrict__ W,
@@ -840,7 +851,8 @@ __global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict_
             z[m] = make_double2(sa[q], hasB ? sb[q] : 0.0);
         }
         __syncthreads();
-        fft_lds<BIG, FftT<BIG>::T, DCT_MAXM>(z, n, rd, W);
+        if constexpr (PLAN == 2) fft_8192<DCT_T>(z, W);
+        else fft_lds<BIG, FftT<BIG>::T, DCT_MAXM>(z, n, rd, W);
         double2 y[PER];
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
@@ -896,7 +908,8 @@ __global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict_
         }
     }
     __syncthreads();
-    fft_lds<BIG, FftT<BIG>::T, DCT_MAXM>(z, n, rd, W);
+    if constexpr (PLAN == 2) fft_8192<DCT_T>(z, W);
+    else fft_lds<BIG, FftT<BIG>::T, DCT_MAXM>(z, n, rd, W);
     const double s = scale / n;
     for (int m = tid; m < n; m += DCT_T) {
         const double2 R = z[m];
@@ -969,9 +982,11 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
     RMT_HIP(hipMalloc(&P->T, (size_t)nx * ny * sizeof(double)));
     static bool attr = false;
     if (!attr) {
-        const void *fs[6] = {(const void *)k_dct2<0, 0>, (const void *)k_dct2<1, 0>,
+        const void *fs[9] = {(const void *)k_dct2<0, 0>, (const void *)k_dct2<1, 0>,
                              (const void *)k_dct2<2, 0>, (const void *)k_dct2<0, 1>,
-                             (const void *)k_dct2<1, 1>, (const void *)k_dct2<2, 1>};
+                             (const void *)k_dct2<1, 1>, (const void *)k_dct2<2, 1>,
+                             (const void *)k_dct2<0, 0, 2>, (const void *)k_dct2<1, 0, 2>,
+                             (const void *)k_dct2<2, 0, 2>};
         for (auto f : fs)
             RMT_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)FFT_LDS_MAX));
@@ -991,12 +1006,18 @@ int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst,
     const unsigned g = (nrows + 1) / 2;
     hipStream_t st = ctx->stream;
 #define DCT2_L(M, B) k_dct2<M, B><<<g, FftT<B>::T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0)
-    if (P->big) {
+#define DCT2_K(M) k_dct2<M, 0, 2><<<g, FftT<0>::T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0)
+    // n = 8192: the compile-time plan (factor(8192) is always 2, 8, 8, 8, 8)
+    const bool k8192 = n == 8192 && rd.n == 5 && rd.p[0].R == 2 && rd.p[4].R == 8;
+    if (k8192) {
+        if (mode == 0) DCT2_K(0); else if (mode == 1) DCT2_K(1); else DCT2_K(2);
+    } else if (P->big) {
         if (mode == 0) DCT2_L(0, 1); else if (mode == 1) DCT2_L(1, 1); else DCT2_L(2, 1);
     } else {
         if (mode == 0) DCT2_L(0, 0); else if (mode == 1) DCT2_L(1, 0); else DCT2_L(2, 0);
     }
 #undef DCT2_L
+#undef DCT2_K
     RMT_LAUNCHED();
     return RMT_OK;
 }

@@ -8,6 +8,11 @@ RMT_LIB=$B timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-m
     tests/test_gpu_mac.py tests/test_gpu_configs.py -k "mac or config5" > "$O/tests.log" 2>&1 \
     || { tail -30 "$O/tests.log"; exit 1; }
 tail -2 "$O/tests.log"
+for L in "$A" "$B"; do
+    RMT_LIB=$L timeout -k 10 200 python -u tools/mac_sha.py 8192 3 > "$O/sha_$(basename "$L" .so).txt" 2>&1 \
+        || { tail -5 "$O/sha_$(basename "$L" .so).txt"; exit 1; }
+    tail -1 "$O/sha_$(basename "$L" .so).txt"
+done
 k=0
 for L in "$A" "$B" "$A" "$B"; do
     k=$((k + 1)); t=$(basename "$L" .so)
