@@ -611,8 +611,11 @@ static int mac_project_impl(rmt_ctx *ctx, const double *us, const double *vs, do
     if (plan) RMT_TRY(dct2_plan(ctx, N, N, dx, dy));
     k_mac_rhs<<<grid1d(n, 256), 256, 0, ctx->stream>>>(us, vs, N, dx, dy, rho / dt, rhs, 0, N);
     RMT_LAUNCHED();
-    RMT_TRY(sub_mean_rows(ctx, rhs, N, N));     // rhs - rhs.mean() (mac.py:135)
-    RMT_TRY(dct2_solve(ctx, rhs, phi));
+    // rhs - rhs.mean() (mac.py:135): the row-tree root here, the subtraction on the DCT's
+    // first load (the values sub_mean_rows would leave in rhs; nothing else reads them)
+    double *root = ctx->red + RED_BLOCKS + 16;
+    RMT_TRY(rowtree_root(ctx, rhs, N, N, root));
+    RMT_TRY(dct2_solve(ctx, rhs, phi, root, (double)N * N));
     if (umax_part)
         k_mac_correct_um<<<MP_BLOCKS, RED_T, 0, ctx->stream>>>(us, vs, phi, N, dx, dy, dt / rho,
                                                                 u, v, umax_part);

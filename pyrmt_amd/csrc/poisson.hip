@@ -837,7 +837,9 @@ __global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict_
                                                        const double2 *__restrict__ Wq, Radices rd,
                                                        const double *__restrict__ lamr,
                                                        const double *__restrict__ lamk, int row0,
-                                                       double scale) {
+                                                       double scale,
+                                                       const double *__restrict__ mroot = nullptr,
+                                                       double mcount = 1.0) {
     constexpr int DCT_T = FftT<BIG>::T;
     extern __shared__ double2 z[];
     constexpr int PER = DCT_MAXM / DCT_T;
@@ -846,9 +848,13 @@ __global__ void __launch_bounds__(FftT<BIG>::T) k_dct2(const double *__restrict_
     const double *sa = src + (long)rA * n, *sb = src + (long)rB * n;
     double *da = dst + (long)rA * n, *db = dst + (long)rB * n;
     if constexpr (MODE != 2) {
+        // mroot (MODE 0, nullable): the rows' tree root -- x - root / count on the load, the
+        // values k_sub_tree_mean would have left in src
+        const double mean = mroot ? mroot[0] / mcount : 0.0;
         for (int m = tid; m < n; m += DCT_T) {
             const int q = mk_src(m, n);
-            z[m] = make_double2(sa[q], hasB ? sb[q] : 0.0);
+            if (mroot) z[m] = make_double2(sa[q] - mean, hasB ? sb[q] - mean : 0.0);
+            else z[m] = make_double2(sa[q], hasB ? sb[q] : 0.0);
         }
         __syncthreads();
         if constexpr (PLAN == 2) fft_8192<DCT_T>(z, W);
@@ -997,7 +1003,7 @@ int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy) {
 
 // one DCT-II pass over nrows rows along axis (0: length nx, 1: length ny; MODE 1 needs 1)
 int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst,
-                     int nrows, int row0) {
+                     int nrows, int row0, const double *mroot, double mcount) {
     Dct2Plan *P = ctx->dct2;
     const int n = axis == 0 ? P->nx : P->ny;
     const Radices rd = axis == 0 ? radices(P->radx, P->npx) : radices(P->rady, P->npy);
@@ -1005,8 +1011,9 @@ int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst,
     const size_t lds = (size_t)n * sizeof(double2);
     const unsigned g = (nrows + 1) / 2;
     hipStream_t st = ctx->stream;
-#define DCT2_L(M, B) k_dct2<M, B><<<g, FftT<B>::T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0)
-#define DCT2_K(M) k_dct2<M, 0, 2><<<g, FftT<0>::T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0)
+    RMT_CHECK(!mroot || mode == 0, RMT_EINVAL, "dct2_pass: the mean is taken on a forward pass");
+#define DCT2_L(M, B) k_dct2<M, B><<<g, FftT<B>::T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0, mroot, mcount)
+#define DCT2_K(M) k_dct2<M, 0, 2><<<g, FftT<0>::T, lds, st>>>(src, dst, nrows, n, W, Q, rd, P->lamx, P->lamy, row0, 1.0, mroot, mcount)
     // n = 8192: the compile-time plan (factor(8192) is always 2, 8, 8, 8, 8)
     const bool k8192 = n == 8192 && rd.n == 5 && rd.p[0].R == 2 && rd.p[4].R == 8;
     if (k8192) {
@@ -1034,11 +1041,11 @@ int dct2_set_lambda(rmt_ctx *ctx, const double *lamx, const double *lamy) {
 }
 
 // mac.py:118-123: p = D^-1 (D rhs / eig), (0,0) -> 0; rhs and p are (ny, nx), may alias
-int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p) {
+int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p, const double *mroot, double mcount) {
     Dct2Plan *P = ctx->dct2;
     RMT_CHECK(P, RMT_EINVAL, "dct2_solve: no plan");
     const int ny = P->ny, nx = P->nx;
-    RMT_TRY(dct2_pass(ctx, 0, 0, rhs, p, ny, 0));
+    RMT_TRY(dct2_pass(ctx, 0, 0, rhs, p, ny, 0, mroot, mcount));
     transpose(ctx, ctx->stream, p, ny, nx, P->T);
     RMT_TRY(dct2_pass(ctx, 1, 1, P->T, P->T, nx, 0));
     transpose(ctx, ctx->stream, P->T, nx, ny, p);

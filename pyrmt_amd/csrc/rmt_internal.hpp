@@ -753,12 +753,14 @@ void transpose(const rmt_ctx *ctx, hipStream_t st, const double *in, int R, int 
                const unsigned char *rowmark = nullptr, int mode = 0);
 // MAC grid (mac.py:104-123): DCT-II Neumann solve on a (ny, nx) cell grid, (0,0) -> 0
 int dct2_plan(rmt_ctx *ctx, int ny, int nx, double dx, double dy);
-int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p);
+// mroot (nullable): rhs's row-tree root; the solve then takes rhs - root / mcount
+int dct2_solve(rmt_ctx *ctx, const double *rhs, double *p, const double *mroot = nullptr,
+               double mcount = 1.0);
 int dct2_set_lambda(rmt_ctx *ctx, const double *lamx, const double *lamy);
 // one DCT-II pass over nrows rows (mode 0 forward, 1 column solve with row0 = global
 // x-frequency of local row 0, 2 inverse; axis 0: length nx, 1: length ny)
 int dct2_pass(rmt_ctx *ctx, int mode, int axis, const double *src, double *dst, int nrows,
-              int row0);
+              int row0, const double *mroot = nullptr, double mcount = 1.0);
 void dct2_destroy(Dct2Plan *P);
 void per_destroy(PerPlan *P);
 void dct_destroy(DctPlan *);
