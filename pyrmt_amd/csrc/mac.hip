@@ -456,6 +456,34 @@ __global__ void k_mac_rhs(const double *__restrict__ u, const double *__restrict
     rhs[c] = coef * d;
 }
 
+// k_mac_rhs with its row sums: one block per row (N rows), each thread the columns t,
+// t + 256, ... -- rhs written as k_mac_rhs writes it, and summed in k_rowsum's order (the
+// strided partials, then the halving tree), so the row-tree root is the one rowtree_root
+// would form from the written plane
+__global__ void __launch_bounds__(256) k_mac_rhs_rows(const double *__restrict__ u,
+                                                      const double *__restrict__ v, int N,
+                                                      double dx, double dy, double coef,
+                                                      double *__restrict__ rhs,
+                                                      double *__restrict__ rs) {
+    __shared__ double s[256];
+    const int j = blockIdx.x;
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < N; i += 256) {
+        const long c = (long)j * N + i, cu = (long)j * (N + 1) + i;
+        const double d = (u[cu + 1] - u[cu]) / dx + (v[c + N] - v[c]) / dy;
+        const double r = coef * d;
+        rhs[c] = r;
+        acc += r;
+    }
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) s[threadIdx.x] = s[threadIdx.x] + s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rs[j] = s[0];
+}
+
 // u = u* - (dt/rho) grad_p_u(phi), v likewise (mac.py:87-101, 137-138)
 __global__ void k_mac_correct(const double *__restrict__ us, const double *__restrict__ vs,
                               const double *__restrict__ phi, int N, double dx, double dy,
@@ -607,14 +635,16 @@ static int mac_project_impl(rmt_ctx *ctx, const double *us, const double *vs, do
                             double dy, double dt, double rho, double *u, double *v, double *phi,
                             double *rhs, bool plan = true, double *umax_part = nullptr) {
     const int N = ctx->nx;
-    const long n = (long)N * N, nf = (long)N * (N + 1);
+    const long nf = (long)N * (N + 1);
     if (plan) RMT_TRY(dct2_plan(ctx, N, N, dx, dy));
-    k_mac_rhs<<<grid1d(n, 256), 256, 0, ctx->stream>>>(us, vs, N, dx, dy, rho / dt, rhs, 0, N);
-    RMT_LAUNCHED();
-    // rhs - rhs.mean() (mac.py:135): the row-tree root here, the subtraction on the DCT's
-    // first load (the values sub_mean_rows would leave in rhs; nothing else reads them)
+    // rhs - rhs.mean() (mac.py:135): the row sums with the rhs, the row-tree root, and the
+    // subtraction on the DCT's first load (the values sub_mean_rows would leave in rhs;
+    // nothing else reads them)
     double *root = ctx->red + RED_BLOCKS + 16;
-    RMT_TRY(rowtree_root(ctx, rhs, N, N, root));
+    RMT_CHECK(N <= ctx->rsum_len, RMT_EINVAL, "mac projection: rows out of range");
+    k_mac_rhs_rows<<<N, 256, 0, ctx->stream>>>(us, vs, N, dx, dy, rho / dt, rhs, ctx->rsum);
+    RMT_LAUNCHED();
+    RMT_TRY(rowtree_sums(ctx, N, root));
     RMT_TRY(dct2_solve(ctx, rhs, phi, root, (double)N * N));
     if (umax_part)
         k_mac_correct_um<<<MP_BLOCKS, RED_T, 0, ctx->stream>>>(us, vs, phi, N, dx, dy, dt / rho,
