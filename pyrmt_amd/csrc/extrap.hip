@@ -231,10 +231,12 @@ __global__ void __launch_bounds__(256) k_ex_none(const u64 *__restrict__ kbits, 
 // k_ex_cand lists the candidates of rows [jb, je) (a thread per word), k_ex_none_list fits
 // them.  Over capacity (cnt > cap), k_ex_none_list runs the row walk above instead.
 __global__ void __launch_bounds__(256) k_ex_cand(const u64 *__restrict__ kbits, int ny, int nx,
-                                                 int W, int jb, int je, int *__restrict__ list,
-                                                 int cap, int *__restrict__ cnt) {
+                                                 int W, int jb, int je, int wb, int we,
+                                                 int *__restrict__ list, int cap,
+                                                 int *__restrict__ cnt) {
+    // words [wb, we) of rows [jb, je)
     const long t = (long)blockIdx.x * 256 + threadIdx.x;
-    const int j = jb + (int)(t / W), w0 = (int)(t % W), lane = threadIdx.x & 63;
+    const int j = jb + (int)(t / (we - wb)), w0 = wb + (int)(t % (we - wb)), lane = threadIdx.x & 63;
     u64 m = (j < je && j >= 1 && j <= ny - 2) ? ex_none_cands(kbits, ny, nx, W, j, w0) : 0;
     // one counter update per wave (a single counter: per-word atomics serialise)
     const int c = __popcll(m);
@@ -845,8 +847,13 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
         if (ctx->ex_none_wide && ctx->ex_cand && je > jb) {
             int *cnt = ctx->ex_cand + ctx->ex_cand_cap;
             RMT_HIP(hipMemsetAsync(cnt, 0, sizeof(int), ctx->stream));
-            k_ex_cand<<<grid1d((long)(je - jb) * W, 256), 256, 0, ctx->stream>>>(
-                ws.kbits, ny, nx, W, jb, je, ctx->ex_cand, ctx->ex_cand_cap, cnt);
+            int wb = 0, we = W;
+            if (ctx->ex_none_cols[1] > ctx->ex_none_cols[0]) {
+                wb = std::max(0, ctx->ex_none_cols[0]);
+                we = std::min(W, ctx->ex_none_cols[1]);
+            }
+            k_ex_cand<<<grid1d((long)(je - jb) * (we - wb), 256), 256, 0, ctx->stream>>>(
+                ws.kbits, ny, nx, W, jb, je, wb, we, ctx->ex_cand, ctx->ex_cand_cap, cnt);
             k_ex_none_list<<<1024, 256, 0, ctx->stream>>>(ws.kbits, ny, nx, W, dx, dy, r * r,
                                                            ws.ctl, jb, je, ctx->ex_cand,
                                                            ctx->ex_cand_cap, cnt);

@@ -903,6 +903,9 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
                 ctx->ex_none_rows[0] = std::max(0, cb[0] - 1);
                 ctx->ex_none_rows[1] = cb[1] > cb[0] ? std::min(N, cb[1] + 1) : 1;
                 if (cb[1] <= cb[0]) ctx->ex_none_rows[0] = 0;   // (empty map: one row, no candidate)
+                // likewise the columns [cb2 - 1, cb3 + 1): their 64-column words
+                ctx->ex_none_cols[0] = std::max(0, cb[2] - 1) >> 6;
+                ctx->ex_none_cols[1] = cb[3] > cb[2] ? (std::min(N - 1, cb[3]) >> 6) + 1 : 1;
             }
             ctx->ex_cand = S->cand; ctx->ex_cand_cap = mac_cand_cap(N);
             ctx->ex_none_host = ctx->opt.mac_noop_host != 0;
@@ -910,6 +913,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
                                        S->X2n, S->flags + 2, S->kbits);
             ctx->ex_none_wide = false;
             ctx->ex_none_rows[0] = ctx->ex_none_rows[1] = 0;
+            ctx->ex_none_cols[0] = ctx->ex_none_cols[1] = 0;
             ctx->ex_cand = nullptr; ctx->ex_cand_cap = 0;
             ctx->ex_none_host = false;
             RMT_TRY(es);

@@ -150,6 +150,7 @@ struct rmt_ctx {
     // optional (mac.hip box mode): the rows [ex_none_rows[0], ex_none_rows[1]) hold every
     // candidate target (the known plane is zero outside them); je <= jb: every row
     int ex_none_rows[2] = {0, 0};
+    int ex_none_cols[2] = {0, 0};   // (and the 64-column words [c0, c1) of those rows)
     // optional (mac.hip): a candidate list of ex_cand_cap cells + its counter, for the
     // no-op test's fit-per-wave form (k_ex_cand / k_ex_none_list) under ex_none_wide
     int *ex_cand = nullptr;
