@@ -78,9 +78,9 @@ int rmt_ctx_kernel_ms(rmt_ctx *ctx, double *ms2);
  * dct_rocfft, transpose2, sim_hiprio, sim_sync, early_geometry, early_transpose, fused_fluid,
  * no_overlap, side_tail, par_overlap, fused_fixprep, merged_join, test_delay_side,
  * test_delay_main, chain_cols, chain_layer_groups, edge_slots, edge_stream, sl_phi,
- * mac_boxes, skip_marked_rows, tail_stream, diag_first, mac_noop_host, mac_face_sl.  Set them
- * before creating a sim or slab on the context (sim_hiprio is read at rmt_sim_create); a change ends
- * a carried step state.
+ * mac_boxes, skip_marked_rows, tail_stream, diag_first, mac_noop_host, mac_face_sl,
+ * mac_m2_bound.  Set them before creating a sim or slab on the context (sim_hiprio is read
+ * at rmt_sim_create); a change ends a carried step state.
  * Unknown name: RMT_EINVAL. */
 int rmt_ctx_set_option(rmt_ctx *ctx, const char *name, int value);
 int rmt_ctx_get_option(rmt_ctx *ctx, const char *name, int *value);

@@ -512,9 +512,11 @@ __global__ void __launch_bounds__(RED_T) k_mac_correct_um(const double *__restri
                                                           double dx, double dy, double c0,
                                                           double *__restrict__ u,
                                                           double *__restrict__ v,
-                                                          double *__restrict__ part) {
+                                                          double *__restrict__ part,
+                                                          double *__restrict__ partv = nullptr) {
+    // partv (nullable): the same NaN-propagating max |v| partials (k_m2_bound)
     __shared__ double s[RED_T];
-    double acc = 0.0;
+    double acc = 0.0, accv = 0.0;
     const long nuf = (long)N * (N + 1), tot = 2 * nuf;
     // CU_U faces per trip: their loads issued together, then written in face order (the max
     // is exact in any order)
@@ -550,7 +552,9 @@ __global__ void __launch_bounds__(RED_T) k_mac_correct_um(const double *__restri
                 const long q = t - nuf;
                 const int j = dv32(q, N);
                 const double g = (j == 0 || j == N) ? 0.0 : (p1[m] - p0[m]) / dy;
-                v[q] = a[m] - c0 * g;
+                const double y = a[m] - c0 * g;
+                v[q] = y;
+                accv = nanmax(accv, fabs(y));
             }
         }
     }
@@ -561,6 +565,42 @@ __global__ void __launch_bounds__(RED_T) k_mac_correct_um(const double *__restri
         __syncthreads();
     }
     if (threadIdx.x == 0) part[blockIdx.x] = s[0];
+    if (!partv) return;
+    __syncthreads();
+    s[threadIdx.x] = accv;
+    __syncthreads();
+    for (int w = RED_T / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) s[threadIdx.x] = nanmax(s[threadIdx.x], s[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partv[blockIdx.x] = s[0];
+}
+// The next step's SL bound from the correction's face maxima (u, v unchanged since): a cell
+// centre value is the mean of two faces, so |u_c| <= max |u|, |v_c| <= max |v| and
+// m2 = max|u|^2 + max|v|^2 bounds max(u_c^2 + v_c^2) -- the block-skip certificate only needs
+// a bound, and a looser one only skips fewer tiles (the same values either way).  The
+// non-finite flag: a face NaN / inf makes the max NaN / inf (a centre value is then
+// non-finite as well; two finite faces whose sum overflows are the one case not flagged).
+__global__ void __launch_bounds__(1024) k_m2_bound(const double *__restrict__ pu,
+                                                   const double *__restrict__ pv, int G,
+                                                   int *__restrict__ bad, double *__restrict__ out) {
+    __shared__ double s[2][1024];
+    double a = 0.0, b = 0.0;
+    for (int k = threadIdx.x; k < G; k += 1024) { a = nanmax(a, pu[k]); b = nanmax(b, pv[k]); }
+    s[0][threadIdx.x] = a; s[1][threadIdx.x] = b;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            s[0][threadIdx.x] = nanmax(s[0][threadIdx.x], s[0][threadIdx.x + w]);
+            s[1][threadIdx.x] = nanmax(s[1][threadIdx.x], s[1][threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double mu = s[0][0], mv = s[1][0];
+        if (!(isfinite(mu) && isfinite(mv))) atomicOr(bad, 1);
+        *out = mu * mu + mv * mv;
+    }
 }
 
 // per-disc centroid sums over phi <= 0 (x, y, count) and max|u| partials (u nullable: the
@@ -633,7 +673,8 @@ __global__ void __launch_bounds__(MS_TPB) k_mac_diag(DiscSet D, const double *__
 
 static int mac_project_impl(rmt_ctx *ctx, const double *us, const double *vs, double dx,
                             double dy, double dt, double rho, double *u, double *v, double *phi,
-                            double *rhs, bool plan = true, double *umax_part = nullptr) {
+                            double *rhs, bool plan = true, double *umax_part = nullptr,
+                            double *vmax_part = nullptr) {
     const int N = ctx->nx;
     const long nf = (long)N * (N + 1);
     if (plan) RMT_TRY(dct2_plan(ctx, N, N, dx, dy));
@@ -648,7 +689,7 @@ static int mac_project_impl(rmt_ctx *ctx, const double *us, const double *vs, do
     RMT_TRY(dct2_solve(ctx, rhs, phi, root, (double)N * N));
     if (umax_part)
         k_mac_correct_um<<<MP_BLOCKS, RED_T, 0, ctx->stream>>>(us, vs, phi, N, dx, dy, dt / rho,
-                                                                u, v, umax_part);
+                                                                u, v, umax_part, vmax_part);
     else
         k_mac_correct<<<grid1d(2 * nf, 256), 256, 0, ctx->stream>>>(us, vs, phi, N, dx, dy,
                                                                     dt / rho, u, v,
@@ -672,6 +713,7 @@ struct rmt_mac_sim {
     int *flags;
     int2 *bres;                  // per-block column extents of the box passes (box_fold)
     double *mpart;               // per-block maxima of the fused reduction passes
+    double *mpartv;              // (the correction's max |v| partials: k_m2_bound)
     int *dbox;                   // [K][4] device support boxes (k_box_reduce), host copy:
     int hbox[RMT_MAC_MAXD][4];
     double t = 0;
@@ -761,7 +803,8 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     S->ctx = ctx; S->P = *prm;
     const long n = (long)N * N, nf = (long)N * (N + 1);
     const int K = prm->n_discs;
-    const size_t dbl = 5 * nf + (9 + 3 * K) * n + 2 * N + (2 + MD_VALS) * MS_BLOCKS + 64 + 32 + MP_BLOCKS;
+    const size_t dbl = 5 * nf + (9 + 3 * K) * n + 2 * N + (2 + MD_VALS) * MS_BLOCKS + 64 + 32 +
+                       2 * MP_BLOCKS;
     RMT_HIP(hipMalloc(&S->block, dbl * 8 + 64));
     RMT_HIP(hipMemsetAsync(S->block, 0, dbl * 8 + 64, ctx->stream));
     double *q = (double *)S->block;
@@ -784,6 +827,7 @@ int rmt_mac_sim_create(rmt_ctx *ctx, const rmt_mac_params *prm, rmt_mac_sim **ou
     S->part = q; q += (2 + MD_VALS) * MS_BLOCKS;   // J range, then centroid partials
     S->out = q; q += 32;
     S->mpart = q; q += MP_BLOCKS;
+    S->mpartv = q; q += MP_BLOCKS;
     S->dbox = (int *)q; q += 4 * RMT_MAC_MAXD / 2;
     S->flags = (int *)q;
     // index-grid coordinates (mac_multi_disc_lid.py:41): Xg = arange(N) * dx
@@ -865,13 +909,18 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         // with max |u_c|^2, which bounds every velocity sample of the backtraces (the SL
         // block skip)
         const bool face_sl = ctx->opt.mac_face_sl != 0;
-        if (face_sl)
+        // within a call the previous step's correction has the face maxima (m2_bound)
+        const bool m2b = face_sl && it > 0 && ctx->opt.mac_m2_bound != 0;
+        if (m2b)
+            k_m2_bound<<<1, 1024, 0, st>>>(S->mpart, S->mpartv, MP_BLOCKS, S->flags, S->out + 8);
+        else if (face_sl)
             k_mac_centres_m2<false><<<MP_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc,
                                                                  S->flags, S->mpart);
         else
             k_mac_centres_m2<true><<<MP_BLOCKS, RED_T, 0, st>>>(S->u, S->v, N, S->uc, S->vc,
                                                                 S->flags, S->mpart);
-        k_max_partials<false><<<1, 1024, 0, st>>>(S->mpart, MP_BLOCKS, -INFINITY, S->out + 8);
+        if (!m2b)
+            k_max_partials<false><<<1, 1024, 0, st>>>(S->mpart, MP_BLOCKS, -INFINITY, S->out + 8);
         RMT_LAUNCHED();
         for (int k = 0; k < K; ++k) {
             int cb[4] = {0, N, 0, N};   // the cells this disc's passes cover
@@ -951,7 +1000,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         RMT_LAUNCHED();
         // max |u| from the correction's pass, folded on the device into out[9]
         RMT_TRY(mac_project_impl(ctx, S->us, S->vs, dx, dx, dt, P.rho, S->u, S->v, S->p,
-                                 S->X1n, true, S->mpart));
+                                 S->X1n, true, S->mpart, S->mpartv));
         k_max_partials<true><<<1, 1024, 0, st>>>(S->mpart, MP_BLOCKS, 0.0, S->out + 9);
         int dr0 = 0, dr1 = N;   // the rows holding every box
         if (D.bx.n) {

@@ -43,6 +43,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"diag_first", "RMT_DIAG_FIRST", &rmt_opts::diag_first},
     {"mac_noop_host", "RMT_MAC_NOOP_HOST", &rmt_opts::mac_noop_host},
     {"mac_face_sl", "RMT_MAC_FACE_SL", &rmt_opts::mac_face_sl},
+    {"mac_m2_bound", "RMT_MAC_M2_BOUND", &rmt_opts::mac_m2_bound},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;

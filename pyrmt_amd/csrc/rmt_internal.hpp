@@ -107,6 +107,7 @@ struct rmt_opts {
     int diag_first = 0;       // RMT_DIAG_FIRST: the step's diagnostics ahead of the next geometry
     int mac_noop_host = 1;    // RMT_MAC_NOOP_HOST: MAC extrapolation's no-op verdict read on the host
     int mac_face_sl = 1;      // RMT_MAC_FACE_SL: MAC advection samples the face planes (no centre planes)
+    int mac_m2_bound = 1;     // RMT_MAC_M2_BOUND: MAC SL bound from the last correction's face maxima
 };
 
 #ifndef RMT_EDGE_SLOTS

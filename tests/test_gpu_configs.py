@@ -214,7 +214,7 @@ def test_config5_schedule_switches_are_bit_identical(gpu):
     import gc
     from pyrmt_amd.mac import MacMultiDisc
     out = []
-    for opts in ({}, {"mac_noop_host": 0, "mac_face_sl": 0}):
+    for opts in ({}, {"mac_noop_host": 0, "mac_face_sl": 0, "mac_m2_bound": 0}):
         sim = MacMultiDisc(8192, n_discs=3, seed=3, options=opts or None)
         sim.step(3)
         d = sim.diagnostics()

@@ -103,10 +103,13 @@ def test_mac_box_mode_is_bit_identical(M, N, calls):
     starts from a full pass; the boxes then come back with the per-step diagnostics).  Also
     the no-op verdict kept on the device (mac_noop_host = 0: every extrapolation pass launched
     and exiting on the device flag) against the default host read-back, and the advection
-    through the cell-centre planes (mac_face_sl = 0) against its default face sampling."""
+    through the cell-centre planes (mac_face_sl = 0) against its default face sampling, and
+    the SL certificate's exact max |u_c|^2 pass (mac_m2_bound = 0) against the face-maxima
+    bound the correction leaves."""
     out = []
     for opts in ({"mac_boxes": 0}, {"mac_boxes": 1}, {"mac_boxes": 1, "mac_noop_host": 0},
-                 {"mac_boxes": 1, "mac_face_sl": 0}, {"mac_boxes": 0, "mac_face_sl": 0}):
+                 {"mac_boxes": 1, "mac_face_sl": 0}, {"mac_boxes": 0, "mac_face_sl": 0},
+                 {"mac_boxes": 1, "mac_m2_bound": 0}):
         sim = M.MacMultiDisc(N, n_discs=3, seed=3, options=opts)
         for c in calls:
             sim.step(c)
