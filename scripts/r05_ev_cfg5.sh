@@ -13,8 +13,8 @@ run kt5 300 --kernel-trace --stats -T -f csv -d "$O/kt5" -o kt -- $B5 --steps 4 
 run f5 200 --pmc FETCH_SIZE --kernel-trace -T -f csv -d "$O/f5" -o f -- $B5 --steps 3 --warmup 1
 run w5 200 --pmc WRITE_SIZE --kernel-trace -T -f csv -d "$O/w5" -o w -- $B5 --steps 3 --warmup 1
 rev=$(cat .git_rev 2>/dev/null || echo unknown)
-python3 tools/pmc_traffic.py "$O/f5" "$O/w5" "$O/pmc_traffic_cfg5_n8192.json" "$rev" k_mac_centres_m2 | head -8
+python3 tools/pmc_traffic.py "$O/f5" "$O/w5" "$O/pmc_traffic_cfg5_n8192.json" "$rev" k_mac_centres_m2,k_m2_bound | head -8
 f=$(find "$O/kt5" -name "*kernel_stats.csv" | head -1); cp "$f" "$O/kt_stats_cfg5.csv"
 t=$(find "$O/kt5" -name "*kernel_trace.csv" | head -1)
-python3 tools/step_window.py "$t" 2 k_mac_centres_m2 > "$O/step_window_cfg5.txt" && tail -1 "$O/step_window_cfg5.txt"
+python3 tools/step_window.py "$t" 1 k_m2_bound > "$O/step_window_cfg5.txt" && tail -1 "$O/step_window_cfg5.txt"
 echo done
