@@ -32,7 +32,7 @@ run f3 200 --pmc FETCH_SIZE --kernel-trace -T -f csv -d "$O/f3" -o f -- $B3 --st
 run w3 200 --pmc WRITE_SIZE --kernel-trace -T -f csv -d "$O/w3" -o w -- $B3 --steps 4 --warmup 1
 rev=$(cat .git_rev 2>/dev/null || echo unknown)
 python3 tools/pmc_traffic.py "$O/f4" "$O/w4" "$O/pmc_traffic_n4096.json" "$rev" | head -8
-python3 tools/pmc_traffic.py "$O/f5" "$O/w5" "$O/pmc_traffic_cfg5_n8192.json" "$rev" k_mac_centres_m2 | head -3
+python3 tools/pmc_traffic.py "$O/f5" "$O/w5" "$O/pmc_traffic_cfg5_n8192.json" "$rev" k_mac_centres_m2,k_m2_bound | head -3
 python3 tools/pmc_traffic.py "$O/f3" "$O/w3" "$O/pmc_traffic_cfg3_n1024.json" "$rev" | head -3
 python3 tools/f64_roof.py "$O" "$O/f64_roof_n4096.json" "$rev" | tail -2
 for c in 4 5 3; do
@@ -41,5 +41,5 @@ done
 t=$(find "$O/kt4" -name "*kernel_trace.csv" | head -1)
 python3 tools/step_window.py "$t" 12 > "$O/step_window_n4096.txt" && tail -1 "$O/step_window_n4096.txt"
 t=$(find "$O/kt5" -name "*kernel_trace.csv" | head -1)
-python3 tools/step_window.py "$t" 2 k_mac_centres_m2 > "$O/step_window_cfg5.txt" && tail -1 "$O/step_window_cfg5.txt"
+python3 tools/step_window.py "$t" 1 k_m2_bound > "$O/step_window_cfg5.txt" && tail -1 "$O/step_window_cfg5.txt"
 echo done
