@@ -701,7 +701,7 @@ __global__ void __launch_bounds__(EXW * 64) k_ex_sweep(ExSweep A, long long *gpr
     }
     if (lane == 0) {
         atomicAdd(&A.status[0], filled);
-        if (!ok) atomicExch(&A.status[1], 1);
+        if (!ok) exa_report(A.status, exa_code(EXA_SWEEP, 0, 0));
         if constexpr (PROF)
             for (int k = 0; k < EX_NPROF; ++k) atomicAdd((unsigned long long *)&gprof[k], prof[k]);
     }
@@ -1015,8 +1015,24 @@ extern "C" int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, con
     int hs[2] = {0, 0};
     RMT_HIP(hipMemcpyAsync(hs, dst, sizeof(hs), hipMemcpyDeviceToHost, ctx->stream));
     RMT_HIP(hipStreamSynchronize(ctx->stream));
-    RMT_CHECK(!hs[1], RMT_EDEVICE, "extrapolation aborted (progress wait timed out)");
+    RMT_CHECK(!hs[1], RMT_EDEVICE, rmt::extrap_abort_detail(hs[1]));
     return RMT_OK;
+}
+
+std::string rmt::extrap_abort_detail(int code) {
+    std::string m = "extrapolation aborted (progress wait timed out)";
+    if (!(code & rmt::EXA_TAG)) return m;   // (a test's forced abort, or an older word)
+    static const char *kinds[] = {"?", "ring throttle", "record guard", "far source",
+                                  "local source", "critical source", "wave sequence",
+                                  "relink order", "fallback sweep", "parallel combine"};
+    const int kind = (code >> 26) & 15, part = (code >> 22) & 15, id = code & 0x3fffff;
+    m += ": ";
+    m += kind < 10 ? kinds[kind] : "?";
+    m += ", part " + std::to_string(part);
+    if (kind == rmt::EXA_FAR) m += ", producer slot " + std::to_string(id);
+    else if (kind == rmt::EXA_LOCAL || kind == rmt::EXA_CRIT) m += ", producer ordinal " + std::to_string(id);
+    else m += ", fit ordinal " + std::to_string(id);
+    return m;
 }
 
 extern "C" int rmt_extrap_set_mode(int mode) {

@@ -447,7 +447,7 @@ __global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
             long spin = 0;
             while (freeg[slot] != gi) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spin > SPIN) { if (lane == 0) atomicExch(ws.status + 1, 1); return; }
+                if (++spin > SPIN) { if (lane == 0) exa_report(ws.status, exa_code(EXA_PAR, 0, 0)); return; }
             }
             const double *src = ws.spk + (long)(s0 + gi) * PX_PB;
             double v[PX_PB / 64];
@@ -485,7 +485,7 @@ __global__ void __launch_bounds__(64 * (PX_NP + 1)) k_px_comb(ExWs ws, int L,
         if (rd != gi) {
             long spin = 0;
             while (ready[slot] != gi)
-                if (++spin > SPIN) { if (lane == 0) atomicExch(ws.status + 1, 1); return; }
+                if (++spin > SPIN) { if (lane == 0) exa_report(ws.status, exa_code(EXA_PAR, 0, 0)); return; }
             read_block();
         }
         const int nF = (int)h0, nL = (int)h1, kind = (int)h2, lo = (int)h3, n = (int)h4;

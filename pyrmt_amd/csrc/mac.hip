@@ -1025,7 +1025,7 @@ int rmt_mac_sim_step(rmt_mac_sim *S, int nsteps, double t_end) {
         RMT_HIP(hipStreamSynchronize(st));
         RMT_CHECK(!fl[0] && !fl[1], RMT_ENONFINITE,
                   "advect_reference_map: non-finite velocity (the simulation diverged)");
-        RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
+        RMT_CHECK(!fl[3], RMT_EDEVICE, extrap_abort_detail(fl[3]));
         S->t += dt;
         rmt_mac_diag r{};
         r.t = S->t; r.dt = dt; r.n_discs = K;

@@ -32,6 +32,8 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"merged_join", "RMT_MERGED_JOIN", &rmt_opts::merged_join},
     {"test_delay_side", "RMT_TEST_DELAY_SIDE", &rmt_opts::test_delay_side},
     {"test_delay_main", "RMT_TEST_DELAY_MAIN", &rmt_opts::test_delay_main},
+    {"test_delay_geo", "RMT_TEST_DELAY_GEO", &rmt_opts::test_delay_geo},
+    {"test_nowait_drop", "RMT_TEST_NOWAIT_DROP", &rmt_opts::test_nowait_drop},
     {"chain_cols", "RMT_CH_PARTS", &rmt_opts::ch_cols},
     {"chain_layer_groups", "RMT_CH_LAYERS", &rmt_opts::ch_lgroups},
     {"edge_slots", "RMT_EDGE_SLOTS_USED", &rmt_opts::edge_slots},
@@ -53,6 +55,7 @@ static rmt_opts opts_from_env() {
     if (const char *e = getenv("RMT_EX_ARENA")) o.ex_arena_bump = !strcmp(e, "bump");
     o.test_delay_side = std::max(0, o.test_delay_side);
     o.test_delay_main = std::max(0, o.test_delay_main);
+    o.test_delay_geo = std::max(0, o.test_delay_geo);
     return o;
 }
 

@@ -95,6 +95,9 @@ struct rmt_opts {
     int merged_join = 1;      // RMT_MERGED_JOIN
     int test_delay_side = 0;  // RMT_TEST_DELAY_SIDE: sleep units on the second stream (tests)
     int test_delay_main = 0;  // RMT_TEST_DELAY_MAIN: ... on the main stream (tests)
+    int test_delay_geo = 0;   // RMT_TEST_DELAY_GEO: ... ahead of a slab's early geometry (tests)
+    int test_nowait_drop = 0; // RMT_TEST_NOWAIT_DROP: a dropped slab geometry is not waited for
+                              // (the pre-fix behaviour, to show the hazard the wait removes)
     int ch_cols = 2;          // RMT_CH_PARTS: chain workgroups per layer group (column ranges)
     int ch_lgroups = 0;       // RMT_CH_LAYERS: chain layer groups (0: one per layer)
     int edge_slots = 64;      // RMT_EDGE_SLOTS_USED: edge-tile lists kept (1..64; fewer evict)
@@ -781,6 +784,9 @@ int extrap_geometry(rmt_ctx *ctx, const double *X1, const double *X2, const doub
                     const unsigned long long *kin);
 // the extrapolation's device status words {fitted, aborted} (valid until the next geometry)
 const int *extrap_status(rmt_ctx *ctx, int max_layers);
+// the error message for a nonzero abort word (status[1]; extrap.hpp EXA_*): what timed out,
+// in which chain part, waiting for which producer
+std::string extrap_abort_detail(int code);
 int extrap_finish(rmt_ctx *ctx, double dx, double dy, int max_layers, double *X1o, double *X2o,
                   int *dev_status);
 // the fallback sweep of the last extrap_finish on stream s (ctx->ex_sweep_defer), ordered after

@@ -863,7 +863,7 @@ static int sim_record(rmt_sim *S, const double *dv, double m2, double dt, const 
     const rmt_sim_params &P = S->P;
     RMT_CHECK(!fl[0], RMT_ENONFINITE, "advect_reference_map: non-finite velocity (the "
                                       "simulation diverged)");
-    RMT_CHECK(!fl[3], RMT_EDEVICE, "extrapolation sweep aborted (progress wait timed out)");
+    RMT_CHECK(!fl[3], RMT_EDEVICE, extrap_abort_detail(fl[3]));
     S->t += dt;
     rmt_diag r{};
     r.t = S->t; r.dt = dt;
@@ -1290,7 +1290,10 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 // they land in the ring slot this step's record takes below.  diag_first: ahead
                 // of the geometry, beside the latency-bound fix-up stages (behind it they
                 // overlapped the projection's DCT passes)
-                const bool early_diag = side_tail && S->split_proj && !P.energies;
+                // J is final here only with the fused fix-up prep (it writes J and records e_kb
+                // on completion); without it momentum_fixup's prep writes J on the main stream
+                // later, so the diagnostics stay in the tail
+                const bool early_diag = fixprep && side_tail && S->split_proj && !P.energies;
                 auto diag_now = [&]() {
                     DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1n, S->X2n, ny, nx,
                                P.energies, P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s,

@@ -305,7 +305,8 @@ class DistributedSim:
     """
 
     def __init__(self, N, comm, *, bc_kind, lid, disc, mu_s, kappa, rho_s, eta_s, mu_f,
-                 rho_f, w_t, layers, cfl, dt_cap, stress_band=False, detg_clamp=3.0):
+                 rho_f, w_t, layers, cfl, dt_cap, stress_band=False, detg_clamp=3.0,
+                 options=None):
         torch = F._torch()
         self.torch, self.comm, self.N, self.G = torch, comm, N, comm.G
         self.X, self.Y, self.dx, self.dy = F.create_grid(N, N, 1.0, 1.0)
@@ -322,7 +323,12 @@ class DistributedSim:
         self.params, self.cfl = P, cfl
         self.rsplits = even_splits(N, self.G, HALO)
         self.csplits = even_splits(N, self.G, 2)
-        self.ctx = F.ctx_for(N, N)
+        if options:
+            self.ctx = F._Ctx(N, N, torch.cuda.current_device())
+            for k, v in options.items():
+                self.ctx.set_option(k, v)
+        else:
+            self.ctx = F.ctx_for(N, N)
         self.slabs = [Slab(self.ctx, P, self.G, r, self.rsplits, self.csplits)
                       for r in comm.ranks]
         self.dt_const = self.slabs[0].dt_const
@@ -643,7 +649,10 @@ class DistributedSim:
         if fl & 2:
             raise L.RMTError("slab step: a departure point left the halo rows")
         if fl & 4:
-            raise L.RMTError("extrapolation sweep aborted (progress wait timed out)")
+            who = [f"slab {k}: " + abort_detail(int(-sc[k, SC_FIT]))
+                   for k in range(sc.shape[0]) if int(sc[k, SC_FLAGS]) & 4]
+            raise L.RMTError("extrapolation sweep aborted (progress wait timed out; "
+                             + "; ".join(who) + ")")
         d = sc[:, SC_DIAG:SC_DIAG + 10]
         sx, sy, cnt = (float(sum(d[:, k])) for k in (0, 1, 2))
         self.m2 = float(sc[:, SC_M2].max())
@@ -661,18 +670,36 @@ class DistributedSim:
 _STATE = ("u", "v", "p", "X1", "X2")   # a step's inputs (owned rows; the halo is exchanged)
 
 
+_ABORT_KINDS = ("?", "ring throttle", "record guard", "far source", "local source",
+                "critical source", "wave sequence", "relink order", "fallback sweep",
+                "parallel combine")
+
+
+def abort_detail(code):
+    """The extrapolation's abort word (csrc/extrap.hpp EXA_*: tag | kind << 26 | part << 22 |
+    id), as extrap_abort_detail (extrap.hip) words it: what timed out, in which chain part,
+    waiting for which producer."""
+    if not code & (1 << 30):
+        return "abort word %d" % code
+    kind, part, ident = (code >> 26) & 15, (code >> 22) & 15, code & 0x3FFFFF
+    what = {3: "producer slot", 4: "producer ordinal", 5: "producer ordinal"}.get(kind, "fit ordinal")
+    name = _ABORT_KINDS[kind] if kind < len(_ABORT_KINDS) else "?"
+    return f"{name}, part {part}, {what} {ident}"
+
+
 def _rim_capacity(count):
     """Rim entries moved per slab by the asynchronous step: 1.5x the largest slab rim seen,
     rounded up to 4096 (a slab's rim grows by a few cells per step)."""
     return int(-(-int(1.5 * float(count) + 4096) // 4096) * 4096)
 
 
-def soft_disc_in_lid_driven(N, comm):
+def soft_disc_in_lid_driven(N, comm, options=None):
     """Configs 2/4 physics (soft_disc_in_lid_driven.py:165-199), decomposed over comm.G
-    slabs, from the driver's initial condition."""
+    slabs, from the driver's initial condition.  options: implementation switches of a
+    context of the slabs' own (rmt_ctx_set_option), as simulation.Simulation takes them."""
     from .simulation import soft_disc_params, initial_disc_map
     kw = soft_disc_params(N)
-    sim = DistributedSim(N, comm, **kw)
+    sim = DistributedSim(N, comm, options=options, **kw)
     X1, X2 = initial_disc_map(N, *kw["disc"], kw["layers"])
     z = np.zeros((N, N))
     sim.set_state(u=z, v=z, p=z, X1=X1, X2=X2)

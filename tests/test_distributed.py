@@ -226,3 +226,36 @@ def test_slab_async_rim_overflow_reruns_window(gpu):
     for f in ("u", "v", "p", "X1", "X2"):
         np.testing.assert_array_equal(sim.gather(f), ref.get(f), err_msg=f)
     np.testing.assert_array_equal(d["maxJ"], r["maxJ"])
+
+
+@pytest.mark.gpu
+def test_slab_rerun_after_late_dropped_geometry(gpu):
+    """VERDICT r5 weak 3, hypothesis (a).  A window whose rim outgrows the capacity ends with
+    the next step's extrapolation geometry queued on each slab's second stream; the rerun
+    drops it and runs its first extrapolation in the same workspace.  test_delay_geo starts
+    every slab geometry ~10 ms late, so the dropped one is still pending when the rerun begins:
+    rmt_slab_drop_geometry makes the main stream wait for it, and the run stays bit-identical
+    to the fused step (before that wait, nothing ordered the two)."""
+    from pyrmt_amd import distributed as D
+    N, K = 256, 10
+    ref = _fused(gpu, N, K)
+    sim = D.soft_disc_in_lid_driven(N, D.LocalComm(2), options={"test_delay_geo": 3000})
+    sim.sync_every = 4
+    sim.step(2)
+    sim._rim_cap = 1            # the next window overflows and reruns
+    sim.step(K - 2)
+    assert getattr(sim, "reruns", 0) >= 1
+    d, r = sim.diagnostics(), ref.diagnostics()
+    np.testing.assert_array_equal(d["dt"], r["dt"])
+    for f in ("u", "v", "p", "X1", "X2"):
+        np.testing.assert_array_equal(sim.gather(f), ref.get(f), err_msg=f)
+    np.testing.assert_array_equal(d["maxJ"], r["maxJ"])
+
+
+def test_abort_word_detail():
+    """The extrapolation's abort word (csrc/extrap.hpp EXA_*) decoded as the host reports it."""
+    from pyrmt_amd.distributed import abort_detail
+    code = (1 << 30) | (3 << 26) | (5 << 22) | 1234
+    assert abort_detail(code) == "far source, part 5, producer slot 1234"
+    assert abort_detail((1 << 30) | (1 << 26) | 77) == "ring throttle, part 0, fit ordinal 77"
+    assert abort_detail(1) == "abort word 1"

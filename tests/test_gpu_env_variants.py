@@ -93,6 +93,7 @@ def _same(got, ref):
     {"edge_stream": 0}, {"sl_phi": 0}, {"sl_phi": 0, "fused_fluid": 0},
     {"edge_stream": 0, "sl_phi": 0, "test_delay_side": 300}, {"skip_marked_rows": 0},
     {"tail_stream": 0}, {"tail_stream": 1, "test_delay_side": 300}, {"diag_first": 1},
+    {"fused_fixprep": 0, "diag_first": 1},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(default_run, opts):
     _same(_run(opts), default_run)
