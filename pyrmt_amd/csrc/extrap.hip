@@ -1022,16 +1022,12 @@ extern "C" int rmt_extrapolate_reference_map(rmt_ctx *ctx, const double *X1, con
 std::string rmt::extrap_abort_detail(int code) {
     std::string m = "extrapolation aborted (progress wait timed out)";
     if (!(code & rmt::EXA_TAG)) return m;   // (a test's forced abort, or an older word)
-    static const char *kinds[] = {"?", "ring throttle", "record guard", "far source",
-                                  "local source", "critical source", "wave sequence",
-                                  "relink order", "fallback sweep", "parallel combine"};
+    static const char *kinds[] = {"?", "chain", "?", "?", "?", "?", "?", "relink order",
+                                  "fallback sweep", "parallel combine"};
     const int kind = (code >> 26) & 15, part = (code >> 22) & 15, id = code & 0x3fffff;
     m += ": ";
     m += kind < 10 ? kinds[kind] : "?";
-    m += ", part " + std::to_string(part);
-    if (kind == rmt::EXA_FAR) m += ", producer slot " + std::to_string(id);
-    else if (kind == rmt::EXA_LOCAL || kind == rmt::EXA_CRIT) m += ", producer ordinal " + std::to_string(id);
-    else m += ", fit ordinal " + std::to_string(id);
+    m += " part " + std::to_string(part) + ", fit ordinal " + std::to_string(id);
     return m;
 }
 

@@ -35,12 +35,12 @@ enum { EXC_FALLBACK = 0, EXC_ABORT = 1, EXC_FILLED = 2, EXC_ARENA = 4, EXC_REJ =
 // cross-part hand-off granules (gval) hold this signalling NaN until the fit is published: an
 // arithmetic result is never a signalling NaN (IEEE mode), so the value is its own flag
 constexpr unsigned long long CH_GSENT = 0x7ff00000000bad01ull;
-// The abort word (status[1]) names what timed out: EXA_TAG | kind << 26 | part << 22 | id,
-// id = the awaited producer (a local source's ordinal, a far source's global slot) or the
-// waiting fit's own ordinal; the first abort of a call wins (CAS from 0).  Host side:
-// extrap_abort_detail (rmt_internal.hpp).
-enum { EXA_THROTTLE = 1, EXA_RECORD = 2, EXA_FAR = 3, EXA_LOCAL = 4, EXA_CRIT = 5,
-       EXA_SEQ = 6, EXA_RELINK = 7, EXA_SWEEP = 8, EXA_PAR = 9 };
+// The abort word (status[1]) names what stopped: EXA_TAG | kind << 26 | part << 22 | id, with
+// id the ordinal (within its part) of the chain fit whose wait timed out; the first abort of
+// a call wins (CAS from 0).  Host side: extrap_abort_detail (rmt_internal.hpp).  (Naming the
+// kind of wait inside the chain's fit cost the kernel a register spill at 128 VGPRs, so the
+// chain reports its part and the stopped fit only.)
+enum { EXA_CHAIN = 1, EXA_RELINK = 7, EXA_SWEEP = 8, EXA_PAR = 9 };
 constexpr int EXA_TAG = 1 << 30;
 __device__ __forceinline__ int exa_code(int kind, int part, int id) {
     return EXA_TAG | (kind << 26) | ((part & 15) << 22) | (id < 0 ? 0x3fffff : min(id, 0x3fffff));

@@ -864,7 +864,7 @@ __device__ __forceinline__ double ch_fold_span(double acc, const double *row, in
 // registers -- never written to LDS -- and the terms after kc follow: the reference's order,
 // the same operations.
 template <bool PROF>
-__device__ __forceinline__ int ch_fit(int x, int lane, double *B, double2 *val, int *tag,
+__device__ __forceinline__ bool ch_fit(int x, int lane, double *B, double2 *val, int *tag,
                                         int *cur, int &wm, double &o_out, long &c_out,
                                         long long *pr, long long &tl, double *gval,
                                         int gslot, long long *trace = nullptr, int base = 0) {
@@ -877,7 +877,7 @@ __device__ __forceinline__ int ch_fit(int x, int lane, double *B, double2 *val, 
             m = min(m, __hip_atomic_load(&cur[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         wm = m;
         if (x - CH_R / 2 >= wm) {
-            if (++spins > CH_SPIN_LIMIT) return exa_code(EXA_THROTTLE, 0, x);
+            if (++spins > CH_SPIN_LIMIT) return false;
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -887,7 +887,7 @@ __device__ __forceinline__ int ch_fit(int x, int lane, double *B, double2 *val, 
     const int npad = __builtin_amdgcn_readfirstlane((int)(meta & 0xffffffff));
     const int nd = __builtin_amdgcn_readfirstlane((int)((meta >> 32) & 0x7fffffff));
     const bool pub = __builtin_amdgcn_readfirstlane((int)((unsigned long long)meta >> 63)) != 0;
-    if (npad > CH_TVS || nd > 64 || npad < 0 || nd < 0) return exa_code(EXA_RECORD, 0, x);   // bug guard
+    if (npad > CH_TVS || nd > 64 || npad < 0 || nd < 0) return false;   // bug guard
     const double *dyn = B + CH_HDR;
     double *tv = B + CH_HDR + 4 * nd;
     // wave-uniform solve constants, kept in SGPRs (scalar loads of the global record measured
@@ -944,12 +944,7 @@ __device__ __forceinline__ int ch_fit(int x, int lane, double *B, double2 *val, 
                 for (int off = 32; off > 0; off >>= 1) g = max(g, __shfl_xor(g, off));
                 tr_far = g;
             }
-            if (++sp > CH_SPIN_LIMIT) {   // name the missing producer (its global slot)
-                int g = far && !done ? -e.y - 1 : -1;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) g = max(g, __shfl_xor(g, off));
-                return exa_code(EXA_FAR, 0, g);
-            }
+            if (++sp > CH_SPIN_LIMIT) return false;
             __builtin_amdgcn_s_sleep(1);
         }
         if constexpr (PROF)
@@ -996,12 +991,7 @@ __device__ __forceinline__ int ch_fit(int x, int lane, double *B, double2 *val, 
                 done = true;
             }
             if (__ballot(!done) == 0 || (RMT_CH_ABL & 4)) break;
-            if (++sp > CH_SPIN_LIMIT) {
-                int g = !done ? e.y : -1;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) g = max(g, __shfl_xor(g, off));
-                return exa_code(EXA_LOCAL, 0, g);
-            }
+            if (++sp > CH_SPIN_LIMIT) return false;
         }
         __builtin_amdgcn_s_setprio(3);
         __builtin_amdgcn_wave_barrier();
@@ -1045,7 +1035,7 @@ __device__ __forceinline__ int ch_fit(int x, int lane, double *B, double2 *val, 
                                                                      __HIP_MEMORY_SCOPE_WORKGROUP));
             __builtin_amdgcn_sched_barrier(0);   // all three reads issued, then the tag test
             if (__builtin_amdgcn_readfirstlane(tg) == eyc || (RMT_CH_ABL & 4)) break;
-            if (++sp > CH_SPIN_LIMIT) return exa_code(EXA_CRIT, 0, eyc);
+            if (++sp > CH_SPIN_LIMIT) return false;
         }
         if constexpr (PROF) {
             if (sp) tr_crit = eyc;
@@ -1115,7 +1105,7 @@ __device__ __forceinline__ int ch_fit(int x, int lane, double *B, double2 *val, 
             t[4] = (threadIdx.x >> 6) | (blockIdx.x << 8); t[5] = c_out;
         }
     }
-    return 0;
+    return true;
 }
 
 template <bool PROF>
@@ -1145,7 +1135,7 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
     double2 d0, d1, d2, d3, d4;
     if (x < total) CH_LOAD(r);
     int wm = 0;
-    int code = 0;   // the abort word (extrap.hpp EXA_*), 0: ok
+    bool ok = true;
     long long pr[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tl = 0;
     if constexpr (PROF) tl = __builtin_amdgcn_s_memtime();
     double o = 0.0;      // previous fit's value (lane 0: X1, lane 3: X2) and cell
@@ -1163,22 +1153,22 @@ __global__ void __launch_bounds__(CH_W * 64) k_ex_chain(ChainArgs C, long long *
         const long long nx = __double_as_longlong(B[23]);
         const int x2 = __builtin_amdgcn_readfirstlane((int)(nx >> 32));
         const unsigned r2 = (unsigned)__builtin_amdgcn_readfirstlane((int)(nx & 0xffffffff));
-        if (x2 <= x) { code = exa_code(EXA_SEQ, 0, x); break; }   // bug guard: the wave's sequence must advance
+        if (x2 <= x) { ok = false; break; }   // bug guard: the wave's sequence must advance
         if (x2 < total) CH_LOAD(r2);
         CH_STAMP(6);
-        code = ch_fit<PROF>(x, lane, B, val, tag, cur, wm, o, c, pr, tl, C.ws.gval, base + x,
-                            C.trace, base);
-        if (code) break;
+        const bool fit_ok = ch_fit<PROF>(x, lane, B, val, tag, cur, wm, o, c, pr, tl,
+                                         C.ws.gval, base + x, C.trace, base);
+        if (!fit_ok) { ok = false; break; }
         x = x2; r = r2;
     }
     if constexpr (PROF)
         if (lane == 0)
             for (int k = 0; k < 12; ++k) atomicAdd((unsigned long long *)&gprof[k], pr[k]);
-    if (!code && c >= 0 && (lane == 0 || lane == CH_XL2)) (lane == 0 ? X1e : X2e)[c] = o;
+    if (ok && c >= 0 && (lane == 0 || lane == CH_XL2)) (lane == 0 ? X1e : X2e)[c] = o;
     __hip_atomic_store(&cur[wv], 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (code && lane == 0) {
+    if (!ok && lane == 0) {   // the abort word names this part and the waiting fit (extrap.hpp)
         C.ws.ctl[EXC_ABORT] = 1;
-        exa_report(C.status, code | (part << 22));
+        exa_report(C.status, exa_code(EXA_CHAIN, part, x));
     }
 }
 // ------------------------------------------------------------------ host side ------

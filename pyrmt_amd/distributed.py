@@ -670,21 +670,19 @@ class DistributedSim:
 _STATE = ("u", "v", "p", "X1", "X2")   # a step's inputs (owned rows; the halo is exchanged)
 
 
-_ABORT_KINDS = ("?", "ring throttle", "record guard", "far source", "local source",
-                "critical source", "wave sequence", "relink order", "fallback sweep",
+_ABORT_KINDS = ("?", "chain", "?", "?", "?", "?", "?", "relink order", "fallback sweep",
                 "parallel combine")
 
 
 def abort_detail(code):
     """The extrapolation's abort word (csrc/extrap.hpp EXA_*: tag | kind << 26 | part << 22 |
-    id), as extrap_abort_detail (extrap.hip) words it: what timed out, in which chain part,
-    waiting for which producer."""
+    id), as extrap_abort_detail (extrap.hip) words it: what stopped, in which chain part, at
+    which fit (its ordinal within the part)."""
     if not code & (1 << 30):
         return "abort word %d" % code
     kind, part, ident = (code >> 26) & 15, (code >> 22) & 15, code & 0x3FFFFF
-    what = {3: "producer slot", 4: "producer ordinal", 5: "producer ordinal"}.get(kind, "fit ordinal")
     name = _ABORT_KINDS[kind] if kind < len(_ABORT_KINDS) else "?"
-    return f"{name}, part {part}, {what} {ident}"
+    return f"{name} part {part}, fit ordinal {ident}"
 
 
 def _rim_capacity(count):

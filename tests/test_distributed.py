@@ -255,7 +255,7 @@ def test_slab_rerun_after_late_dropped_geometry(gpu):
 def test_abort_word_detail():
     """The extrapolation's abort word (csrc/extrap.hpp EXA_*) decoded as the host reports it."""
     from pyrmt_amd.distributed import abort_detail
-    code = (1 << 30) | (3 << 26) | (5 << 22) | 1234
-    assert abort_detail(code) == "far source, part 5, producer slot 1234"
-    assert abort_detail((1 << 30) | (1 << 26) | 77) == "ring throttle, part 0, fit ordinal 77"
+    code = (1 << 30) | (1 << 26) | (5 << 22) | 1234
+    assert abort_detail(code) == "chain part 5, fit ordinal 1234"
+    assert abort_detail((1 << 30) | (8 << 26)) == "fallback sweep part 0, fit ordinal 0"
     assert abort_detail(1) == "abort word 1"
