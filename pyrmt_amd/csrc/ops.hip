@@ -46,6 +46,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"mac_noop_host", "RMT_MAC_NOOP_HOST", &rmt_opts::mac_noop_host},
     {"mac_face_sl", "RMT_MAC_FACE_SL", &rmt_opts::mac_face_sl},
     {"mac_m2_bound", "RMT_MAC_M2_BOUND", &rmt_opts::mac_m2_bound},
+    {"diag_seg", "RMT_DIAG_SEG", &rmt_opts::diag_seg},
 };
 static rmt_opts opts_from_env() {
     rmt_opts o;

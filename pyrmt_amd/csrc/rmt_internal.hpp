@@ -111,6 +111,8 @@ struct rmt_opts {
     int mac_noop_host = 1;    // RMT_MAC_NOOP_HOST: MAC extrapolation's no-op verdict read on the host
     int mac_face_sl = 1;      // RMT_MAC_FACE_SL: MAC advection samples the face planes (no centre planes)
     int mac_m2_bound = 1;     // RMT_MAC_M2_BOUND: MAC SL bound from the last correction's face maxima
+    int diag_seg = 1;         // RMT_DIAG_SEG: the step's diagnostics read only the segments that
+                              // can hold a solid cell or J != 1 (k_diag_seg)
 };
 
 #ifndef RMT_EDGE_SLOTS

@@ -67,6 +67,9 @@ struct rmt_sim {
     // the projection's row pass runs beside the chain; only the rows of the fix-up tiles
     // (+-1 for the Rhie-Chow stencil) are redone after it
     unsigned char *rowmark = nullptr;
+    // per 64 x 16 fix-up tile: listed this step (k_mark_rows; the diagnostics read those tiles
+    // whole, k_diag_seg)
+    unsigned char *tmark = nullptr;
     bool split_proj = false;
     // the advection split: the rim cells (within 7 of the known/unknown interface, all the
     // extrapolation reads) before the chain, the rest beside it on the second stream
@@ -574,12 +577,15 @@ __global__ void __launch_bounds__(256) k_dt_part(const double *__restrict__ part
 }
 // rows [16 ty - 1, 16 ty + 17) of every listed fix-up tile: the rows whose Rhie-Chow rhs
 // (u*, v* at j-1 .. j+1) the tile re-run can change
+// (tmark, nullable: the listed tiles themselves, one byte per tile)
 __global__ void k_mark_rows(const int *__restrict__ tiles, const int *__restrict__ count,
-                            int tiles_x, int ny, unsigned char *__restrict__ rowmark) {
+                            int tiles_x, int ny, unsigned char *__restrict__ rowmark,
+                            unsigned char *__restrict__ tmark = nullptr) {
     const int cnt = *count;
     for (int b = blockIdx.x; b < cnt; b += gridDim.x) {   // list_grid launch
         const int j = (tiles[b] / tiles_x) * MOM_TY - 1 + (int)threadIdx.x;
         if (threadIdx.x < MOM_TY + 2 && j >= 0 && j < ny) rowmark[j] = 1;
+        if (tmark && threadIdx.x == 0) tmark[tiles[b]] = 1;
     }
 }
 // completes a ring record after k_diag_p2 wrote its diagnostics: max |u|^2, dt, flags
@@ -600,6 +606,9 @@ struct DiagArgs {
     int ny, nx, energies;
     double dx, dy, w_t, rho_s, rho_f, mu_f, eta_s, mu_s, kappa;
     int jb, je;   // rows reduced (global indices; the whole grid: 0, ny)
+    // k_diag_seg (both set, energies off, nx % 64 == 0): this step's pure-fluid bits per
+    // (row, 64-column segment) from the SL pass and its fix-up tile marks
+    const unsigned char *fbits = nullptr, *tmark = nullptr;
 };
 // partial [sx, sy, cnt, Jmin, Jmax, ke, se, diss, ymin, ymax] per block
 __global__ void __launch_bounds__(DIAG_T) k_diag_p1(DiagArgs A, double *__restrict__ part) {
@@ -660,6 +669,82 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p1(DiagArgs A, double *__restri
         __syncthreads();
     }
     if (threadIdx.x < DIAG_VALS) part[blockIdx.x * DIAG_VALS + threadIdx.x] = s[threadIdx.x][0];
+}
+// k_diag_p1 (energies off) over the (row, 64-column segment) pieces that can hold a solid cell
+// or J != 1.  A segment whose cells are all fluid (phi > max(w_t, w_cut, 0), bit 0 of the SL
+// pass's fbits; NaN is not fluid) and that lies in no fix-up tile (where the fix-up prep
+// rewrote phi and J after that pass) holds no phi <= 0 cell and J == 1 in every cell (the
+// prep's value outside the stress region), so it adds nothing to the centroid sums and 1 to
+// the J extrema; its phi and J are not read.  Every other cell is visited once, as in
+// k_diag_p1: block b takes segments [b SPB, (b + 1) SPB) in order, a wave one quarter of them
+// (64-segment flag words by ballot), a lane one column; then k_diag_p1's block tree, so
+// k_diag_p2 reduces the same DIAG_BLOCKS partials.  The centroid sums add the same terms in
+// another order than k_diag_p1 (rounding-level differences of cx, cy; J extrema exact).
+__global__ void __launch_bounds__(DIAG_T) k_diag_seg(DiagArgs A, double *__restrict__ part) {
+    __shared__ double s[DIAG_VALS][DIAG_T];
+    double v[DIAG_VALS] = {0, 0, 0, INFINITY, -INFINITY, 0, 0, 0, INFINITY, -INFINITY};
+    const int W = A.nx >> 6, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int tiles_x = W;   // 64-column stage tiles: one segment wide
+    const long nseg = (long)(A.je - A.jb) * W, s0 = (long)A.jb * W;
+    const long spb = (nseg + DIAG_BLOCKS - 1) / DIAG_BLOCKS, spw = (spb + 3) / 4;
+    const long b0 = s0 + min(nseg, (long)blockIdx.x * spb), b1 = s0 + min(nseg, ((long)blockIdx.x + 1) * spb);
+    const long w0 = min(b1, b0 + wv * spw), w1 = min(b1, w0 + spw);
+    bool skipped = false;
+    for (long g = w0; g < w1; g += 64) {
+        const long sg = g + lane;
+        bool need = false;
+        if (sg < w1) {
+            const int j = (int)(sg / W), sx = (int)(sg - (long)j * W);
+            need = !A.fbits || !(A.fbits[sg] & 1) || A.tmark[(j / MOM_TY) * tiles_x + sx];
+            skipped = skipped || !need;
+        }
+        unsigned long long m = __ballot(need);
+        while (m) {
+            // up to 4 segments' loads in flight
+            long sq[4];
+            int nq = 0;
+            for (; nq < 4 && m; ++nq, m &= m - 1) sq[nq] = g + __builtin_ctzll(m);
+            double phq[4], Jq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const long c = k < nq ? sq[k] * 64 + lane : 0;
+                phq[k] = k < nq ? A.phi[c] : 0.0;
+                Jq[k] = k < nq ? A.J[c] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k >= nq) break;
+                const int j = (int)(sq[k] / W), i = (int)(sq[k] - (long)j * W) * 64 + lane;
+                if (phq[k] <= 0.0) {
+                    v[0] += A.xs[i]; v[1] += A.ys[j]; v[2] += 1.0;
+                    v[8] = fmin(v[8], A.ys[j]); v[9] = fmax(v[9], A.ys[j]);
+                }
+                v[3] = fmin(v[3], Jq[k]); v[4] = fmax(v[4], Jq[k]);
+            }
+        }
+    }
+    if (__ballot(skipped)) { v[3] = fmin(v[3], 1.0); v[4] = fmax(v[4], 1.0); }
+    for (int k = 0; k < DIAG_VALS; ++k) s[k][threadIdx.x] = v[k];
+    __syncthreads();
+    for (int w = DIAG_T / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < DIAG_VALS; ++k) {
+                double x = s[k][threadIdx.x], y = s[k][threadIdx.x + w];
+                s[k][threadIdx.x] = (k == 3 || k == 8) ? fmin(x, y) : (k == 4 || k == 9) ? fmax(x, y) : x + y;
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < DIAG_VALS) part[blockIdx.x * DIAG_VALS + threadIdx.x] = s[threadIdx.x][0];
+}
+// the step's diagnostics partials.  Energies off and nx % 64 == 0: k_diag_seg, whether or
+// not a step's fluid bits let it skip segments (fbits null: every segment) -- a skipped
+// segment adds nothing to any lane's sums, so every schedule gives the same bits; else (and
+// with the diag_seg switch off) k_diag_p1
+static void diag_partials(const DiagArgs &D, double *part, hipStream_t st, bool seg_on) {
+    if (seg_on && !D.energies && D.nx % 64 == 0 && MOM_TX == 64)
+        k_diag_seg<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, part);
+    else
+        k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, part);
 }
 __global__ void __launch_bounds__(DIAG_T) k_diag_p2(const double *__restrict__ part,
                                                     double *__restrict__ out) {
@@ -798,7 +883,8 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     const size_t Wn = (size_t)(nx + 63) / 64;
     RMT_HIP(hipMalloc(&S->m2part, ((size_t)S->m2n + (size_t)RING_N * RING_VALS + ny / 8 + 8 +
                                    (size_t)ny * Wn + ny / 2 + 8 + (size_t)ny * Wn +
-                                   (size_t)ny * ((nx + 255) / 256) / 2 + 8 + 8) * sizeof(double)));
+                                   (size_t)ny * ((nx + 255) / 256) / 2 + 8 + 8 +
+                                   (size_t)S->max_tiles / 8 + 8) * sizeof(double)));
     S->ring = S->m2part + S->m2n;
     S->rowmark = (unsigned char *)(S->ring + (size_t)RING_N * RING_VALS);
     S->rimw = (unsigned long long *)(S->ring + (size_t)RING_N * RING_VALS + ny / 8 + 8);
@@ -806,6 +892,7 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     S->kbits_next = (unsigned long long *)((double *)S->rimcnt + ny / 2 + 8);
     S->segs = (int *)(S->kbits_next + (size_t)ny * Wn);
     S->m2acc = (unsigned long long *)(S->segs + (((size_t)ny * ((nx + 255) / 256) + 3) & ~(size_t)1));
+    S->tmark = (unsigned char *)(S->m2acc + 8);   // max_tiles bytes
     RMT_HIP(hipMemsetAsync(S->m2acc, 0, 2 * sizeof(unsigned long long), ctx->stream));
     if (nx % 64 == 0) RMT_HIP(hipMalloc(&S->pconst, (size_t)ny * (nx / 64)));
     if (S->st2) {
@@ -938,7 +1025,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
     double *pend_e = nullptr;
     // the pending tail's diagnostics already ran (on the second stream after the next step's
     // geometry, beside the projection: they read phi and J only, final after the fix-up)
-    bool pend_diag_done = false, diag_early = false;
+    bool pend_diag_done = false, diag_early = false, pend_seg = false;
     // after_sl: the second stream already waits for this step's e_sl, recorded on the main
     // stream after the tail's projection -- no event of its own (a record right after the
     // velocity correction cost the critical path ~5 us); else one recorded now
@@ -976,7 +1063,12 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         tail_p = ts_st != S->st2;
         if (tail_p) RMT_HIP(hipEventRecord(S->e_tailp, ts_st));
         if (!pend_diag_done) {
-            k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, S->st2>>>(D, S->dscr);
+            // (this step's SL pass and fix-up marks come after this on the same stream)
+            if (pend_seg) {
+                D.fbits = fluid_bits_buf(mom_work(S->mw, (long)ny * nx, S->mbytes, S->flag + 1));
+                D.tmark = S->tmark;
+            }
+            diag_partials(D, S->dscr, S->st2, ctx->opt.diag_seg != 0);
             k_diag_p2<<<1, DIAG_T, 0, S->st2>>>(S->dscr, pend_e);
             RMT_LAUNCHED();
         }
@@ -1088,6 +1180,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         const bool par_ov = ctx->opt.par_overlap != 0;
         const bool overlap = solid && S->st2 && !no_overlap && (!par || par_ov);
         bool fixprep = false;   // the fused fix-up prep (set where the extrapolation runs)
+        bool seg_diag = false;  // this step's fbits and fix-up tile marks are set (k_diag_seg)
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
             // 2. advect the reference map with the pre-advection level set and mask
@@ -1181,10 +1274,13 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                 const int fs = extrap_fix_tiles(ctx, P.layers, 12, S->tiles, S->tcount);
                 ctx->stream = st;
                 RMT_TRY(fs);
+                const bool tm = ctx->opt.diag_seg != 0;
                 if (S->split_proj) {
                     RMT_HIP(hipMemsetAsync(S->rowmark, 0, ny, S->st2));
+                    if (tm) RMT_HIP(hipMemsetAsync(S->tmark, 0, S->max_tiles, S->st2));
                     k_mark_rows<<<list_grid(S->max_tiles), 64, 0, S->st2>>>(
-                        S->tiles, S->tcount, (nx + MOM_TX - 1) / MOM_TX, ny, S->rowmark);
+                        S->tiles, S->tcount, (nx + MOM_TX - 1) / MOM_TX, ny, S->rowmark,
+                        tm ? S->tmark : nullptr);
                     RMT_LAUNCHED();
                 }
                 MomWork Wf = W;
@@ -1207,6 +1303,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                         sl_phi ? nb : nullptr);
                     RMT_LAUNCHED();
                 }
+                seg_diag = sl_phi && S->split_proj && tm && !P.energies;
                 if (sl_phi) {
                     Wf.fluid_bits = fluid_bits_buf(W);
                 } else if (fl_ok) {
@@ -1298,7 +1395,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                     DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1n, S->X2n, ny, nx,
                                P.energies, P.dx, P.dy, P.w_t, P.rho_s, P.rho_f, P.mu_f, P.eta_s,
                                P.mu_s, P.kappa, 0, ny};
-                    k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, sg>>>(D, S->dscr);
+                    if (seg_diag) { D.fbits = fluid_bits_buf(W); D.tmark = S->tmark; }
+                    diag_partials(D, S->dscr, sg, ctx->opt.diag_seg != 0);
                     k_diag_p2<<<1, DIAG_T, 0, sg>>>(S->dscr, S->ring + (size_t)slot * RING_VALS);
                     diag_early = true;
                 };
@@ -1389,6 +1487,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             double *e = S->ring + (size_t)slot * RING_VALS;
             pend_e = e;
             pending = true;
+            pend_seg = seg_diag;
             pend_diag_done = diag_early;
             diag_early = false;
             ring_e = e;
@@ -1396,7 +1495,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             if (++slot == S->sync_every) RMT_TRY(flush());
             continue;
         }
-        k_diag_p1<<<DIAG_BLOCKS, DIAG_T, 0, st>>>(D, S->dscr);
+        diag_partials(D, S->dscr, st, ctx->opt.diag_seg != 0);
         if (async) {
             double *e = S->ring + (size_t)slot * RING_VALS;
             k_diag_p2<<<1, DIAG_T, 0, st>>>(S->dscr, e);

@@ -41,6 +41,11 @@ environment variables still set a new context's defaults.
                         ahead of its SL pass instead of beside it on the edge-tile stream
   diag_first=1          the step's diagnostics ahead of the next step's geometry instead of
                         behind it
+
+Every variant above runs the diagnostics through k_diag_seg (its segment skip adds nothing to
+any lane's sums, so the skip pattern does not change the bits).  diag_seg=0 (k_diag_p1's
+strided visit order: the same terms summed in another order) is compared separately:
+fields and J extrema exact, the centroid to rounding.
 """
 import os
 import subprocess
@@ -102,6 +107,16 @@ def test_schedule_switch_is_bit_identical(default_run, opts):
 @pytest.mark.parametrize("opts", [None, {"fused_fixprep": 0}], ids=["fixprep", "no_fixprep"])
 def test_forced_fallback_sweep_is_bit_identical(default_run, opts):
     _same(_run(opts, ex_mode=2), default_run)
+
+
+def test_diag_seg_switch(default_run):
+    got = _run({"diag_seg": 0})
+    for f in FIELDS:
+        np.testing.assert_array_equal(got[f], default_run[f], err_msg=f)
+    for k in ("d_minJ", "d_maxJ", "d_dt", "d_t"):
+        np.testing.assert_array_equal(got[k], default_run[k], err_msg=k)
+    for k in ("d_cx", "d_cy"):
+        np.testing.assert_allclose(got[k], default_run[k], rtol=1e-14, err_msg=k)
 
 
 def test_option_names_and_errors(gpu):
