@@ -676,8 +676,9 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_p1(DiagArgs A, double *__restri
 // rewrote phi and J after that pass) holds no phi <= 0 cell and J == 1 in every cell (the
 // prep's value outside the stress region), so it adds nothing to the centroid sums and 1 to
 // the J extrema; its phi and J are not read.  Every other cell is visited once, as in
-// k_diag_p1: block b takes segments [b SPB, (b + 1) SPB) in order, a wave one quarter of them
-// (64-segment flag words by ballot), a lane one column; then k_diag_p1's block tree, so
+// k_diag_p1: segments dealt to (block, wave, lane) round robin over the grid (64 flags per
+// wave by ballot, then up to 8 needed segments' loads in flight), a lane one column of each;
+// then k_diag_p1's block tree, so
 // k_diag_p2 reduces the same DIAG_BLOCKS partials.  The centroid sums add the same terms in
 // another order than k_diag_p1 (rounding-level differences of cx, cy; J extrema exact).
 __global__ void __launch_bounds__(DIAG_T) k_diag_seg(DiagArgs A, double *__restrict__ part) {
@@ -686,33 +687,34 @@ __global__ void __launch_bounds__(DIAG_T) k_diag_seg(DiagArgs A, double *__restr
     const int W = A.nx >> 6, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tiles_x = W;   // 64-column stage tiles: one segment wide
     const long nseg = (long)(A.je - A.jb) * W, s0 = (long)A.jb * W;
-    const long spb = (nseg + DIAG_BLOCKS - 1) / DIAG_BLOCKS, spw = (spb + 3) / 4;
-    const long b0 = s0 + min(nseg, (long)blockIdx.x * spb), b1 = s0 + min(nseg, ((long)blockIdx.x + 1) * spb);
-    const long w0 = min(b1, b0 + wv * spw), w1 = min(b1, w0 + spw);
+    // segment q of this block (q = 4 (64 c + lane) + wave, chunk c) is s0 + block + DIAG_BLOCKS q:
+    // every block and wave takes an even share of the grid (and of the disc's segments)
+    constexpr long STR = (long)DIAG_BLOCKS * DIAG_T;   // one chunk of every wave of every block
     bool skipped = false;
-    for (long g = w0; g < w1; g += 64) {
-        const long sg = g + lane;
+    for (long base = s0 + blockIdx.x + (long)DIAG_BLOCKS * wv; base < s0 + nseg; base += STR) {
+        const long sg = base + (long)DIAG_BLOCKS * 4 * lane;
         bool need = false;
-        if (sg < w1) {
+        if (sg < s0 + nseg) {
             const int j = (int)(sg / W), sx = (int)(sg - (long)j * W);
             need = !A.fbits || !(A.fbits[sg] & 1) || A.tmark[(j / MOM_TY) * tiles_x + sx];
             skipped = skipped || !need;
         }
         unsigned long long m = __ballot(need);
         while (m) {
-            // up to 4 segments' loads in flight
-            long sq[4];
+            // up to 8 segments' loads in flight
+            long sq[8];
             int nq = 0;
-            for (; nq < 4 && m; ++nq, m &= m - 1) sq[nq] = g + __builtin_ctzll(m);
-            double phq[4], Jq[4];
+            for (; nq < 8 && m; ++nq, m &= m - 1)
+                sq[nq] = base + (long)DIAG_BLOCKS * 4 * __builtin_ctzll(m);
+            double phq[8], Jq[8];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 8; ++k) {
                 const long c = k < nq ? sq[k] * 64 + lane : 0;
                 phq[k] = k < nq ? A.phi[c] : 0.0;
                 Jq[k] = k < nq ? A.J[c] : 0.0;
             }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < 8; ++k) {
                 if (k >= nq) break;
                 const int j = (int)(sq[k] / W), i = (int)(sq[k] - (long)j * W) * 64 + lane;
                 if (phq[k] <= 0.0) {
