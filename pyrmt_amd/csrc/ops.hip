@@ -48,6 +48,8 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"mac_m2_bound", "RMT_MAC_M2_BOUND", &rmt_opts::mac_m2_bound},
     {"diag_seg", "RMT_DIAG_SEG", &rmt_opts::diag_seg},
 };
+int g_list_blocks = getenv("RMT_LIST_BLOCKS") ? std::max(1, atoi(getenv("RMT_LIST_BLOCKS")))
+                                                : LIST_BLOCKS;
 static rmt_opts opts_from_env() {
     rmt_opts o;
     for (const auto &k : kOpts)

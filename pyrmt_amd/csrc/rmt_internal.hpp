@@ -21,8 +21,9 @@ namespace rmt {
 // b = blockIdx.x, b + gridDim.x, ... < *count; a fix-up list is a few hundred tiles, and a
 // launch of max_tiles mostly-empty workgroups costs its dispatch.
 constexpr int LIST_BLOCKS = 1024;
+extern int g_list_blocks;   // RMT_LIST_BLOCKS (A/B of the list launches' grid; ops.hip)
 inline unsigned list_grid(long max_tiles) {
-    return (unsigned)std::max(1L, std::min<long>(max_tiles, LIST_BLOCKS));
+    return (unsigned)std::max(1L, std::min<long>(max_tiles, g_list_blocks));
 }
 
 // NaN-propagating max (a NaN operand wins; fmax would drop it)
