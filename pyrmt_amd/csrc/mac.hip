@@ -598,7 +598,10 @@ __global__ void __launch_bounds__(1024) k_m2_bound(const double *__restrict__ pu
     }
     if (threadIdx.x == 0) {
         const double mu = s[0][0], mv = s[1][0];
-        if (!(isfinite(mu) && isfinite(mv))) atomicOr(bad, 1);
+        // a face above DBL_MAX / 2 may give an overflowing centre velocity (the sum of two
+        // faces): flagged as k_mac_centres flagged a non-finite centre
+        const double half_max = 0x1.fffffffffffffp1022;
+        if (!(isfinite(mu) && isfinite(mv)) || mu > half_max || mv > half_max) atomicOr(bad, 1);
         *out = mu * mu + mv * mv;
     }
 }

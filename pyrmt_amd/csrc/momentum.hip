@@ -870,23 +870,29 @@ static int stage_edge_tiles(rmt_ctx *ctx, RowWin ws, int ntiles, int tiles_x, co
 
 // The edge-tile stream of the full-grid stages (opt.edge_stream; nullptr: off, or no stream of
 // the context's own to pair with), created at the priority of the stream it serves.
+// One edge stream per priority is kept (callers of different priorities sharing a
+// context -- rmt_sim's streams, a DistributedSim, the torch stream of the operator entry -- no
+// longer destroy and re-create it, with a host sync, at every switch).
 int edge_stream(rmt_ctx *ctx, hipStream_t *out) {
     *out = nullptr;
     if (!ctx->opt.edge_stream || !ctx->stream) return RMT_OK;
     int prio = 0;
     RMT_HIP(hipStreamGetPriority(ctx->stream, &prio));
-    if (ctx->edge_st && ctx->edge_prio != prio) {
-        RMT_HIP(hipStreamSynchronize(ctx->edge_st));
-        RMT_HIP(hipStreamDestroy(ctx->edge_st));
-        ctx->edge_st = nullptr;
+    int k = 0;
+    while (k < RMT_EDGE_PRIOS && ctx->edge_sts[k] && ctx->edge_prios[k] != prio) ++k;
+    if (k == RMT_EDGE_PRIOS) {   // (more priorities than slots: the last slot is re-created)
+        k = RMT_EDGE_PRIOS - 1;
+        RMT_HIP(hipStreamSynchronize(ctx->edge_sts[k]));
+        RMT_HIP(hipStreamDestroy(ctx->edge_sts[k]));
+        ctx->edge_sts[k] = nullptr;
     }
-    if (!ctx->edge_st) {
-        RMT_HIP(hipStreamCreateWithPriority(&ctx->edge_st, hipStreamNonBlocking, prio));
-        ctx->edge_prio = prio;
+    if (!ctx->edge_sts[k]) {
+        RMT_HIP(hipStreamCreateWithPriority(&ctx->edge_sts[k], hipStreamNonBlocking, prio));
+        ctx->edge_prios[k] = prio;
     }
     for (auto &e : ctx->edge_ev)
         if (!e) RMT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    *out = ctx->edge_st;
+    *out = ctx->edge_sts[k];
     return RMT_OK;
 }
 

@@ -830,10 +830,12 @@ int rmt_ctx_destroy(rmt_ctx *ctx) {
     if (ctx->dct) dct_destroy(ctx->dct);
     if (ctx->dct2) dct2_destroy(ctx->dct2);
     if (ctx->per) per_destroy(ctx->per);
-    if (ctx->edge_st) (void)hipStreamSynchronize(ctx->edge_st);
+    for (auto es : ctx->edge_sts)
+        if (es) (void)hipStreamSynchronize(es);
     for (auto &e : ctx->edge)
         if (e.list) (void)hipFree(e.list);
-    if (ctx->edge_st) (void)hipStreamDestroy(ctx->edge_st);
+    for (auto es : ctx->edge_sts)
+        if (es) (void)hipStreamDestroy(es);
     for (auto &e : ctx->edge_ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->ev)

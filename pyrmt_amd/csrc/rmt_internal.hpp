@@ -116,6 +116,7 @@ struct rmt_opts {
                               // can hold a solid cell or J != 1 (k_diag_seg)
 };
 
+#define RMT_EDGE_PRIOS 2   // edge-tile streams kept, one per priority (momentum.hip edge_stream)
 #ifndef RMT_EDGE_SLOTS
 #define RMT_EDGE_SLOTS 64   // >= every (window, grid) key of a step: 8 slabs x 4 stages + the fused 4
 #endif
@@ -172,8 +173,8 @@ struct rmt_ctx {
     // momentum.hip (opt.edge_stream): the stream the edge-tile launches of the full-grid stages
     // run on, beside the interior launch, at the priority of the stream it serves; events:
     // [0] the stage inputs ready, [1 + s] interior stage s done, [5 + s] edge stage s done
-    hipStream_t edge_st = nullptr;
-    int edge_prio = 0;
+    hipStream_t edge_sts[RMT_EDGE_PRIOS] = {};   // one per stream priority served
+    int edge_prios[RMT_EDGE_PRIOS] = {};
     hipEvent_t edge_ev[9] = {};
     void *imex[2] = {nullptr, nullptr};   // imex.hip: the DST preconditioner plans (u, v)
     rmt_opts opt;   // implementation switches (above)

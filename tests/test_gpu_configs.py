@@ -295,4 +295,15 @@ def test_config4_N4096_100_steps_parallel_mode(gpu):
           f"(step {int(cen.argmax()) + 1}); first step past 1e-6: {first}; t {rel[:, 0].max():.3g} "
           f"minJ {rel[:, 4].max():.3g} maxJ {rel[:, 5].max():.3g}")
     floor = 5.781624386615219e-07   # lid_n4096_100.json: nudge_1ulp, max of cx / cy max_rel
+    # (2 x floor = 1.156e-6 was chosen with this mode's 1.147e-6 already measured: it pins the
+    # measured state, it does not qualify the mode -- north_star's bar is 1e-6, which the mode
+    # holds for the first 20 steps only, asserted separately)
     assert np.all(cen <= 2 * floor), (cen.max(), int(cen.argmax()) + 1)
+    assert np.all(cen[:20] <= 1e-6), (cen[:20].max(), int(cen[:20].argmax()) + 1)
+    # the J range against the reference's 1-ulp floor over the same 100 steps (nudge_1ulp:
+    # minJ 3.146e-4, maxJ 6.092e-4 max_rel): minJ stays within twice it (6.08e-4 measured, the
+    # CPU centred evaluation), maxJ does not -- 3.52e-3, 5.8 x the floor:
+    # asserted at the measured level so that a regression shows, and recorded as a gap
+    jfloor_min, jfloor_max = 3.1461450124562043e-04, 6.091788058037263e-04
+    assert rel[:, 4].max() <= 2 * jfloor_min, rel[:, 4].max()
+    assert rel[:, 5].max() <= 6 * jfloor_max, rel[:, 5].max()
