@@ -675,6 +675,9 @@ __device__ __forceinline__ void ms_tile(
 // DC: K.den_const known on the host (drops the IEEE density division's registers: the
 // interior stages 0-2 then run 6 waves per SIMD, LDS 50 KB per block)
 template <bool IN, bool SQ, bool S3, bool DC>
+#ifndef RMT_LIST_WAVES
+#define RMT_LIST_WAVES 2
+#endif
 #ifndef RMT_MS_WAVES
 #define RMT_MS_WAVES 4
 #endif
@@ -722,7 +725,7 @@ __global__ void __launch_bounds__(IN ? MS_TI : MS_T, (IN && DC && !S3) ? RMT_MS_
 // (A kernel per kind of tile -- the interior one at two workgroups per CU -- measured slower:
 // 27-32 us per interior launch plus ~9 us for the edge launch, against 21-25 us.)
 template <bool SQ>
-__global__ void __launch_bounds__(MS_T, 2) k_mom_stage_list(
+__global__ void __launch_bounds__(MS_T, RMT_LIST_WAVES) k_mom_stage_list(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
     const double *__restrict__ sxx, const double *__restrict__ sxy,

@@ -11,7 +11,7 @@ if [ "$T" != "-" ]; then
 fi
 for r in 1 2; do
   for e in "$@"; do
-    tag=$(echo "$e" | tr ',=' '__')
+    tag=$(echo "$e" | tr ',=/.' '____' | tail -c 48)
     envs=$( [ "$e" = "-" ] && echo "" || echo "$e" | tr ',' ' ')
     env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/b_${r}_${tag}.log 2>&1 || { tail -20 $O/b_${r}_${tag}.log; exit 1; }
     echo "$e: $(tail -1 $O/b_${r}_${tag}.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"], 4), round(d["roofline"]["frac"], 4))')"
