@@ -326,10 +326,15 @@ class MacMultiDisc:
                 "rmt_mac_sim_create")
         self.h, self.params = h, P
         self._views = {}
-        for k, (X1, X2, phi) in enumerate(initial_maps(N, self.specs)):
-            self.field("X1", k).copy_(torch.as_tensor(X1))
-            self.field("X2", k).copy_(torch.as_tensor(X2))
-            self.field("phi", k).copy_(torch.as_tensor(phi))
+        # the initial maps go up through one pinned staging plane: a DMA copy per map instead of
+        # the runtime's pageable staging (≈0.6 MB chunks: ~7,800 copies at N=8192)
+        stage = torch.empty((N, N), dtype=torch.float64, pin_memory=True)
+        cur = torch.cuda.current_stream()
+        for k, maps in enumerate(initial_maps(N, self.specs)):
+            for name, a in zip(("X1", "X2", "phi"), maps):
+                stage.numpy()[...] = a
+                self.field(name, k).copy_(stage, non_blocking=True)
+                cur.synchronize()   # (before the staging plane is refilled)
 
     def __del__(self):
         try:
