@@ -45,9 +45,9 @@ CONFIGS = {
 # HBM bytes per launch and per step from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
 # bench (scripts/r06_evidence.sh -> tools/pmc_traffic.py; FETCH x2 per the gfx950 calibration)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r06", "ev", "pmc_traffic_n4096.json")
-# the same passes for the config-3 / config-5 lines (scripts/r05_evidence.sh)
-PMC_TRAFFIC_CFG = {3: os.path.join(ROOT, "profiles", "r05", "ev2", "pmc_traffic_cfg3_n1024.json"),
-                   5: os.path.join(ROOT, "profiles", "r05", "ev4", "pmc_traffic_cfg5_n8192.json")}
+# the same passes for the config-3 / config-5 lines (scripts/r06_evidence.sh OUT 53)
+PMC_TRAFFIC_CFG = {3: os.path.join(ROOT, "profiles", "r06", "ev", "pmc_traffic_cfg3_n1024.json"),
+                   5: os.path.join(ROOT, "profiles", "r06", "ev", "pmc_traffic_cfg5_n8192.json")}
 # fp64 VALU counts of the same kernel and the measured FMA peak (scripts/pmc_f64.sh ->
 # tools/f64_roof.py): k_mom_stage is VALU-issue-bound, not HBM-bound
 F64_ROOF = os.path.join(ROOT, "profiles", "r06", "ev", "f64_roof_n4096.json")
