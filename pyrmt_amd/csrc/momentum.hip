@@ -674,13 +674,13 @@ __device__ __forceinline__ void ms_tile(
 // interior geometry.
 // DC: K.den_const known on the host (drops the IEEE density division's registers: the
 // interior stages 0-2 then run 6 waves per SIMD, LDS 50 KB per block)
-template <bool IN, bool SQ, bool S3, bool DC>
 #ifndef RMT_LIST_WAVES
-#define RMT_LIST_WAVES 2
+#define RMT_LIST_WAVES 2   // k_mom_stage_list waves per SIMD (3 / 4: slower)
 #endif
 #ifndef RMT_MS_WAVES
 #define RMT_MS_WAVES 4
 #endif
+template <bool IN, bool SQ, bool S3, bool DC>
 __global__ void __launch_bounds__(IN ? MS_TI : MS_T, (IN && DC && !S3) ? RMT_MS_WAVES : 4) k_mom_stage(
     const double *__restrict__ u, const double *__restrict__ v, const double *__restrict__ kpu,
     const double *__restrict__ kpv, double coef, int stage, int bc, double lid,
@@ -716,9 +716,6 @@ __global__ void __launch_bounds__(IN ? MS_TI : MS_T, (IN && DC && !S3) ? RMT_MS_
     ms_tile<IN, SQ, S3, T, DC>(u, v, kpu, kpv, coef, stage, bc, lid, sxx, sxy, syy, H, solid, visc, mu_f, eta_s, rho_s, rho_f, p, dt6, dx, dy, ny, nx, tiles_x, ntiles, ku, kv, ainu, ainv, accu, accv, outu, outv, rw, tlist, tcount, dtp, olo, ohi, k2u, k2v, fluid_tiles, K, i0, j0, su, sv, gx, gm, gy, wfl);
 }
 
-// The listed tiles (momentum_fixup), interior and edge alike, in one launch of at most
-// LIST_BLOCKS workgroups looping over the list: a fix-up list holds a few hundred tiles, so
-// one round of workgroups covers it and the stage costs one tile's latency, not two launches'.
 // The listed tiles (momentum_fixup), interior and edge alike, in one launch of at most
 // LIST_BLOCKS workgroups looping over the list: a fix-up list holds a few hundred tiles, so
 // one round of workgroups covers it and the stage costs one tile's latency, not two launches'.
