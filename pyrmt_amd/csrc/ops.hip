@@ -47,6 +47,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"mac_face_sl", "RMT_MAC_FACE_SL", &rmt_opts::mac_face_sl},
     {"mac_m2_bound", "RMT_MAC_M2_BOUND", &rmt_opts::mac_m2_bound},
     {"diag_seg", "RMT_DIAG_SEG", &rmt_opts::diag_seg},
+    {"sl_zero_flags", "RMT_SL_ZERO_FLAGS", &rmt_opts::sl_zero_flags},
 };
 int g_list_blocks = getenv("RMT_LIST_BLOCKS") ? std::max(1, atoi(getenv("RMT_LIST_BLOCKS")))
                                                 : LIST_BLOCKS;

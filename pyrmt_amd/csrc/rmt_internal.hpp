@@ -114,6 +114,8 @@ struct rmt_opts {
     int mac_m2_bound = 1;     // RMT_MAC_M2_BOUND: MAC SL bound from the last correction's face maxima
     int diag_seg = 1;         // RMT_DIAG_SEG: the step's diagnostics read only the segments that
                               // can hold a solid cell or J != 1 (k_diag_seg)
+    int sl_zero_flags = 1;    // RMT_SL_ZERO_FLAGS: the side SL pass skips the loads and stores of
+                              // tiles whose map stays +0.0 (zero-tile flags, k_sim_sl_t)
 };
 
 #define RMT_EDGE_PRIOS 2   // edge-tile streams kept, one per priority (momentum.hip edge_stream)

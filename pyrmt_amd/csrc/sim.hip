@@ -83,6 +83,11 @@ struct rmt_sim {
     bool bits_ready = false;
     // k_mom_prep's per-segment skip flags (MomWork::prep_const), cleared at each call's start
     unsigned char *pconst = nullptr;
+    // zero-tile flags of the two map buffers (k_sim_sl_t, sl_zero_flags): zf[zcur] belongs to
+    // the buffer X1 / X2 point at, zf[zcur ^ 1] to X1n / X2n; zv: written in this call
+    unsigned char *zf[2] = {nullptr, nullptr};
+    int zcur = 0;
+    bool zv[2] = {false, false};
     int *segs = nullptr;     // rim row segments (k_rim_segments): ny * ceil(nx / 256) + count
     unsigned long long *m2acc = nullptr;   // k_dt_part's atomic max + block counter (zeroed)
     bool prof = false;
@@ -225,25 +230,82 @@ __device__ __forceinline__ double bl_tile(const double *__restrict__ s,
 
 // grid ((nx + 63) / 64, (ny + 3) / 4); mode 0 (kbits optional) or 2 (the non-rim cells).
 // FACE: a, b are the MAC u / v face planes (cell_vel), nx == ny
-template <int FACE = 0>
-__global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
+template <int FACE>
+__device__ __forceinline__ void sl_tile(
     const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ a,
     const double *__restrict__ b, const double *__restrict__ xs, const double *__restrict__ ys,
-    int ny, int nx, double dt_arg, DivK Kx, DivK Ky, double x0, double y0, double R,
+    int ny, int nx, double dt, const DivK &Kx, const DivK &Ky, double x0, double y0, double R,
     double *__restrict__ X1n, double *__restrict__ X2n, double *__restrict__ phi_pre, int *bad,
-    unsigned long long *__restrict__ kbits, const double *m2, const double *__restrict__ dtp,
-    int mode, const unsigned long long *__restrict__ rimw, double *__restrict__ phi = nullptr,
-    double thr = 0.0, unsigned char *__restrict__ fbits = nullptr,
-    unsigned long long *__restrict__ nbits = nullptr, int tbx0 = 0, int tby0 = 0) {
-    __shared__ double s1[SLT_SY * SLT_SX], s2[SLT_SY * SLT_SX];
-    __shared__ double sa[SLT_SY * SLT_SX], sb[SLT_SY * SLT_SX];
-    const double dt = dtp ? *dtp : dt_arg;
-    // (tbx0, tby0: the tile of block (0, 0) -- a launch over a box of tiles)
-    const int i0 = (blockIdx.x + tbx0) * SLT_X, j0 = (blockIdx.y + tby0) * SLT_Y;
+    unsigned long long *__restrict__ kbits, const double *m2, int mode,
+    const unsigned long long *__restrict__ rimw, double *__restrict__ phi, double thr,
+    unsigned char *__restrict__ fbits, unsigned long long *__restrict__ nbits,
+    const unsigned char *__restrict__ zin, unsigned char *__restrict__ zout, int zout_ok,
+    int tcol, int trow, double *s1, double *s2, double *sa, double *sb) {
+    const int i0 = tcol * SLT_X, j0 = trow * SLT_Y;
     const int tx = threadIdx.x & (SLT_X - 1), ty = threadIdx.x / SLT_X;
     const int i = i0 + tx, j = j0 + ty, sj0 = j0 - 1, si0 = i0 - 1;
     const bool in = i < nx && j < ny;
     const long c = (long)j * nx + i;
+    // Zero-tile flags (mode 2 with phi, nx % 64 == 0; sl_zero_flags).  zout[t] = 1 when this
+    // pass took the zero branch on tile t and the tile holds no rim cell: only this pass writes
+    // its non-rim cells, so after the step the tile's map is +0.0 in every cell and its phi is
+    // disc_phi(0, 0) (the fix-up prep recomputes the same value from the same +0.0).  zin: those
+    // flags of the input map (the previous step's output buffer), zout_ok: zout still holds the
+    // output buffer's flags from the step that last wrote it.  When the 3 x 3 tiles around a
+    // tile (every cell the staged region reads) are flagged in zin, the tile holds no rim cell
+    // and the velocity bound holds, the zero test's answer is known without its loads; the
+    // advected map's +0.0 and phi's constant are then written only where the buffers may hold
+    // something else.  The bits of every plane are those of the pass without the flags.
+    const int TW = (nx + SLT_X - 1) / SLT_X, TH = (ny + SLT_Y - 1) / SLT_Y;
+    const long tid = (long)trow * TW + tcol;
+    bool tile_rim = false, z = false, dst_zero = false;
+    if (zout) {
+        // every flag load issued at once (one round trip): the tile's rim words, the input
+        // flags of the 3 x 3 tiles around it (off the grid: +0.0, as the staging reads them),
+        // the output buffer's flag
+        const int W = (nx + 63) / 64;
+        unsigned long long rw = 0;
+#pragma unroll
+        for (int r = 0; r < SLT_Y; ++r)
+            rw |= j0 + r < ny ? rimw[(long)(j0 + r) * W + (i0 >> 6)] : 0ull;
+        unsigned zf = 1;
+        if (zin) {
+#pragma unroll
+            for (int dr = -1; dr <= 1; ++dr)
+#pragma unroll
+                for (int dc = -1; dc <= 1; ++dc) {
+                    const int r = trow + dr, cc = tcol + dc;
+                    zf &= (r >= 0 && r < TH && cc >= 0 && cc < TW) ? zin[(long)r * TW + cc] : 1u;
+                }
+        }
+        dst_zero = zout_ok && zout[tid];
+        tile_rim = rw != 0;
+        z = zin && zf && !tile_rim;
+    }
+    if (z && sl_skip_ok(m2, dt, fmin(Kx.d, Ky.d))) {
+        {
+            const double ph = disc_phi(0.0, 0.0, x0, y0, R);
+            if (in) {
+                if (!dst_zero) { X1n[c] = 0.0; X2n[c] = 0.0; }
+                if (!zin[tid]) phi[c] = ph;
+            }
+            if (kbits) {
+                const unsigned long long w = __ballot(in && ph < 0);
+                if (tx == 0 && j < ny) kbits[(long)j * ((nx + 63) / 64) + (i0 >> 6)] = w;
+            }
+            if (nbits) {
+                const unsigned long long wn = __ballot(in && ph < 0);
+                if (tx == 0 && j < ny) nbits[(long)j * (nx >> 6) + (i0 >> 6)] = wn;
+            }
+            const unsigned long long w = __ballot(!in || ph > thr);
+            if (tx == 0 && j < ny)
+                fbits[(long)j * (nx >> 6) + (i0 >> 6)] =
+                    (unsigned char)((w == ~0ull) | (((w & 3ull) == 3ull) << 1) | (((w >> 62) == 3ull) << 2));
+            __syncthreads();   // (every wave has read zout[tid])
+            if (threadIdx.x == 0) zout[tid] = 1;
+            return;
+        }
+    }
     unsigned long long bits = 0;
     for (int q = threadIdx.x; q < SLT_SY * SLT_SX; q += SLT_X * SLT_Y) {
         const int jj = sj0 + q / SLT_SX, ii = si0 + q % SLT_SX;
@@ -344,6 +406,32 @@ __global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
             fbits[(long)j * (nx >> 6) + (i0 >> 6)] =
                 (unsigned char)((w == ~0ull) | (((w & 3ull) == 3ull) << 1) | (((w >> 62) == 3ull) << 2));
     }
+    if (zout && threadIdx.x == 0) zout[tid] = zero && !tile_rim;
+}
+
+// grid ((nx + 63) / 64, (ny + 3) / 4): one tile per workgroup, (tbx0, tby0) the tile of block
+// (0, 0) for a launch over a box of tiles.  mode 0 (kbits optional) or 2 (the non-rim cells).
+// FACE: a, b are the MAC u / v face planes (cell_vel), nx == ny.  (A fixed grid walking the
+// tiles measured slower: 89 VGPRs, 5 waves per SIMD.)
+template <int FACE = 0>
+__global__ void __launch_bounds__(SLT_X * SLT_Y) k_sim_sl_t(
+    const double *__restrict__ X1, const double *__restrict__ X2, const double *__restrict__ a,
+    const double *__restrict__ b, const double *__restrict__ xs, const double *__restrict__ ys,
+    int ny, int nx, double dt_arg, DivK Kx, DivK Ky, double x0, double y0, double R,
+    double *__restrict__ X1n, double *__restrict__ X2n, double *__restrict__ phi_pre, int *bad,
+    unsigned long long *__restrict__ kbits, const double *m2, const double *__restrict__ dtp,
+    int mode, const unsigned long long *__restrict__ rimw, double *__restrict__ phi = nullptr,
+    double thr = 0.0, unsigned char *__restrict__ fbits = nullptr,
+    unsigned long long *__restrict__ nbits = nullptr, int tbx0 = 0, int tby0 = 0,
+    const unsigned char *__restrict__ zin = nullptr, unsigned char *__restrict__ zout = nullptr,
+    int zout_ok = 0) {
+    __shared__ double s1[SLT_SY * SLT_SX], s2[SLT_SY * SLT_SX];
+    __shared__ double sa[SLT_SY * SLT_SX], sb[SLT_SY * SLT_SX];
+    const double dt = dtp ? *dtp : dt_arg;
+#define SLT_ARGS(TC, TR) X1, X2, a, b, xs, ys, ny, nx, dt, Kx, Ky, x0, y0, R, X1n, X2n, phi_pre, \
+        bad, kbits, m2, mode, rimw, phi, thr, fbits, nbits, zin, zout, zout_ok, TC, TR, s1, s2, sa, sb
+    sl_tile<FACE>(SLT_ARGS(blockIdx.x + tbx0, blockIdx.y + tby0));
+#undef SLT_ARGS
 }
 
 // the row segments holding a rim cell, listed (any order)
@@ -790,7 +878,7 @@ int sl_disc_map(rmt_ctx *ctx, const double *X1, const double *X2, const double *
     kern<<<dim3(tx1 - tx0, ty1 - ty0), SLT_X * SLT_Y, 0, ctx->stream>>>(
         X1, X2, a, b, xs, ys, ctx->ny, ctx->nx, dt, divk_make(dx), divk_make(dy), x0, y0, R, X1n,
         X2n, phi_pre, bad, kbits, dev_m2, nullptr, 0, nullptr, nullptr, 0.0, nullptr, nullptr,
-        tx0, ty0);
+        tx0, ty0, nullptr, nullptr, 0);
     RMT_LAUNCHED();
     return RMT_OK;
 }
@@ -897,6 +985,11 @@ int rmt_sim_create(rmt_ctx *ctx, const rmt_sim_params *prm, rmt_sim **out) {
     S->tmark = (unsigned char *)(S->m2acc + 8);   // max_tiles bytes
     RMT_HIP(hipMemsetAsync(S->m2acc, 0, 2 * sizeof(unsigned long long), ctx->stream));
     if (nx % 64 == 0) RMT_HIP(hipMalloc(&S->pconst, (size_t)ny * (nx / 64)));
+    if (S->st2 && nx % 64 == 0) {
+        const size_t ntl = (size_t)(nx / SLT_X) * ((ny + SLT_Y - 1) / SLT_Y);
+        RMT_HIP(hipMalloc(&S->zf[0], 2 * ntl));
+        S->zf[1] = S->zf[0] + ntl;
+    }
     if (S->st2) {
         RMT_HIP(hipEventCreateWithFlags(&S->e_bits, hipEventDisableTiming));
         RMT_HIP(hipEventCreateWithFlags(&S->e_proj, hipEventDisableTiming));
@@ -919,6 +1012,7 @@ int rmt_sim_destroy(rmt_sim *S) {
     (void)hipFree(S->block);
     if (S->m2part) (void)hipFree(S->m2part);
     if (S->pconst) (void)hipFree(S->pconst);
+    if (S->zf[0]) (void)hipFree(S->zf[0]);
     if (S->tiles) (void)hipFree(S->tiles);
     if (S->e_sl) (void)hipEventDestroy(S->e_sl);
     if (S->e_mom) (void)hipEventDestroy(S->e_mom);
@@ -1001,6 +1095,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
             (void)hipMemcpyAsync(S->X2h, S->X2, b, hipMemcpyDeviceToDevice, S->ctx->stream);
             std::swap(S->X1, S->X1n);
             std::swap(S->X2, S->X2n);
+            S->zcur ^= 1;
         }
     } map_home{S};
     if (S->st1) {
@@ -1117,6 +1212,8 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                        S->carry_cfg == extrap_config_gen();
     const bool m2_ok = carry && S->m2_valid;
     S->carry_valid = false;
+    // the zero-tile flags describe maps this call wrote (the caller may change them between calls)
+    S->zv[0] = S->zv[1] = false;
     if (!carry) {
         S->bits_ready = false;   // the caller may have changed the map between calls
         // ... or the prep planes: the first prep of a call writes every segment
@@ -1185,6 +1282,11 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         bool seg_diag = false;  // this step's fbits and fix-up tile marks are set (k_diag_seg)
         if (S->prof) RMT_HIP(hipEventRecord(S->pev[1], st));
         if (solid) {
+            // (the output buffer's zero-tile flags hold only when the flagged pass writes it;
+            // the flagged pass reads them first: the rim pass and the chain below write only rim
+            // cells, and a tile with a rim cell never uses them)
+            const bool zo_valid = S->zv[S->zcur ^ 1];
+            S->zv[S->zcur ^ 1] = false;
             // 2. advect the reference map with the pre-advection level set and mask
             // (on the asynchronous path the previous step's ring record -- k_dt_part or k_ring_put --
             // cleared it)
@@ -1295,15 +1397,21 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
                                     fl_ok && ctx->opt.sl_phi;
                 if (P.scheme == RMT_SCHEME_SEMILAGRANGIAN && S->e_bits) {
                     // the advection of every non-rim cell, once the chain has started (earlier
-                    // its blocks would crowd out the one-workgroup band passes)
+                    // its blocks would crowd out the one-workgroup band passes); with the
+                    // zero-tile flags (sl_zero_flags, with sl_phi) the tiles that stay +0.0 move
+                    // no map or phi bytes
+                    const bool zon = sl_phi && S->zf[0] && ctx->opt.sl_zero_flags;
+                    const int zi = S->zcur, zo = S->zcur ^ 1;
                     k_sim_sl_t<0><<<dim3((nx + SLT_X - 1) / SLT_X, (ny + SLT_Y - 1) / SLT_Y),
                                  SLT_X * SLT_Y, 0, S->st2>>>(
                         S->X1, S->X2, S->u, S->v, S->xs, S->ys, ny, nx, dt, divk_make(P.dx),
                         divk_make(P.dy), P.x0, P.y0, P.R, S->X1n, S->X2n, S->phi_pre, S->flag,
                         nullptr, sc, dtp, 2, S->rimw, sl_phi ? S->phi : nullptr,
                         fluid_threshold(&M), sl_phi ? fluid_bits_buf(W) : nullptr,
-                        sl_phi ? nb : nullptr);
+                        sl_phi ? nb : nullptr, 0, 0, zon && S->zv[zi] ? S->zf[zi] : nullptr,
+                        zon ? S->zf[zo] : nullptr, zon && zo_valid);
                     RMT_LAUNCHED();
+                    S->zv[zo] = zon;
                 }
                 seg_diag = sl_phi && S->split_proj && tm && !P.energies;
                 if (sl_phi) {
@@ -1478,6 +1586,7 @@ int rmt_sim_step(rmt_sim *S, int nsteps, double t_end) {
         // buffers swap roles instead of copying the map back (restored at the call's end)
         std::swap(S->X1, S->X1n);
         std::swap(S->X2, S->X2n);
+        S->zcur ^= 1;
         // 7. diagnostics (running them beside the projection on the second stream measured
         // no gain: both are HBM-bound)
         DiagArgs D{S->phi, S->J, S->xs, S->ys, S->u, S->v, S->X1, S->X2, ny, nx, P.energies,

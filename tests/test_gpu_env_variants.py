@@ -41,6 +41,8 @@ environment variables still set a new context's defaults.
                         ahead of its SL pass instead of beside it on the edge-tile stream
   diag_first=1          the step's diagnostics ahead of the next step's geometry instead of
                         behind it
+  sl_zero_flags=0       the second stream's SL pass loads and stores every tile instead of
+                        skipping the tiles its zero-tile flags prove +0.0
 
 Every variant above runs the diagnostics through k_diag_seg (its segment skip adds nothing to
 any lane's sums, so the skip pattern does not change the bits).  diag_seg=0 (k_diag_p1's
@@ -98,7 +100,7 @@ def _same(got, ref):
     {"edge_stream": 0}, {"sl_phi": 0}, {"sl_phi": 0, "fused_fluid": 0},
     {"edge_stream": 0, "sl_phi": 0, "test_delay_side": 300}, {"skip_marked_rows": 0},
     {"tail_stream": 0}, {"tail_stream": 1, "test_delay_side": 300}, {"diag_first": 1},
-    {"fused_fixprep": 0, "diag_first": 1},
+    {"fused_fixprep": 0, "diag_first": 1}, {"sl_zero_flags": 0},
 ], ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_schedule_switch_is_bit_identical(default_run, opts):
     _same(_run(opts), default_run)
@@ -150,3 +152,29 @@ def test_environment_sets_context_defaults(tmp_path, default_run):
     got = np.load(out)
     for f in FIELDS:
         np.testing.assert_array_equal(got[f], default_run[f], err_msg=f)
+
+
+def _split_run(options, edit):
+    """Three calls of 4 steps; between the first two the map is edited from outside (a +0.0
+    tile of X1 set to 1e-300, then back to +0.0 after the second), so the zero-tile flags must
+    be rebuilt at every call."""
+    from pyrmt_amd.simulation import soft_disc_in_lid_driven
+    s = soft_disc_in_lid_driven(256, options=options)
+    s.step(4)
+    if edit:
+        x = s.get("X1"); x[2:6, 2:66] = 1e-300; s.set_field("X1", x); s.invalidate()
+    s.step(4)
+    if edit:
+        x = s.get("X1"); x[2:6, 2:66] = 0.0; s.set_field("X1", x); s.invalidate()
+    s.step(4)
+    out = {f: s.get(f) for f in FIELDS}
+    out.update({"d_" + k: np.asarray(v) for k, v in s.diagnostics().items()})
+    return out
+
+
+@pytest.mark.parametrize("edit", [False, True], ids=["plain", "edited"])
+def test_sl_zero_flags_across_calls(gpu, edit):
+    """The zero-tile flags (sl_zero_flags) are valid only for maps the call itself wrote: split
+    calls, with and without an outside edit of the map in between, give the bits of the pass
+    without them."""
+    _same(_split_run(None, edit), _split_run({"sl_zero_flags": 0}, edit))
