@@ -6,7 +6,8 @@
 // the real and imaginary parts of one complex sequence come back separated in Re and Im.
 // scipy's inverse DCT-I is the forward one scaled by 1/(2(n-1)) per axis.
 //
-// Main path (n - 1 < 4096, a product of radices 2..23): k_dct1 -- one workgroup per row,
+// Main path (n - 1 < 4096, a product of radices 2..23, 29, 31 -- the last two as matrix-form
+// passes, fft_pass_mat): k_dct1 -- one workgroup per row,
 // the row's even extension packed as a length-(n-1) complex sequence resident in LDS
 // (<= 64 KB, two workgroups per CU), a mixed-radix Stockham FFT (radices grouped into
 // in-register composite butterflies of up to 10; twiddles from a global per-pass table),
@@ -37,6 +38,7 @@ struct DctPlan {
     // LDS FFT path
     bool lds = false;
     int big = 0;                            // a radix above 13 present
+    int mat = 0;                            // a matrix-form radix (29, 31) present
     double2 *Wx = nullptr, *Wy = nullptr;   // per-pass twiddle tables (twiddles())
     int radx[16] = {0}, rady[16] = {0}, npx = 0, npy = 0;
 };
@@ -90,12 +92,17 @@ constexpr int K1_MAXN = DCT_MAXM / 2;   // k_dct1's complex FFT length (n <= 409
 
 // Radix plan of a length-M FFT: prime factors (2 .. 23), then 2s grouped into 8 / 4, 3s into
 // 9, a leftover 2 with a 5 (10) or a 3 (6): M = 8190 = 2 3^2 5 7 13 runs as 9, 10, 7, 13 --
-// four LDS passes instead of six.  false if a prime factor > 23 remains.
-static bool factor(int M, int *rad, int *np) {
+// four LDS passes instead of six.  mat: also 29 and 31, as matrix-form passes (fft_pass_mat;
+// k_dct1 only).  false if a prime factor > 23 (> 31 with mat) remains.
+static bool is_mat_radix(int R) { return R == 29 || R == 31; }
+static bool factor(int M, int *rad, int *np, bool mat = false) {
     if (M < 2 || M > DCT_MAXM) return false;
-    int cnt[24] = {0}, m = M;
+    int cnt[32] = {0}, m = M;
     for (int q : {2, 3, 5, 7, 11, 13, 17, 19, 23})
         while (m % q == 0) { ++cnt[q]; m /= q; }
+    if (mat)
+        for (int q : {29, 31})
+            while (m % q == 0) { ++cnt[q]; m /= q; }
     if (m != 1) return false;
     int n = 0;
     auto put = [&](int r) { if (n < 16) rad[n++] = r; };
@@ -104,7 +111,7 @@ static bool factor(int M, int *rad, int *np) {
     while (cnt[3] >= 2) { put(9); cnt[3] -= 2; }
     if (cnt[2] && cnt[5]) { put(10); --cnt[2]; --cnt[5]; }
     if (cnt[2] && cnt[3]) { put(6); --cnt[2]; --cnt[3]; }
-    for (int q : {2, 3, 5, 7, 11, 13, 17, 19, 23})
+    for (int q : {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31})
         while (cnt[q]) { put(q); --cnt[q]; }
     // ascending: the largest radix runs last, where Ns (the base-twiddle count) is M / R
     std::sort(rad, rad + n);
@@ -113,7 +120,11 @@ static bool factor(int M, int *rad, int *np) {
 }
 
 static bool big_radix(const int *rad, int np) {
-    for (int k = 0; k < np; ++k) if (rad[k] > 13) return true;
+    for (int k = 0; k < np; ++k) if (rad[k] > 13 && !is_mat_radix(rad[k])) return true;
+    return false;
+}
+static bool mat_radix(const int *rad, int np) {
+    for (int k = 0; k < np; ++k) if (is_mat_radix(rad[k])) return true;
     return false;
 }
 
@@ -163,9 +174,12 @@ int dct_plan(rmt_ctx *ctx, double dx, double dy) {
         // k_dct1's complex FFT length: N = n - 1 (half the even extension)
         const int Nx = P->nx - 1, Ny = P->ny - 1;
         P->lds = !ctx->opt.dct_rocfft && Nx >= 2 && Ny >= 2 && Nx < K1_MAXN && Ny < K1_MAXN &&
-                 factor(Nx, P->radx, &P->npx) && factor(Ny, P->rady, &P->npy) &&
+                 factor(Nx, P->radx, &P->npx, true) && factor(Ny, P->rady, &P->npy, true) &&
                  lds_fits(Nx) && lds_fits(Ny);
         P->big = big_radix(P->radx, P->npx) || big_radix(P->rady, P->npy);
+        P->mat = mat_radix(P->radx, P->npx) || mat_radix(P->rady, P->npy);
+        // (a matrix pass needs a second length-M buffer: both planes within the LDS budget)
+        if (P->mat) P->lds = P->lds && lds_fits(2 * Nx + 64) && lds_fits(2 * Ny + 64);
     }
     if (!P->lds && !g_rocfft_ready) { RMT_TRY(rf(rocfft_setup(), "setup")); g_rocfft_ready = true; }
     if (P->lds && !P->Wx) {
@@ -404,9 +418,62 @@ __device__ __forceinline__ void fft_pass(double2 *z, int M, const Pass &ps,
     __syncthreads();
 }
 
-// the radix passes of rd over z[0..M), M <= MAXN, NT threads
+// A Stockham pass of an odd prime radix R too large for one butterfly per thread (29, 31:
+// the radix-31 pass of M = 1023 has 33 butterflies, and a register butterfly holds 31 complex
+// values), in matrix form: every (butterfly, input) pair stages its twiddled input in t, then
+// every (butterfly, output pair m / R - m) forms dft<R>'s sums A_m, S_m from them -- the same
+// operations in the same order as dft<R>, spread over the workgroup.  t: M + R complex LDS
+// entries after z (the R roots of unity at t + M).
+template <int R, int NT>
+__device__ void fft_pass_mat(double2 *z, int M, const Pass &ps, const double2 *__restrict__ tw,
+                             double2 *t) {
+    constexpr int K = (R - 1) / 2;
+    const int nb = M / R, Ns = ps.Ns;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    double2 *cs = t + M;
+    if (tid < R) cs[tid] = make_double2(Rc<R>::c[tid], Rc<R>::s[tid]);
+    for (int q = tid; q < nb * R; q += NT) {
+        const int j = q / R, r = q - j * R;
+        double2 v = z[j + r * nb];
+        if (Ns > 1 && r > 0) {
+            const int k = j % Ns;
+            v = cmul(v, tw[ps.tw + (r - 1) * Ns + k]);
+        }
+        t[q] = v;
+    }
+    __syncthreads();
+    for (int q = tid; q < nb * (K + 1); q += NT) {
+        const int j = q / (K + 1), m = q - j * (K + 1);
+        const double2 *v = t + j * R;
+        const int g = j / Ns, k = j - g * Ns, o = g * Ns * R + k;
+        if (m == 0) {
+            double2 x0 = v[0];
+            for (int i = 1; i <= K; ++i) x0 = cadd(x0, cadd(v[i], v[R - i]));
+            z[o] = x0;
+        } else {
+            double2 A = v[0], S = make_double2(0.0, 0.0);
+            int e = 0;
+            for (int i = 1; i <= K; ++i) {
+                e += m;
+                if (e >= R) e -= R;   // (i m) mod R
+                const double2 a = cadd(v[i], v[R - i]), b = csub(v[i], v[R - i]), w = cs[e];
+                A.x = __builtin_fma(a.x, w.x, A.x);
+                A.y = __builtin_fma(a.y, w.x, A.y);
+                S.x = __builtin_fma(b.x, w.y, S.x);
+                S.y = __builtin_fma(b.y, w.y, S.y);
+            }
+            z[o + m * Ns] = make_double2(A.x + S.y, A.y - S.x);         // A - i S
+            z[o + (R - m) * Ns] = make_double2(A.x - S.y, A.y + S.x);   // A + i S
+        }
+    }
+    __syncthreads();
+}
+
+// the radix passes of rd over z[0..M), M <= MAXN, NT threads (scr: fft_pass_mat's buffer)
 template <int BIG, int NT, int MAXN>
-__device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__restrict__ tw) {
+__device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__restrict__ tw,
+                        double2 *scr = nullptr) {
     for (int q = 0; q < rd.n; ++q) {
         const Pass &ps = rd.p[q];
         switch (ps.R) {
@@ -421,6 +488,8 @@ __device__ void fft_lds(double2 *z, int M, const Radices &rd, const double2 *__r
             case 10: fft_pass<10, NT, MAXN>(z, M, ps, tw); break;
             case 11: fft_pass<11, NT, MAXN>(z, M, ps, tw); break;
             case 13: fft_pass<13, NT, MAXN>(z, M, ps, tw); break;
+            case 29: fft_pass_mat<29, NT>(z, M, ps, tw, scr); break;
+            case 31: fft_pass_mat<31, NT>(z, M, ps, tw, scr); break;
             default:
                 if constexpr (BIG) {
                     switch (ps.R) {
@@ -544,7 +613,7 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
     for (int it = 0; it < (SOLVE ? 2 : 1); ++it) {
         __syncthreads();
         if constexpr (PLAN == 1) fft_4095<NT>(z, W);
-        else fft_lds<BIG, NT, K1_MAXN>(z, N, rd, W);
+        else fft_lds<BIG, NT, K1_MAXN>(z, N, rd, W, z + N);
         // opaque per iteration: keeps the twiddle / eigenvalue loads below from being hoisted
         // above the FFT (they would hold ~40 registers across it)
         const double2 *Wq = Wq0;
@@ -679,7 +748,8 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     const int *rad = axis == 0 ? P->radx : P->rady, np = axis == 0 ? P->npx : P->npy;
     const Radices rd = radices(rad, np);
     const double2 *W = axis == 0 ? P->Wx : P->Wy;
-    const size_t lds = (size_t)(n - 1) * sizeof(double2);
+    // (a matrix-form pass stages a second length-(n - 1) sequence and its R roots after the row)
+    const size_t lds = (size_t)(P->mat ? 2 * (n - 1) + 32 : n - 1) * sizeof(double2);
     const unsigned g = (unsigned)nrows;   // one row per workgroup
     hipStream_t st = ctx->stream;
     const bool k4095 = n == 4096 && !P->big && np == 4 && rad[0] == 5 &&

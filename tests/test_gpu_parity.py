@@ -197,11 +197,13 @@ def test_momentum_solid_tolerance(gpu):
 
 
 @pytest.mark.parametrize("shape", [(49, 49), (65, 65), (257, 129), (256, 256), (130, 200),
-                                   (300, 4096), (1024, 1024), (4096, 4096)])
+                                   (300, 4096), (1024, 1024), (4096, 4096), (32, 32),
+                                   (30, 94)])
 def test_dct_solve_sizes(gpu, oracle, shape):
     """functions.py:1107-1119 against scipy's pocketfft (the reference's own call) on random
     right-hand sides.  Covers the LDS FFT's radix sets (2..13: 49, 65, 129, 4096; up to 23:
-    256, 300) and the rocFFT fallback (130, 200, 1024: a prime factor > 23 in 2(n-1)).
+    256, 300; the matrix-form 29 / 31 passes: 1024 (n - 1 = 3 11 31), 32, 30, 94) and the
+    rocFFT fallback (130, 200: a prime factor > 31 in n - 1).
     Bar: |p_gpu - p_ref| <= 1e-13 * max|p_ref| (different FFT algorithms round differently)."""
     ny, nx = shape
     dx, dy = 1.0 / (nx - 1), 1.0 / (ny - 1)
