@@ -79,7 +79,7 @@ int rmt_ctx_kernel_ms(rmt_ctx *ctx, double *ms2);
  * no_overlap, side_tail, par_overlap, fused_fixprep, merged_join, test_delay_side,
  * test_delay_main, chain_cols, chain_layer_groups, edge_slots, edge_stream, sl_phi,
  * mac_boxes, skip_marked_rows, tail_stream, diag_first, mac_noop_host, mac_face_sl,
- * mac_m2_bound, diag_seg, sl_zero_flags, and the test-only test_delay_geo / test_nowait_drop (a slab's
+ * mac_m2_bound, diag_seg, sl_zero_flags, dct_desc, and the test-only test_delay_geo / test_nowait_drop (a slab's
  * early geometry delayed; a dropped geometry not waited for).  Set them before creating a sim or slab on the context (sim_hiprio is read
  * at rmt_sim_create); a change ends a carried step state.
  * Unknown name: RMT_EINVAL. */

@@ -48,6 +48,7 @@ static const struct { const char *name, *env; int rmt_opts::*f; } kOpts[] = {
     {"mac_m2_bound", "RMT_MAC_M2_BOUND", &rmt_opts::mac_m2_bound},
     {"diag_seg", "RMT_DIAG_SEG", &rmt_opts::diag_seg},
     {"sl_zero_flags", "RMT_SL_ZERO_FLAGS", &rmt_opts::sl_zero_flags},
+    {"dct_desc", "RMT_DCT_DESC", &rmt_opts::dct_desc},
 };
 int g_list_blocks = getenv("RMT_LIST_BLOCKS") ? std::max(1, atoi(getenv("RMT_LIST_BLOCKS")))
                                                 : LIST_BLOCKS;

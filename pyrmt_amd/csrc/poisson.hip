@@ -95,7 +95,7 @@ constexpr int K1_MAXN = DCT_MAXM / 2;   // k_dct1's complex FFT length (n <= 409
 // four LDS passes instead of six.  mat: also 29 and 31, as matrix-form passes (fft_pass_mat;
 // k_dct1 only).  false if a prime factor > 23 (> 31 with mat) remains.
 static bool is_mat_radix(int R) { return R == 29 || R == 31; }
-static bool factor(int M, int *rad, int *np, bool mat = false) {
+static bool factor(int M, int *rad, int *np, bool mat = false, bool desc = false) {
     if (M < 2 || M > DCT_MAXM) return false;
     int cnt[32] = {0}, m = M;
     for (int q : {2, 3, 5, 7, 11, 13, 17, 19, 23})
@@ -115,6 +115,7 @@ static bool factor(int M, int *rad, int *np, bool mat = false) {
         while (cnt[q]) { put(q); --cnt[q]; }
     // ascending: the largest radix runs last, where Ns (the base-twiddle count) is M / R
     std::sort(rad, rad + n);
+    if (desc) std::reverse(rad, rad + n);
     *np = n;
     return n < 16;
 }
@@ -174,7 +175,8 @@ int dct_plan(rmt_ctx *ctx, double dx, double dy) {
         // k_dct1's complex FFT length: N = n - 1 (half the even extension)
         const int Nx = P->nx - 1, Ny = P->ny - 1;
         P->lds = !ctx->opt.dct_rocfft && Nx >= 2 && Ny >= 2 && Nx < K1_MAXN && Ny < K1_MAXN &&
-                 factor(Nx, P->radx, &P->npx, true) && factor(Ny, P->rady, &P->npy, true) &&
+                 factor(Nx, P->radx, &P->npx, true, ctx->opt.dct_desc && Nx == 4095) &&
+                 factor(Ny, P->rady, &P->npy, true, ctx->opt.dct_desc && Ny == 4095) &&
                  lds_fits(Nx) && lds_fits(Ny);
         P->big = big_radix(P->radx, P->npx) || big_radix(P->rady, P->npy);
         P->mat = mat_radix(P->radx, P->npx) || mat_radix(P->rady, P->npy);
@@ -551,6 +553,15 @@ __device__ __forceinline__ void fft_4095(double2 *z, const double2 *__restrict__
     fft_pass_k<9, 35, NT, 4095>(z, W + 34);
     fft_pass_k<13, 315, NT, 4095>(z, W + 314);
 }
+// descending (dct_desc): 13, 9, 7, 5, twiddle offsets 0, 12, 116, 818 -- the radix-13
+// butterflies need no twiddles (Ns = 1), the radix-5 pass takes the large table
+template <int NT>
+__device__ __forceinline__ void fft_4095d(double2 *z, const double2 *__restrict__ W) {
+    fft_pass_k<13, 1, NT, 4095>(z, W);
+    fft_pass_k<9, 13, NT, 4095>(z, W + 12);
+    fft_pass_k<7, 117, NT, 4095>(z, W + 116);
+    fft_pass_k<5, 819, NT, 4095>(z, W + 818);
+}
 
 // DCT-I of one real row per workgroup.  The even extension e (length M = 2N, N = n - 1) is
 // real, so its length-M DFT -- the unnormalised DCT-I -- comes from ONE length-N complex FFT
@@ -603,7 +614,7 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
     extern __shared__ double2 z[];
     __shared__ double red[256];
     // PLAN 1: n = 4096 (compile-time passes, fft_4095)
-    const int N = PLAN == 1 ? 4095 : n - 1, r = blockIdx.x;
+    const int N = PLAN == 1 || PLAN == 3 ? 4095 : n - 1, r = blockIdx.x;
     double *d = (double *)z;
     const double2 *Wq0 = W + (N - 1);   // after the N - 1 pass twiddles: W^k, k = 0 .. N
     put_row_even<NT>(d, N, src + (long)r * n);
@@ -613,6 +624,7 @@ __global__ void __launch_bounds__(K1T<BIG>::T, BIG ? 2 : 4) k_dct1(const double 
     for (int it = 0; it < (SOLVE ? 2 : 1); ++it) {
         __syncthreads();
         if constexpr (PLAN == 1) fft_4095<NT>(z, W);
+        else if constexpr (PLAN == 3) fft_4095d<NT>(z, W);
         else fft_lds<BIG, NT, K1_MAXN>(z, N, rd, W, z + N);
         // opaque per iteration: keeps the twiddle / eigenvalue loads below from being hoisted
         // above the FFT (they would hold ~40 registers across it)
@@ -735,9 +747,10 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     RMT_CHECK(!rowmark || (!solve && !rs), RMT_EINVAL, "dct_pass: row marks on a plain row pass");
     static bool attr = false;
     if (!attr) {
-        const void *fs[6] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
+        const void *fs[8] = {(const void *)k_dct1<false, 0>, (const void *)k_dct1<true, 0>,
                              (const void *)k_dct1<false, 1>, (const void *)k_dct1<true, 1>,
-                             (const void *)k_dct1<false, 0, 1>, (const void *)k_dct1<true, 0, 1>};
+                             (const void *)k_dct1<false, 0, 1>, (const void *)k_dct1<true, 0, 1>,
+                             (const void *)k_dct1<false, 0, 3>, (const void *)k_dct1<true, 0, 3>};
         for (auto f : fs)
             RMT_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         (int)FFT_LDS_MAX));
@@ -754,7 +767,13 @@ int dct_pass(rmt_ctx *ctx, bool solve, int axis, const double *src, double *dst,
     hipStream_t st = ctx->stream;
     const bool k4095 = n == 4096 && !P->big && np == 4 && rad[0] == 5 &&
                        rad[1] == 7 && rad[2] == 9 && rad[3] == 13;   // fft_4095's plan
-    if (k4095 && solve)
+    const bool k4095d = n == 4096 && !P->big && np == 4 && rad[0] == 13 &&
+                        rad[1] == 9 && rad[2] == 7 && rad[3] == 5;   // fft_4095d's
+    if (k4095d && solve)
+        k_dct1<true, 0, 3><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
+    else if (k4095d)
+        k_dct1<false, 0, 3><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark, unmarked);
+    else if (k4095 && solve)
         k_dct1<true, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, P->lamx, P->lamy, row0, nullptr, nullptr);
     else if (k4095)
         k_dct1<false, 0, 1><<<g, K1T<0>::T, lds, st>>>(src, dst, nrows, n, W, rd, scale, nullptr, nullptr, 0, rs, rowmark, unmarked);

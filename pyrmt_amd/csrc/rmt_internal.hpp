@@ -114,6 +114,8 @@ struct rmt_opts {
     int mac_m2_bound = 1;     // RMT_MAC_M2_BOUND: MAC SL bound from the last correction's face maxima
     int diag_seg = 1;         // RMT_DIAG_SEG: the step's diagnostics read only the segments that
                               // can hold a solid cell or J != 1 (k_diag_seg)
+    int dct_desc = 1;         // RMT_DCT_DESC: n = 4096 DCT-I plan 13, 9, 7, 5 (fft_4095d;
+                              // 0: 5, 7, 9, 13, fft_4095)
     int sl_zero_flags = 1;    // RMT_SL_ZERO_FLAGS: the side SL pass skips the loads and stores of
                               // tiles whose map stays +0.0 (zero-tile flags, k_sim_sl_t)
 };
