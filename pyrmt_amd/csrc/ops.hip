@@ -511,14 +511,22 @@ __global__ void k_divergence_rc(const double *__restrict__ a, const double *__re
     if (i >= nx || j >= je) return;
     div_rc_cell(a, b, p, ny, nx, d_f, K, divU, rho, dt, j, i);
 }
-// k_divergence_rc over the whole grid in 64 x 16 tiles staged through LDS: p on the tile + 2
-// (rows and columns), a* on the tile + 1 column, b* on the tile + 1 row.  Each stencil value
-// is loaded from global memory once per tile (the row kernel's five p rows per output row
-// were five L2 round trips per cell, ~70 % of its wave time waiting); the arithmetic is
-// div_rc_cell's on the staged copies, operand for operand.  One-dimensional grid, tiles
-// grouped per XCD (each XCD's L2 sees a contiguous band of tile rows and their halos).
+// k_divergence_rc over the whole grid in 64 x 16 tiles: p staged through LDS on the tile + 2
+// (rows and columns), a* and b* straight into registers (each lane owns one column and four
+// consecutive rows: a*'s east / west neighbours come from the adjacent lanes, b*'s north /
+// south from the lane's own column).  Each stencil value is loaded from global memory once per
+// tile (the row kernel's five p rows per output row were five L2 round trips per cell), and
+// every gradient / face quotient is formed once: gy and fy = (p_{j+1} - p_j) / dy at rows
+// r0 - 1 .. r0 + 4 (r0 + 3) in registers, gx and fx = (p_{i+1} - p_i) / dx of the lane's
+// column with its neighbours' by lane shuffles, the tile's edge columns (gx, fx at i0 - 1, gx
+// at i0 + 64; a* at i0 - 1 and i0 + 64) by the first lanes in one pass: 7 quotients per cell
+// instead of div_rc_cell's 14.  Every value is div_rc_cell's quotient / sum of the same
+// operands in the same order, so the result is bit-identical.  152 vs 161 us per full-grid
+// launch at N = 4096 (profiles/r06/ktdiv; 84 VGPRs, five blocks per CU as before: at 6 or 8
+// waves per SIMD it spills, 8: 276 us).  One-dimensional grid, tiles grouped per XCD (each
+// XCD's L2 sees a contiguous band of tile rows and their halos).
 constexpr int DVT_X = 64, DVT_Y = 16, DVT_PX = DVT_X + 4, DVT_PY = DVT_Y + 4;
-constexpr int DVT_AX = DVT_X + 2, DVT_BY = DVT_Y + 2;
+static_assert(DVT_X == 64 && DVT_Y == 16, "k_divergence_t: a wave per 4 tile rows, a lane per column");
 __global__ void __launch_bounds__(256) k_divergence_t(const double *__restrict__ a,
                                                       const double *__restrict__ b,
                                                       const double *__restrict__ p, int ny, int nx,
@@ -526,76 +534,97 @@ __global__ void __launch_bounds__(256) k_divergence_t(const double *__restrict__
                                                       double *__restrict__ divU, double rho,
                                                       double dt, const double *__restrict__ dtp,
                                                       int tiles_x, int ntiles) {
-    __shared__ double sp[DVT_PY * DVT_PX], sa[DVT_Y * DVT_AX], sb[DVT_BY * DVT_X];
+    __shared__ double sp[DVT_PY * DVT_PX];
     if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
     const int per = ntiles / 8, bk = blockIdx.x;
     const int tile = bk < 8 * per ? (bk % 8) * per + bk / 8 : bk;
     const int i0 = (tile % tiles_x) * DVT_X, j0 = (tile / tiles_x) * DVT_Y;
-    constexpr int NP = (DVT_PY * DVT_PX + 255) / 256, NA = (DVT_Y * DVT_AX + 255) / 256,
-                  NB = (DVT_BY * DVT_X + 255) / 256;
-    double vp[NP], va[NA], vb[NB];
+    const int tx = threadIdx.x & 63, r0 = 4 * (threadIdx.x >> 6), i = i0 + tx;
+    constexpr int NP = (DVT_PY * DVT_PX + 255) / 256;
+    double vp[NP], av[4], bv[6], ae = 0.0;
     // every load issued before the first LDS write (cells outside the grid: never read by an
     // interior cell's stencil, which turns one-sided at the edges)
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
         const int q = threadIdx.x + 256 * k, r = q / DVT_PX, s = q % DVT_PX;
-        const int j = j0 - 2 + r, i = i0 - 2 + s;
-        const bool ok = q < DVT_PY * DVT_PX && j >= 0 && j < ny && i >= 0 && i < nx;
-        vp[k] = ok ? p[(long)j * nx + i] : 0.0;
+        const int j = j0 - 2 + r, ii = i0 - 2 + s;
+        const bool ok = q < DVT_PY * DVT_PX && j >= 0 && j < ny && ii >= 0 && ii < nx;
+        vp[k] = ok ? p[(long)j * nx + ii] : 0.0;
     }
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-        const int q = threadIdx.x + 256 * k, r = q / DVT_AX, s = q % DVT_AX;
-        const int j = j0 + r, i = i0 - 1 + s;
-        const bool ok = q < DVT_Y * DVT_AX && j < ny && i >= 0 && i < nx;
-        va[k] = ok ? a[(long)j * nx + i] : 0.0;
+    for (int q = 0; q < 4; ++q) {   // a* on rows r0 .. r0 + 3
+        const int j = j0 + r0 + q;
+        av[q] = (j < ny && i < nx) ? a[(long)j * nx + i] : 0.0;
     }
 #pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        const int q = threadIdx.x + 256 * k, r = q / DVT_X, s = q % DVT_X;
-        const int j = j0 - 1 + r, i = i0 + s;
-        const bool ok = q < DVT_BY * DVT_X && j >= 0 && j < ny && i < nx;
-        vb[k] = ok ? b[(long)j * nx + i] : 0.0;
+    for (int q = 0; q < 6; ++q) {   // b* on rows r0 - 1 .. r0 + 4
+        const int j = j0 + r0 - 1 + q;
+        bv[q] = (j >= 0 && j < ny && i < nx) ? b[(long)j * nx + i] : 0.0;
+    }
+    if (tx < 8) {   // a* at the tile's edge columns: lane 2q + 0 / 1 -> row r0 + q, i0 - 1 / i0 + 64
+        const int j = j0 + r0 + (tx >> 1), ii = (tx & 1) ? i0 + DVT_X : i0 - 1;
+        if (j < ny && ii >= 0 && ii < nx) ae = a[(long)j * nx + ii];
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
         const int q = threadIdx.x + 256 * k;
         if (q < DVT_PY * DVT_PX) sp[q] = vp[k];
     }
-#pragma unroll
-    for (int k = 0; k < NA; ++k) {
-        const int q = threadIdx.x + 256 * k;
-        if (q < DVT_Y * DVT_AX) sa[q] = va[k];
-    }
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {
-        const int q = threadIdx.x + 256 * k;
-        if (q < DVT_BY * DVT_X) sb[q] = vb[k];
-    }
     __syncthreads();
-    const int tx = threadIdx.x & 63, ty0 = threadIdx.x >> 6;
+    const long PS = DVT_PX;
+    const double *pcol = sp + 2 * DVT_PX + tx + 2;   // tile row 0, column i
+    // gy at tile row rr, fy = (p_{rr+1} - p_rr) / dy (0 where no interior cell reads them)
+    auto gyat = [&](int rr) {
+        const int j = j0 + rr;
+        return (i < nx && j >= 0 && j < ny) ? grad2k(pcol + rr * PS, PS, j, ny, K.y2) : 0.0;
+    };
+    auto fyat = [&](int rr) {
+        const int j = j0 + rr;
+        return (i < nx && j >= 0 && j + 1 < ny) ? divk(pcol[(rr + 1) * PS] - pcol[rr * PS], K.y1) : 0.0;
+    };
+    // a window down the column: gy at rows ty - 1, ty, ty + 1 and fy at ty - 1, ty
+    double gyd = gyat(r0 - 1), gyc = gyat(r0), fys = fyat(r0 - 1);
+    double ex = 0.0;
+    if (tx < 12) {   // lane 3q + 0 / 1 / 2 -> row r0 + q: gx(i0 - 1), fx(i0 - 1), gx(i0 + 64)
+        const int rr = r0 + tx / 3, kind = tx % 3, j = j0 + rr;
+        const double *prow = sp + (rr + 2) * DVT_PX + 2;   // column i0 at [0]
+        if (j < ny) {
+            if (kind == 0) {
+                if (i0 >= 1 && i0 - 1 < nx) ex = grad2k(prow - 1, 1, i0 - 1, nx, K.x2);
+            } else if (kind == 1) {
+                if (i0 >= 1 && i0 < nx) ex = divk(prow[0] - prow[-1], K.x1);
+            } else if (i0 + DVT_X < nx) {
+                ex = grad2k(prow + DVT_X, 1, i0 + DVT_X, nx, K.x2);
+            }
+        }
+    }
 #pragma unroll
-    for (int ty = ty0; ty < DVT_Y; ty += 4) {
-        const int j = j0 + ty, i = i0 + tx;
+    for (int q = 0; q < 4; ++q) {
+        const int ty = r0 + q, j = j0 + ty;
+        const double *pc = pcol + ty * PS;
+        const double gxc = (i < nx && j < ny) ? grad2k(pc, 1, i, nx, K.x2) : 0.0;
+        const double fxc = (i + 1 < nx && j < ny) ? divk(pc[1] - pc[0], K.x1) : 0.0;
+        double gxl = __shfl(gxc, (tx + 63) & 63), gxr = __shfl(gxc, (tx + 1) & 63);
+        double fxl = __shfl(fxc, (tx + 63) & 63);
+        double al = __shfl(av[q], (tx + 63) & 63), ar = __shfl(av[q], (tx + 1) & 63);
+        const double e0 = __shfl(ex, 3 * q), e1 = __shfl(ex, 3 * q + 1), e2 = __shfl(ex, 3 * q + 2);
+        const double a0 = __shfl(ae, 2 * q), a1 = __shfl(ae, 2 * q + 1);
+        if (tx == 0) { gxl = e0; fxl = e1; al = a0; }
+        if (tx == 63) { gxr = e2; ar = a1; }
+        const double gyu = gyat(ty + 1), fyn = fyat(ty);
+        const double gyd_ = gyd, gyc_ = gyc, fys_ = fys;
+        gyd = gyc; gyc = gyu; fys = fyn;
         if (j >= ny || i >= nx) continue;
         const long c = (long)j * nx + i;
         if (j < 1 || j >= ny - 1 || i < 1 || i >= nx - 1) {
             divU[c] = rho > 0 ? (rho * 0.0) / dt : 0.0;
             continue;
         }
-        // div_rc_cell, with p, a, b at the staged copies (strides DVT_PX, 1, DVT_X)
-        const double *pc = sp + (ty + 2) * DVT_PX + tx + 2;
-        const double *ac = sa + ty * DVT_AX + tx + 1;
-        const double *bc = sb + (ty + 1) * DVT_X + tx;
-        const long PS = DVT_PX, BS = DVT_X;
-        double gxl = grad2k(pc - 1, 1, i - 1, nx, K.x2), gxc = grad2k(pc, 1, i, nx, K.x2),
-               gxr = grad2k(pc + 1, 1, i + 1, nx, K.x2);
-        double gyd = grad2k(pc - PS, PS, j - 1, ny, K.y2), gyc = grad2k(pc, PS, j, ny, K.y2),
-               gyu = grad2k(pc + PS, PS, j + 1, ny, K.y2);
-        double ue = 0.5 * (ac[0] + ac[1]) - d_f * (divk(pc[1] - pc[0], K.x1) - 0.5 * (gxc + gxr));
-        double uw = 0.5 * (ac[-1] + ac[0]) - d_f * (divk(pc[0] - pc[-1], K.x1) - 0.5 * (gxl + gxc));
-        double vn = 0.5 * (bc[0] + bc[BS]) - d_f * (divk(pc[PS] - pc[0], K.y1) - 0.5 * (gyc + gyu));
-        double vs = 0.5 * (bc[-BS] + bc[0]) - d_f * (divk(pc[0] - pc[-PS], K.y1) - 0.5 * (gyd + gyc));
+        // div_rc_cell's expressions, operand for operand
+        double ue = 0.5 * (av[q] + ar) - d_f * (fxc - 0.5 * (gxc + gxr));
+        double uw = 0.5 * (al + av[q]) - d_f * (fxl - 0.5 * (gxl + gxc));
+        double vn = 0.5 * (bv[q + 1] + bv[q + 2]) - d_f * (fyn - 0.5 * (gyc_ + gyu));
+        double vs = 0.5 * (bv[q] + bv[q + 1]) - d_f * (fys_ - 0.5 * (gyd_ + gyc_));
         const double d = divk(ue - uw, K.x1) + divk(vn - vs, K.y1);
         divU[c] = rho > 0 ? (rho * d) / dt : d;
     }

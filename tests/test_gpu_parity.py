@@ -216,6 +216,20 @@ def test_dct_solve_sizes(gpu, oracle, shape):
     assert err <= 1e-13, err
 
 
+@pytest.mark.parametrize("shape", [(16, 64), (17, 65), (33, 130), (130, 200), (300, 1001)])
+def test_divergence_rc_tiles_bitwise(gpu, oracle, shape):
+    """functions.py:1016-1070 (Rhie-Chow divergence) bit for bit against the oracle's C
+    restatement, at shapes that end the 64 x 16 tiles of k_divergence_t at every offset:
+    the kernel shares each gradient / face quotient between neighbouring cells (lane
+    shuffles, register reuse down the column), so the tile edges take the extra values."""
+    ny, nx = shape
+    dx, dy = 1.0 / (nx - 1), 1.0 / (ny - 1)
+    rng = np.random.default_rng(ny * 31 + nx)
+    a, b, p = (rng.standard_normal((ny, nx)) for _ in range(3))
+    _eq(gpu._compute_divergence_rc(a, b, p, 2e-3, 1.0, dx, dy),
+        oracle._compute_divergence_rc(a, b, p, 2e-3, 1.0, dx, dy))
+
+
 def test_projection_pieces(gpu):
     o = golden("operators")
     dx, dy = float(o["dx"]), float(o["dy"])
