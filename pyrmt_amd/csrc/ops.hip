@@ -527,18 +527,12 @@ __global__ void k_divergence_rc(const double *__restrict__ a, const double *__re
 // XCD's L2 sees a contiguous band of tile rows and their halos).
 constexpr int DVT_X = 64, DVT_Y = 16, DVT_PX = DVT_X + 4, DVT_PY = DVT_Y + 4;
 static_assert(DVT_X == 64 && DVT_Y == 16, "k_divergence_t: a wave per 4 tile rows, a lane per column");
-__global__ void __launch_bounds__(256) k_divergence_t(const double *__restrict__ a,
-                                                      const double *__restrict__ b,
-                                                      const double *__restrict__ p, int ny, int nx,
-                                                      double d_f, RcDiv K,
-                                                      double *__restrict__ divU, double rho,
-                                                      double dt, const double *__restrict__ dtp,
-                                                      int tiles_x, int ntiles) {
-    __shared__ double sp[DVT_PY * DVT_PX];
-    if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
-    const int per = ntiles / 8, bk = blockIdx.x;
-    const int tile = bk < 8 * per ? (bk % 8) * per + bk / 8 : bk;
-    const int i0 = (tile % tiles_x) * DVT_X, j0 = (tile / tiles_x) * DVT_Y;
+// one 64 x 16 tile at (i0, j0), 256 threads, sp: the block's p tile (DVT_PY x DVT_PX)
+__device__ __forceinline__ void div_rc_tile(const double *__restrict__ a,
+                                            const double *__restrict__ b,
+                                            const double *__restrict__ p, int ny, int nx,
+                                            double d_f, const RcDiv &K, double *__restrict__ divU,
+                                            double rho, double dt, int i0, int j0, double *sp) {
     const int tx = threadIdx.x & 63, r0 = 4 * (threadIdx.x >> 6), i = i0 + tx;
     constexpr int NP = (DVT_PY * DVT_PX + 255) / 256;
     double vp[NP], av[4], bv[6], ae = 0.0;
@@ -629,6 +623,20 @@ __global__ void __launch_bounds__(256) k_divergence_t(const double *__restrict__
         divU[c] = rho > 0 ? (rho * d) / dt : d;
     }
 }
+__global__ void __launch_bounds__(256) k_divergence_t(const double *__restrict__ a,
+                                                      const double *__restrict__ b,
+                                                      const double *__restrict__ p, int ny, int nx,
+                                                      double d_f, RcDiv K,
+                                                      double *__restrict__ divU, double rho,
+                                                      double dt, const double *__restrict__ dtp,
+                                                      int tiles_x, int ntiles) {
+    __shared__ double sp[DVT_PY * DVT_PX];
+    if (dtp) { dt = *dtp; d_f = dt / rho; }   // the host's dt / rho
+    const int per = ntiles / 8, bk = blockIdx.x;
+    const int tile = bk < 8 * per ? (bk % 8) * per + bk / 8 : bk;
+    div_rc_tile(a, b, p, ny, nx, d_f, K, divU, rho, dt, (tile % tiles_x) * DVT_X,
+                (tile / tiles_x) * DVT_Y, sp);
+}
 static int divergence_full(hipStream_t st, const double *a, const double *b, const double *p,
                            int ny, int nx, double d_f, const RcDiv &K, double *divU, double rho,
                            double dt, const double *dtp) {
@@ -645,18 +653,25 @@ __global__ void __launch_bounds__(256) k_divergence_tiles(
     int ny, int nx, RcDiv K, double *__restrict__ divU, double rho, double dt,
     const double *__restrict__ dtp, const int *__restrict__ tiles,
     const int *__restrict__ count, int tiles_x) {
+    static_assert(MOM_TX == DVT_X && MOM_TY == DVT_Y, "k_divergence_tiles: momentum tiles are div_rc_tile's");
+    __shared__ double sp[DVT_PY * DVT_PX];
     if (dtp) dt = *dtp;
     const double d_f = dt / rho;   // as the host's dt / rho
     const int cnt = *count;
-    constexpr int TW = MOM_TX + 2, TH = MOM_TY + 2;
+    constexpr int TW = MOM_TX + 2;
     for (int bk = blockIdx.x; bk < cnt; bk += gridDim.x) {   // list_grid launch
         const int t = tiles[bk];
-        const int i0 = (t % tiles_x) * MOM_TX - 1, j0 = (t / tiles_x) * MOM_TY - 1;
-        for (int e = threadIdx.x; e < TW * TH; e += blockDim.x) {
-            const int j = j0 + e / TW, i = i0 + e % TW;
+        const int ti0 = (t % tiles_x) * MOM_TX, tj0 = (t / tiles_x) * MOM_TY;
+        // the tile itself (k_divergence_t's body), then its one-cell ring cell by cell
+        div_rc_tile(a, b, p, ny, nx, d_f, K, divU, rho, dt, ti0, tj0, sp);
+        for (int e = threadIdx.x; e < 2 * TW + 2 * MOM_TY; e += blockDim.x) {
+            int j, i;
+            if (e < 2 * TW) { j = e < TW ? tj0 - 1 : tj0 + MOM_TY; i = ti0 - 1 + e % TW; }
+            else { const int f = e - 2 * TW; j = tj0 + f % MOM_TY; i = f < MOM_TY ? ti0 - 1 : ti0 + MOM_TX; }
             if (j >= 0 && j < ny && i >= 0 && i < nx)
                 div_rc_cell(a, b, p, ny, nx, d_f, K, divU, rho, dt, j, i);
         }
+        __syncthreads();   // sp is the next tile's
     }
 }
 __global__ void k_divergence_central(const double *__restrict__ a, const double *__restrict__ b,
